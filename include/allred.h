@@ -1,0 +1,234 @@
+/*
+ * allred.h — C-ABI of the MI355X allreduce engine (liballred.so).
+ *
+ * Drop-in boundary for the reference EngineerCharlie/TenstorrentAllreduce.
+ * Plain pointers and sizes only; every entry point names the reference
+ * interface it replaces (file:line under the reference tree).  All functions
+ * return ALLRED_OK (0) or a negative ALLRED_ERR_* code unless documented
+ * otherwise; the reference itself has no error codes (bad configurations hang
+ * the Wormhole) — here they are rejected up front.
+ *
+ * Host-only entry points (schedule, data generation, validation) never touch
+ * the GPU.  Device entry points take a hipStream_t as `void* stream`
+ * (NULL = the default stream) and enqueue asynchronously.
+ */
+#ifndef ALLRED_H
+#define ALLRED_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALLRED_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------- */
+#define ALLRED_OK 0
+#define ALLRED_ERR_ARG (-1)          /* bad argument / size / alignment       */
+#define ALLRED_ERR_SCHEDULE (-2)     /* grid is not a valid allreduce schedule */
+#define ALLRED_ERR_HIP (-3)          /* HIP runtime failure                   */
+#define ALLRED_ERR_RCCL (-4)         /* RCCL failure                          */
+#define ALLRED_ERR_NOMEM (-5)
+#define ALLRED_ERR_UNSUPPORTED (-6)
+#define ALLRED_ERR_TRANSPORT (-7)    /* host exchange callback failed         */
+
+/* ---- enums --------------------------------------------------------------*/
+/* argv[1] "is swing version?" (allred_helper.cpp:205-208) */
+#define ALLRED_RECDUB 0
+#define ALLRED_SWING 1
+/* which reference program: allred_BO_2D with arg 8 = 1 / = 0, allred_mem_2D */
+#define ALLRED_BO 0
+#define ALLRED_LO 1
+#define ALLRED_MEM 2
+/* execution form of a virtual-rank plan */
+#define ALLRED_EXEC_STEPS 0  /* one launch per schedule step (the reference's step structure) */
+#define ALLRED_EXEC_FUSED 1  /* one launch for the whole allreduce, same arithmetic */
+
+#define ALLRED_MAX_NODES 64
+#define ALLRED_MAX_STEPS 6
+
+const char* allred_status_string(int status);
+int allred_abi_version(void);
+
+/* ======================================================================
+ * Schedule — replaces allred_helper.hpp:24-30 / allred_helper.cpp:122-191
+ * and allred_BO_2D.cpp:4-5 / :217-270 (same arguments; the C++ reference
+ * signatures are kept in include/allred_helper.hpp).
+ * ==================================================================== */
+int allred_highest_power_of_two(int value);                          /* allred_helper.cpp:122 */
+uint32_t allred_get_step_directions(int node_x, int node_y);         /* allred_helper.cpp:136 */
+int allred_get_comm_partner_swing_2d(int node, int step, int horizontal_step,
+                                     int side_length, int total_nodes);   /* allred_helper.cpp:166 */
+int allred_get_comm_partner_recdub_2d(int node, int recdub_step, int horizontal_step,
+                                      int message_pass_depth, uint32_t* step_directions,
+                                      int side_length);                   /* allred_helper.cpp:145 */
+void allred_get_swing_block_comm_indexes(int node, int step, uint32_t* blocks /*[2]*/,
+                                         int horizontal_step, int side_length,
+                                         int total_nodes);                /* allred_BO_2D.cpp:220 */
+void allred_get_recdub_block_comm_indexes(int node, int step, uint32_t* blocks /*[2]*/,
+                                          int horizontal_step, int side_length, int total_nodes,
+                                          int message_pass_depth,
+                                          uint32_t* step_directions);     /* allred_BO_2D.cpp:242 */
+/* NUM_TILES normalisation, allred_helper.cpp:224-234 */
+int allred_normalize_tiles(int tiles, int total_nodes, int large_buffer);
+
+/* Whole per-rank schedule, as the per-core loop of allred_BO_2D.cpp:75-212
+ * builds it into runtime args: partners (args 14+2i), send masks (22+2s+2i),
+ * recv masks (22+4s+2i / compute args 6+2i), direction bits (arg 11).
+ * Grids: side in {1,2,4,8}, total a power of two <= 64 (side*side for the
+ * reference's square grids; (2,2), (2,4), (4,8) for 2/4/8 GPUs).
+ * Also validates the schedule (partners in range and symmetric, send ==
+ * partner's recv, reduce-scatter leaves block r at rank r, every rank's
+ * contributor sets disjoint at each merge) and derives tree_order[x]: the
+ * leaf order of the reduction tree rank x evaluates, leaves(x, k) =
+ * leaves(x, k-1) ++ leaves(partner_{k-1}(x), k-1); level k adds adjacent
+ * groups of 2^k leaves.  LO gives rank x the value of tree x; BO gives block
+ * b the value of tree b (reduced at its owner, then all-gathered).  For
+ * RecDub all trees coincide; for Swing they differ (in bf16 rounding only). */
+typedef struct {
+    int32_t algo, side, total, steps;
+    int32_t partner[ALLRED_MAX_NODES][ALLRED_MAX_STEPS];
+    uint64_t send[ALLRED_MAX_NODES][ALLRED_MAX_STEPS];
+    uint64_t recv[ALLRED_MAX_NODES][ALLRED_MAX_STEPS];
+    uint32_t dirs[ALLRED_MAX_NODES];
+    uint8_t tree_order[ALLRED_MAX_NODES][ALLRED_MAX_NODES];
+} allred_schedule;
+int allred_schedule_build(int algo, int side_length, int total_nodes, allred_schedule* out);
+
+/* ======================================================================
+ * Host data — tt-metal bfloat16 helpers the reference calls
+ * (allred_helper.cpp:277-285) and validate_result_vector (:18-120).
+ * ==================================================================== */
+/* create_random_vector_of_bfloat16(num_bytes, rand_max, seed): std::mt19937 +
+ * uniform_real_distribution<float>(0, rand_max); two bf16 per uint32, low
+ * half first.  round_mode 0 = truncating bfloat16(float) (default), 1 = RNE. */
+void allred_random_bf16_vector(size_t num_bytes, int rand_max, int seed, int round_mode, uint32_t* out);
+void allred_constant_bf16_vector(size_t num_bytes, float value, uint32_t* out);
+/* validate_result_vector: expected = bf16((a+b) * (total_nodes/2)); prints the
+ * reference's messages ("All values match!" ...) when verbose != 0.
+ * Returns the number of elements with |actual - expected| > error.          */
+long allred_validate_result_vector(const uint32_t* result_vec, const uint32_t* src_vec_0,
+                                   const uint32_t* src_vec_1, size_t num_els, float error,
+                                   uint32_t total_nodes, int verbose, float* max_error);
+
+/* ======================================================================
+ * Device compute (HIP, gfx950)
+ * ==================================================================== */
+/* dst[i] = bf16_rne(float(dst[i]) + float(src[i])), i < n.  Replaces the
+ * per-tile add_tiles + pack_tile<true> of allred_BO_2D/kernels/compute_kernel.cpp:53-60. */
+int allred_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream);
+/* Same over the blocks named by a 64-bit mask (block b = [b*block_elems, (b+1)*block_elems)),
+ * the BO compute loop of compute_kernel.cpp:35-67 for one step. */
+int allred_bf16_add_masked(uint16_t* dst, const uint16_t* src, uint64_t block_mask,
+                           size_t block_elems, void* stream);
+
+/* ======================================================================
+ * Virtual-rank plan: `total` ranks resident in ONE GPU's HBM, rank r at
+ * ranks + r * rank_stride (elements).  Replaces the 64-core Tensix program
+ * (allred_BO_2D/kernels, allred_LOO_2D/kernels, allred_mem_2D/kernels).
+ * Every rank ends with the allreduced vector, in place.
+ * ==================================================================== */
+typedef struct allred_plan allred_plan;
+typedef struct {
+    int32_t algo;          /* ALLRED_SWING / ALLRED_RECDUB                      */
+    int32_t variant;       /* ALLRED_BO / ALLRED_LO / ALLRED_MEM                */
+    int32_t exec;          /* ALLRED_EXEC_STEPS / ALLRED_EXEC_FUSED             */
+    int32_t side_length;   /* 1, 2, 4, 8                                        */
+    int32_t total_nodes;   /* 0 = side*side                                     */
+    int32_t device;        /* HIP device ordinal (-1 = current)                 */
+    uint64_t elems_per_rank; /* bf16 elements; BO/MEM need a multiple of 8*total, LO of 8 */
+} allred_plan_desc;
+int allred_plan_create(const allred_plan_desc* desc, allred_plan** out);
+int allred_plan_destroy(allred_plan* plan);
+size_t allred_plan_workspace_bytes(const allred_plan* plan);
+/* workspace: device memory of allred_plan_workspace_bytes() (may be NULL when 0) */
+int allred_plan_execute(allred_plan* plan, uint16_t* ranks, uint64_t rank_stride,
+                        void* workspace, void* stream);
+/* number of kernel launches one execute enqueues (for per-launch accounting) */
+int allred_plan_launches(const allred_plan* plan);
+
+/* ======================================================================
+ * Reference program surface: AllredConfig (allred_helper.hpp:47-97) +
+ * the mains of allred_BO_2D.cpp:7-215 / allred_LO_2D.cpp:9-106 /
+ * allred_mem_2D.cpp:4-165, with the same 8 positional arguments.
+ * ==================================================================== */
+typedef struct {
+    int32_t variant;         /* ALLRED_BO (bo flag decides BO vs LO), ALLRED_LO (legacy binary), ALLRED_MEM */
+    int32_t swing;           /* argv[1] == 1                                     */
+    int32_t run_kernel;      /* argv[2] == 1                                     */
+    int32_t side_length;     /* highest_power_of_two(argv[3])                    */
+    int32_t seed;            /* argv[4]: < 0 -> all ones                          */
+    int32_t tiles;           /* argv[5] (raw, >= 1)                              */
+    int32_t error;           /* argv[6]                                          */
+    int32_t print_core;      /* argv[7]                                          */
+    int32_t bandwidth_optimal; /* argv[8]                                        */
+    int32_t total_nodes;     /* extension (ALLRED_NODES env / argv[9]); 0 = side^2 */
+    int32_t exec;            /* extension (ALLRED_EXEC env): steps (default) / fused */
+    int32_t round_mode;      /* extension (ALLRED_BF16_ROUND env): 0 trunc, 1 rne */
+    int32_t num_tiles;       /* derived: normalised NUM_TILES                    */
+} allred_args;
+/* Parses argv exactly like AllredConfig's ctor (std::stoi semantics: leading
+ * integer, junk -> ALLRED_ERR_ARG where the reference would throw).          */
+int allred_args_parse(int argc, const char* const* argv, int variant, allred_args* out);
+
+typedef struct {
+    int64_t mismatches;      /* validate_result_vector count, -1 if not run      */
+    float max_error;
+    double device_seconds;   /* hipEvent time of the device-resident allreduce */
+    double e2e_seconds;      /* pinned H2D + allreduce + D2H                     */
+    uint64_t bytes_per_rank;
+    int32_t total_nodes;
+    int32_t launches;
+} allred_report;
+/* Generate inputs, H2D, run (if run_kernel), D2H of print_core, validate
+ * (printing like the reference when verbose), report timing.               */
+int allred_run(const allred_args* args, int verbose, allred_report* report);
+
+/* ======================================================================
+ * Multi-GPU: one process per GPU, RCCL point-to-point over xGMI.
+ * The grid (side_length, total_nodes) maps GPUs onto the reference's own
+ * 2D schedule: 2 GPUs (2,2), 4 GPUs (2,4), 8 GPUs (4,8).
+ * ==================================================================== */
+#define ALLRED_UNIQUE_ID_BYTES 128
+typedef struct allred_comm allred_comm;
+int allred_comm_get_unique_id(uint8_t* id /*[128]*/);
+int allred_comm_init(const uint8_t* id, int nranks, int rank, int device, allred_comm** out);
+int allred_comm_destroy(allred_comm* comm);
+
+typedef struct {
+    int32_t algo;           /* ALLRED_SWING / ALLRED_RECDUB                     */
+    int32_t variant;        /* ALLRED_BO or ALLRED_LO                           */
+    int32_t side_length;    /* GPU grid                                         */
+    int32_t total_nodes;    /* == nranks                                        */
+    uint64_t elems;         /* bf16 elements per GPU bucket (multiple of 8*total for BO) */
+    /* hierarchical extension: the bucket holds local_ranks virtual ranks
+     * (stride `elems`), reduced on-GPU first with the local_side grid. 1 = flat. */
+    int32_t local_ranks;
+    int32_t local_side;
+    int32_t local_algo;
+    int32_t chunks;         /* pipeline chunks per step (>=1)                   */
+} allred_dist_desc;
+/* Scratch device bytes the call needs (recv staging + hierarchical partial). */
+size_t allred_dist_workspace_bytes(const allred_dist_desc* desc);
+int allred_dist_allreduce(allred_comm* comm, const allred_dist_desc* desc, uint16_t* buf,
+                          void* workspace, void* stream);
+
+/* Host-memory twin of allred_dist_allreduce for CPU tests and loopback
+ * checks: the same per-rank step program, exchanges done by a callback.     */
+typedef struct {
+    void* ptr;
+    uint64_t bytes;
+} allred_seg;
+/* Exchange with `peer`: send every send segment, receive every recv segment
+ * (in list order on both sides).  Return 0 on success. */
+typedef int (*allred_exchange_fn)(void* ctx, int peer, int nsend, const allred_seg* send,
+                                  int nrecv, const allred_seg* recv);
+int allred_dist_allreduce_host(const allred_dist_desc* desc, int rank, uint16_t* buf,
+                               uint16_t* scratch, allred_exchange_fn exchange, void* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALLRED_H */

@@ -1,0 +1,244 @@
+"""MI355X-native allreduce engine with the capabilities of
+EngineerCharlie/TenstorrentAllreduce (2D Swing / Recursive-Doubling
+allreduce, bandwidth-optimal / latency-optimal / shared-memory variants).
+
+The engine is C++/HIP (``liballred.so``, C-ABI in ``include/allred.h``) plus
+the reference's executables (``bin/allred_BO_2D`` ...).  This package is a
+thin Python view of that C-ABI for tests and ``bench.py``: device memory and
+streams come from PyTorch (plumbing), every computation runs in the library.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Callable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import (BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, RECDUB, SWING, AllredError, Args, DistDesc,  # noqa: F401
+                   PlanDesc, Report, Schedule, Seg, check, lib)
+
+__all__ = [
+    "BO", "LO", "MEM", "SWING", "RECDUB", "EXEC_STEPS", "EXEC_FUSED", "AllredError", "schedule",
+    "highest_power_of_two", "get_step_directions", "get_comm_partner_swing_2D", "get_comm_partner_recdub_2D",
+    "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
+    "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "bf16_add",
+    "bf16_add_masked", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
+    "dist_allreduce_host", "dist_workspace_bytes",
+]
+
+
+# ---------------------------------------------------------------- schedule
+def highest_power_of_two(v: int) -> int:  # allred_helper.cpp:122
+    return lib.allred_highest_power_of_two(v)
+
+
+def get_step_directions(x: int, y: int) -> int:  # allred_helper.cpp:136
+    return lib.allred_get_step_directions(x, y)
+
+
+def get_comm_partner_swing_2D(node, step, horizontal_step, side, total) -> int:  # allred_helper.cpp:166
+    return lib.allred_get_comm_partner_swing_2d(node, step, int(bool(horizontal_step)), side, total)
+
+
+def get_comm_partner_recdub_2D(node, step, horizontal_step, depth, step_directions, side):
+    """allred_helper.cpp:145; returns (partner, updated step_directions)."""
+    d = C.c_uint32(step_directions)
+    p = lib.allred_get_comm_partner_recdub_2d(node, step, int(bool(horizontal_step)), depth, C.byref(d), side)
+    return p, d.value
+
+
+def get_swing_block_comm_indexes(node, step, blocks, horizontal_step, side, total) -> int:
+    """allred_BO_2D.cpp:220; ORs into the 64-bit mask `blocks`, returns it."""
+    b = (C.c_uint32 * 2)(blocks & 0xFFFFFFFF, blocks >> 32)
+    lib.allred_get_swing_block_comm_indexes(node, step, b, int(bool(horizontal_step)), side, total)
+    return b[0] | (b[1] << 32)
+
+
+def get_recdub_block_comm_indexes(node, step, blocks, horizontal_step, side, total, depth, step_directions=0):
+    """allred_BO_2D.cpp:242; returns (mask, step_directions)."""
+    b = (C.c_uint32 * 2)(blocks & 0xFFFFFFFF, blocks >> 32)
+    d = C.c_uint32(step_directions)
+    lib.allred_get_recdub_block_comm_indexes(node, step, b, int(bool(horizontal_step)), side, total, depth,
+                                             C.byref(d))
+    return b[0] | (b[1] << 32), d.value
+
+
+def normalize_tiles(tiles: int, total_nodes: int, large_buffer: bool) -> int:  # allred_helper.cpp:224
+    return lib.allred_normalize_tiles(tiles, total_nodes, int(bool(large_buffer)))
+
+
+def schedule(algo: int, side: int, total: int | None = None) -> dict:
+    """The per-rank schedule of allred_BO_2D.cpp:75-212 (validated)."""
+    total = side * side if total is None else total
+    s = Schedule()
+    check(lib.allred_schedule_build(algo, side, total, C.byref(s)), f"schedule({algo},{side},{total})")
+    T, K = s.total, s.steps
+    return {
+        "algo": s.algo, "side": s.side, "total": T, "steps": K,
+        "partner": [[s.partner[r][k] for k in range(K)] for r in range(T)],
+        "send": [[s.send[r][k] for k in range(K)] for r in range(T)],
+        "recv": [[s.recv[r][k] for k in range(K)] for r in range(T)],
+        "dirs": [s.dirs[r] for r in range(T)],
+        "tree_order": [[s.tree_order[x][i] for i in range(T)] for x in range(T)],
+    }
+
+
+# ---------------------------------------------------------------- host data
+def random_bf16_vector(num_bytes: int, seed: int, rand_max: int = 100, round_mode: int = 0) -> np.ndarray:
+    """tt-metal create_random_vector_of_bfloat16 (packed uint32, low half first)."""
+    out = np.empty(num_bytes // 4, dtype=np.uint32)
+    lib.allred_random_bf16_vector(num_bytes, rand_max, seed, round_mode, out.ctypes.data)
+    return out
+
+
+def constant_bf16_vector(num_bytes: int, value: float) -> np.ndarray:
+    out = np.empty(num_bytes // 4, dtype=np.uint32)
+    lib.allred_constant_bf16_vector(num_bytes, value, out.ctypes.data)
+    return out
+
+
+def validate_result_vector(result, src0, src1, num_els: int, error: float, total_nodes: int,
+                           verbose: bool = False):
+    """allred_helper.cpp:18-120; returns (mismatches, max_error)."""
+    arrs = [np.ascontiguousarray(x, dtype=np.uint32) for x in (result, src0, src1)]
+    m = C.c_float(0)
+    bad = lib.allred_validate_result_vector(arrs[0].ctypes.data, arrs[1].ctypes.data, arrs[2].ctypes.data,
+                                            num_els, error, total_nodes, int(verbose), C.byref(m))
+    return int(bad), float(m.value)
+
+
+# ---------------------------------------------------------------- device
+def _stream_ptr(stream) -> int | None:
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream  # torch.cuda.Stream
+
+
+def bf16_add(dst_ptr: int, src_ptr: int, n: int, stream=None) -> None:
+    check(lib.allred_bf16_add(dst_ptr, src_ptr, n, _stream_ptr(stream)), "bf16_add")
+
+
+def bf16_add_masked(dst_ptr: int, src_ptr: int, mask: int, block_elems: int, stream=None) -> None:
+    check(lib.allred_bf16_add_masked(dst_ptr, src_ptr, mask, block_elems, _stream_ptr(stream)), "bf16_add_masked")
+
+
+class Plan:
+    """N virtual ranks in one GPU's HBM (allred_plan_*)."""
+
+    def __init__(self, algo: int, variant: int, side: int, elems_per_rank: int, total: int = 0,
+                 exec_mode: int = EXEC_STEPS, device: int = -1):
+        d = PlanDesc(algo, variant, exec_mode, side, total, device, elems_per_rank)
+        h = C.c_void_p()
+        check(lib.allred_plan_create(C.byref(d), C.byref(h)), "plan_create")
+        self._h = h
+        self.total = total or side * side
+        self.elems = elems_per_rank
+        self.workspace_bytes = lib.allred_plan_workspace_bytes(h)
+        self.launches = lib.allred_plan_launches(h)
+
+    def execute(self, ranks_ptr: int, stride: int, workspace_ptr: int | None = None, stream=None) -> None:
+        check(lib.allred_plan_execute(self._h, ranks_ptr, stride, workspace_ptr, _stream_ptr(stream)),
+              "plan_execute")
+
+    def close(self):
+        if self._h:
+            lib.allred_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---------------------------------------------------------------- program surface
+def parse_args(argv: Sequence[str], variant: int = BO) -> Args:
+    arr = (C.c_char_p * len(argv))(*[a.encode() for a in argv])
+    a = Args()
+    check(lib.allred_args_parse(len(argv), arr, variant, C.byref(a)), "args_parse")
+    return a
+
+
+def run(argv: Sequence[str], variant: int = BO, verbose: bool = False) -> Report:
+    """AllredConfig(argv) + RunProgram() in-process (allred_helper.hpp:47-97)."""
+    a = parse_args(argv, variant)
+    r = Report()
+    check(lib.allred_run(C.byref(a), int(verbose), C.byref(r)), "run")
+    return r
+
+
+def run_cli(binary: str, args: Sequence[str], env: dict | None = None, timeout: float = 300):
+    """Run bin/<binary> (allred_BO_2D / allred_LO_2D / allred_mem_2D) like the reference."""
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([os.path.join(_lib.BIN_DIR, binary), *map(str, args)], capture_output=True, text=True,
+                          env=e, timeout=timeout)
+
+
+# ---------------------------------------------------------------- multi-GPU
+class Comm:
+    """One RCCL communicator per process/GPU (allred_comm_*)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * _lib.UNIQUE_ID_BYTES)()
+        check(lib.allred_comm_get_unique_id(buf), "comm_get_unique_id")
+        return bytes(buf)
+
+    def __init__(self, uid: bytes, nranks: int, rank: int, device: int):
+        buf = (C.c_uint8 * _lib.UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        check(lib.allred_comm_init(buf, nranks, rank, device, C.byref(h)), "comm_init")
+        self._h = h
+        self.nranks, self.rank = nranks, rank
+
+    def close(self):
+        if self._h:
+            lib.allred_comm_destroy(self._h)
+            self._h = None
+
+
+def dist_desc(algo: int, variant: int, side: int, total: int, elems: int, local_ranks: int = 1,
+              local_side: int = 1, local_algo: int = SWING, chunks: int = 1) -> DistDesc:
+    return DistDesc(algo, variant, side, total, elems, local_ranks, local_side, local_algo, chunks)
+
+
+def dist_workspace_bytes(desc: DistDesc) -> int:
+    return lib.allred_dist_workspace_bytes(C.byref(desc))
+
+
+def dist_allreduce(comm: Comm, desc: DistDesc, buf_ptr: int, workspace_ptr: int, stream=None) -> None:
+    check(lib.allred_dist_allreduce(comm._h, C.byref(desc), buf_ptr, workspace_ptr, _stream_ptr(stream)),
+          "dist_allreduce")
+
+
+def dist_allreduce_host(desc: DistDesc, rank: int, buf: np.ndarray, scratch: np.ndarray,
+                        exchange: Callable[[int, list, list], None]) -> None:
+    """Host-memory twin: `exchange(peer, sends, recvs)` gets lists of writable
+    uint8 numpy views and must send every send view / fill every recv view."""
+
+    def _cb(_ctx, peer, nsend, send, nrecv, recv):
+        try:
+            def views(segs, n):
+                out = []
+                for i in range(n):
+                    s = segs[i]
+                    out.append(np.ctypeslib.as_array((C.c_uint8 * s.bytes).from_address(s.ptr)))
+                return out
+            exchange(peer, views(send, nsend), views(recv, nrecv))
+            return 0
+        except Exception:  # pragma: no cover - surfaced as ALLRED_ERR_TRANSPORT
+            import traceback
+            traceback.print_exc()
+            return 1
+
+    cb = _lib.EXCHANGE_FN(_cb)
+    assert buf.dtype == np.uint16 and scratch.dtype == np.uint16
+    check(lib.allred_dist_allreduce_host(C.byref(desc), rank, buf.ctypes.data, scratch.ctypes.data, cb, None),
+          "dist_allreduce_host")

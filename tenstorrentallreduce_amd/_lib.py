@@ -1,0 +1,142 @@
+"""ctypes binding of liballred.so (include/allred.h).
+
+The product is the C-ABI library built in-tree by ``make -C
+tenstorrentallreduce_amd`` (``__graft_entry__.build()``).  This module only
+declares its symbols; there is no Python or CPU fallback for any device entry
+point — if the library is missing, importing the package fails loudly.
+
+HIP runtime note: ``import torch`` must come before the library is loaded so
+that liballred.so binds (by soname ``libamdhip64.so.7`` / ``librccl.so.1``)
+to the one HIP runtime and RCCL torch already loaded, never a second copy.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+try:  # plumbing only: one HIP runtime per process (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is always present in this image
+    torch = None
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "liballred.so")
+BIN_DIR = os.path.join(HERE, "bin")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"{LIB_PATH} is missing: build the HIP engine first "
+        "(python -c 'import __graft_entry__ as g; g.build()' or make -C tenstorrentallreduce_amd)")
+
+lib = C.CDLL(LIB_PATH)
+
+# ---- status / enums (allred.h) ------------------------------------------
+OK, ERR_ARG, ERR_SCHEDULE, ERR_HIP, ERR_RCCL, ERR_NOMEM, ERR_UNSUPPORTED, ERR_TRANSPORT = 0, -1, -2, -3, -4, -5, -6, -7
+RECDUB, SWING = 0, 1
+BO, LO, MEM = 0, 1, 2
+EXEC_STEPS, EXEC_FUSED = 0, 1
+MAX_NODES, MAX_STEPS = 64, 6
+UNIQUE_ID_BYTES = 128
+
+
+class AllredError(RuntimeError):
+    def __init__(self, status: int, what: str = ""):
+        self.status = status
+        msg = lib.allred_status_string(status).decode()
+        super().__init__(f"{what}: {msg} ({status})" if what else f"{msg} ({status})")
+
+
+def check(status: int, what: str = "") -> int:
+    if status != OK:
+        raise AllredError(status, what)
+    return status
+
+
+class Schedule(C.Structure):
+    _fields_ = [
+        ("algo", C.c_int32), ("side", C.c_int32), ("total", C.c_int32), ("steps", C.c_int32),
+        ("partner", (C.c_int32 * MAX_STEPS) * MAX_NODES),
+        ("send", (C.c_uint64 * MAX_STEPS) * MAX_NODES),
+        ("recv", (C.c_uint64 * MAX_STEPS) * MAX_NODES),
+        ("dirs", C.c_uint32 * MAX_NODES),
+        ("tree_order", (C.c_uint8 * MAX_NODES) * MAX_NODES),
+    ]
+
+
+class PlanDesc(C.Structure):
+    _fields_ = [
+        ("algo", C.c_int32), ("variant", C.c_int32), ("exec", C.c_int32), ("side_length", C.c_int32),
+        ("total_nodes", C.c_int32), ("device", C.c_int32), ("elems_per_rank", C.c_uint64),
+    ]
+
+
+class Args(C.Structure):
+    _fields_ = [(n, C.c_int32) for n in (
+        "variant", "swing", "run_kernel", "side_length", "seed", "tiles", "error", "print_core",
+        "bandwidth_optimal", "total_nodes", "exec", "round_mode", "num_tiles")]
+
+
+class Report(C.Structure):
+    _fields_ = [
+        ("mismatches", C.c_int64), ("max_error", C.c_float), ("device_seconds", C.c_double),
+        ("e2e_seconds", C.c_double), ("bytes_per_rank", C.c_uint64), ("total_nodes", C.c_int32),
+        ("launches", C.c_int32),
+    ]
+
+
+class DistDesc(C.Structure):
+    _fields_ = [
+        ("algo", C.c_int32), ("variant", C.c_int32), ("side_length", C.c_int32), ("total_nodes", C.c_int32),
+        ("elems", C.c_uint64), ("local_ranks", C.c_int32), ("local_side", C.c_int32), ("local_algo", C.c_int32),
+        ("chunks", C.c_int32),
+    ]
+
+
+class Seg(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
+
+
+EXCHANGE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int, C.POINTER(Seg), C.c_int, C.POINTER(Seg))
+
+_P = C.c_void_p
+_u16p = C.c_void_p
+# (name, restype, argtypes) for every entry point declared in include/allred.h
+SIGNATURES = [
+    ("allred_status_string", C.c_char_p, [C.c_int]),
+    ("allred_abi_version", C.c_int, []),
+    ("allred_highest_power_of_two", C.c_int, [C.c_int]),
+    ("allred_get_step_directions", C.c_uint32, [C.c_int, C.c_int]),
+    ("allred_get_comm_partner_swing_2d", C.c_int, [C.c_int] * 5),
+    ("allred_get_comm_partner_recdub_2d", C.c_int,
+     [C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32), C.c_int]),
+    ("allred_get_swing_block_comm_indexes", None,
+     [C.c_int, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_int]),
+    ("allred_get_recdub_block_comm_indexes", None,
+     [C.c_int, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32)]),
+    ("allred_normalize_tiles", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("allred_schedule_build", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(Schedule)]),
+    ("allred_random_bf16_vector", None, [C.c_size_t, C.c_int, C.c_int, C.c_int, _P]),
+    ("allred_constant_bf16_vector", None, [C.c_size_t, C.c_float, _P]),
+    ("allred_validate_result_vector", C.c_long,
+     [_P, _P, _P, C.c_size_t, C.c_float, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
+    ("allred_bf16_add", C.c_int, [_u16p, _u16p, C.c_size_t, _P]),
+    ("allred_bf16_add_masked", C.c_int, [_u16p, _u16p, C.c_uint64, C.c_size_t, _P]),
+    ("allred_plan_create", C.c_int, [C.POINTER(PlanDesc), C.POINTER(_P)]),
+    ("allred_plan_destroy", C.c_int, [_P]),
+    ("allred_plan_workspace_bytes", C.c_size_t, [_P]),
+    ("allred_plan_execute", C.c_int, [_P, _u16p, C.c_uint64, _P, _P]),
+    ("allred_plan_launches", C.c_int, [_P]),
+    ("allred_args_parse", C.c_int, [C.c_int, C.POINTER(C.c_char_p), C.c_int, C.POINTER(Args)]),
+    ("allred_run", C.c_int, [C.POINTER(Args), C.c_int, C.POINTER(Report)]),
+    ("allred_comm_get_unique_id", C.c_int, [_P]),
+    ("allred_comm_init", C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    ("allred_comm_destroy", C.c_int, [_P]),
+    ("allred_dist_workspace_bytes", C.c_size_t, [C.POINTER(DistDesc)]),
+    ("allred_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
+    ("allred_dist_allreduce_host", C.c_int, [C.POINTER(DistDesc), C.c_int, _u16p, _u16p, EXCHANGE_FN, _P]),
+]
+
+for _name, _res, _args in SIGNATURES:
+    _f = getattr(lib, _name)  # AttributeError here = the library lacks a declared symbol
+    _f.restype = _res
+    _f.argtypes = _args

@@ -1,0 +1,355 @@
+// engine.cpp — virtual-rank allreduce plans (N ranks in one GPU's HBM) and
+// the reference program surface (AllredConfig + RunProgram).
+//
+// A plan replaces the 64-core Tensix program of the reference:
+//   BO  = reduce-scatter + all-gather over the schedule's block masks
+//         (allred_BO_2D/kernels/dataflow_kernel.cpp:152-267, compute_kernel.cpp:35-67)
+//   LO  = full-vector exchange + add per step (same kernels, bandwidth_optimal = 0;
+//         allred_LOO_2D/kernels/dataflow_kernel.cpp for NUM_TILES < 64)
+//   MEM = reduce own block from the shared buffer, then read everything back
+//         (allred_mem_2D/kernels/*)
+// ALLRED_EXEC_STEPS keeps the reference's step structure (one launch per
+// schedule step, all ranks at once); ALLRED_EXEC_FUSED does the identical
+// arithmetic in one HBM pass (BO/LO: k_tree, MEM: k_mem<true>).
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "internal.hpp"
+
+using namespace tsa;
+
+struct allred_plan {
+    allred_plan_desc desc{};
+    allred_schedule sched{};
+    int total = 1;
+    int device = 0;
+    size_t n = 0;           // elements per rank
+    size_t block_elems = 0; // BO/MEM block
+    // device tables
+    int16_t* d_partner = nullptr;           // [steps][total]
+    int16_t* d_rs_blocks = nullptr;         // per step: total * m_k entries (recv mask blocks)
+    int16_t* d_ag_blocks = nullptr;         // per step: total * m_k entries (send mask blocks)
+    std::vector<size_t> blk_off;            // offset of step k in the block tables
+    std::vector<int> blk_per_rank;          // m_k
+    uint8_t* d_order = nullptr;
+    size_t ws_bytes = 0;
+    int launches = 0;
+};
+
+namespace {
+
+int popcount64(uint64_t x) { return __builtin_popcountll(x); }
+
+void free_plan(allred_plan* p) {
+    if (!p) return;
+    if (p->d_partner) (void)hipFree(p->d_partner);
+    if (p->d_rs_blocks) (void)hipFree(p->d_rs_blocks);
+    if (p->d_ag_blocks) (void)hipFree(p->d_ag_blocks);
+    if (p->d_order) (void)hipFree(p->d_order);
+    delete p;
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& host) {
+    if (host.empty()) return ALLRED_OK;
+    if (hipMalloc((void**)dst, host.size() * sizeof(T)) != hipSuccess) return ALLRED_ERR_NOMEM;
+    if (hipMemcpy(*dst, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
+        return ALLRED_ERR_HIP;
+    return ALLRED_OK;
+}
+
+bool env_is(const char* name, const char* value) {
+    const char* v = std::getenv(name);
+    return v && std::string(v) == value;
+}
+
+}  // namespace
+
+extern "C" {
+
+int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
+    if (!desc || !out) return ALLRED_ERR_ARG;
+    *out = nullptr;
+    const int side = desc->side_length;
+    const int total = desc->total_nodes > 0 ? desc->total_nodes : side * side;
+    if (desc->variant < ALLRED_BO || desc->variant > ALLRED_MEM) return ALLRED_ERR_ARG;
+    if (desc->exec != ALLRED_EXEC_STEPS && desc->exec != ALLRED_EXEC_FUSED) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)desc->elems_per_rank;
+    if (n == 0 || n % 8) return ALLRED_ERR_ARG;
+    if (desc->variant != ALLRED_LO && n % (8 * (size_t)total)) return ALLRED_ERR_ARG;
+
+    auto* p = new allred_plan();
+    p->desc = *desc;
+    p->total = total;
+    p->n = n;
+    p->block_elems = n / (size_t)total;
+    int st = build_schedule(desc->algo, side, total, &p->sched, nullptr);
+    if (st != ALLRED_OK) { free_plan(p); return st; }
+    if (desc->device >= 0) {
+        if (hipSetDevice(desc->device) != hipSuccess) { free_plan(p); return ALLRED_ERR_HIP; }
+        p->device = desc->device;
+    } else {
+        (void)hipGetDevice(&p->device);
+    }
+    const int steps = p->sched.steps;
+    std::vector<int16_t> partner((size_t)steps * total);
+    std::vector<int16_t> rs, ag;
+    for (int k = 0; k < steps; ++k) {
+        p->blk_off.push_back(rs.size());
+        p->blk_per_rank.push_back(popcount64(p->sched.recv[0][k]));
+        for (int r = 0; r < total; ++r) {
+            partner[(size_t)k * total + r] = (int16_t)p->sched.partner[r][k];
+            for (int b = 0; b < total; ++b) {
+                if ((p->sched.recv[r][k] >> b) & 1ull) rs.push_back((int16_t)b);
+                if ((p->sched.send[r][k] >> b) & 1ull) ag.push_back((int16_t)b);
+            }
+        }
+    }
+    std::vector<uint8_t> order(&p->sched.tree_order[0][0],
+                               &p->sched.tree_order[0][0] + ALLRED_MAX_NODES * ALLRED_MAX_NODES);
+    if ((st = upload(&p->d_partner, partner)) || (st = upload(&p->d_rs_blocks, rs)) ||
+        (st = upload(&p->d_ag_blocks, ag)) || (st = upload(&p->d_order, order))) {
+        free_plan(p);
+        return st;
+    }
+    // workspace and launch count per execute
+    if (desc->exec == ALLRED_EXEC_FUSED) {
+        p->launches = 1;
+    } else if (desc->variant == ALLRED_BO) {
+        p->launches = 2 * steps;
+    } else if (desc->variant == ALLRED_LO) {
+        p->ws_bytes = (size_t)total * n * 2;
+        p->launches = steps + (steps % 2);
+    } else {
+        p->ws_bytes = n * 2;
+        p->launches = 2;
+    }
+    *out = p;
+    return ALLRED_OK;
+}
+
+int allred_plan_destroy(allred_plan* plan) {
+    free_plan(plan);
+    return ALLRED_OK;
+}
+
+size_t allred_plan_workspace_bytes(const allred_plan* plan) { return plan ? plan->ws_bytes : 0; }
+
+int allred_plan_launches(const allred_plan* plan) { return plan ? plan->launches : 0; }
+
+int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* workspace, void* stream) {
+    if (!p || !ranks || stride < p->n) return ALLRED_ERR_ARG;
+    if (p->ws_bytes && !workspace) return ALLRED_ERR_ARG;
+    const int N = p->total, steps = p->sched.steps;
+    int st = ALLRED_OK;
+    if (p->desc.exec == ALLRED_EXEC_FUSED) {
+        if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
+        if (p->desc.variant == ALLRED_LO) return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, stream);
+        return launch_tree_fused(ranks, stride, p->n, N, p->d_order, stream);
+    }
+    if (p->desc.variant == ALLRED_BO) {
+        for (int k = 0; k < steps && st == ALLRED_OK; ++k)
+            st = launch_rs_step(ranks, stride, N, p->d_partner + (size_t)k * N, p->d_rs_blocks + p->blk_off[k],
+                                p->blk_per_rank[k], p->block_elems, stream);
+        for (int k = steps - 1; k >= 0 && st == ALLRED_OK; --k)
+            st = launch_ag_step(ranks, stride, N, p->d_partner + (size_t)k * N, p->d_ag_blocks + p->blk_off[k],
+                                p->blk_per_rank[k], p->block_elems, stream);
+        return st;
+    }
+    if (p->desc.variant == ALLRED_LO) {
+        uint16_t* ws = static_cast<uint16_t*>(workspace);
+        for (int k = 0; k < steps && st == ALLRED_OK; ++k) {
+            const bool to_ws = (k % 2) == 0;
+            st = launch_lo_step(to_ws ? ranks : ws, to_ws ? stride : p->n, to_ws ? ws : ranks, to_ws ? p->n : stride,
+                                N, p->d_partner + (size_t)k * N, p->n, stream);
+        }
+        if (st == ALLRED_OK && steps % 2) st = launch_copy_ranks(ws, p->n, ranks, stride, N, p->n, stream);
+        return st;
+    }
+    uint16_t* dst = static_cast<uint16_t*>(workspace);
+    st = launch_mem_reduce(ranks, stride, p->n, N, dst, stream);
+    if (st == ALLRED_OK) st = launch_broadcast(ranks, stride, p->n, N, dst, stream);
+    return st;
+}
+
+int allred_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream) {
+    return launch_bf16_add(dst, src, n, stream);
+}
+
+int allred_bf16_add_masked(uint16_t* dst, const uint16_t* src, uint64_t mask, size_t block_elems, void* stream) {
+    uint8_t blocks[ALLRED_MAX_NODES];
+    int nb = 0;
+    for (int b = 0; b < 64; ++b)
+        if ((mask >> b) & 1ull) blocks[nb++] = (uint8_t)b;
+    return launch_bf16_add_blocks(dst, src, blocks, nb, block_elems, stream);
+}
+
+// ---------------------------------------------------------------------------
+// argv parsing: AllredConfig::AllredConfig (allred_helper.cpp:205-220) and the
+// mains (allred_BO_2D.cpp:22-24, allred_LO_2D.cpp:15, allred_mem_2D.cpp:11)
+// ---------------------------------------------------------------------------
+static int stoi_like(const char* s, int* out) {  // std::stoi: leading integer, else throw
+    if (!s) return ALLRED_ERR_ARG;
+    char* end = nullptr;
+    errno = 0;
+    const long v = std::strtol(s, &end, 10);
+    if (end == s || errno == ERANGE || v > 2147483647L || v < -2147483647L - 1) return ALLRED_ERR_ARG;
+    *out = (int)v;
+    return ALLRED_OK;
+}
+
+int allred_args_parse(int argc, const char* const* argv, int variant, allred_args* a) {
+    if (!a || argc < 0 || (argc > 0 && !argv)) return ALLRED_ERR_ARG;
+    std::memset(a, 0, sizeof(*a));
+    int v = 0;
+    a->variant = variant;
+    if (argc >= 2) { if (stoi_like(argv[1], &v)) return ALLRED_ERR_ARG; a->swing = v == 1; }
+    if (argc >= 3) { if (stoi_like(argv[2], &v)) return ALLRED_ERR_ARG; a->run_kernel = v == 1; }
+    a->side_length = 1;
+    if (argc >= 4) { if (stoi_like(argv[3], &v)) return ALLRED_ERR_ARG; a->side_length = allred_highest_power_of_two(v); }
+    if (argc >= 5) { if (stoi_like(argv[4], &v)) return ALLRED_ERR_ARG; a->seed = v; }
+    a->tiles = 1;
+    if (argc >= 6) { if (stoi_like(argv[5], &v)) return ALLRED_ERR_ARG; a->tiles = v < 1 ? 1 : v; }
+    a->error = 1;
+    if (argc >= 7) { if (stoi_like(argv[6], &v)) return ALLRED_ERR_ARG; a->error = v; }
+    if (variant == ALLRED_BO) {
+        if (argc >= 8) { if (stoi_like(argv[7], &v)) return ALLRED_ERR_ARG; a->print_core = v; }
+        if (argc >= 9) { if (stoi_like(argv[8], &v)) return ALLRED_ERR_ARG; a->bandwidth_optimal = v != 0; }
+    }
+    // extension: rank count (argv[9] or ALLRED_NODES), 0 = side^2
+    int total = 0;
+    const char* env_nodes = std::getenv("ALLRED_NODES");
+    if (argc >= 10) { if (stoi_like(argv[9], &total)) return ALLRED_ERR_ARG; }
+    else if (env_nodes && stoi_like(env_nodes, &total)) return ALLRED_ERR_ARG;
+    a->total_nodes = total > 0 ? total : a->side_length * a->side_length;
+    a->exec = env_is("ALLRED_EXEC", "fused") ? ALLRED_EXEC_FUSED : ALLRED_EXEC_STEPS;
+    a->round_mode = env_is("ALLRED_BF16_ROUND", "rne") ? 1 : 0;
+    const bool large = variant == ALLRED_MEM || (variant == ALLRED_BO && a->bandwidth_optimal);
+    a->num_tiles = allred_normalize_tiles(a->tiles, a->total_nodes, large ? 1 : 0);
+    return ALLRED_OK;
+}
+
+// ---------------------------------------------------------------------------
+// allred_run: AllredConfig ctor data setup (allred_helper.cpp:264-288) +
+// RunProgram (allred_helper.hpp:84-96) on the HIP engine.
+// ---------------------------------------------------------------------------
+#define HIPCK(x)                                   \
+    do {                                           \
+        if ((x) != hipSuccess) { st = ALLRED_ERR_HIP; goto done; } \
+    } while (0)
+#define ST(x)                                      \
+    do {                                           \
+        st = (x);                                  \
+        if (st != ALLRED_OK) goto done;            \
+    } while (0)
+
+int allred_run(const allred_args* a, int verbose, allred_report* rep) {
+    if (!a) return ALLRED_ERR_ARG;
+    allred_report local_rep{};
+    allred_report* R = rep ? rep : &local_rep;
+    std::memset(R, 0, sizeof(*R));
+    R->mismatches = -1;
+    const int N = a->total_nodes;
+    const size_t n = (size_t)a->num_tiles * 1024;  // bf16 per rank (2048-byte tiles)
+    const size_t bytes = n * 2;
+    const int variant = a->variant == ALLRED_MEM ? ALLRED_MEM
+                        : (a->variant == ALLRED_BO && a->bandwidth_optimal) ? ALLRED_BO : ALLRED_LO;
+    const int print_core = a->print_core;
+    if (print_core < 0 || print_core >= N) return ALLRED_ERR_ARG;
+    R->bytes_per_rank = bytes;
+    R->total_nodes = N;
+
+    allred_plan_desc d{};
+    d.algo = a->swing ? ALLRED_SWING : ALLRED_RECDUB;
+    d.variant = variant;
+    d.exec = a->exec;
+    d.side_length = a->side_length;
+    d.total_nodes = N;
+    d.device = -1;
+    d.elems_per_rank = n;
+    allred_plan* plan = nullptr;
+    int st = allred_plan_create(&d, &plan);
+    if (st != ALLRED_OK) return st;
+    R->launches = plan->launches;
+
+    std::vector<uint32_t> src0(bytes / 4), src1(bytes / 4);
+    uint16_t *h_in = nullptr, *h_out = nullptr, *d_ranks = nullptr, *d_scratch = nullptr;
+    void* d_ws = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
+    hipStream_t s = nullptr;
+    const size_t all_bytes = (size_t)N * bytes;
+    float ms = 0;
+    if (a->seed < 0) {
+        allred_constant_bf16_vector(bytes, 1.0f, src0.data());
+        src1 = src0;
+    } else {
+        allred_random_bf16_vector(bytes, 100, a->seed, a->round_mode, src0.data());
+        allred_random_bf16_vector(bytes, 100, a->seed + 1, a->round_mode, src1.data());
+    }
+    HIPCK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIPCK(hipHostMalloc((void**)&h_in, all_bytes, hipHostMallocDefault));
+    HIPCK(hipHostMalloc((void**)&h_out, all_bytes, hipHostMallocDefault));
+    // even x loads src_1, odd x loads src_0 (allred_BO_2D.cpp:79-85)
+    for (int r = 0; r < N; ++r)
+        std::memcpy(h_in + (size_t)r * n, ((r % a->side_length) % 2 == 0) ? src1.data() : src0.data(), bytes);
+    HIPCK(hipMalloc((void**)&d_ranks, all_bytes));
+    HIPCK(hipMalloc((void**)&d_scratch, all_bytes));
+    if (plan->ws_bytes) HIPCK(hipMalloc(&d_ws, plan->ws_bytes));
+    HIPCK(hipEventCreate(&e0));
+    HIPCK(hipEventCreate(&e1));
+    HIPCK(hipEventCreate(&e2));
+    HIPCK(hipEventCreate(&e3));
+    // warm-up on a scratch copy (first-launch code-object load stays out of the timing)
+    HIPCK(hipMemcpyAsync(d_scratch, h_in, all_bytes, hipMemcpyHostToDevice, s));
+    if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, n, d_ws, s));
+    HIPCK(hipStreamSynchronize(s));
+    // timed: H2D | allreduce | D2H
+    HIPCK(hipEventRecord(e0, s));
+    HIPCK(hipMemcpyAsync(d_ranks, h_in, all_bytes, hipMemcpyHostToDevice, s));
+    HIPCK(hipEventRecord(e1, s));
+    if (a->run_kernel) ST(allred_plan_execute(plan, d_ranks, n, d_ws, s));
+    HIPCK(hipEventRecord(e2, s));
+    HIPCK(hipMemcpyAsync(h_out, d_ranks, all_bytes, hipMemcpyDeviceToHost, s));
+    HIPCK(hipEventRecord(e3, s));
+    HIPCK(hipStreamSynchronize(s));
+    HIPCK(hipEventElapsedTime(&ms, e1, e2));
+    R->device_seconds = ms * 1e-3;
+    HIPCK(hipEventElapsedTime(&ms, e0, e3));
+    R->e2e_seconds = ms * 1e-3;
+    {
+        float maxe = 0;
+        const uint32_t* res = reinterpret_cast<const uint32_t*>(h_out + (size_t)print_core * n);
+        R->mismatches = allred_validate_result_vector(res, src0.data(), src1.data(), bytes / 4, (float)a->error,
+                                                      (uint32_t)N, verbose, &maxe);
+        R->max_error = maxe;
+        if (std::getenv("ALLRED_CHECK_ALL")) {  // extension: the reference checks one core only
+            for (int r = 0; r < N; ++r) {
+                if (r == print_core) continue;
+                R->mismatches += allred_validate_result_vector(
+                    reinterpret_cast<const uint32_t*>(h_out + (size_t)r * n), src0.data(), src1.data(), bytes / 4,
+                    (float)a->error, (uint32_t)N, 0, nullptr);
+            }
+        }
+    }
+done:
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (e2) (void)hipEventDestroy(e2);
+    if (e3) (void)hipEventDestroy(e3);
+    if (d_ws) (void)hipFree(d_ws);
+    if (d_ranks) (void)hipFree(d_ranks);
+    if (d_scratch) (void)hipFree(d_scratch);
+    if (h_in) (void)hipHostFree(h_in);
+    if (h_out) (void)hipHostFree(h_out);
+    if (s) (void)hipStreamDestroy(s);
+    allred_plan_destroy(plan);
+    return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// internal.hpp — shared declarations inside liballred.so (not installed).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "allred.h"
+
+namespace tsa {
+
+// ---------------- bf16 (host) ----------------
+inline float bf16_to_float(uint16_t h) {
+    uint32_t u = (uint32_t)h << 16;
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+inline uint16_t bf16_from_float_rne(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40u);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+inline uint16_t bf16_from_float_trunc(float f) {
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return (uint16_t)(u >> 16);
+}
+
+// ---------------- schedule ----------------
+int steps_for(int total_nodes);
+// Build + validate (see allred_schedule_build in allred.h).
+int build_schedule(int algo, int side, int total, allred_schedule* out, std::string* why);
+
+// ---------------- device launchers (kernels.hip) ----------------
+// All take hipStream_t as void* and return ALLRED_OK / ALLRED_ERR_*.
+struct RankTable;  // opaque device tables of a plan
+int launch_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream);
+int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* blocks, int nblocks,
+                           size_t block_elems, void* stream);
+int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order,
+                      void* stream);
+int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
+                     void* stream);
+int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total,
+                       const uint8_t* order, uint16_t* out, void* stream);
+int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src,
+                     void* stream);
+int launch_rs_step(uint16_t* ranks, uint64_t stride, int total, const int16_t* d_partner,
+                   const int16_t* d_blocks, int blocks_per_rank, size_t block_elems, void* stream);
+int launch_ag_step(uint16_t* ranks, uint64_t stride, int total, const int16_t* d_partner,
+                   const int16_t* d_blocks, int blocks_per_rank, size_t block_elems, void* stream);
+int launch_lo_step(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint64_t dst_stride,
+                   int total, const int16_t* d_partner, size_t n, void* stream);
+int launch_copy_ranks(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint64_t dst_stride,
+                      int total, size_t n, void* stream);
+int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, uint16_t* dst,
+                      void* stream);
+int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream);
+
+int hip_status(int hip_err);  // maps hipError_t -> ALLRED_*
+
+}  // namespace tsa

@@ -1,0 +1,471 @@
+// kernels.hip — CDNA4 (gfx950) kernels of the allreduce engine.
+//
+// Every kernel is HBM-bound integer/bf16 streaming work: 16-byte (8 x bf16)
+// accesses per lane, fp32 add, v_cvt_pk_bf16_f32 (round-to-nearest-even)
+// back to bf16.  No MFMA: a pointwise add is not a contraction.
+//
+// Replaces the Tensix compute kernels of the reference:
+//   add_tiles + pack_tile<true>      allred_BO_2D/kernels/compute_kernel.cpp:53-60
+//   LO_2D add loop                   allred_LO_2D/kernels/compute_kernel.cpp:50-62
+//   mem_2D dest-reuse accumulate     allred_mem_2D/kernels/compute_kernel.cpp:43-72
+// and the NoC block moves of the dataflow kernels (RS / AG loops,
+// allred_BO_2D/kernels/dataflow_kernel.cpp:152-267) for ranks resident in
+// one GPU's HBM, where a "send" is a load of the partner's bytes.
+#include <hip/hip_runtime.h>
+
+#include "internal.hpp"
+
+namespace tsa {
+namespace {
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float lo_f(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_f(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// two fp32 -> packed bf16x2, round to nearest even (one v_cvt_pk_bf16_f32)
+__device__ __forceinline__ uint32_t pack_rne(float lo, float hi) {
+    f32x2 v = {lo, hi};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+
+__device__ __forceinline__ uint32_t add2(uint32_t a, uint32_t b) {
+    return pack_rne(lo_f(a) + lo_f(b), hi_f(a) + hi_f(b));
+}
+
+// 8 x bf16 add with one bf16 rounding per element (Tensix add_tiles with
+// fp32_dest_acc_en = false, allred_helper.cpp:331-335)
+__device__ __forceinline__ uint4 add8(uint4 a, uint4 b) {
+    uint4 o;
+    o.x = add2(a.x, b.x);
+    o.y = add2(a.y, b.y);
+    o.z = add2(a.z, b.z);
+    o.w = add2(a.w, b.w);
+    return o;
+}
+
+__device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
+    uint4 o;
+    o.x = (uint32_t)__shfl_xor((int)v.x, m);
+    o.y = (uint32_t)__shfl_xor((int)v.y, m);
+    o.z = (uint32_t)__shfl_xor((int)v.z, m);
+    o.w = (uint32_t)__shfl_xor((int)v.w, m);
+    return o;
+}
+
+__device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gthreads() { return (uint64_t)gridDim.x * blockDim.x; }
+
+constexpr int kBlock = 256;          // 4 waves per workgroup
+constexpr int kMaxGrid = 256 * 8;    // 256 CUs x 8 resident workgroups, then grid-stride
+
+inline unsigned grid_for(uint64_t work_items) {
+    uint64_t g = (work_items + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > (uint64_t)kMaxGrid) g = kMaxGrid;
+    return (unsigned)g;
+}
+
+// ---------------------------------------------------------------------------
+// dst += src over n_vec 16-byte vectors (+ scalar tail).  4 vectors in flight
+// per lane per iteration, grid-stride so each wave's loads stay coalesced.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_add(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                uint64_t n_vec) {
+    const uint64_t T = gthreads();
+    uint64_t i = gtid();
+    for (; i + 3 * T < n_vec; i += 4 * T) {
+        uint4 a0 = dst[i], a1 = dst[i + T], a2 = dst[i + 2 * T], a3 = dst[i + 3 * T];
+        uint4 b0 = src[i], b1 = src[i + T], b2 = src[i + 2 * T], b3 = src[i + 3 * T];
+        dst[i] = add8(a0, b0);
+        dst[i + T] = add8(a1, b1);
+        dst[i + 2 * T] = add8(a2, b2);
+        dst[i + 3 * T] = add8(a3, b3);
+    }
+    for (; i < n_vec; i += T) dst[i] = add8(dst[i], src[i]);
+}
+
+__global__ void k_add_scalar(uint16_t* __restrict__ dst, const uint16_t* __restrict__ src, uint64_t n) {
+    for (uint64_t i = gtid(); i < n; i += gthreads()) {
+        float s = __uint_as_float((uint32_t)dst[i] << 16) + __uint_as_float((uint32_t)src[i] << 16);
+        dst[i] = (uint16_t)(pack_rne(s, 0.0f) & 0xffffu);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// dst[b] += src[b] for the blocks b listed (one BO compute step of one rank)
+// ---------------------------------------------------------------------------
+struct BlockList {
+    uint8_t b[ALLRED_MAX_NODES];
+};
+
+__global__ __launch_bounds__(kBlock) void k_add_blocks(uint4* __restrict__ dst, const uint4* __restrict__ src,
+                                                       BlockList list, uint64_t block_vec) {
+    const uint64_t off = (uint64_t)list.b[blockIdx.y] * block_vec;
+    for (uint64_t v = gtid(); v < block_vec; v += gthreads()) dst[off + v] = add8(dst[off + v], src[off + v]);
+}
+
+// ---------------------------------------------------------------------------
+// BO allreduce of P ranks in one pass.  Block b of the result is what the
+// reference's reduce-scatter computes at b's owner: a binary tree whose leaf
+// order is order[b] (allred_schedule.tree_order, row stride 64) and whose
+// level-k nodes add adjacent groups of 2^k leaves, each add rounded to bf16.
+// The all-gather then copies it to every rank, so the pass stores it to all.
+// block_vec == 0 selects row 0 for the whole vector (hierarchical partials).
+//
+// Lane layout (P = 64): lane = g * CH + c.  The 8 lanes of chunk column c
+// each load 8 leaves (ranks order[b][8g .. 8g+7]) of the same 16-byte chunk,
+// reduce them locally (tree levels 0-2), then combine across lanes with
+// xor-shuffles (levels 3-5).  Every lane then holds the result and stores it
+// to its own 8 ranks.  Each rank's chunk is read and written by one lane only,
+// so the pass is safe in place.
+// ---------------------------------------------------------------------------
+template <int P, bool WRITE_ALL>
+__global__ __launch_bounds__(kBlock) void k_tree(uint16_t* __restrict__ ranks, uint64_t stride, uint64_t n_vec,
+                                                 const uint8_t* __restrict__ order, uint64_t block_vec,
+                                                 uint16_t* __restrict__ out) {
+    constexpr int LEAVES = P >= 8 ? 8 : P;  // leaves per lane
+    constexpr int LANES = P / LEAVES;        // lanes per chunk
+    constexpr int CH = 64 / LANES;           // chunks per wave
+    const int lane = threadIdx.x & 63;
+    const int g = lane / CH;
+    const int c = lane % CH;
+    uint4* rows[LEAVES];
+    uint64_t cur = ~0ull;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t base = wave * CH; base < n_vec; base += waves * CH) {
+        const uint64_t v = base + c;
+        const bool ok = v < n_vec;
+        const uint64_t b = (block_vec && ok) ? v / block_vec : 0;
+        if (b != cur) {  // wave-uniform whenever block_vec % CH == 0
+            cur = b;
+#pragma unroll
+            for (int i = 0; i < LEAVES; ++i)
+                rows[i] = reinterpret_cast<uint4*>(ranks + (uint64_t)order[b * ALLRED_MAX_NODES + g * LEAVES + i] * stride);
+        }
+        uint4 x[LEAVES];
+#pragma unroll
+        for (int i = 0; i < LEAVES; ++i) x[i] = ok ? rows[i][v] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int w = 1; w < LEAVES; w *= 2)
+#pragma unroll
+            for (int i = 0; i < LEAVES; i += 2 * w) x[i] = add8(x[i], x[i + w]);
+        uint4 acc = x[0];
+#pragma unroll
+        for (int m = CH; m < 64; m *= 2) acc = add8(acc, shfl_xor4(acc, m));
+        if (ok) {
+            if (WRITE_ALL) {
+#pragma unroll
+                for (int i = 0; i < LEAVES; ++i) rows[i][v] = acc;
+            } else if (g == 0) {
+                reinterpret_cast<uint4*>(out)[v] = acc;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LO allreduce of P ranks in one pass: the butterfly itself.  Rank x keeps
+// its own tree (for Swing the P results differ in bf16 rounding, exactly as
+// the reference's per-core LO results do).  Lane (q, x) = q * P + x holds
+// rank x's chunk; step k adds the value of lane q * P + partner_k(x),
+// fetched with ds_bpermute, and rounds to bf16.  U consecutive chunks per
+// lane keep each rank's 128-byte lines in flight together.
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_butterfly(uint16_t* __restrict__ ranks, uint64_t stride, uint64_t n_vec,
+                                                      const int16_t* __restrict__ partner, int steps) {
+    constexpr int Q = 64 / P;  // rank groups per wave
+    constexpr int U = 8;       // chunks per lane per iteration
+    const int lane = threadIdx.x & 63;
+    const int x = lane % P;
+    const int q = lane / P;
+    int src[ALLRED_MAX_STEPS];
+#pragma unroll
+    for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src[k] = k < steps ? (q * P + partner[k * P + x]) * 4 : lane * 4;
+    uint4* row = reinterpret_cast<uint4*>(ranks + (uint64_t)x * stride);
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t base = wave * (Q * U); base < n_vec; base += waves * (Q * U)) {
+        uint4 val[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t v = base + (uint64_t)q * U + u;
+            val[u] = v < n_vec ? row[v] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+            if (k >= steps) break;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                uint4 o;
+                o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(src[k], (int)val[u].x);
+                o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(src[k], (int)val[u].y);
+                o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(src[k], (int)val[u].z);
+                o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(src[k], (int)val[u].w);
+                val[u] = add8(val[u], o);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t v = base + (uint64_t)q * U + u;
+            if (v < n_vec) row[v] = val[u];
+        }
+    }
+}
+
+// ranks[r] = src for every r (all-gather of a reduced vector)
+__global__ __launch_bounds__(kBlock) void k_broadcast(uint16_t* __restrict__ ranks, uint64_t stride, int total,
+                                                      const uint4* __restrict__ src, uint64_t n_vec) {
+    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) {
+        const uint4 x = src[v];
+        for (int r = 0; r < total; ++r) reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride)[v] = x;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Schedule-faithful steps: all ranks' step-k work in one launch.
+// RS: ranks[r][b] += ranks[p][b] for b in recv_mask_k(r)   (in place: the
+//     pair's recv masks are disjoint, so nobody reads what another writes)
+// AG: ranks[r][b]  = ranks[p][b] for b in send_mask_k(r) (= recv_mask_k(p))
+// grid.y = rank * blocks_per_rank + j
+// ---------------------------------------------------------------------------
+template <bool ADD>
+__global__ __launch_bounds__(kBlock) void k_step(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                 const int16_t* __restrict__ partner,
+                                                 const int16_t* __restrict__ blocks, int blocks_per_rank,
+                                                 uint64_t block_vec) {
+    const int t = blockIdx.y;
+    const int r = t / blocks_per_rank;
+    const int p = partner[r];
+    const uint64_t off = (uint64_t)blocks[t] * block_vec;
+    uint4* L = reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + off;
+    const uint4* R = reinterpret_cast<const uint4*>(ranks + (uint64_t)p * stride) + off;
+    for (uint64_t v = gtid(); v < block_vec; v += gthreads()) L[v] = ADD ? add8(L[v], R[v]) : R[v];
+}
+
+// LO step (full vector): dst[r] = src[r] + src[p(r)], ping-pong buffers
+__global__ __launch_bounds__(kBlock) void k_lo_step(const uint16_t* __restrict__ src, uint64_t src_stride,
+                                                    uint16_t* __restrict__ dst, uint64_t dst_stride,
+                                                    const int16_t* __restrict__ partner, uint64_t n_vec) {
+    const int r = blockIdx.y;
+    const int p = partner[r];
+    const uint4* A = reinterpret_cast<const uint4*>(src + (uint64_t)r * src_stride);
+    const uint4* B = reinterpret_cast<const uint4*>(src + (uint64_t)p * src_stride);
+    uint4* D = reinterpret_cast<uint4*>(dst + (uint64_t)r * dst_stride);
+    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) D[v] = add8(A[v], B[v]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_ranks(const uint16_t* __restrict__ src, uint64_t src_stride,
+                                                       uint16_t* __restrict__ dst, uint64_t dst_stride,
+                                                       uint64_t n_vec) {
+    const uint4* A = reinterpret_cast<const uint4*>(src + (uint64_t)blockIdx.y * src_stride);
+    uint4* D = reinterpret_cast<uint4*>(dst + (uint64_t)blockIdx.y * dst_stride);
+    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) D[v] = A[v];
+}
+
+// ---------------------------------------------------------------------------
+// mem_2D: block b (owner rank b) summed over every rank's copy in fp32,
+// starting from the owner's own block, then ranks 0..N-1 in order, rounded
+// once (allred_mem_2D/kernels/compute_kernel.cpp:43-72 with the own-block
+// seed).  WRITE_ALL: store to every rank (fused one-shot form);
+// else store to `out` (the shared dst buffer, allred_mem_2D dataflow :169-174).
+// ---------------------------------------------------------------------------
+template <bool WRITE_ALL>
+__global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, uint64_t stride, int total,
+                                                uint64_t n_vec, uint64_t block_vec, uint16_t* __restrict__ out) {
+    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) {
+        const int own = (int)(v / block_vec);
+        const uint4 s = reinterpret_cast<const uint4*>(ranks + (uint64_t)own * stride)[v];
+        float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
+        for (int r = 0; r < total; ++r) {
+            if (r == own) continue;
+            const uint4 y = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride)[v];
+            a[0] += lo_f(y.x); a[1] += hi_f(y.x);
+            a[2] += lo_f(y.y); a[3] += hi_f(y.y);
+            a[4] += lo_f(y.z); a[5] += hi_f(y.z);
+            a[6] += lo_f(y.w); a[7] += hi_f(y.w);
+        }
+        uint4 o;
+        o.x = pack_rne(a[0], a[1]);
+        o.y = pack_rne(a[2], a[3]);
+        o.z = pack_rne(a[4], a[5]);
+        o.w = pack_rne(a[6], a[7]);
+        if (WRITE_ALL) {
+            for (int r = 0; r < total; ++r) reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride)[v] = o;
+        } else {
+            reinterpret_cast<uint4*>(out)[v] = o;
+        }
+    }
+}
+
+inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+int last_error() { return hip_status((int)hipGetLastError()); }
+
+template <bool WRITE_ALL>
+int tree_dispatch(uint16_t* ranks, uint64_t stride, uint64_t n_vec, int total, const uint8_t* order,
+                  uint64_t block_vec, uint16_t* out, hipStream_t st) {
+    const int lanes = total >= 8 ? total / 8 : 1;
+    const uint64_t chunk_groups = (n_vec + (64 / lanes) - 1) / (64 / lanes);  // one per wave
+    uint64_t blocks = (chunk_groups + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    const dim3 grid((unsigned)blocks), blk(kBlock);
+    switch (total) {
+        case 1: hipLaunchKernelGGL((k_tree<1, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        case 2: hipLaunchKernelGGL((k_tree<2, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        case 4: hipLaunchKernelGGL((k_tree<4, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        case 8: hipLaunchKernelGGL((k_tree<8, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        case 16: hipLaunchKernelGGL((k_tree<16, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        case 32: hipLaunchKernelGGL((k_tree<32, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        case 64: hipLaunchKernelGGL((k_tree<64, WRITE_ALL>), grid, blk, 0, st, ranks, stride, n_vec, order, block_vec, out); break;
+        default: return ALLRED_ERR_UNSUPPORTED;
+    }
+    return last_error();
+}
+
+}  // namespace
+
+int hip_status(int e) { return e == (int)hipSuccess ? ALLRED_OK : ALLRED_ERR_HIP; }
+
+int launch_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) return ALLRED_OK;
+    if (!dst || !src) return ALLRED_ERR_ARG;
+    if (aligned16(dst) && aligned16(src)) {
+        const uint64_t nv = n / 8;
+        if (nv) hipLaunchKernelGGL(k_add, dim3(grid_for(nv / 4 + 1)), dim3(kBlock), 0, st,
+                                   reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), nv);
+        const uint64_t tail = n - nv * 8;
+        if (tail) hipLaunchKernelGGL(k_add_scalar, dim3(1), dim3(64), 0, st, dst + nv * 8, src + nv * 8, tail);
+    } else {
+        hipLaunchKernelGGL(k_add_scalar, dim3(grid_for(n)), dim3(kBlock), 0, st, dst, src, (uint64_t)n);
+    }
+    return last_error();
+}
+
+int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* blocks, int nblocks,
+                           size_t block_elems, void* stream) {
+    if (nblocks <= 0) return ALLRED_OK;
+    if (nblocks > ALLRED_MAX_NODES || block_elems % 8 || !aligned16(dst) || !aligned16(src)) return ALLRED_ERR_ARG;
+    BlockList list{};
+    for (int i = 0; i < nblocks; ++i) list.b[i] = blocks[i];
+    const uint64_t bv = block_elems / 8;
+    hipLaunchKernelGGL(k_add_blocks, dim3(grid_for(bv) > 64 ? 64 : grid_for(bv), nblocks), dim3(kBlock), 0,
+                       (hipStream_t)stream, reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src),
+                       list, bv);
+    return last_error();
+}
+
+int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream) {
+    if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
+    return tree_dispatch<true>(ranks, stride, n / 8, total, order, n / 8 / total, nullptr, (hipStream_t)stream);
+}
+
+int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
+                     void* stream) {
+    if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    const int Q = 64 / total;
+    uint64_t waves = (nv + (uint64_t)Q * 8 - 1) / ((uint64_t)Q * 8);
+    uint64_t blocks = (waves + 3) / 4;
+    if (blocks < 1) blocks = 1;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    const dim3 grid((unsigned)blocks), blk(kBlock);
+    hipStream_t st = (hipStream_t)stream;
+    switch (total) {
+        case 1: return ALLRED_OK;  // one rank: nothing to reduce
+        case 2: hipLaunchKernelGGL(k_butterfly<2>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        case 4: hipLaunchKernelGGL(k_butterfly<4>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        case 8: hipLaunchKernelGGL(k_butterfly<8>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        case 16: hipLaunchKernelGGL(k_butterfly<16>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        case 32: hipLaunchKernelGGL(k_butterfly<32>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        case 64: hipLaunchKernelGGL(k_butterfly<64>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        default: return ALLRED_ERR_UNSUPPORTED;
+    }
+    return last_error();
+}
+
+int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order,
+                       uint16_t* out, void* stream) {
+    if (n % 8 || stride % 8 || !aligned16(ranks) || !aligned16(out)) return ALLRED_ERR_ARG;
+    return tree_dispatch<false>(const_cast<uint16_t*>(ranks), stride, n / 8, total, order, 0, out,
+                                (hipStream_t)stream);
+}
+
+int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src, void* stream) {
+    if (n % 8 || stride % 8 || !aligned16(ranks) || !aligned16(src)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    hipLaunchKernelGGL(k_broadcast, dim3(grid_for(nv)), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, total,
+                       reinterpret_cast<const uint4*>(src), nv);
+    return last_error();
+}
+
+static int launch_step(bool add, uint16_t* ranks, uint64_t stride, int total, const int16_t* d_partner,
+                       const int16_t* d_blocks, int blocks_per_rank, size_t block_elems, void* stream) {
+    if (block_elems % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
+    const uint64_t bv = block_elems / 8;
+    unsigned gx = grid_for(bv);
+    if (gx > 64) gx = 64;
+    const dim3 grid(gx, (unsigned)(total * blocks_per_rank));
+    if (add)
+        hipLaunchKernelGGL(k_step<true>, grid, dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_partner,
+                           d_blocks, blocks_per_rank, bv);
+    else
+        hipLaunchKernelGGL(k_step<false>, grid, dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_partner,
+                           d_blocks, blocks_per_rank, bv);
+    return last_error();
+}
+
+int launch_rs_step(uint16_t* ranks, uint64_t stride, int total, const int16_t* d_partner, const int16_t* d_blocks,
+                   int blocks_per_rank, size_t block_elems, void* stream) {
+    return launch_step(true, ranks, stride, total, d_partner, d_blocks, blocks_per_rank, block_elems, stream);
+}
+
+int launch_ag_step(uint16_t* ranks, uint64_t stride, int total, const int16_t* d_partner, const int16_t* d_blocks,
+                   int blocks_per_rank, size_t block_elems, void* stream) {
+    return launch_step(false, ranks, stride, total, d_partner, d_blocks, blocks_per_rank, block_elems, stream);
+}
+
+int launch_lo_step(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint64_t dst_stride, int total,
+                   const int16_t* d_partner, size_t n, void* stream) {
+    if (n % 8 || src_stride % 8 || dst_stride % 8 || !aligned16(src) || !aligned16(dst)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    unsigned gx = grid_for(nv);
+    if (gx > 128) gx = 128;
+    hipLaunchKernelGGL(k_lo_step, dim3(gx, total), dim3(kBlock), 0, (hipStream_t)stream, src, src_stride, dst,
+                       dst_stride, d_partner, nv);
+    return last_error();
+}
+
+int launch_copy_ranks(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint64_t dst_stride, int total,
+                      size_t n, void* stream) {
+    if (n % 8 || src_stride % 8 || dst_stride % 8 || !aligned16(src) || !aligned16(dst)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    unsigned gx = grid_for(nv);
+    if (gx > 128) gx = 128;
+    hipLaunchKernelGGL(k_copy_ranks, dim3(gx, total), dim3(kBlock), 0, (hipStream_t)stream, src, src_stride, dst,
+                       dst_stride, nv);
+    return last_error();
+}
+
+int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, uint16_t* dst, void* stream) {
+    if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks) || !aligned16(dst)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    hipLaunchKernelGGL(k_mem<false>, dim3(grid_for(nv)), dim3(kBlock), 0, (hipStream_t)stream,
+                       const_cast<uint16_t*>(ranks), stride, total, nv, nv / total, dst);
+    return last_error();
+}
+
+int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream) {
+    if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    hipLaunchKernelGGL(k_mem<true>, dim3(grid_for(nv)), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride,
+                       total, nv, nv / total, nullptr);
+    return last_error();
+}
+
+}  // namespace tsa
