@@ -1,0 +1,339 @@
+#!/usr/bin/env python3
+"""bench.py — allreduce GB/s of the MI355X engine (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N ... bench.py --gpus N --steps K --warmup W
+
+A step is one allreduce of device-resident bf16 buckets:
+  N = 1  BASELINE config 2: the 8x8 Swing BO allreduce of 64 virtual ranks x
+         655,360 B (5 tiles per block) in one MI355X's HBM, executed as the
+         one-pass fused HIP kernel (k_tree<64>, bit-exact with the 12-step
+         schedule).  8 rotating bucket sets (320 MiB > the 256 MiB Infinity
+         Cache) so every step streams from HBM; the K steps are replayed from
+         a captured HIP graph.
+  N > 1  weak scaling: every GPU holds the same 64 x 640 kB ranks; on-GPU tree
+         reduce -> 2D Swing BO over RCCL/xGMI between the N GPUs (grid (2,2),
+         (2,4), (4,8)) -> broadcast back to the 64 ranks.
+value = bytes of all ranks' buckets allreduced per second, whole job (GB/s, 1e9).
+Rank 0 prints ONE JSON line.  See DESIGN.md §Measurement for every field.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402  (plumbing: device memory, streams, events, gloo)
+import torch.distributed as dist  # noqa: E402
+
+import tenstorrentallreduce_amd as t  # noqa: E402
+
+HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+XGMI_LINK_DIR_GBPS = 76.8     # 153.6 GB/s per link quoted bidirectional -> per direction
+SIDE, RANKS, TILES = 8, 64, 5
+ELEMS = t.normalize_tiles(TILES, RANKS, True) * 1024   # 327,680 bf16 = 655,360 B per rank
+GRIDS = {1: (1, 1), 2: (2, 2), 4: (2, 4), 8: (4, 8)}
+
+
+def cpu_cores() -> int:
+    n = len(os.sched_getaffinity(0))
+    try:  # cgroup v2 quota (the GPU box shares its CPUs: 16 per GPU)
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) / int(p))))
+    except Exception:
+        pass
+    return n
+
+
+def fill_reference_convention(buf: torch.Tensor, seed: int) -> None:
+    """Synthetic inputs of the reference's shape: uniform [0,100) bf16, even-x
+    ranks get src_1, odd-x ranks src_0 (allred_BO_2D.cpp:79-85)."""
+    g = torch.Generator(device=buf.device).manual_seed(seed)
+    n = buf.shape[1]
+    a = (torch.rand(n, generator=g, device=buf.device) * 100).to(torch.bfloat16).view(torch.int16)
+    b = (torch.rand(n, generator=g, device=buf.device) * 100).to(torch.bfloat16).view(torch.int16)
+    for r in range(buf.shape[0]):
+        buf[r].copy_(b if (r % SIDE) % 2 == 0 else a)
+
+
+def cpu_baseline() -> dict:
+    """The oracle's loopback multi-process restatement (oracle/allred_oracle_cli)
+    on this host's cores: same config 2 allreduce, ~10 s of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+    argv = [1, 1, SIDE, 13, TILES, 32, 0, 1]
+    probe = oracle.loopback("bo", argv, reps=3)
+    reps = int(min(400, max(5, 10.0 / max(probe["median_s"], 1e-4))))
+    out = oracle.loopback("bo", argv, reps=reps, timeout=300)
+    bytes_all = RANKS * ELEMS * 2
+    return {
+        "value": round(bytes_all / out["median_s"] / 1e9, 4),
+        "unit": "GB/s",
+        "cores": min(RANKS, cpu_cores()),
+        "kind": "port",
+        "sample": (f"oracle loopback (64 forked rank processes, shared-memory buffers, semaphore handshakes) "
+                   f"of the full config-2 allreduce, {reps} reps, median {out['median_s'] * 1e3:.3f} ms "
+                   f"(min {out['min_s'] * 1e3:.3f}, max {out['max_s'] * 1e3:.3f}); mismatches {out['mismatches']}"),
+    }
+
+
+def pmc_traffic(kernel_key: str):
+    """HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        return d["kernels"][kernel_key]["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def bench_single(args) -> dict:
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.Stream(device=dev)
+    nsets = args.sets
+    sets = [torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev) for _ in range(nsets)]
+    for i, s in enumerate(sets):
+        fill_reference_convention(s, 1000 + i)
+    torch.cuda.synchronize()
+    plan = t.Plan(t.SWING, t.BO, SIDE, ELEMS, RANKS, t.EXEC_FUSED)
+    steps_plan = t.Plan(t.SWING, t.BO, SIDE, ELEMS, RANKS, t.EXEC_STEPS)
+
+    def step(i, p=plan):
+        p.execute(sets[i % nsets].data_ptr(), ELEMS, None, stream)
+
+    with torch.cuda.stream(stream):
+        for i in range(args.warmup):
+            step(i)
+    torch.cuda.synchronize()
+
+    graph = None
+    if not args.eager:
+        try:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=stream):
+                for i in range(args.steps):
+                    step(i)
+            torch.cuda.synchronize()
+        except Exception as e:  # fall back to eager launches, say so
+            print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
+            graph = None
+
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    t0 = time.perf_counter()
+    with torch.cuda.stream(stream):  # the graph launches on the current stream
+        if graph is not None:
+            graph.replay()
+        else:
+            for i in range(args.steps):
+                step(i)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1)
+    ms_per_step = ms / args.steps
+
+    bytes_all = RANKS * ELEMS * 2
+    steps_ms = hot_ms = float("nan")
+    if args.main_only:  # profiling runs: nothing but the timed workload (+ warmup)
+        plan.close()
+        steps_plan.close()
+        return {"ms_per_step": ms_per_step, "value": bytes_all / (ms_per_step * 1e-3) / 1e9}
+
+    # schedule-faithful form (12 launches: 6 RS + 6 AG steps), same buckets, eager
+    with torch.cuda.stream(stream):
+        for i in range(3):
+            step(i, steps_plan)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for i in range(args.steps):
+        step(i, steps_plan)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    steps_ms = e0.elapsed_time(e1) / args.steps
+
+    # cache-resident (one bucket set, 40 MiB stays in the Infinity Cache)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        for i in range(args.steps):
+            plan.execute(sets[0].data_ptr(), ELEMS, None, stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    hot_ms = e0.elapsed_time(e1) / args.steps
+
+    alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
+    achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
+    out = {
+        "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
+        "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
+        "unit": "GB/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform [0,100) bf16, reference rank convention); 8 rotating bucket sets in HBM",
+        "config": {"workload": "BASELINE config 2: 8x8 Swing BO allreduce, 64 virtual ranks x 655,360 B bf16 "
+                               "(5 tiles/block) on one MI355X, fused one-pass HIP kernel, no RCCL",
+                   "ranks": RANKS, "bytes_per_rank": ELEMS * 2, "algo": "swing", "variant": "BO",
+                   "exec": "fused", "launches_per_step": plan.launches, "hip_graph": graph is not None},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic("k_tree64"),
+                     "kernel": "k_tree<64,true>", "algorithmic_bytes_per_launch": alg_bytes},
+        "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
+                              "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
+        "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
+        "host_wall_s": round(wall, 6),
+    }
+    plan.close()
+    steps_plan.close()
+    return out
+
+
+def bench_multi(args, rank, world, local_rank) -> dict | None:
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+    side, total = GRIDS[world]
+    uid = [t.Comm.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(uid, src=0)
+    comm = t.Comm(uid[0], world, rank, local_rank)
+    stream = torch.cuda.Stream(device=dev)
+    desc = t.dist_desc(t.SWING, t.BO, side, total, ELEMS, local_ranks=RANKS, local_side=SIDE, local_algo=t.SWING)
+    buf = torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev)
+    fill_reference_convention(buf, 77 + rank)
+    ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)
+    partial = torch.empty(ELEMS, dtype=torch.int16, device=dev)
+
+    def step():
+        t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
+    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+    ms_per_step = ms.item() / args.steps
+
+    # local phases alone (tree reduce of 64 ranks + broadcast): the HBM kernels
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(args.steps):
+        t.tree_reduce(buf.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, partial.data_ptr(), stream)
+        t.broadcast(buf.data_ptr(), ELEMS, ELEMS, RANKS, partial.data_ptr(), stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    local_ms = e0.elapsed_time(e1) / args.steps
+
+    # flat xGMI Swing BO on a large bucket (config 4 regime) and config 3 (RecDub, 640 kB)
+    extras = {}
+    if args.extras:
+        for name, algo, nbytes, reps in (("config4_swing_bo_256MiB", t.SWING, 256 << 20, 5),
+                                         ("config3_recdub_bo_640kB", t.RECDUB, ELEMS * 2, 50)):
+            n = nbytes // 2
+            d2 = t.dist_desc(algo, t.BO, side, total, n)
+            b2 = torch.zeros(n, dtype=torch.int16, device=dev)
+            w2 = torch.empty(t.dist_workspace_bytes(d2), dtype=torch.uint8, device=dev)
+            for _ in range(2):
+                t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            e0.record(stream)
+            for _ in range(reps):
+                t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            m = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64)
+            dist.all_reduce(m, op=dist.ReduceOp.MAX)
+            sec = m.item() * 1e-3
+            busbw = 2 * (world - 1) / world * nbytes / sec / 1e9
+            extras[name] = {"ms": round(m.item(), 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
+                            "busbw_GBps": round(busbw, 3),
+                            "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
+            del b2, w2
+    comm.close()
+    if rank != 0:
+        return None
+    bytes_all = world * RANKS * ELEMS * 2
+    local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
+    achieved = local_bytes / (local_ms * 1e-3) / 1e9
+    return {
+        "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
+        "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (uniform [0,100) bf16, reference rank convention)",
+        "config": {"workload": f"config 2 per GPU (64 virtual ranks x 655,360 B, 8x8 Swing) x {world} GPUs: "
+                               f"on-GPU tree reduce, 2D Swing BO over RCCL/xGMI on grid {GRIDS[world]}, broadcast",
+                   "ranks": RANKS * world, "bytes_per_rank": ELEMS * 2, "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "k_tree<64,false> + k_broadcast (local phases)",
+                     "algorithmic_bytes_per_launch": local_bytes},
+        "xgmi": extras,
+        "host_wall_s": round(wall, 6),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--sets", type=int, default=8, help="rotating bucket sets (N=1)")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
+    ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
+    ap.add_argument("--no-extras", dest="extras", action="store_false")
+    ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
+    args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+        out = bench_multi(args, rank, world, local_rank)
+        dist.destroy_process_group()
+    else:
+        out = bench_single(args)
+        if args.cpu and not args.main_only:
+            try:
+                out["cpu_baseline"] = cpu_baseline()
+            except Exception as e:  # reported, never silently dropped
+                out["cpu_baseline"] = {"value": None, "error": repr(e)}
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -124,6 +124,15 @@ int allred_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream);
 int allred_bf16_add_masked(uint16_t* dst, const uint16_t* src, uint64_t block_mask,
                            size_t block_elems, void* stream);
 
+/* Reduce `total` virtual ranks (rank r at ranks + r*rank_stride) into `out`
+ * with the reduction tree of rank 0 of the (algo, side, total) schedule (one
+ * HBM pass; the hierarchical first stage), and the matching broadcast of one
+ * vector back to every rank (the all-gather's data movement). n % 8 == 0. */
+int allred_tree_reduce(const uint16_t* ranks, uint64_t rank_stride, size_t n, int algo, int side_length,
+                       int total_nodes, uint16_t* out, void* stream);
+int allred_broadcast(uint16_t* ranks, uint64_t rank_stride, size_t n, int total_nodes, const uint16_t* src,
+                     void* stream);
+
 /* ======================================================================
  * Virtual-rank plan: `total` ranks resident in ONE GPU's HBM, rank r at
  * ranks + r * rank_stride (elements).  Replaces the 64-core Tensix program

@@ -25,7 +25,7 @@ __all__ = [
     "highest_power_of_two", "get_step_directions", "get_comm_partner_swing_2D", "get_comm_partner_recdub_2D",
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "bf16_add",
-    "bf16_add_masked", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
+    "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
     "dist_allreduce_host", "dist_workspace_bytes",
 ]
 
@@ -125,6 +125,16 @@ def bf16_add(dst_ptr: int, src_ptr: int, n: int, stream=None) -> None:
 
 def bf16_add_masked(dst_ptr: int, src_ptr: int, mask: int, block_elems: int, stream=None) -> None:
     check(lib.allred_bf16_add_masked(dst_ptr, src_ptr, mask, block_elems, _stream_ptr(stream)), "bf16_add_masked")
+
+
+def tree_reduce(ranks_ptr: int, stride: int, n: int, algo: int, side: int, total: int, out_ptr: int,
+                stream=None) -> None:
+    check(lib.allred_tree_reduce(ranks_ptr, stride, n, algo, side, total, out_ptr, _stream_ptr(stream)),
+          "tree_reduce")
+
+
+def broadcast(ranks_ptr: int, stride: int, n: int, total: int, src_ptr: int, stream=None) -> None:
+    check(lib.allred_broadcast(ranks_ptr, stride, n, total, src_ptr, _stream_ptr(stream)), "broadcast")
 
 
 class Plan:

@@ -121,6 +121,8 @@ SIGNATURES = [
      [_P, _P, _P, C.c_size_t, C.c_float, C.c_uint32, C.c_int, C.POINTER(C.c_float)]),
     ("allred_bf16_add", C.c_int, [_u16p, _u16p, C.c_size_t, _P]),
     ("allred_bf16_add_masked", C.c_int, [_u16p, _u16p, C.c_uint64, C.c_size_t, _P]),
+    ("allred_tree_reduce", C.c_int, [_u16p, C.c_uint64, C.c_size_t, C.c_int, C.c_int, C.c_int, _u16p, _P]),
+    ("allred_broadcast", C.c_int, [_u16p, C.c_uint64, C.c_size_t, C.c_int, _u16p, _P]),
     ("allred_plan_create", C.c_int, [C.POINTER(PlanDesc), C.POINTER(_P)]),
     ("allred_plan_destroy", C.c_int, [_P]),
     ("allred_plan_workspace_bytes", C.c_size_t, [_P]),

@@ -29,8 +29,6 @@ using namespace tsa;
 struct allred_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
-    std::map<std::tuple<int, int, int>, uint8_t*> orders;  // (algo, side, total) -> device tree order
-    std::mutex mu;
 };
 
 namespace {
@@ -125,9 +123,46 @@ void host_tree_reduce(const uint16_t* ranks, size_t stride, size_t n, const allr
     }
 }
 
+// device copy of tree_order[0] of a (algo, side, total) schedule, cached for the process
+std::mutex g_order_mu;
+std::map<std::tuple<int, int, int, int>, uint8_t*> g_orders;
+
+int device_order(int algo, int side, int total, const uint8_t** out) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(g_order_mu);
+    auto key = std::make_tuple(dev, algo, side, total);
+    auto it = g_orders.find(key);
+    if (it == g_orders.end()) {
+        allred_schedule s;
+        int st = build_schedule(algo, side, total, &s, nullptr);
+        if (st != ALLRED_OK) return st;
+        uint8_t* p = nullptr;
+        if (hipMalloc((void**)&p, ALLRED_MAX_NODES) != hipSuccess) return ALLRED_ERR_NOMEM;
+        if (hipMemcpy(p, s.tree_order[0], ALLRED_MAX_NODES, hipMemcpyHostToDevice) != hipSuccess) return ALLRED_ERR_HIP;
+        it = g_orders.emplace(key, p).first;
+    }
+    *out = it->second;
+    return ALLRED_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
+int allred_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int algo, int side, int total,
+                       uint16_t* out, void* stream) {
+    if (!ranks || !out || stride < n) return ALLRED_ERR_ARG;
+    const uint8_t* order = nullptr;
+    int st = device_order(algo, side, total, &order);
+    if (st != ALLRED_OK) return st;
+    return launch_tree_reduce(ranks, stride, n, total, order, out, stream);
+}
+
+int allred_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src, void* stream) {
+    if (!ranks || !src || stride < n || total < 1) return ALLRED_ERR_ARG;
+    return launch_broadcast(ranks, stride, n, total, src, stream);
+}
 
 int allred_comm_get_unique_id(uint8_t* id) {
     if (!id) return ALLRED_ERR_ARG;
@@ -157,7 +192,6 @@ int allred_comm_init(const uint8_t* id, int nranks, int rank, int device, allred
 
 int allred_comm_destroy(allred_comm* c) {
     if (!c) return ALLRED_OK;
-    for (auto& kv : c->orders) (void)hipFree(kv.second);
     if (c->comm) ncclCommDestroy(c->comm);
     delete c;
     return ALLRED_OK;
@@ -179,26 +213,9 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
     const size_t n = (size_t)d->elems;
     uint16_t* staging = static_cast<uint16_t*>(workspace);
     uint16_t* bucket = buf;
-    const uint8_t* d_order = nullptr;
-    allred_schedule ls;
     if (d->local_ranks > 1) {
-        st = build_schedule(d->local_algo, d->local_side, d->local_ranks, &ls, nullptr);
-        if (st != ALLRED_OK) return st;
-        {
-            std::lock_guard<std::mutex> g(c->mu);
-            auto key = std::make_tuple(d->local_algo, d->local_side, d->local_ranks);
-            auto it = c->orders.find(key);
-            if (it == c->orders.end()) {
-                uint8_t* p = nullptr;
-                if (hipMalloc((void**)&p, ALLRED_MAX_NODES) != hipSuccess) return ALLRED_ERR_NOMEM;
-                if (hipMemcpy(p, ls.tree_order[0], ALLRED_MAX_NODES, hipMemcpyHostToDevice) != hipSuccess)
-                    return ALLRED_ERR_HIP;
-                it = c->orders.emplace(key, p).first;
-            }
-            d_order = it->second;
-        }
         bucket = staging + n;  // the GPU's partial
-        st = launch_tree_reduce(buf, n, n, d->local_ranks, d_order, bucket, stream);
+        st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
     const std::vector<Step> prog = program(s, c->rank, d->variant, n);

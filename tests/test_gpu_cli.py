@@ -1,0 +1,82 @@
+"""The reference's executables and invocations, unchanged, on the MI355X build
+(README.md:23-45, python/timing_taker.py:60-65).  Pass signal = the
+reference's own stdout line "All values match!" (allred_helper.cpp:75)."""
+import json
+
+import pytest
+
+import tenstorrentallreduce_amd as t
+
+pytestmark = pytest.mark.gpu
+
+
+def run(binary, argv, **env):
+    p = t.run_cli(binary, argv, env={"ALLRED_REPORT": "1", "ALLRED_CHECK_ALL": "1", **env})
+    assert p.returncode == 0, p.stderr
+    rep = json.loads(p.stderr.strip().splitlines()[-1])
+    return p.stdout, rep
+
+
+@pytest.mark.parametrize("argv", [
+    ["0", "1", "2", "-1", "1", "32", "0", "0"],      # BASELINE config 1: 2x2 RecDub LO, 1 tile, all ones
+    ["1", "1", "8", "13", "5", "32", "0", "1"],      # BASELINE config 2: 8x8 Swing BO, 5 tiles
+    ["0", "1", "8", "13", "5", "32", "0", "1"],      # 8x8 RecDub BO
+    ["1", "1", "8", "13", "320", "32", "0", "0"],    # LO 640 kB
+    ["0", "1", "8", "13", "3", "32", "0", "0"],      # LO 8 kB (LOO-sized)
+    ["1", "1", "4", "13", "2", "32", "3", "1"],      # 4x4 BO
+])
+def test_allred_BO_2D(argv):
+    out, rep = run("allred_BO_2D", argv)
+    assert "All values match!" in out
+    assert rep["mismatches"] == 0
+
+
+@pytest.mark.parametrize("exec_mode", ["steps", "fused"])
+@pytest.mark.parametrize("size", [1, 2, 4, 8, 16, 32, 64, 128, 192, 256, 320])
+@pytest.mark.parametrize("swing", ["0", "1"])
+def test_timing_taker_lo_sweep(swing, size, exec_mode):
+    """python/timing_taker.py:125,172-176 LO sizes: <bin> <swing> 1 8 13 <size> 32 0 0."""
+    out, rep = run("allred_BO_2D", [swing, "1", "8", "13", str(size), "32", "0", "0"], ALLRED_EXEC=exec_mode)
+    assert "All values match!" in out
+
+
+@pytest.mark.parametrize("size", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("binary", ["allred_BO_2D", "allred_mem_2D"])
+def test_timing_taker_bo_mem_sweep(binary, size):
+    argv = ["1", "1", "8", "13", str(size), "32"] + (["0", "1"] if binary == "allred_BO_2D" else [])
+    out, rep = run(binary, argv)
+    assert "All values match!" in out
+    assert rep["bytes_per_rank"] == size * 128 * 1024
+
+
+@pytest.mark.parametrize("bo", ["0", "1"])
+def test_exact_under_rne_ctor(bo):
+    """With the RNE bfloat16(float) ctor for inputs and expected values, the
+    engine's result equals the reference's expected vector exactly (ERROR 0):
+    RNE(a+b) * N/2 == RNE((a+b) * N/2)."""
+    out, rep = run("allred_BO_2D", ["1", "1", "8", "13", "5", "0", "0", bo], ALLRED_BF16_ROUND="rne")
+    assert "All values match!" in out and rep["max_error"] == 0
+
+
+def test_allred_LO_2D_legacy():
+    out, rep = run("allred_LO_2D", ["1", "1", "8", "13", "4", "32"])
+    assert "All values match!" in out
+
+
+def test_rank_count_extension_rectangular_grid():
+    # 8 ranks on a 4x2 grid (the 8-GPU mapping), via the trailing extension argument
+    out, rep = run("allred_BO_2D", ["1", "1", "4", "13", "40", "32", "0", "1", "8"])
+    assert "All values match!" in out and rep["ranks"] == 8 and rep["bytes_per_rank"] == 655360
+
+
+def test_mismatch_report_when_kernel_not_run():
+    """RUN_KERNEL = 0 still reads back and validates (allred_helper.hpp:85-93):
+    the inputs are not reduced, so the reference's mismatch report appears."""
+    p = t.run_cli("allred_BO_2D", ["1", "0", "2", "13", "1", "32", "0", "1"])
+    assert p.returncode == 0
+    assert "Mismatch at index 0:" in p.stdout and "Max error:" in p.stdout
+
+
+def test_bad_argument_fails_like_stoi():
+    p = t.run_cli("allred_BO_2D", ["x"])
+    assert p.returncode != 0 and "stoi" in p.stderr

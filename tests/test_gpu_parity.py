@@ -1,0 +1,216 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle.
+
+Integer/byte movement and the per-add bf16 rounding are deterministic, so the
+bar is BIT-EXACT equality with the oracle on the same inputs (same schedule,
+same add order, each add rounded to nearest even).  The reference's own
+tolerance (±32, README.md:31) is checked on top with its validate function.
+"""
+import numpy as np
+import pytest
+
+import oracle
+import tenstorrentallreduce_amd as t
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def to_dev(ranks):
+    return torch.from_numpy(np.stack(ranks).view(np.int16)).to(DEV)
+
+
+def from_dev(buf):
+    torch.cuda.synchronize()
+    return buf.cpu().numpy().view(np.uint16)
+
+
+def rand_ranks(total, n, seed, lo=0x3F80, hi=0x42C8):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(lo, hi, n).astype(np.uint16) for _ in range(total)]
+
+
+def run_plan(algo, variant, side, total, ranks, exec_mode, stride=None):
+    n = ranks[0].size
+    stride = stride or n
+    host = np.zeros((total, stride), dtype=np.uint16)
+    for r in range(total):
+        host[r, :n] = ranks[r]
+    buf = torch.from_numpy(host.view(np.int16)).to(DEV)
+    plan = t.Plan(algo, variant, side, n, total, exec_mode)
+    ws = torch.empty(max(plan.workspace_bytes, 16), dtype=torch.uint8, device=DEV)
+    plan.execute(buf.data_ptr(), stride, ws.data_ptr(), torch.cuda.current_stream())
+    out = from_dev(buf)[:, :n]
+    plan.close()
+    return out
+
+
+# ------------------------------------------------------------------ bf16 add
+def torch_add_ref(a_u16, b_u16):
+    a = torch.from_numpy(a_u16.view(np.int16)).view(torch.bfloat16).float()
+    b = torch.from_numpy(b_u16.view(np.int16)).view(torch.bfloat16).float()
+    return (a + b).to(torch.bfloat16).view(torch.int16).numpy().view(np.uint16)
+
+
+@pytest.mark.parametrize("n", [1, 7, 8, 9, 1000, 1 << 20, (1 << 20) + 13])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_bf16_add_matches_oracle_and_fp32_reference(n, offset):
+    rng = np.random.default_rng(n + offset)
+    a = rng.integers(0, 0x10000, n + offset).astype(np.uint16)
+    b = rng.integers(0, 0x10000, n + offset).astype(np.uint16)
+    # keep NaNs out of the bit-exact comparison; covered below
+    for x in (a, b):
+        nan = (x & 0x7F80) == 0x7F80
+        x[nan] &= 0x807F
+    da = torch.from_numpy(a.view(np.int16)).to(DEV)
+    db = torch.from_numpy(b.view(np.int16)).to(DEV)
+    t.bf16_add(da.data_ptr() + 2 * offset, db.data_ptr() + 2 * offset, n, torch.cuda.current_stream())
+    got = from_dev(da)[offset:]
+    want = np.array([oracle.bf16_add(int(x), int(y)) for x, y in zip(a[offset:offset + 4096], b[offset:offset + 4096])],
+                    dtype=np.uint16)
+    assert (got[:4096] == want).all()
+    ref = torch_add_ref(a[offset:], b[offset:])
+    gf = got.astype(np.uint32) << 16
+    rf = ref.astype(np.uint32) << 16
+    bothnan = np.isnan(gf.view(np.float32)) & np.isnan(rf.view(np.float32))
+    assert ((got == ref) | bothnan).all()
+
+
+def test_bf16_add_nan_inf():
+    vals = np.array([0x7F80, 0xFF80, 0x7FC0, 0x0001, 0x8001, 0x7F7F, 0x3F80], dtype=np.uint16)
+    a = np.repeat(vals, len(vals))
+    b = np.tile(vals, len(vals))
+    da = torch.from_numpy(a.view(np.int16)).to(DEV)
+    db = torch.from_numpy(b.view(np.int16)).to(DEV)
+    t.bf16_add(da.data_ptr(), db.data_ptr(), a.size)
+    got = from_dev(da).astype(np.uint32) << 16
+    want = torch_add_ref(a, b).astype(np.uint32) << 16
+    g, w = got.view(np.float32), want.view(np.float32)
+    assert ((g == w) | (np.isnan(g) & np.isnan(w))).all()
+
+
+def test_bf16_add_masked():
+    n_blk, blk = 64, 1024
+    rng = np.random.default_rng(3)
+    a = rng.integers(0x3F80, 0x42C8, n_blk * blk).astype(np.uint16)
+    b = rng.integers(0x3F80, 0x42C8, n_blk * blk).astype(np.uint16)
+    mask = 0x9900009999000099
+    da = torch.from_numpy(a.view(np.int16)).to(DEV)
+    db = torch.from_numpy(b.view(np.int16)).to(DEV)
+    t.bf16_add_masked(da.data_ptr(), db.data_ptr(), mask, blk)
+    got = from_dev(da)
+    summed = torch_add_ref(a, b)
+    for k in range(n_blk):
+        sl = slice(k * blk, (k + 1) * blk)
+        assert (got[sl] == (summed[sl] if (mask >> k) & 1 else a[sl])).all()
+
+
+# ------------------------------------------------------------------ plans
+GRIDS = [(1, 1), (2, 2), (2, 4), (4, 8), (4, 16), (8, 64)]
+
+
+@pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
+@pytest.mark.parametrize("variant", ["bo", "lo", "mem"])
+@pytest.mark.parametrize("algo", [t.SWING, t.RECDUB])
+@pytest.mark.parametrize("grid", GRIDS)
+def test_plan_bit_exact_vs_oracle(grid, algo, variant, exec_mode):
+    side, total = grid
+    n = 8 * total * 24
+    ranks = rand_ranks(total, n, seed=total * 7 + algo)
+    got = run_plan(algo, {"bo": t.BO, "lo": t.LO, "mem": t.MEM}[variant], side, total, ranks, exec_mode)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce(variant, algo, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
+@pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
+def test_plan_padded_stride(exec_mode):
+    side, total, n = 8, 64, 64 * 8 * 3
+    ranks = rand_ranks(total, n, seed=11)
+    got = run_plan(t.SWING, t.BO, side, total, ranks, exec_mode, stride=n + 64)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("bo", t.SWING, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
+@pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
+@pytest.mark.parametrize("algo", [t.SWING, t.RECDUB])
+def test_config2_reference_inputs(algo, exec_mode):
+    """BASELINE config 2: 8x8, 5 tiles per block (640 kB per rank), seed 13."""
+    side, total = 8, 64
+    n = t.normalize_tiles(5, total, True) * 1024
+    s0, s1, ranks = oracle.reference_inputs(side, total, n, 13)
+    got = run_plan(algo, t.BO, side, total, ranks, exec_mode)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("bo", algo, side, want, total)
+    assert (got == np.stack(want)).all()
+    for r in (0, 17, 63):
+        bad, maxe = oracle.validate(got[r].view(np.uint32), s0, s1, total, 32.0)
+        assert bad == 0
+
+
+@pytest.mark.parametrize("tiles", [1, 2, 16, 64, 128, 320])
+@pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
+def test_lo_sizes_reference_inputs(tiles, exec_mode):
+    side, total = 8, 64
+    n = t.normalize_tiles(tiles, total, False) * 1024
+    s0, s1, ranks = oracle.reference_inputs(side, total, n, 13)
+    got = run_plan(t.SWING, t.LO, side, total, ranks, exec_mode)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("lo", t.SWING, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
+def test_config1_known_answer():
+    s0, s1, ranks = oracle.reference_inputs(2, 4, 1024, -1)
+    for exec_mode in (t.EXEC_STEPS, t.EXEC_FUSED):
+        got = run_plan(t.RECDUB, t.LO, 2, 4, ranks, exec_mode)
+        assert (got == 0x4080).all()  # 4.0
+
+
+def test_plan_argument_errors():
+    with pytest.raises(t.AllredError) as e:
+        t.Plan(t.SWING, t.BO, 8, 100, 64)          # not a multiple of 8 * total
+    assert e.value.status == -1
+    with pytest.raises(t.AllredError) as e:
+        t.Plan(t.RECDUB, t.BO, 8, 8 * 16 * 4, 16)   # invalid rectangle
+    assert e.value.status == -2
+    p = t.Plan(t.SWING, t.LO, 8, 1024, 64)
+    with pytest.raises(t.AllredError):
+        p.execute(0, 1024)                          # null buffer
+    p.close()
+
+
+# ------------------------------------------------------------------ size-independent properties at full size
+@pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
+def test_config4_sized_bucket_closed_form(exec_mode):
+    """1 GiB per rank, 8 ranks (4x2 Swing BO) on one GPU: with the reference
+    input convention every later add is an exact doubling, so the result is
+    RNE(a+b) * N/2 exactly — checked on the GPU with torch."""
+    side, total = 4, 8
+    n = (1 << 30) // 2
+    g = torch.Generator(device=DEV).manual_seed(5)
+    a = (torch.rand(n, generator=g, device=DEV) * 100).to(torch.bfloat16)
+    b = (torch.rand(n, generator=g, device=DEV) * 100).to(torch.bfloat16)
+    buf = torch.empty((total, n), dtype=torch.bfloat16, device=DEV)
+    for r in range(total):
+        buf[r] = b if (r % side) % 2 == 0 else a
+    plan = t.Plan(t.SWING, t.BO, side, n, total, exec_mode)
+    plan.execute(buf.data_ptr(), n, None, torch.cuda.current_stream())
+    expect = ((a.float() + b.float()).to(torch.bfloat16).float() * (total // 2)).to(torch.bfloat16)
+    for r in range(total):
+        assert torch.equal(buf[r], expect), r
+    plan.close()
+
+
+def test_linearity_and_idempotent_layout():
+    """allreduce(x) of a rank set that already holds identical vectors v gives
+    RNE-doubling chains: N*v exactly for power-of-two N and small v."""
+    side, total, n = 8, 64, 64 * 8 * 64
+    v = torch.full((n,), 3.0, dtype=torch.bfloat16, device=DEV)
+    buf = v.repeat(total, 1).contiguous()
+    plan = t.Plan(t.SWING, t.BO, side, n, total, t.EXEC_FUSED)
+    plan.execute(buf.data_ptr(), n)
+    torch.cuda.synchronize()
+    assert torch.equal(buf, torch.full_like(buf, 192.0))
+    plan.close()

@@ -1,0 +1,53 @@
+"""HBM traffic per launch from rocprofv3 --pmc CSVs (MI355X_MICROARCH.md §HBM).
+
+  python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> \
+      <kernel-substring> <key> <algorithmic_bytes_per_launch> [out.json]
+
+Counters are collected in SEPARATE passes (FETCH_SIZE uses 3 TCC slots,
+WRITE_SIZE 2).  Both are in KiB.  gfx950 correction: FETCH_SIZE reports half
+the bytes of a wide coalesced streaming read (16 B/lane) — doubled here;
+WRITE_SIZE is exact for 16-B-per-lane streaming stores.
+"""
+import csv
+import json
+import statistics
+import sys
+from collections import defaultdict
+
+
+def per_dispatch(path, counter, kernel_sub):
+    vals = defaultdict(float)
+    for r in csv.DictReader(open(path)):
+        if kernel_sub not in r.get("Kernel_Name", ""):
+            continue
+        if r.get("Counter_Name") != counter:
+            continue
+        vals[r.get("Dispatch_Id") or r.get("Correlation_Id")] += float(r["Counter_Value"])
+    return list(vals.values())
+
+
+def main():
+    fetch_csv, write_csv, kernel_sub, key, alg = sys.argv[1:6]
+    out_path = sys.argv[6] if len(sys.argv) > 6 else None
+    alg = int(alg)
+    f = per_dispatch(fetch_csv, "FETCH_SIZE", kernel_sub)
+    w = per_dispatch(write_csv, "WRITE_SIZE", kernel_sub)
+    fetch_b = 2 * 1024 * statistics.median(f)  # gfx950: FETCH_SIZE reads half of wide streaming loads
+    write_b = 1024 * statistics.median(w)
+    res = {"kernel": kernel_sub, "dispatches": [len(f), len(w)], "fetch_size_kib_median": statistics.median(f),
+           "write_size_kib_median": statistics.median(w), "read_bytes_corrected": fetch_b, "write_bytes": write_b,
+           "hbm_bytes_per_launch": int(fetch_b + write_b), "algorithmic_bytes_per_launch": alg,
+           "ratio_to_algorithmic": round((fetch_b + write_b) / alg, 4)}
+    print(json.dumps(res, indent=1))
+    if out_path:
+        try:
+            d = json.load(open(out_path))
+        except Exception:
+            d = {"note": "HBM bytes per launch, rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, "
+                         "FETCH_SIZE x2 (gfx950 wide-load correction), KiB x1024", "kernels": {}}
+        d["kernels"][key] = res
+        json.dump(d, open(out_path, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
