@@ -99,15 +99,16 @@ def bench_single(args) -> dict:
     dev = torch.device("cuda:0")
     stream = torch.cuda.Stream(device=dev)
     nsets = args.sets
-    sets = [torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev) for _ in range(nsets)]
+    stride = t.preferred_rank_stride(ELEMS)   # 128-byte skew between rank rows
+    sets = [torch.empty((RANKS, stride), dtype=torch.int16, device=dev) for _ in range(nsets)]
     for i, s in enumerate(sets):
-        fill_reference_convention(s, 1000 + i)
+        fill_reference_convention(s[:, :ELEMS], 1000 + i)
     torch.cuda.synchronize()
     plan = t.Plan(t.SWING, t.BO, SIDE, ELEMS, RANKS, t.EXEC_FUSED)
     steps_plan = t.Plan(t.SWING, t.BO, SIDE, ELEMS, RANKS, t.EXEC_STEPS)
 
     def step(i, p=plan):
-        p.execute(sets[i % nsets].data_ptr(), ELEMS, None, stream)
+        p.execute(sets[i % nsets].data_ptr(), stride, None, stream)
 
     with torch.cuda.stream(stream):
         for i in range(args.warmup):
@@ -166,10 +167,16 @@ def bench_single(args) -> dict:
     with torch.cuda.stream(stream):
         e0.record(stream)
         for i in range(args.steps):
-            plan.execute(sets[0].data_ptr(), ELEMS, None, stream)
+            plan.execute(sets[0].data_ptr(), stride, None, stream)
         e1.record(stream)
     torch.cuda.synchronize()
     hot_ms = e0.elapsed_time(e1) / args.steps
+
+    # host-staged end to end (buckets start and end in pinned host memory): the
+    # reference program surface, H2D of all 64 buckets + allreduce + D2H
+    rep = t.run(["allred_BO_2D", "1", "1", str(SIDE), "13", str(TILES), "32", "0", "1"], t.BO, False, t.EXEC_FUSED)
+    e2e = {"e2e_ms": round(rep.e2e_seconds * 1e3, 4), "device_ms": round(rep.device_seconds * 1e3, 4),
+           "value": round(bytes_all / rep.e2e_seconds / 1e9, 3), "mismatches": int(rep.mismatches)}
 
     alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
@@ -185,17 +192,19 @@ def bench_single(args) -> dict:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (uniform [0,100) bf16, reference rank convention); 8 rotating bucket sets in HBM",
+        "data": "synthetic (uniform [0,100) bf16, reference rank convention); 8 rotating bucket sets in HBM, "
+                "rank rows 655,360 B + 128 B skew",
         "config": {"workload": "BASELINE config 2: 8x8 Swing BO allreduce, 64 virtual ranks x 655,360 B bf16 "
                                "(5 tiles/block) on one MI355X, fused one-pass HIP kernel, no RCCL",
                    "ranks": RANKS, "bytes_per_rank": ELEMS * 2, "algo": "swing", "variant": "BO",
                    "exec": "fused", "launches_per_step": plan.launches, "hip_graph": graph is not None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic("k_tree64"),
-                     "kernel": "k_tree<64,true>", "algorithmic_bytes_per_launch": alg_bytes},
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic("k_tree_lds64"),
+                     "kernel": "k_tree_lds<64>", "algorithmic_bytes_per_launch": alg_bytes},
         "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
                               "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
+        "host_staged": e2e,
         "host_wall_s": round(wall, 6),
     }
     plan.close()
@@ -270,7 +279,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
             m = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64)
             dist.all_reduce(m, op=dist.ReduceOp.MAX)
             sec = m.item() * 1e-3
-            busbw = 2 * (world - 1) / world * nbytes / sec / 1e9
+            busbw = 2 * (world - 1) / world * nbytes / sec / 1e9  # nccl-tests convention
             extras[name] = {"ms": round(m.item(), 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
                             "busbw_GBps": round(busbw, 3),
                             "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
@@ -316,12 +325,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     ap.add_argument("--no-extras", dest="extras", action="store_false")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
+    ap.add_argument("--force-dist", action="store_true", help="run the N>1 code path on one GPU (1-rank RCCL)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo")
+    if world > 1 or args.force_dist:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29511")
+            dist.init_process_group("gloo", rank=0, world_size=1)
+        else:
+            dist.init_process_group("gloo")
         out = bench_multi(args, rank, world, local_rank)
         dist.destroy_process_group()
     else:

@@ -150,6 +150,11 @@ typedef struct {
     uint64_t elems_per_rank; /* bf16 elements; BO/MEM need a multiple of 8*total, LO of 8 */
 } allred_plan_desc;
 int allred_plan_create(const allred_plan_desc* desc, allred_plan** out);
+/* HBM layout helper: the rank stride (elements) this engine lays virtual ranks
+ * out with — elems rounded up to 64, plus a 128-byte skew so the P rank rows
+ * of a tile do not start on the same HBM channel (655,360-byte rows are
+ * 5 * 2^17 apart: +5.6 % on the fused pass). */
+uint64_t allred_preferred_rank_stride(uint64_t elems_per_rank);
 int allred_plan_destroy(allred_plan* plan);
 size_t allred_plan_workspace_bytes(const allred_plan* plan);
 /* workspace: device memory of allred_plan_workspace_bytes() (may be NULL when 0) */

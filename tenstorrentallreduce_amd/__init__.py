@@ -24,7 +24,7 @@ __all__ = [
     "BO", "LO", "MEM", "SWING", "RECDUB", "EXEC_STEPS", "EXEC_FUSED", "AllredError", "schedule",
     "highest_power_of_two", "get_step_directions", "get_comm_partner_swing_2D", "get_comm_partner_recdub_2D",
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
-    "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "bf16_add",
+    "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
     "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
     "dist_allreduce_host", "dist_workspace_bytes",
 ]
@@ -137,6 +137,10 @@ def broadcast(ranks_ptr: int, stride: int, n: int, total: int, src_ptr: int, str
     check(lib.allred_broadcast(ranks_ptr, stride, n, total, src_ptr, _stream_ptr(stream)), "broadcast")
 
 
+def preferred_rank_stride(elems: int) -> int:
+    return lib.allred_preferred_rank_stride(elems)
+
+
 class Plan:
     """N virtual ranks in one GPU's HBM (allred_plan_*)."""
 
@@ -175,9 +179,11 @@ def parse_args(argv: Sequence[str], variant: int = BO) -> Args:
     return a
 
 
-def run(argv: Sequence[str], variant: int = BO, verbose: bool = False) -> Report:
+def run(argv: Sequence[str], variant: int = BO, verbose: bool = False, exec_mode: int | None = None) -> Report:
     """AllredConfig(argv) + RunProgram() in-process (allred_helper.hpp:47-97)."""
     a = parse_args(argv, variant)
+    if exec_mode is not None:
+        a.exec = exec_mode
     r = Report()
     check(lib.allred_run(C.byref(a), int(verbose), C.byref(r)), "run")
     return r

@@ -123,6 +123,7 @@ SIGNATURES = [
     ("allred_bf16_add_masked", C.c_int, [_u16p, _u16p, C.c_uint64, C.c_size_t, _P]),
     ("allred_tree_reduce", C.c_int, [_u16p, C.c_uint64, C.c_size_t, C.c_int, C.c_int, C.c_int, _u16p, _P]),
     ("allred_broadcast", C.c_int, [_u16p, C.c_uint64, C.c_size_t, C.c_int, _u16p, _P]),
+    ("allred_preferred_rank_stride", C.c_uint64, [C.c_uint64]),
     ("allred_plan_create", C.c_int, [C.POINTER(PlanDesc), C.POINTER(_P)]),
     ("allred_plan_destroy", C.c_int, [_P]),
     ("allred_plan_workspace_bytes", C.c_size_t, [_P]),

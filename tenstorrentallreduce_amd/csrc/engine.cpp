@@ -134,6 +134,8 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
     return ALLRED_OK;
 }
 
+uint64_t allred_preferred_rank_stride(uint64_t elems) { return (elems + 63) / 64 * 64 + 64; }
+
 int allred_plan_destroy(allred_plan* plan) {
     free_plan(plan);
     return ALLRED_OK;
@@ -284,6 +286,8 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
     hipStream_t s = nullptr;
     const size_t all_bytes = (size_t)N * bytes;
+    const size_t stride = (size_t)allred_preferred_rank_stride(n);
+    const size_t dev_bytes = (size_t)N * stride * 2;
     float ms = 0;
     if (a->seed < 0) {
         allred_constant_bf16_vector(bytes, 1.0f, src0.data());
@@ -298,24 +302,24 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     // even x loads src_1, odd x loads src_0 (allred_BO_2D.cpp:79-85)
     for (int r = 0; r < N; ++r)
         std::memcpy(h_in + (size_t)r * n, ((r % a->side_length) % 2 == 0) ? src1.data() : src0.data(), bytes);
-    HIPCK(hipMalloc((void**)&d_ranks, all_bytes));
-    HIPCK(hipMalloc((void**)&d_scratch, all_bytes));
+    HIPCK(hipMalloc((void**)&d_ranks, dev_bytes));
+    HIPCK(hipMalloc((void**)&d_scratch, dev_bytes));
     if (plan->ws_bytes) HIPCK(hipMalloc(&d_ws, plan->ws_bytes));
     HIPCK(hipEventCreate(&e0));
     HIPCK(hipEventCreate(&e1));
     HIPCK(hipEventCreate(&e2));
     HIPCK(hipEventCreate(&e3));
     // warm-up on a scratch copy (first-launch code-object load stays out of the timing)
-    HIPCK(hipMemcpyAsync(d_scratch, h_in, all_bytes, hipMemcpyHostToDevice, s));
-    if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, n, d_ws, s));
+    HIPCK(hipMemcpy2DAsync(d_scratch, stride * 2, h_in, bytes, bytes, N, hipMemcpyHostToDevice, s));
+    if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, stride, d_ws, s));
     HIPCK(hipStreamSynchronize(s));
     // timed: H2D | allreduce | D2H
     HIPCK(hipEventRecord(e0, s));
-    HIPCK(hipMemcpyAsync(d_ranks, h_in, all_bytes, hipMemcpyHostToDevice, s));
+    HIPCK(hipMemcpy2DAsync(d_ranks, stride * 2, h_in, bytes, bytes, N, hipMemcpyHostToDevice, s));
     HIPCK(hipEventRecord(e1, s));
-    if (a->run_kernel) ST(allred_plan_execute(plan, d_ranks, n, d_ws, s));
+    if (a->run_kernel) ST(allred_plan_execute(plan, d_ranks, stride, d_ws, s));
     HIPCK(hipEventRecord(e2, s));
-    HIPCK(hipMemcpyAsync(h_out, d_ranks, all_bytes, hipMemcpyDeviceToHost, s));
+    HIPCK(hipMemcpy2DAsync(h_out, bytes, d_ranks, stride * 2, bytes, N, hipMemcpyDeviceToHost, s));
     HIPCK(hipEventRecord(e3, s));
     HIPCK(hipStreamSynchronize(s));
     HIPCK(hipEventElapsedTime(&ms, e1, e2));

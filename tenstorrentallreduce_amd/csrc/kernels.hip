@@ -13,6 +13,8 @@
 // one GPU's HBM, where a "send" is a load of the partner's bytes.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "internal.hpp"
 
 namespace tsa {
@@ -54,11 +56,35 @@ __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
     return o;
 }
 
+// Streaming (nontemporal) 16-byte accesses: every byte of a bucket is read
+// once and written once per pass, so nothing is worth keeping in L2 / MALL
+// (measured: the fused tree pass 19.2 -> 16.0 us, the tile-sum 5.9 -> 6.4 TB/s).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(uint4* p, uint4 v) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) const uint32_t global_u32;
+
 __device__ __forceinline__ uint64_t gtid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t gthreads() { return (uint64_t)gridDim.x * blockDim.x; }
 
 constexpr int kBlock = 256;          // 4 waves per workgroup
 constexpr int kMaxGrid = 256 * 8;    // 256 CUs x 8 resident workgroups, then grid-stride
+
+// one item per thread up to 2^30 threads
+inline unsigned grid_all(uint64_t work_items) {
+    uint64_t g = (work_items + kBlock - 1) / kBlock;
+    if (g < 1) g = 1;
+    if (g > (1ull << 22)) g = 1ull << 22;
+    return (unsigned)g;
+}
 
 inline unsigned grid_for(uint64_t work_items) {
     uint64_t g = (work_items + kBlock - 1) / kBlock;
@@ -68,22 +94,13 @@ inline unsigned grid_for(uint64_t work_items) {
 }
 
 // ---------------------------------------------------------------------------
-// dst += src over n_vec 16-byte vectors (+ scalar tail).  4 vectors in flight
-// per lane per iteration, grid-stride so each wave's loads stay coalesced.
+// dst += src over n_vec 16-byte vectors: one vector per lane (grid covers the
+// whole range; the loop only runs past 2^31 threads).  Many short-lived waves
+// stream HBM better than a capped grid-stride loop (6.4 vs 5.0 TB/s at 256 MiB).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_add(uint4* __restrict__ dst, const uint4* __restrict__ src,
                                                 uint64_t n_vec) {
-    const uint64_t T = gthreads();
-    uint64_t i = gtid();
-    for (; i + 3 * T < n_vec; i += 4 * T) {
-        uint4 a0 = dst[i], a1 = dst[i + T], a2 = dst[i + 2 * T], a3 = dst[i + 3 * T];
-        uint4 b0 = src[i], b1 = src[i + T], b2 = src[i + 2 * T], b3 = src[i + 3 * T];
-        dst[i] = add8(a0, b0);
-        dst[i + T] = add8(a1, b1);
-        dst[i + 2 * T] = add8(a2, b2);
-        dst[i + 3 * T] = add8(a3, b3);
-    }
-    for (; i < n_vec; i += T) dst[i] = add8(dst[i], src[i]);
+    for (uint64_t i = gtid(); i < n_vec; i += gthreads()) st_nt(dst + i, add8(ld_nt(dst + i), ld_nt(src + i)));
 }
 
 __global__ void k_add_scalar(uint16_t* __restrict__ dst, const uint16_t* __restrict__ src, uint64_t n) {
@@ -103,7 +120,8 @@ struct BlockList {
 __global__ __launch_bounds__(kBlock) void k_add_blocks(uint4* __restrict__ dst, const uint4* __restrict__ src,
                                                        BlockList list, uint64_t block_vec) {
     const uint64_t off = (uint64_t)list.b[blockIdx.y] * block_vec;
-    for (uint64_t v = gtid(); v < block_vec; v += gthreads()) dst[off + v] = add8(dst[off + v], src[off + v]);
+    for (uint64_t v = gtid(); v < block_vec; v += gthreads())
+        st_nt(dst + off + v, add8(ld_nt(dst + off + v), ld_nt(src + off + v)));
 }
 
 // ---------------------------------------------------------------------------
@@ -147,7 +165,7 @@ __global__ __launch_bounds__(kBlock) void k_tree(uint16_t* __restrict__ ranks, u
         }
         uint4 x[LEAVES];
 #pragma unroll
-        for (int i = 0; i < LEAVES; ++i) x[i] = ok ? rows[i][v] : make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < LEAVES; ++i) x[i] = ok ? ld_nt(rows[i] + v) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int w = 1; w < LEAVES; w *= 2)
 #pragma unroll
@@ -158,11 +176,61 @@ __global__ __launch_bounds__(kBlock) void k_tree(uint16_t* __restrict__ ranks, u
         if (ok) {
             if (WRITE_ALL) {
 #pragma unroll
-                for (int i = 0; i < LEAVES; ++i) rows[i][v] = acc;
+                for (int i = 0; i < LEAVES; ++i) st_nt(rows[i] + v, acc);
             } else if (g == 0) {
                 reinterpret_cast<uint4*>(out)[v] = acc;
             }
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// The same BO pass staged through LDS (the shipped form for P >= 8): one
+// workgroup = one tile of 256 elements (512 B) of all P ranks.  HBM -> LDS by
+// global_load_lds, 1 KiB contiguous per wave-instruction (two ranks' rows);
+// the LDS tile turns the rank-major HBM layout into the per-column leaf reads
+// of the tree; the result row leaves with 1 KiB contiguous wave-stores.
+// Wave w stages ranks [P/4 w, P/4 (w+1)) and reduces tree positions
+// [P/4 w, P/4 (w+1)) of every column (lane = h * 32 + column: h picks the
+// half, levels below P/8 in registers, one xor-32 shuffle); the four wave
+// partials meet in LDS rows 0-3 (free once every wave has read its leaves).
+// 16.0 us vs 17.3 us for k_tree at 64 x 640 kB (= a 42+42 MB copy's time).
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                     const uint8_t* __restrict__ order, uint64_t block_vec) {
+    constexpr int TV = 32;          // 16-byte vectors per rank row of a tile
+    constexpr int RPW = P / 4;      // ranks staged (and tree leaves reduced) per wave
+    constexpr int LPL = RPW / 2;    // leaves per lane
+    __shared__ __attribute__((aligned(16))) uint4 tile[P * TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const uint64_t v0 = (uint64_t)blockIdx.x * TV;
+#pragma unroll
+    for (int k = 0; k < RPW / 2; ++k) {
+        const int r = RPW * w + 2 * k + h;
+        const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + v0 + c;
+        __builtin_amdgcn_global_load_lds((global_u32*)src, (lds_u32*)&tile[(RPW * w + 2 * k) * TV], 16, 0, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const uint8_t* ord = order + (v0 / block_vec) * ALLRED_MAX_NODES + RPW * w + LPL * h;
+    uint4 x[LPL];
+#pragma unroll
+    for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+    for (int s = 1; s < LPL; s *= 2)
+#pragma unroll
+        for (int i = 0; i < LPL; i += 2 * s) x[i] = add8(x[i], x[i + s]);
+    const uint4 part = add8(x[0], shfl_xor4(x[0], 32));
+    __syncthreads();
+    if (h == 0) tile[w * TV + c] = part;
+    __syncthreads();
+    const uint4 res = add8(add8(tile[0 * TV + c], tile[1 * TV + c]), add8(tile[2 * TV + c], tile[3 * TV + c]));
+#pragma unroll
+    for (int k = 0; k < RPW / 2; ++k) {
+        const int r = RPW * w + 2 * k + h;
+        st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res);
     }
 }
 
@@ -221,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void k_broadcast(uint16_t* __restrict__ ran
                                                       const uint4* __restrict__ src, uint64_t n_vec) {
     for (uint64_t v = gtid(); v < n_vec; v += gthreads()) {
         const uint4 x = src[v];
-        for (int r = 0; r < total; ++r) reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride)[v] = x;
+        for (int r = 0; r < total; ++r) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v, x);
     }
 }
 
@@ -243,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void k_step(uint16_t* __restrict__ ranks, u
     const uint64_t off = (uint64_t)blocks[t] * block_vec;
     uint4* L = reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + off;
     const uint4* R = reinterpret_cast<const uint4*>(ranks + (uint64_t)p * stride) + off;
-    for (uint64_t v = gtid(); v < block_vec; v += gthreads()) L[v] = ADD ? add8(L[v], R[v]) : R[v];
+    for (uint64_t v = gtid(); v < block_vec; v += gthreads()) st_nt(L + v, ADD ? add8(ld_nt(L + v), ld_nt(R + v)) : ld_nt(R + v));
 }
 
 // LO step (full vector): dst[r] = src[r] + src[p(r)], ping-pong buffers
@@ -255,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_lo_step(const uint16_t* __restrict__
     const uint4* A = reinterpret_cast<const uint4*>(src + (uint64_t)r * src_stride);
     const uint4* B = reinterpret_cast<const uint4*>(src + (uint64_t)p * src_stride);
     uint4* D = reinterpret_cast<uint4*>(dst + (uint64_t)r * dst_stride);
-    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) D[v] = add8(A[v], B[v]);
+    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) st_nt(D + v, add8(ld_nt(A + v), ld_nt(B + v)));
 }
 
 __global__ __launch_bounds__(kBlock) void k_copy_ranks(const uint16_t* __restrict__ src, uint64_t src_stride,
@@ -263,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_copy_ranks(const uint16_t* __restric
                                                        uint64_t n_vec) {
     const uint4* A = reinterpret_cast<const uint4*>(src + (uint64_t)blockIdx.y * src_stride);
     uint4* D = reinterpret_cast<uint4*>(dst + (uint64_t)blockIdx.y * dst_stride);
-    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) D[v] = A[v];
+    for (uint64_t v = gtid(); v < n_vec; v += gthreads()) st_nt(D + v, ld_nt(A + v));
 }
 
 // ---------------------------------------------------------------------------
@@ -303,11 +371,32 @@ __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, ui
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// ALLRED_TREE=registers selects the register-only k_tree for the fused BO pass
+// (A/B and fallback); the LDS-staged k_tree_lds is the default.
+bool tree_force_registers() {
+    static const bool v = [] {
+        const char* e = std::getenv("ALLRED_TREE");
+        return e && e[0] == 'r';
+    }();
+    return v;
+}
+
 int last_error() { return hip_status((int)hipGetLastError()); }
 
 template <bool WRITE_ALL>
 int tree_dispatch(uint16_t* ranks, uint64_t stride, uint64_t n_vec, int total, const uint8_t* order,
                   uint64_t block_vec, uint16_t* out, hipStream_t st) {
+    if (WRITE_ALL && total >= 8 && block_vec && block_vec % 32 == 0 && !tree_force_registers()) {
+        const dim3 grid((unsigned)(n_vec / 32)), blk(kBlock);
+        switch (total) {
+            case 8: hipLaunchKernelGGL(k_tree_lds<8>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
+            case 16: hipLaunchKernelGGL(k_tree_lds<16>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
+            case 32: hipLaunchKernelGGL(k_tree_lds<32>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
+            case 64: hipLaunchKernelGGL(k_tree_lds<64>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
+            default: return ALLRED_ERR_UNSUPPORTED;
+        }
+        return last_error();
+    }
     const int lanes = total >= 8 ? total / 8 : 1;
     const uint64_t chunk_groups = (n_vec + (64 / lanes) - 1) / (64 / lanes);  // one per wave
     uint64_t blocks = (chunk_groups + 3) / 4;
@@ -337,7 +426,7 @@ int launch_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream) 
     if (!dst || !src) return ALLRED_ERR_ARG;
     if (aligned16(dst) && aligned16(src)) {
         const uint64_t nv = n / 8;
-        if (nv) hipLaunchKernelGGL(k_add, dim3(grid_for(nv / 4 + 1)), dim3(kBlock), 0, st,
+        if (nv) hipLaunchKernelGGL(k_add, dim3(grid_all(nv)), dim3(kBlock), 0, st,
                                    reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src), nv);
         const uint64_t tail = n - nv * 8;
         if (tail) hipLaunchKernelGGL(k_add_scalar, dim3(1), dim3(64), 0, st, dst + nv * 8, src + nv * 8, tail);
@@ -354,7 +443,7 @@ int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* bl
     BlockList list{};
     for (int i = 0; i < nblocks; ++i) list.b[i] = blocks[i];
     const uint64_t bv = block_elems / 8;
-    hipLaunchKernelGGL(k_add_blocks, dim3(grid_for(bv) > 64 ? 64 : grid_for(bv), nblocks), dim3(kBlock), 0,
+    hipLaunchKernelGGL(k_add_blocks, dim3(grid_all(bv), nblocks), dim3(kBlock), 0,
                        (hipStream_t)stream, reinterpret_cast<uint4*>(dst), reinterpret_cast<const uint4*>(src),
                        list, bv);
     return last_error();
@@ -399,7 +488,7 @@ int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tot
 int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src, void* stream) {
     if (n % 8 || stride % 8 || !aligned16(ranks) || !aligned16(src)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
-    hipLaunchKernelGGL(k_broadcast, dim3(grid_for(nv)), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, total,
+    hipLaunchKernelGGL(k_broadcast, dim3(grid_all(nv)), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, total,
                        reinterpret_cast<const uint4*>(src), nv);
     return last_error();
 }
@@ -408,8 +497,7 @@ static int launch_step(bool add, uint16_t* ranks, uint64_t stride, int total, co
                        const int16_t* d_blocks, int blocks_per_rank, size_t block_elems, void* stream) {
     if (block_elems % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8;
-    unsigned gx = grid_for(bv);
-    if (gx > 64) gx = 64;
+    const unsigned gx = grid_all(bv);
     const dim3 grid(gx, (unsigned)(total * blocks_per_rank));
     if (add)
         hipLaunchKernelGGL(k_step<true>, grid, dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_partner,
@@ -434,8 +522,7 @@ int launch_lo_step(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint
                    const int16_t* d_partner, size_t n, void* stream) {
     if (n % 8 || src_stride % 8 || dst_stride % 8 || !aligned16(src) || !aligned16(dst)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
-    unsigned gx = grid_for(nv);
-    if (gx > 128) gx = 128;
+    const unsigned gx = grid_all(nv);
     hipLaunchKernelGGL(k_lo_step, dim3(gx, total), dim3(kBlock), 0, (hipStream_t)stream, src, src_stride, dst,
                        dst_stride, d_partner, nv);
     return last_error();
@@ -445,8 +532,7 @@ int launch_copy_ranks(const uint16_t* src, uint64_t src_stride, uint16_t* dst, u
                       size_t n, void* stream) {
     if (n % 8 || src_stride % 8 || dst_stride % 8 || !aligned16(src) || !aligned16(dst)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
-    unsigned gx = grid_for(nv);
-    if (gx > 128) gx = 128;
+    const unsigned gx = grid_all(nv);
     hipLaunchKernelGGL(k_copy_ranks, dim3(gx, total), dim3(kBlock), 0, (hipStream_t)stream, src, src_stride, dst,
                        dst_stride, nv);
     return last_error();

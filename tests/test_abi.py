@@ -1,0 +1,145 @@
+"""The C-ABI boundary without a GPU: every symbol include/allred.h declares is
+exported, the host-only entry points behave like the reference's, and the
+source-compatible allred_helper.hpp compiles, links and runs."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+import tenstorrentallreduce_amd as t
+from tenstorrentallreduce_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "allred.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"\b(allred_\w+)\s*\(", src))
+    return sorted(n for n in names if not n.endswith("_fn"))
+
+
+def test_every_declared_symbol_is_exported_and_bound():
+    names = declared_functions()
+    assert len(names) >= 30
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    for n in names:
+        assert hasattr(_lib.lib, n), n
+        assert n in bound, f"{n} declared in allred.h but not bound in _lib.SIGNATURES"
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    for n in names:
+        assert re.search(rf"\bT {n}\b", nm), n
+
+
+def test_status_strings():
+    assert _lib.lib.allred_abi_version() == 1
+    for st in range(0, -8, -1):
+        assert _lib.lib.allred_status_string(st)
+
+
+REF_DEFAULTS = dict(swing=0, run_kernel=0, side_length=1, seed=0, tiles=1, error=1, print_core=0, bandwidth_optimal=0)
+
+
+@pytest.mark.parametrize("argv,want", [
+    ([], {}),
+    (["1"], {"swing": 1}),
+    (["2"], {"swing": 0}),                                     # only == 1 selects Swing
+    (["1", "1", "8", "13", "5", "32", "0", "1"],
+     {"swing": 1, "run_kernel": 1, "side_length": 8, "seed": 13, "tiles": 5, "error": 32, "bandwidth_optimal": 1,
+      "num_tiles": 320, "total_nodes": 64}),
+    (["0", "1", "5", "-1", "0", "32", "3", "0"],               # side 5 -> 4; tiles 0 -> 1
+     {"run_kernel": 1, "side_length": 4, "seed": -1, "tiles": 1, "error": 32, "print_core": 3, "num_tiles": 1}),
+    (["0", "1", "100", "7", "65", "1", "0", "0"], {"run_kernel": 1, "side_length": 8, "seed": 7, "tiles": 65,
+                                                  "num_tiles": 128}),
+    (["1", "1", "8", "13", "3", "32", "0", "0"],               # LO: next power of two
+     {"swing": 1, "run_kernel": 1, "side_length": 8, "seed": 13, "tiles": 3, "error": 32, "num_tiles": 4}),
+    (["0", "1", "4", "13", "40", "32", "0", "1", "8"],         # rank-count extension: 4x2 grid
+     {"run_kernel": 1, "side_length": 4, "seed": 13, "tiles": 40, "error": 32, "bandwidth_optimal": 1,
+      "total_nodes": 8, "num_tiles": 320}),
+    ([" 12abc"], {"swing": 0}),                                 # std::stoi reads the leading integer
+])
+def test_args_parse_like_allredconfig(argv, want):
+    a = t.parse_args(["allred_BO_2D", *argv], t.BO)
+    exp = dict(REF_DEFAULTS)
+    exp.update(want)
+    for k, v in exp.items():
+        assert getattr(a, k) == v, (k, getattr(a, k), v)
+
+
+def test_args_parse_variants():
+    # allred_mem_2D: large_buffer = true (allred_mem_2D.cpp:15); args 7/8 ignored
+    a = t.parse_args(["allred_mem_2D", "1", "1", "8", "13", "5", "32", "9", "0"], t.MEM)
+    assert a.num_tiles == 320 and a.print_core == 0
+    a = t.parse_args(["allred_LO_2D", "1", "1", "8", "13", "5", "32"], t.LO)
+    assert a.num_tiles == 8
+
+
+@pytest.mark.parametrize("bad", [["x"], ["1", "1", "abc"], ["1", "1", "8", "13", "99999999999"]])
+def test_args_parse_rejects_junk_like_stoi(bad):
+    with pytest.raises(t.AllredError):
+        t.parse_args(["allred_BO_2D", *bad], t.BO)
+
+
+def test_validate_matches_oracle_counts():
+    n = 4096
+    s0 = t.random_bf16_vector(2 * n, 13)
+    s1 = t.random_bf16_vector(2 * n, 14)
+    _, _, ranks = oracle.reference_inputs(8, 64, n, 13)
+    good = ranks[0].copy()
+    oracle.allreduce("bo", oracle.SWING, 8, [r.copy() for r in ranks], 64)
+    rs = [r.copy() for r in ranks]
+    oracle.allreduce("bo", oracle.SWING, 8, rs, 64)
+    res = rs[0].view(np.uint32)
+    assert t.validate_result_vector(res, s0, s1, n // 2, 32, 64)[0] == 0
+    assert oracle.validate(res, s0, s1, 64, 32)[0] == 0
+    bad = rs[0].copy()
+    bad[::97] ^= 0x0100  # perturb exponent bits of some elements
+    b1, m1 = t.validate_result_vector(bad.view(np.uint32), s0, s1, n // 2, 32, 64)
+    b2, m2 = oracle.validate(bad.view(np.uint32), s0, s1, 64, 32)
+    assert b1 == b2 > 0
+    del good
+
+
+def test_validate_prints_reference_messages():
+    code = (
+        "import sys; sys.path.insert(0, %r); import numpy as np, tenstorrentallreduce_amd as t;"
+        "a = t.constant_bf16_vector(2048, 1.0); r = t.constant_bf16_vector(2048, 4.0);"
+        "t.validate_result_vector(r, a, a, 512, 1, 4, True);"
+        "w = t.constant_bf16_vector(2048, 5.0); t.validate_result_vector(w, a, a, 512, 0, 4, True)" % ROOT)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True).stdout
+    assert out.startswith("All values match!\n")
+    assert "Mismatch at index 0:\n  Expected: 4\n  Actual  : 5\n" in out
+    assert "Total matches: 0" in out and "Max error: 1.000000" in out and "Mismatch blocks: 0 " in out
+
+
+def test_allred_helper_hpp_compiles_and_runs(tmp_path):
+    """A reference-style host program against the source-compatible header."""
+    prog = tmp_path / "p.cpp"
+    prog.write_text(r'''
+#include "allred_helper.hpp"
+#include <cstdio>
+int main() {
+    uint32_t dirs = 0;
+    int p = get_comm_partner_recdub_2D(0, 0, true, 1, dirs, 8);
+    uint32_t blocks[2] = {0, 0};
+    get_swing_block_comm_indexes(1, 1, blocks, false, 8, 64);
+    std::vector<uint32_t> a(256, 0x3f803f80u), r(256, 0x40803f80u | 0x00004080u);
+    for (auto& x : r) x = 0x40804080u;
+    validate_result_vector(r, a, a, 256, 0, 4);
+    std::printf("%d %u %u %u %d\n", p, dirs, blocks[0], blocks[1], highest_power_of_two(6));
+    return 0;
+}
+''')
+    exe = tmp_path / "p"
+    lib_dir = os.path.dirname(_lib.LIB_PATH)
+    subprocess.run(["g++", "-std=c++17", f"-I{ROOT}/include", str(prog), "-o", str(exe), f"-L{lib_dir}", "-lallred",
+                    f"-Wl,-rpath,{lib_dir}", "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    assert out[0] == "All values match!"
+    p, dirs, b0, b1, hp = out[1].split()
+    assert (int(p), int(dirs), int(hp)) == (1, 1, 4)
+    assert int(b0) | (int(b1) << 32) == t.get_swing_block_comm_indexes(1, 1, 0, False, 8, 64)
