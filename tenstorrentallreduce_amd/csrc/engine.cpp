@@ -310,16 +310,19 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     HIPCK(hipEventCreate(&e2));
     HIPCK(hipEventCreate(&e3));
     // warm-up on a scratch copy (first-launch code-object load stays out of the timing)
-    HIPCK(hipMemcpy2DAsync(d_scratch, stride * 2, h_in, bytes, bytes, N, hipMemcpyHostToDevice, s));
+    for (int r = 0; r < N; ++r)
+        HIPCK(hipMemcpyAsync(d_scratch + (size_t)r * stride, h_in + (size_t)r * n, bytes, hipMemcpyHostToDevice, s));
     if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, stride, d_ws, s));
     HIPCK(hipStreamSynchronize(s));
     // timed: H2D | allreduce | D2H
     HIPCK(hipEventRecord(e0, s));
-    HIPCK(hipMemcpy2DAsync(d_ranks, stride * 2, h_in, bytes, bytes, N, hipMemcpyHostToDevice, s));
+    for (int r = 0; r < N; ++r)  // each rank's bucket is its own host buffer: one H2D per rank
+        HIPCK(hipMemcpyAsync(d_ranks + (size_t)r * stride, h_in + (size_t)r * n, bytes, hipMemcpyHostToDevice, s));
     HIPCK(hipEventRecord(e1, s));
     if (a->run_kernel) ST(allred_plan_execute(plan, d_ranks, stride, d_ws, s));
     HIPCK(hipEventRecord(e2, s));
-    HIPCK(hipMemcpy2DAsync(h_out, bytes, d_ranks, stride * 2, bytes, N, hipMemcpyDeviceToHost, s));
+    for (int r = 0; r < N; ++r)
+        HIPCK(hipMemcpyAsync(h_out + (size_t)r * n, d_ranks + (size_t)r * stride, bytes, hipMemcpyDeviceToHost, s));
     HIPCK(hipEventRecord(e3, s));
     HIPCK(hipStreamSynchronize(s));
     HIPCK(hipEventElapsedTime(&ms, e1, e2));
