@@ -242,11 +242,11 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ rank
 // fetched with ds_bpermute, and rounds to bf16.  U consecutive chunks per
 // lane keep each rank's 128-byte lines in flight together.
 // ---------------------------------------------------------------------------
-template <int P>
+template <int P, int U>
 __global__ __launch_bounds__(kBlock) void k_butterfly(uint16_t* __restrict__ ranks, uint64_t stride, uint64_t n_vec,
                                                       const int16_t* __restrict__ partner, int steps) {
     constexpr int Q = 64 / P;  // rank groups per wave
-    constexpr int U = 8;       // chunks per lane per iteration
+                               // U: chunks per lane per iteration (1 for small buckets: latency)
     const int lane = threadIdx.x & 63;
     const int x = lane % P;
     const int q = lane / P;
@@ -281,6 +281,104 @@ __global__ __launch_bounds__(kBlock) void k_butterfly(uint16_t* __restrict__ ran
             const uint64_t v = base + (uint64_t)q * U + u;
             if (v < n_vec) row[v] = val[u];
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LO pass for 64 ranks staged through LDS: a tile of 256 elements of all 64
+// ranks comes in with global_load_lds (1 KiB contiguous per wave-instruction),
+// each lane x then holds rank x's columns (transposed LDS reads), runs the
+// butterfly across lanes with ds_bpermute, writes back, and the rows leave
+// with 1 KiB contiguous stores.  Row x's column c lives in 16-byte slot
+// c ^ (x & 31) (swizzle applied on the global side, so global_load_lds's
+// linear destination stays legal) — the 64 lanes' transposed reads of one
+// column are then bank-conflict free.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_butterfly_lds64(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                            const int16_t* __restrict__ partner, int steps) {
+    constexpr int TV = 32;
+    __shared__ __attribute__((aligned(16))) uint4 tile[64 * TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const uint64_t v0 = (uint64_t)blockIdx.x * TV;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int r = 16 * w + 2 * k + h;
+        const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (r & 31));
+        __builtin_amdgcn_global_load_lds((global_u32*)src, (lds_u32*)&tile[(16 * w + 2 * k) * TV], 16, 0, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // lane = rank x; wave w owns columns 8w .. 8w+7
+    const int x = lane;
+    uint4 val[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) val[j] = tile[x * TV + ((8 * w + j) ^ (x & 31))];
+    for (int k = 0; k < steps; ++k) {
+        const int src = (int)partner[k * 64 + x] * 4;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint4 o;
+            o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)val[j].x);
+            o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)val[j].y);
+            o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)val[j].z);
+            o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)val[j].w);
+            val[j] = add8(val[j], o);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[x * TV + ((8 * w + j) ^ (x & 31))] = val[j];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int r = 16 * w + 2 * k + h;
+        st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (r & 31)),
+              tile[(16 * w + 2 * k + h) * TV + l32]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// mem_2D one-pass through LDS: tile of 256 elements of all P ranks (32 KiB at
+// P = 64); thread t owns dword t of the tile row and accumulates the P copies
+// in fp32 in the reference order (owner's block first, then ranks 0..P-1),
+// rounds once, and the result row is stored to every rank (1 KiB per
+// wave-instruction).  128 threads: 2 waves.
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, uint64_t stride, uint64_t block_vec) {
+    constexpr int TV = 32;                      // 16-byte vectors per rank row
+    constexpr int RPW = P / 2;                  // rank rows staged per wave
+    __shared__ __attribute__((aligned(16))) uint4 tile[P * TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const uint64_t v0 = (uint64_t)blockIdx.x * TV;
+#pragma unroll
+    for (int k = 0; k < RPW / 2; ++k) {
+        const int r = RPW * w + 2 * k + h;
+        const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + v0 + l32;
+        __builtin_amdgcn_global_load_lds((global_u32*)src, (lds_u32*)&tile[(RPW * w + 2 * k) * TV], 16, 0, 2);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int own = (int)(v0 / block_vec);
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(tile);
+    const int d = threadIdx.x;                   // dword column 0..127
+    uint32_t y = t32[own * TV * 4 + d];
+    float a0 = lo_f(y), a1 = hi_f(y);
+    for (int r = 0; r < P; ++r) {
+        if (r == own) continue;
+        y = t32[r * TV * 4 + d];
+        a0 += lo_f(y);
+        a1 += hi_f(y);
+    }
+    __syncthreads();
+    reinterpret_cast<uint32_t*>(tile)[d] = pack_rne(a0, a1);
+    __syncthreads();
+    const uint4 res = tile[l32];
+#pragma unroll 4
+    for (int k = 0; k < RPW / 2; ++k) {
+        const int r = RPW * w + 2 * k + h;
+        st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + l32, res);
     }
 }
 
@@ -458,23 +556,34 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
                      void* stream) {
     if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
+    hipStream_t st = (hipStream_t)stream;
+    if (total == 64 && nv % 32 == 0 && nv >= 32 * 256) {  // >= 256 tiles: the LDS-staged form pays
+        hipLaunchKernelGGL(k_butterfly_lds64, dim3((unsigned)(nv / 32)), dim3(kBlock), 0, st, ranks, stride, d_partner,
+                           steps);
+        return last_error();
+    }
     const int Q = 64 / total;
-    uint64_t waves = (nv + (uint64_t)Q * 8 - 1) / ((uint64_t)Q * 8);
+    const bool small = nv < (uint64_t)Q * 8 * 1024;   // fewer than 1024 waves at U = 8: go wide instead
+    const int U = small ? 1 : 8;
+    uint64_t waves = (nv + (uint64_t)Q * U - 1) / ((uint64_t)Q * U);
     uint64_t blocks = (waves + 3) / 4;
     if (blocks < 1) blocks = 1;
     if (blocks > 256 * 16) blocks = 256 * 16;
     const dim3 grid((unsigned)blocks), blk(kBlock);
-    hipStream_t st = (hipStream_t)stream;
+#define TSA_BFLY(PP)                                                                                          \
+    if (small) hipLaunchKernelGGL((k_butterfly<PP, 1>), grid, blk, 0, st, ranks, stride, nv, d_partner, steps); \
+    else hipLaunchKernelGGL((k_butterfly<PP, 8>), grid, blk, 0, st, ranks, stride, nv, d_partner, steps);
     switch (total) {
         case 1: return ALLRED_OK;  // one rank: nothing to reduce
-        case 2: hipLaunchKernelGGL(k_butterfly<2>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
-        case 4: hipLaunchKernelGGL(k_butterfly<4>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
-        case 8: hipLaunchKernelGGL(k_butterfly<8>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
-        case 16: hipLaunchKernelGGL(k_butterfly<16>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
-        case 32: hipLaunchKernelGGL(k_butterfly<32>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
-        case 64: hipLaunchKernelGGL(k_butterfly<64>, grid, blk, 0, st, ranks, stride, nv, d_partner, steps); break;
+        case 2: TSA_BFLY(2) break;
+        case 4: TSA_BFLY(4) break;
+        case 8: TSA_BFLY(8) break;
+        case 16: TSA_BFLY(16) break;
+        case 32: TSA_BFLY(32) break;
+        case 64: TSA_BFLY(64) break;
         default: return ALLRED_ERR_UNSUPPORTED;
     }
+#undef TSA_BFLY
     return last_error();
 }
 
@@ -549,6 +658,19 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream) {
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
+    const uint64_t bv = nv / total;
+    if (bv % 32 == 0 && total >= 4) {
+        const dim3 grid((unsigned)(nv / 32)), blk(128);
+        hipStream_t st = (hipStream_t)stream;
+        switch (total) {
+            case 4: hipLaunchKernelGGL(k_mem_lds<4>, grid, blk, 0, st, ranks, stride, bv); return last_error();
+            case 8: hipLaunchKernelGGL(k_mem_lds<8>, grid, blk, 0, st, ranks, stride, bv); return last_error();
+            case 16: hipLaunchKernelGGL(k_mem_lds<16>, grid, blk, 0, st, ranks, stride, bv); return last_error();
+            case 32: hipLaunchKernelGGL(k_mem_lds<32>, grid, blk, 0, st, ranks, stride, bv); return last_error();
+            case 64: hipLaunchKernelGGL(k_mem_lds<64>, grid, blk, 0, st, ranks, stride, bv); return last_error();
+            default: break;
+        }
+    }
     hipLaunchKernelGGL(k_mem<true>, dim3(grid_for(nv)), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride,
                        total, nv, nv / total, nullptr);
     return last_error();

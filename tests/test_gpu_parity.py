@@ -123,6 +123,22 @@ def test_plan_bit_exact_vs_oracle(grid, algo, variant, exec_mode):
     assert (got == np.stack(want)).all()
 
 
+@pytest.mark.parametrize("variant", ["bo", "lo", "mem"])
+@pytest.mark.parametrize("algo", [t.SWING, t.RECDUB])
+@pytest.mark.parametrize("grid", [(2, 4), (4, 16), (8, 64)])
+def test_fused_lds_forms_bit_exact(grid, algo, variant):
+    """Sizes that take the LDS-staged fused kernels (k_tree_lds, k_butterfly_lds64,
+    k_mem_lds: blocks of whole 256-element tiles, >= 256 tiles for LO)."""
+    side, total = grid
+    n = 256 * total * 8 if total >= 8 else 256 * 64 * 8
+    ranks = rand_ranks(total, n, seed=3 * total + algo)
+    got = run_plan(algo, {"bo": t.BO, "lo": t.LO, "mem": t.MEM}[variant], side, total, ranks, t.EXEC_FUSED,
+                   stride=t.preferred_rank_stride(n))
+    want = [r.copy() for r in ranks]
+    oracle.allreduce(variant, algo, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
 @pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
 def test_plan_padded_stride(exec_mode):
     side, total, n = 8, 64, 64 * 8 * 3
