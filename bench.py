@@ -258,14 +258,20 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     torch.cuda.synchronize()
     local_ms = e0.elapsed_time(e1) / args.steps
 
-    # flat xGMI Swing BO on a large bucket (config 4 regime) and config 3 (RecDub, 640 kB)
+    # flat xGMI allreduces (BASELINE configs 3/4 regimes): 2D Swing BO on a 256 MiB bucket with
+    # every link in use (link-spreading channels) and on one link (the plain schedule), 2D RecDub
+    # BO on 640 kB, and the hierarchical step with its partial spread over all links
     extras = {}
     if args.extras:
-        for name, algo, nbytes, reps in (("config4_swing_bo_256MiB", t.SWING, 256 << 20, 5),
-                                         ("config3_recdub_bo_640kB", t.RECDUB, ELEMS * 2, 50)):
+        arms = [("config4_swing_bo_256MiB_all_links", t.SWING, 256 << 20, 5, 0, 1),
+                ("config4_swing_bo_256MiB_one_link", t.SWING, 256 << 20, 3, 1, 1),
+                ("config3_recdub_bo_640kB", t.RECDUB, ELEMS * 2, 50, 0, 1),
+                ("hierarchical_all_links", t.SWING, ELEMS * 2, 50, world - 1, RANKS)]
+        for name, algo, nbytes, reps, chans, local in arms:
             n = nbytes // 2
-            d2 = t.dist_desc(algo, t.BO, side, total, n)
-            b2 = torch.zeros(n, dtype=torch.int16, device=dev)
+            d2 = t.dist_desc(algo, t.BO, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
+                             channels=chans)
+            b2 = torch.zeros((local, n), dtype=torch.int16, device=dev)
             w2 = torch.empty(t.dist_workspace_bytes(d2), dtype=torch.uint8, device=dev)
             for _ in range(2):
                 t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream)
@@ -281,7 +287,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
             sec = m.item() * 1e-3
             busbw = 2 * (world - 1) / world * nbytes / sec / 1e9  # nccl-tests convention
             extras[name] = {"ms": round(m.item(), 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
-                            "busbw_GBps": round(busbw, 3),
+                            "busbw_GBps": round(busbw, 3), "channels": chans,
                             "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
             del b2, w2
     comm.close()

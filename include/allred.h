@@ -222,7 +222,8 @@ typedef struct {
     int32_t local_ranks;
     int32_t local_side;
     int32_t local_algo;
-    int32_t chunks;         /* pipeline chunks per step (>=1)                   */
+    int32_t channels;       /* link-spreading channels: 0 = auto (all 2^S-1 links for
+                               buckets >= 1 MiB on XOR grids), 1 = the plain schedule */
 } allred_dist_desc;
 /* Scratch device bytes the call needs (recv staging + hierarchical partial). */
 size_t allred_dist_workspace_bytes(const allred_dist_desc* desc);

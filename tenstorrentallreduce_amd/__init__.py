@@ -221,8 +221,8 @@ class Comm:
 
 
 def dist_desc(algo: int, variant: int, side: int, total: int, elems: int, local_ranks: int = 1,
-              local_side: int = 1, local_algo: int = SWING, chunks: int = 1) -> DistDesc:
-    return DistDesc(algo, variant, side, total, elems, local_ranks, local_side, local_algo, chunks)
+              local_side: int = 1, local_algo: int = SWING, channels: int = 0) -> DistDesc:
+    return DistDesc(algo, variant, side, total, elems, local_ranks, local_side, local_algo, channels)
 
 
 def dist_workspace_bytes(desc: DistDesc) -> int:

@@ -88,7 +88,7 @@ class DistDesc(C.Structure):
     _fields_ = [
         ("algo", C.c_int32), ("variant", C.c_int32), ("side_length", C.c_int32), ("total_nodes", C.c_int32),
         ("elems", C.c_uint64), ("local_ranks", C.c_int32), ("local_side", C.c_int32), ("local_algo", C.c_int32),
-        ("chunks", C.c_int32),
+        ("channels", C.c_int32),
     ]
 
 

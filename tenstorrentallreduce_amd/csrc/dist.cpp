@@ -37,56 +37,158 @@ struct Seg {
     size_t off, len;  // elements
 };
 
-struct Step {
+// One exchange with one peer inside a step.
+struct Exch {
     int peer = -1;
     std::vector<Seg> send;          // from the bucket
     std::vector<Seg> recv;          // into staging (add) or into the bucket (AG)
     bool recv_to_bucket = false;
     bool add = false;               // bucket[recv segs] += staging[recv segs]
+    size_t blk = 0;                 // block size of this exchange's channel (elements)
+    size_t base = 0;                // channel slice start (elements)
 };
 
-void runs(uint64_t mask, int total, size_t blk, std::vector<Seg>* out) {
+// A step = the exchanges of every channel, issued as one RCCL group.
+struct Step {
+    std::vector<Exch> ex;
+};
+
+void runs(uint64_t mask, int total, size_t blk, size_t base, std::vector<Seg>* out) {
     int b = 0;
     while (b < total) {
         if (!((mask >> b) & 1ull)) { ++b; continue; }
         int e = b;
         while (e < total && ((mask >> e) & 1ull)) ++e;
-        out->push_back(Seg{(size_t)b * blk, (size_t)(e - b) * blk});
+        out->push_back(Seg{base + (size_t)b * blk, (size_t)(e - b) * blk});
         b = e;
     }
 }
 
-// the rank's program; chunks > 1 splits every step's segments into pieces so
-// the add of one piece can overlap the transfer of the next
-std::vector<Step> program(const allred_schedule& s, int rank, int variant, size_t n) {
+// ---- link-spreading channels ---------------------------------------------
+// On the GPU grids (2,2), (2,4), (4,8) both schedules are XOR schedules:
+// partner_k(x) = x ^ m_k with (m_0 .. m_{S-1}) a basis of GF(2)^S (Swing 4x2:
+// 1, 4, 3; RecDub 4x2: 1, 4, 2).  Channel c relabels rank r as x = a^c * r in
+// GF(2^S) (a = the primitive element), so its step-k partner is
+// r ^ a^-c * m_k: at every step the 2^S - 1 channels use 2^S - 1 distinct
+// masks = every peer of the full xGMI mesh at once.  Each channel
+// allreduces its own slice of the bucket with the unmodified schedule in the
+// relabeled ids, so every slice is an exact BO (or LO) allreduce.
+int gf_mul(int a, int b, int S) {
+    static const int poly[4] = {0, 0x3, 0x7, 0xb};  // x+1 (trivial), x^2+x+1, x^3+x+1
+    int r = 0;
+    for (int i = 0; i < S; ++i)
+        if ((b >> i) & 1) r ^= a << i;
+    for (int i = 2 * S - 2; i >= S; --i)
+        if ((r >> i) & 1) r ^= poly[S] << (i - S);
+    return r;
+}
+
+int gf_pow_alpha(int c, int S) {  // a^c, a = x (= 2) for S >= 2; a = 1 for S = 1
+    int v = 1;
+    for (int i = 0; i < c; ++i) v = S >= 2 ? gf_mul(v, 2, S) : 1;
+    return v;
+}
+
+// channels usable on this schedule: 2^S - 1 for an XOR schedule with S <= 3, else 1
+int max_channels(const allred_schedule& s) {
+    if (s.steps < 1 || s.steps > 3) return 1;
+    for (int k = 0; k < s.steps; ++k) {
+        const int m = s.partner[0][k];
+        for (int x = 0; x < s.total; ++x)
+            if (s.partner[x][k] != (x ^ m)) return 1;
+    }
+    return (1 << s.steps) - 1;
+}
+
+int channels_for(const allred_schedule& s, int requested, size_t n) {
+    const int cmax = max_channels(s);
+    if (requested > 0) return requested < cmax ? requested : cmax;
+    // auto: spread buckets of >= 1 MiB over every link; small ones stay latency-optimal
+    return n * 2 >= (1u << 20) ? cmax : 1;
+}
+
+// slice of channel c: whole units of 8*N elements (keeps blocks 16-byte aligned)
+void slice_of(size_t n, int N, int C, int c, size_t* base, size_t* len) {
+    const size_t unit = 8 * (size_t)N, units = n / unit;
+    const size_t q = units / C, r = units % C;
+    const size_t before = q * c + (c < (int)r ? c : r);
+    *base = before * unit;
+    *len = (q + (c < (int)r ? 1 : 0)) * unit;
+}
+
+// the rank's program (LO: n need only be a multiple of 8; one channel)
+std::vector<Step> program(const allred_schedule& s, int rank, int variant, size_t n, int C) {
+    const int N = s.total, S = s.steps;
+    if (variant == ALLRED_LO && n % (8 * (size_t)N)) C = 1;
     std::vector<Step> prog;
-    const int N = s.total;
-    const size_t blk = n / (size_t)N;
+    auto chan = [&](int c, size_t* base, size_t* len) {
+        if (C == 1) { *base = 0; *len = n; return; }
+        slice_of(n, N, C, c, base, len);
+    };
+    auto id_of = [&](int c, int r) { return C == 1 ? r : gf_mul(gf_pow_alpha(c, S), r, S); };
+    // peer of real rank r on channel c at step k: the real rank whose relabel is partner(x, k)
+    auto peer_of = [&](int c, int r, int k) {
+        const int x = id_of(c, r);
+        const int px = s.partner[x][k];
+        if (C == 1) return px;
+        for (int q = 0; q < N; ++q)
+            if (id_of(c, q) == px) return q;
+        return -1;
+    };
     if (variant == ALLRED_LO) {
-        for (int k = 0; k < s.steps; ++k) {
+        for (int k = 0; k < S; ++k) {
             Step st;
-            st.peer = s.partner[rank][k];
-            st.send.push_back(Seg{0, n});
-            st.recv.push_back(Seg{0, n});
-            st.add = true;
+            for (int c = 0; c < C; ++c) {
+                size_t base, len;
+                chan(c, &base, &len);
+                if (!len) continue;
+                Exch e;
+                e.peer = peer_of(c, rank, k);
+                e.send.push_back(Seg{base, len});
+                e.recv.push_back(Seg{base, len});
+                e.add = true;
+                e.base = base;
+                e.blk = len;
+                st.ex.push_back(e);
+            }
             prog.push_back(st);
         }
         return prog;
     }
-    for (int k = 0; k < s.steps; ++k) {
+    for (int k = 0; k < S; ++k) {  // reduce-scatter
         Step st;
-        st.peer = s.partner[rank][k];
-        runs(s.send[rank][k], N, blk, &st.send);
-        runs(s.recv[rank][k], N, blk, &st.recv);
-        st.add = true;
+        for (int c = 0; c < C; ++c) {
+            size_t base, len;
+            chan(c, &base, &len);
+            if (!len) continue;
+            const int x = id_of(c, rank);
+            Exch e;
+            e.peer = peer_of(c, rank, k);
+            e.blk = len / (size_t)N;
+            e.base = base;
+            runs(s.send[x][k], N, e.blk, base, &e.send);
+            runs(s.recv[x][k], N, e.blk, base, &e.recv);
+            e.add = true;
+            st.ex.push_back(e);
+        }
         prog.push_back(st);
     }
-    for (int k = s.steps - 1; k >= 0; --k) {
+    for (int k = S - 1; k >= 0; --k) {  // all-gather
         Step st;
-        st.peer = s.partner[rank][k];
-        runs(s.recv[rank][k], N, blk, &st.send);
-        runs(s.send[rank][k], N, blk, &st.recv);
-        st.recv_to_bucket = true;
+        for (int c = 0; c < C; ++c) {
+            size_t base, len;
+            chan(c, &base, &len);
+            if (!len) continue;
+            const int x = id_of(c, rank);
+            Exch e;
+            e.peer = peer_of(c, rank, k);
+            e.blk = len / (size_t)N;
+            e.base = base;
+            runs(s.recv[x][k], N, e.blk, base, &e.send);
+            runs(s.send[x][k], N, e.blk, base, &e.recv);
+            e.recv_to_bucket = true;
+            st.ex.push_back(e);
+        }
         prog.push_back(st);
     }
     return prog;
@@ -218,27 +320,31 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
         st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
-    const std::vector<Step> prog = program(s, c->rank, d->variant, n);
-    const size_t blk = n / (size_t)s.total;
+    const int C = channels_for(s, d->channels, n);
+    const std::vector<Step> prog = program(s, c->rank, d->variant, n, C);
     for (const Step& step : prog) {
         if (ncclGroupStart() != ncclSuccess) return ALLRED_ERR_RCCL;
-        for (const Seg& g : step.send)
-            if (ncclSend(bucket + g.off, g.len * 2, ncclUint8, step.peer, c->comm, hs) != ncclSuccess)
-                return ALLRED_ERR_RCCL;
-        for (const Seg& g : step.recv)
-            if (ncclRecv((step.recv_to_bucket ? bucket : staging) + g.off, g.len * 2, ncclUint8, step.peer, c->comm,
-                         hs) != ncclSuccess)
-                return ALLRED_ERR_RCCL;
+        for (const Exch& e : step.ex) {
+            for (const Seg& g : e.send)
+                if (ncclSend(bucket + g.off, g.len * 2, ncclUint8, e.peer, c->comm, hs) != ncclSuccess)
+                    return ALLRED_ERR_RCCL;
+            for (const Seg& g : e.recv)
+                if (ncclRecv((e.recv_to_bucket ? bucket : staging) + g.off, g.len * 2, ncclUint8, e.peer, c->comm,
+                             hs) != ncclSuccess)
+                    return ALLRED_ERR_RCCL;
+        }
         if (ncclGroupEnd() != ncclSuccess) return ALLRED_ERR_RCCL;
-        if (step.add) {
+        for (const Exch& e : step.ex) {
+            if (!e.add) continue;
             if (d->variant == ALLRED_LO) {
-                st = launch_bf16_add(bucket, staging, n, stream);
+                st = launch_bf16_add(bucket + e.base, staging + e.base, e.blk, stream);
             } else {
                 uint8_t blocks[ALLRED_MAX_NODES];
                 int nb = 0;
-                for (const Seg& g : step.recv)
-                    for (size_t b = g.off / blk; b < (g.off + g.len) / blk; ++b) blocks[nb++] = (uint8_t)b;
-                st = launch_bf16_add_blocks(bucket, staging, blocks, nb, blk, stream);
+                for (const Seg& g : e.recv)
+                    for (size_t b = (g.off - e.base) / e.blk; b < (g.off - e.base + g.len) / e.blk; ++b)
+                        blocks[nb++] = (uint8_t)b;
+                st = launch_bf16_add_blocks(bucket + e.base, staging + e.base, blocks, nb, e.blk, stream);
             }
             if (st != ALLRED_OK) return st;
         }
@@ -263,18 +369,22 @@ int allred_dist_allreduce_host(const allred_dist_desc* d, int rank, uint16_t* bu
         bucket = scratch + n;
         host_tree_reduce(buf, n, n, ls, bucket);
     }
-    const std::vector<Step> prog = program(s, rank, d->variant, n);
+    const int C = channels_for(s, d->channels, n);
+    const std::vector<Step> prog = program(s, rank, d->variant, n, C);
     std::vector<allred_seg> snd, rcv;
     for (const Step& step : prog) {
-        snd.clear();
-        rcv.clear();
-        for (const Seg& g : step.send) snd.push_back(allred_seg{bucket + g.off, g.len * 2});
-        for (const Seg& g : step.recv)
-            rcv.push_back(allred_seg{(step.recv_to_bucket ? bucket : scratch) + g.off, g.len * 2});
-        if (exchange(ctx, step.peer, (int)snd.size(), snd.data(), (int)rcv.size(), rcv.data()) != 0)
-            return ALLRED_ERR_TRANSPORT;
-        if (step.add)
-            for (const Seg& g : step.recv) host_add(bucket + g.off, scratch + g.off, g.len);
+        for (const Exch& e : step.ex) {  // channels in order: every channel is a perfect matching
+            snd.clear();
+            rcv.clear();
+            for (const Seg& g : e.send) snd.push_back(allred_seg{bucket + g.off, g.len * 2});
+            for (const Seg& g : e.recv)
+                rcv.push_back(allred_seg{(e.recv_to_bucket ? bucket : scratch) + g.off, g.len * 2});
+            if (exchange(ctx, e.peer, (int)snd.size(), snd.data(), (int)rcv.size(), rcv.data()) != 0)
+                return ALLRED_ERR_TRANSPORT;
+        }
+        for (const Exch& e : step.ex)
+            if (e.add)
+                for (const Seg& g : e.recv) host_add(bucket + g.off, scratch + g.off, g.len);
     }
     if (d->local_ranks > 1)
         for (int r = 0; r < d->local_ranks; ++r) std::memcpy(buf + (size_t)r * n, bucket, n * 2);

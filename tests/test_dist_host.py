@@ -34,10 +34,38 @@ def gloo_exchange(peer, sends, recvs):
 
 def cases(world):
     out = []
+    cmax = world - 1  # 2^S - 1 link-spreading channels on the XOR grids
     for variant in ("bo", "lo"):
         for algo in (0, 1):
-            out.append((variant, algo, 1))     # flat: one bucket per process
-            out.append((variant, algo, 4))     # hierarchical: 4 virtual ranks per process (2x2 local grid)
+            out.append((variant, algo, 1, 1))      # flat: one bucket per process
+            out.append((variant, algo, 4, 1))      # hierarchical: 4 virtual ranks per process (2x2 local grid)
+            if cmax > 1:
+                out.append((variant, algo, 1, cmax))   # every link at every step
+                out.append((variant, algo, 4, 2))      # fewer channels than links
+    return out
+
+
+def gf_mul(a, b, S):
+    poly = {1: 0x3, 2: 0x7, 3: 0xB}[S]
+    r = 0
+    for i in range(S):
+        if (b >> i) & 1:
+            r ^= a << i
+    for i in range(2 * S - 2, S - 1, -1):
+        if (r >> i) & 1:
+            r ^= poly << (i - S)
+    return r
+
+
+def slices(n, N, C):
+    unit = 8 * N
+    units = n // unit
+    q, rem = divmod(units, C)
+    out, start = [], 0
+    for c in range(C):
+        ln = (q + (1 if c < rem else 0)) * unit
+        out.append((start, ln))
+        start += ln
     return out
 
 
@@ -46,20 +74,41 @@ def inputs(world, local, n, seed):
     return [[rng.integers(0x3F80, 0x42C8, n).astype(np.uint16) for _ in range(local)] for _ in range(world)]
 
 
-def expected(variant, algo, world, local, data):
+def channel_allreduce(oracle, variant, algo, side, total, vecs, C):
+    """C link-spreading channels: channel c allreduces its slice with rank r
+    relabelled as a^c * r in GF(2^S) (a = x), i.e. the plain schedule run on
+    the permuted ranks."""
+    if C == 1:
+        oracle.allreduce(variant, algo, side, vecs, total)
+        return
+    S = total.bit_length() - 1
+    for c, (b0, ln) in enumerate(slices(vecs[0].size, total, C)):
+        a = 1
+        for _ in range(c):
+            a = gf_mul(a, 2, S)
+        lab = [gf_mul(a, r, S) for r in range(total)]
+        base = [None] * total
+        for r in range(total):
+            base[lab[r]] = vecs[r][b0:b0 + ln].copy()
+        oracle.allreduce(variant, algo, side, base, total)
+        for r in range(total):
+            vecs[r][b0:b0 + ln] = base[lab[r]]
+
+
+def expected(variant, algo, world, local, data, C):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     side, total = GRIDS[world]
     if local == 1:
         ranks = [d[0].copy() for d in data]
-        oracle.allreduce(variant, algo, side, ranks, total)
+        channel_allreduce(oracle, variant, algo, side, total, ranks, C)
         return [[r] for r in ranks]
     partials = []
     for d in data:  # on-GPU tree of local rank 0 (== LO value of local rank 0), Swing 2x2
         loc = [x.copy() for x in d]
         oracle.allreduce("lo", 1, 2, loc, local)
         partials.append(loc[0])
-    oracle.allreduce(variant, algo, side, partials, total)
+    channel_allreduce(oracle, variant, algo, side, total, partials, C)
     return [[p.copy() for _ in range(local)] for p in partials]
 
 
@@ -71,16 +120,16 @@ def worker(rank, world, port, q):
     side, total = GRIDS[world]
     n = 8 * total * 16
     fails = []
-    for ci, (variant, algo, local) in enumerate(cases(world)):
+    for ci, (variant, algo, local, chans) in enumerate(cases(world)):
         data = inputs(world, local, n, seed=100 * world + ci)
         buf = np.concatenate(data[rank]).astype(np.uint16)
         scratch = np.zeros(2 * n, dtype=np.uint16)
         desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, side, total, n, local_ranks=local, local_side=2,
-                           local_algo=t.SWING)
+                           local_algo=t.SWING, channels=chans)
         t.dist_allreduce_host(desc, rank, buf, scratch, gloo_exchange)
-        want = np.concatenate(expected(variant, algo, world, local, data)[rank])
+        want = np.concatenate(expected(variant, algo, world, local, data, chans)[rank])
         if not np.array_equal(buf, want):
-            fails.append((variant, algo, local, int((buf != want).sum())))
+            fails.append((variant, algo, local, chans, int((buf != want).sum())))
     dist.barrier()
     dist.destroy_process_group()
     q.put((rank, fails))
