@@ -266,10 +266,14 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         arms = [("config4_swing_bo_256MiB_all_links", t.SWING, 256 << 20, 5, 0, 1),
                 ("config4_swing_bo_256MiB_one_link", t.SWING, 256 << 20, 3, 1, 1),
                 ("config3_recdub_bo_640kB", t.RECDUB, ELEMS * 2, 50, 0, 1),
-                ("hierarchical_all_links", t.SWING, ELEMS * 2, 50, world - 1, RANKS)]
+                ("hierarchical_all_links", t.SWING, ELEMS * 2, 50, world - 1, RANKS),
+                ("hierarchical_lo_partial", t.SWING, ELEMS * 2, 50, 1, RANKS)]
+        # BASELINE config 5: flat 2D Swing LO, 2 kB .. 128 kB per GPU (latency regime)
+        arms += [(f"config5_swing_lo_{kb}kB", t.SWING, kb << 10, 100, 1, 1) for kb in (2, 8, 32, 128)]
         for name, algo, nbytes, reps, chans, local in arms:
             n = nbytes // 2
-            d2 = t.dist_desc(algo, t.BO, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
+            variant = t.LO if ("_lo_" in name) else t.BO
+            d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
                              channels=chans)
             b2 = torch.zeros((local, n), dtype=torch.int16, device=dev)
             w2 = torch.empty(t.dist_workspace_bytes(d2), dtype=torch.uint8, device=dev)
@@ -286,6 +290,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
             dist.all_reduce(m, op=dist.ReduceOp.MAX)
             sec = m.item() * 1e-3
             busbw = 2 * (world - 1) / world * nbytes / sec / 1e9  # nccl-tests convention
+            if variant == t.LO:
+                busbw = nbytes / sec / 1e9  # LO moves the whole bucket every step: report algbw
             extras[name] = {"ms": round(m.item(), 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
                             "busbw_GBps": round(busbw, 3), "channels": chans,
                             "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}

@@ -196,9 +196,10 @@ __global__ __launch_bounds__(kBlock) void k_tree(uint16_t* __restrict__ ranks, u
 // partials meet in LDS rows 0-3 (free once every wave has read its leaves).
 // 16.0 us vs 17.3 us for k_tree at 64 x 640 kB (= a 42+42 MB copy's time).
 // ---------------------------------------------------------------------------
-template <int P>
+template <int P, bool WRITE_ALL>
 __global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                     const uint8_t* __restrict__ order, uint64_t block_vec) {
+                                                     const uint8_t* __restrict__ order, uint64_t block_vec,
+                                                     uint16_t* __restrict__ out) {
     constexpr int TV = 32;          // 16-byte vectors per rank row of a tile
     constexpr int RPW = P / 4;      // ranks staged (and tree leaves reduced) per wave
     constexpr int LPL = RPW / 2;    // leaves per lane
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ rank
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    const uint8_t* ord = order + (v0 / block_vec) * ALLRED_MAX_NODES + RPW * w + LPL * h;
+    const uint8_t* ord = order + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * h;
     uint4 x[LPL];
 #pragma unroll
     for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
@@ -227,6 +228,10 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ rank
     if (h == 0) tile[w * TV + c] = part;
     __syncthreads();
     const uint4 res = add8(add8(tile[0 * TV + c], tile[1 * TV + c]), add8(tile[2 * TV + c], tile[3 * TV + c]));
+    if (!WRITE_ALL) {  // hierarchical partial: one row out
+        if (w == 0 && h == 0) st_nt(reinterpret_cast<uint4*>(out) + v0 + c, res);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < RPW / 2; ++k) {
         const int r = RPW * w + 2 * k + h;
@@ -383,11 +388,14 @@ __global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, u
 }
 
 // ranks[r] = src for every r (all-gather of a reduced vector)
+// grid.y picks a group of up to 8 ranks, so even a 640 kB vector fills the chip
 __global__ __launch_bounds__(kBlock) void k_broadcast(uint16_t* __restrict__ ranks, uint64_t stride, int total,
                                                       const uint4* __restrict__ src, uint64_t n_vec) {
+    const int r0 = blockIdx.y * 8;
+    const int r1 = r0 + 8 < total ? r0 + 8 : total;
     for (uint64_t v = gtid(); v < n_vec; v += gthreads()) {
         const uint4 x = src[v];
-        for (int r = 0; r < total; ++r) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v, x);
+        for (int r = r0; r < r1; ++r) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v, x);
     }
 }
 
@@ -484,13 +492,15 @@ int last_error() { return hip_status((int)hipGetLastError()); }
 template <bool WRITE_ALL>
 int tree_dispatch(uint16_t* ranks, uint64_t stride, uint64_t n_vec, int total, const uint8_t* order,
                   uint64_t block_vec, uint16_t* out, hipStream_t st) {
-    if (WRITE_ALL && total >= 8 && block_vec && block_vec % 32 == 0 && !tree_force_registers()) {
+    // LDS-staged form: whole 32-vector tiles inside one block (any tile when block_vec == 0)
+    if (total >= 8 && n_vec % 32 == 0 && (block_vec == 0 || block_vec % 32 == 0) && (block_vec || !WRITE_ALL) &&
+        !tree_force_registers()) {
         const dim3 grid((unsigned)(n_vec / 32)), blk(kBlock);
         switch (total) {
-            case 8: hipLaunchKernelGGL(k_tree_lds<8>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
-            case 16: hipLaunchKernelGGL(k_tree_lds<16>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
-            case 32: hipLaunchKernelGGL(k_tree_lds<32>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
-            case 64: hipLaunchKernelGGL(k_tree_lds<64>, grid, blk, 0, st, ranks, stride, order, block_vec); break;
+            case 8: hipLaunchKernelGGL((k_tree_lds<8, WRITE_ALL>), grid, blk, 0, st, ranks, stride, order, block_vec, out); break;
+            case 16: hipLaunchKernelGGL((k_tree_lds<16, WRITE_ALL>), grid, blk, 0, st, ranks, stride, order, block_vec, out); break;
+            case 32: hipLaunchKernelGGL((k_tree_lds<32, WRITE_ALL>), grid, blk, 0, st, ranks, stride, order, block_vec, out); break;
+            case 64: hipLaunchKernelGGL((k_tree_lds<64, WRITE_ALL>), grid, blk, 0, st, ranks, stride, order, block_vec, out); break;
             default: return ALLRED_ERR_UNSUPPORTED;
         }
         return last_error();
@@ -597,7 +607,8 @@ int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tot
 int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src, void* stream) {
     if (n % 8 || stride % 8 || !aligned16(ranks) || !aligned16(src)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
-    hipLaunchKernelGGL(k_broadcast, dim3(grid_all(nv)), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, total,
+    hipLaunchKernelGGL(k_broadcast, dim3(grid_all(nv), (total + 7) / 8), dim3(kBlock), 0, (hipStream_t)stream, ranks,
+                       stride, total,
                        reinterpret_cast<const uint4*>(src), nv);
     return last_error();
 }
