@@ -328,6 +328,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
 
 
 def main():
+    # RCCL and gloo print banners on stdout; keep stdout for the one JSON line
+    real_stdout = os.dup(1)
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -359,7 +362,8 @@ def main():
             except Exception as e:  # reported, never silently dropped
                 out["cpu_baseline"] = {"value": None, "error": repr(e)}
     if out is not None:
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(real_stdout, (json.dumps(out) + "\n").encode())
 
 
 if __name__ == "__main__":
