@@ -38,6 +38,9 @@ extern "C" {
 /* argv[1] "is swing version?" (allred_helper.cpp:205-208) */
 #define ALLRED_RECDUB 0
 #define ALLRED_SWING 1
+/* the 1D schedules of the reference's prototypes (side_length ignored) */
+#define ALLRED_RECDUB_1D 2  /* scratch_work/recdub_multicore_1D/recdub_multicore_1D.cpp:165-175 */
+#define ALLRED_SWING_1D 3   /* scratch_work/all_red_swing_1D/all_red_swing_1D.cpp:32-36 */
 /* which reference program: allred_BO_2D with arg 8 = 1 / = 0, allred_mem_2D */
 #define ALLRED_BO 0
 #define ALLRED_LO 1
@@ -73,12 +76,17 @@ void allred_get_recdub_block_comm_indexes(int node, int step, uint32_t* blocks /
                                           uint32_t* step_directions);     /* allred_BO_2D.cpp:242 */
 /* NUM_TILES normalisation, allred_helper.cpp:224-234 */
 int allred_normalize_tiles(int tiles, int total_nodes, int large_buffer);
+/* 1D partners of the reference's 8-core prototypes */
+int allred_get_comm_partner_swing_1d(int node, int step, int num_nodes);          /* all_red_swing_1D.cpp:32 */
+int allred_get_comm_partner_recdub_1d(int node, int step, uint32_t* step_directions); /* recdub_multicore_1D.cpp:165 */
 
 /* Whole per-rank schedule, as the per-core loop of allred_BO_2D.cpp:75-212
  * builds it into runtime args: partners (args 14+2i), send masks (22+2s+2i),
  * recv masks (22+4s+2i / compute args 6+2i), direction bits (arg 11).
  * Grids: side in {1,2,4,8}, total a power of two <= 64 (side*side for the
- * reference's square grids; (2,2), (2,4), (4,8) for 2/4/8 GPUs).
+ * reference's square grids; (2,2), (2,4), (4,8) for 2/4/8 GPUs).  algo may
+ * also be ALLRED_RECDUB_1D / ALLRED_SWING_1D (any power-of-two total; the
+ * block masks then come from the same "reachable at later steps" rule).
  * Also validates the schedule (partners in range and symmetric, send ==
  * partner's recv, reduce-scatter leaves block r at rank r, every rank's
  * contributor sets disjoint at each merge) and derives tree_order[x]: the

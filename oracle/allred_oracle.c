@@ -171,8 +171,29 @@ int or_partner_recdub(int node, int step, int side, int* sends_se) {
     return horizontal ? row * side + q : q * side + col;
 }
 
+/* scratch_work/all_red_swing_1D/all_red_swing_1D.cpp:32-36 */
+int or_partner_swing_1d(int node, int step, int total) {
+    int d = swing_rho(step);
+    int p = (node % 2 == 0) ? node + d : node - d;
+    return (p + total) % total;
+}
+
+/* scratch_work/recdub_multicore_1D/recdub_multicore_1D.cpp:165-175 */
+int or_partner_recdub_1d(int node, int step, int* sends_se) {
+    int depth = 1 << step;
+    int se = (node % (2 * depth)) < depth;
+    if (sends_se) *sends_se = se;
+    return se ? node + depth : node - depth;
+}
+
+/* algo: 0 RecDub 2D, 1 Swing 2D, 2 RecDub 1D, 3 Swing 1D */
 static int partner_of(int swing, int node, int step, int side, int total) {
-    return swing ? or_partner_swing(node, step, side, total) : or_partner_recdub(node, step, side, NULL);
+    switch (swing) {
+        case 1: return or_partner_swing(node, step, side, total);
+        case 2: return or_partner_recdub_1d(node, step, NULL);
+        case 3: return or_partner_swing_1d(node, step, total);
+        default: return or_partner_recdub(node, step, side, NULL);
+    }
 }
 
 /* allred_BO_2D.cpp:220-270 restated without recursion: the set of nodes
@@ -196,6 +217,7 @@ static uint64_t reach(int swing, int node, int from_step, int side, int total, i
 
 int or_build_schedule(int swing, int side, int total, or_schedule* s) {
     memset(s, 0, sizeof(*s));
+    if (swing >= 2) side = total;
     s->swing = swing; s->side = side; s->total = total; s->steps = or_steps(total);
     if (total < 1 || total > OR_MAX_NODES || side < 1 || (total & (total - 1))) return -1;
     int bad = 0;
@@ -203,14 +225,18 @@ int or_build_schedule(int swing, int side, int total, or_schedule* s) {
         uint32_t dirs = 0;
         for (int k = 0; k < s->steps; ++k) {
             int se = 0;
-            int p = swing ? or_partner_swing(r, k, side, total) : or_partner_recdub(r, k, side, &se);
+            int p = swing == 1 ? or_partner_swing(r, k, side, total)
+                    : swing == 2 ? or_partner_recdub_1d(r, k, &se)
+                    : swing == 3 ? or_partner_swing_1d(r, k, total)
+                                 : or_partner_recdub(r, k, side, &se);
             s->partner[r][k] = p;
-            if (!swing && se) dirs |= 1u << k;
+            if ((swing == 0 || swing == 2) && se) dirs |= 1u << k;
             if (p < 0 || p >= total) { bad = 1; continue; }
             s->send[r][k] = reach(swing, p, k + 1, side, total, s->steps, &bad);
             s->recv[r][k] = reach(swing, r, k + 1, side, total, s->steps, &bad);
         }
-        s->dirs[r] = swing ? (or_step_directions(r % side, r / side) & ((1u << s->steps) - 1u)) : dirs;
+        s->dirs[r] = swing == 1 ? (or_step_directions(r % side, r / side) & ((1u << s->steps) - 1u))
+                     : swing == 3 ? 0u : dirs;
     }
     return bad ? -1 : 0;
 }

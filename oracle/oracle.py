@@ -54,7 +54,7 @@ _o.or_validate.restype = C.c_long
 _o.or_validate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_float, C.c_uint32, C.c_int,
                            C.POINTER(C.c_float)]
 
-SWING, RECDUB = 1, 0
+SWING, RECDUB, RECDUB_1D, SWING_1D = 1, 0, 2, 3
 
 
 def bf16_add(a: int, b: int) -> int:

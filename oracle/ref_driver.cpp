@@ -7,6 +7,8 @@
 //       get_comm_partner_recdub_2D, get_comm_partner_swing_2D
 //   /root/reference/allred_BO_2D/allred_BO_2D.cpp:217-270
 //       get_swing_block_comm_indexes, get_recdub_block_comm_indexes
+//   /root/reference/scratch_work/all_red_swing_1D/all_red_swing_1D.cpp:32-36
+//       get_comm_partner (the 1D Swing partner of the 8-core prototype)
 // Those line ranges need only <cmath>/<cstdint>; nothing of tt-metal is
 // stubbed.  This file restates the per-core schedule loop of
 // allred_BO_2D.cpp:75-202 (which lives inside the tt-metal `main` and cannot
@@ -94,6 +96,17 @@ int main() {
     for (int y = 0; y < 8; ++y)
         for (int x = 0; x < 8; ++x)
             std::printf("%s[%d, %d, %u]", (x || y) ? ", " : "", x, y, get_step_directions(x, y));
+    std::printf("],\n \"swing_1d\": [");
+    for (int nn = 2; nn <= 64; nn *= 2) {
+        int st = (int)std::log2((double)nn);
+        std::printf("%s{\"total\": %d, \"partners\": [", nn > 2 ? ", " : "", nn);
+        for (int node = 0; node < nn; ++node) {
+            std::printf("%s[", node ? ", " : "");
+            for (int k = 0; k < st; ++k) std::printf("%s%d", k ? ", " : "", ref1d::get_comm_partner(node, k, nn));
+            std::printf("]");
+        }
+        std::printf("]}");
+    }
     std::printf("],\n \"grids\": [\n");
     for (int g = 0; g < ng; ++g) {
         emit(true, grids[g].side, grids[g].total, false);

@@ -17,11 +17,12 @@ from typing import Callable, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, RECDUB, SWING, AllredError, Args, DistDesc,  # noqa: F401
+from ._lib import (BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, RECDUB, RECDUB_1D, SWING, SWING_1D, AllredError, Args, DistDesc,  # noqa: F401
                    PlanDesc, Report, Schedule, Seg, check, lib)
 
 __all__ = [
-    "BO", "LO", "MEM", "SWING", "RECDUB", "EXEC_STEPS", "EXEC_FUSED", "AllredError", "schedule",
+    "BO", "LO", "MEM", "SWING", "RECDUB", "SWING_1D", "RECDUB_1D", "get_comm_partner_swing_1D",
+    "get_comm_partner_recdub_1D", "EXEC_STEPS", "EXEC_FUSED", "AllredError", "schedule",
     "highest_power_of_two", "get_step_directions", "get_comm_partner_swing_2D", "get_comm_partner_recdub_2D",
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
@@ -64,6 +65,16 @@ def get_recdub_block_comm_indexes(node, step, blocks, horizontal_step, side, tot
     lib.allred_get_recdub_block_comm_indexes(node, step, b, int(bool(horizontal_step)), side, total, depth,
                                              C.byref(d))
     return b[0] | (b[1] << 32), d.value
+
+
+def get_comm_partner_swing_1D(node: int, step: int, num_nodes: int) -> int:  # all_red_swing_1D.cpp:32
+    return lib.allred_get_comm_partner_swing_1d(node, step, num_nodes)
+
+
+def get_comm_partner_recdub_1D(node: int, step: int, step_directions: int = 0):  # recdub_multicore_1D.cpp:165
+    d = C.c_uint32(step_directions)
+    p = lib.allred_get_comm_partner_recdub_1d(node, step, C.byref(d))
+    return p, d.value
 
 
 def normalize_tiles(tiles: int, total_nodes: int, large_buffer: bool) -> int:  # allred_helper.cpp:224

@@ -32,7 +32,7 @@ lib = C.CDLL(LIB_PATH)
 
 # ---- status / enums (allred.h) ------------------------------------------
 OK, ERR_ARG, ERR_SCHEDULE, ERR_HIP, ERR_RCCL, ERR_NOMEM, ERR_UNSUPPORTED, ERR_TRANSPORT = 0, -1, -2, -3, -4, -5, -6, -7
-RECDUB, SWING = 0, 1
+RECDUB, SWING, RECDUB_1D, SWING_1D = 0, 1, 2, 3
 BO, LO, MEM = 0, 1, 2
 EXEC_STEPS, EXEC_FUSED = 0, 1
 MAX_NODES, MAX_STEPS = 64, 6
@@ -114,6 +114,8 @@ SIGNATURES = [
     ("allred_get_recdub_block_comm_indexes", None,
      [C.c_int, C.c_int, C.POINTER(C.c_uint32), C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint32)]),
     ("allred_normalize_tiles", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("allred_get_comm_partner_swing_1d", C.c_int, [C.c_int, C.c_int, C.c_int]),
+    ("allred_get_comm_partner_recdub_1d", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint32)]),
     ("allred_schedule_build", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(Schedule)]),
     ("allred_random_bf16_vector", None, [C.c_size_t, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_constant_bf16_vector", None, [C.c_size_t, C.c_float, _P]),

@@ -149,6 +149,20 @@ int allred_normalize_tiles(int tiles, int total_nodes, int large_buffer) {
     return p;
 }
 
+int allred_get_comm_partner_swing_1d(int node, int step, int num_nodes) {
+    const int d = swing_distance(step);
+    const int p = (node % 2 == 0) ? node + d : node - d;
+    return ((p % num_nodes) + num_nodes) % num_nodes;
+}
+
+int allred_get_comm_partner_recdub_1d(int node, int step, uint32_t* step_directions) {
+    const int depth = 1 << step;
+    const bool lower_half = (node % (2 * depth)) < depth;
+    if (step_directions)
+        *step_directions = lower_half ? (*step_directions | (1u << step)) : (*step_directions & ~(1u << step));
+    return lower_half ? node + depth : node - depth;
+}
+
 int allred_schedule_build(int algo, int side_length, int total_nodes, allred_schedule* out) {
     return build_schedule(algo, side_length, total_nodes, out, nullptr);
 }
@@ -158,13 +172,17 @@ int allred_schedule_build(int algo, int side_length, int total_nodes, allred_sch
 namespace tsa {
 
 int build_schedule(int algo, int side, int total, allred_schedule* out, std::string* why) {
+    // (side is adjusted for the 1D algorithms)
     auto fail = [&](const std::string& m) {
         if (why) *why = m;
         return ALLRED_ERR_SCHEDULE;
     };
     if (!out) return ALLRED_ERR_ARG;
     std::memset(out, 0, sizeof(*out));
-    if (side < 1 || side > 8 || (side & (side - 1)) || total < 1 || total > ALLRED_MAX_NODES ||
+    const bool one_d = algo == ALLRED_RECDUB_1D || algo == ALLRED_SWING_1D;
+    if (algo < ALLRED_RECDUB || algo > ALLRED_SWING_1D) return fail("unknown algorithm");
+    if (one_d) side = total;
+    if (side < 1 || (!one_d && (side > 8 || (side & (side - 1)))) || total < 1 || total > ALLRED_MAX_NODES ||
         (total & (total - 1)) || total % side)
         return fail("grid must be side in {1,2,4,8}, total a power of two <= 64 and a multiple of side");
     const int steps = steps_for(total);
@@ -173,7 +191,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
     out->total = total;
     out->steps = steps;
 
-    // per-core loop of allred_BO_2D.cpp:95-198
+    // per-core loop of allred_BO_2D.cpp:95-198 (2D) / the 1D prototypes' partner loops
     uint32_t step_directions = 0, dummy = 0;
     for (int r = 0; r < total; ++r) {
         bool h = true;
@@ -183,13 +201,18 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
             int p;
             if (algo == ALLRED_SWING) {
                 p = allred_get_comm_partner_swing_2d(r, k, h, side, total);
-            } else {
+            } else if (algo == ALLRED_RECDUB) {
                 p = allred_get_comm_partner_recdub_2d(r, k, h, depth, &step_directions, side);
+            } else if (algo == ALLRED_SWING_1D) {
+                p = allred_get_comm_partner_swing_1d(r, k, total);
+            } else {
+                p = allred_get_comm_partner_recdub_1d(r, k, &step_directions);
             }
             if (p < 0 || p >= total)
                 return fail("rank " + std::to_string(r) + " step " + std::to_string(k) +
                             ": partner " + std::to_string(p) + " outside the grid");
             out->partner[r][k] = p;
+            if (one_d) continue;  // masks below, from the full partner table
             set_bit(snd, p);
             set_bit(rcv, r);
             if (algo == ALLRED_SWING) {
@@ -207,7 +230,26 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
         }
         const uint32_t keep = steps >= 32 ? ~0u : ((1u << steps) - 1u);
         out->dirs[r] = (algo == ALLRED_SWING ? allred_get_step_directions(r % side, r / side)
-                                             : step_directions) & keep;
+                        : algo == ALLRED_SWING_1D ? 0u : step_directions) & keep;
+    }
+    if (one_d) {
+        // the 2D recursion's rule on the 1D partner table: a rank's step-k
+        // blocks are every rank reachable from it at steps > k
+        auto reach = [&](int node, int from) {
+            uint64_t set = 1ull << node;
+            for (int k2 = from; k2 < steps; ++k2) {
+                uint64_t add = 0;
+                for (int v = 0; v < total; ++v)
+                    if ((set >> v) & 1ull) add |= 1ull << out->partner[v][k2];
+                set |= add;
+            }
+            return set;
+        };
+        for (int r = 0; r < total; ++r)
+            for (int k = 0; k < steps; ++k) {
+                out->send[r][k] = reach(out->partner[r][k], k + 1);
+                out->recv[r][k] = reach(r, k + 1);
+            }
     }
 
     // ---- validation: the schedule must be an allreduce ----

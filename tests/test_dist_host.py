@@ -36,6 +36,8 @@ def cases(world):
     out = []
     cmax = world - 1  # 2^S - 1 link-spreading channels on the XOR grids
     for variant in ("bo", "lo"):
+        out.append((variant, 3, 1, 1))             # 1D Swing prototype schedule (no channels: not XOR)
+        out.append((variant, 2, 1, cmax))          # 1D RecDub (an XOR schedule)
         for algo in (0, 1):
             out.append((variant, algo, 1, 1))      # flat: one bucket per process
             out.append((variant, algo, 4, 1))      # hierarchical: 4 virtual ranks per process (2x2 local grid)
@@ -78,6 +80,8 @@ def channel_allreduce(oracle, variant, algo, side, total, vecs, C):
     """C link-spreading channels: channel c allreduces its slice with rank r
     relabelled as a^c * r in GF(2^S) (a = x), i.e. the plain schedule run on
     the permuted ranks."""
+    if algo >= 2:
+        side = 1
     if C == 1:
         oracle.allreduce(variant, algo, side, vecs, total)
         return
@@ -124,7 +128,8 @@ def worker(rank, world, port, q):
         data = inputs(world, local, n, seed=100 * world + ci)
         buf = np.concatenate(data[rank]).astype(np.uint16)
         scratch = np.zeros(2 * n, dtype=np.uint16)
-        desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, side, total, n, local_ranks=local, local_side=2,
+        desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
+                           local_ranks=local, local_side=2,
                            local_algo=t.SWING, channels=chans)
         t.dist_allreduce_host(desc, rank, buf, scratch, gloo_exchange)
         want = np.concatenate(expected(variant, algo, world, local, data, chans)[rank])

@@ -110,6 +110,20 @@ GRIDS = [(1, 1), (2, 2), (2, 4), (4, 8), (4, 16), (8, 64)]
 
 
 @pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
+@pytest.mark.parametrize("variant", ["bo", "lo"])
+@pytest.mark.parametrize("algo", [t.SWING_1D, t.RECDUB_1D])
+@pytest.mark.parametrize("total", [2, 8, 16, 64])
+def test_plan_1d_schedules_bit_exact(total, algo, variant, exec_mode):
+    """The prototypes' 1D Swing / RecDub schedules (scratch_work/*_1D) as plans."""
+    n = 8 * total * 32
+    ranks = rand_ranks(total, n, seed=total + 17 * algo)
+    got = run_plan(algo, {"bo": t.BO, "lo": t.LO}[variant], 1, total, ranks, exec_mode)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce(variant, algo, 1, want, total)
+    assert (got == np.stack(want)).all()
+
+
+@pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
 @pytest.mark.parametrize("variant", ["bo", "lo", "mem"])
 @pytest.mark.parametrize("algo", [t.SWING, t.RECDUB])
 @pytest.mark.parametrize("grid", GRIDS)
