@@ -251,6 +251,28 @@ typedef int (*allred_exchange_fn)(void* ctx, int peer, int nsend, const allred_s
 int allred_dist_allreduce_host(const allred_dist_desc* desc, int rank, uint16_t* buf,
                                uint16_t* scratch, allred_exchange_fn exchange, void* ctx);
 
+/* ======================================================================
+ * Peer-mapped one-shot allreduce across GPUs: the shared-memory variant
+ * (allred_mem_2D.cpp:4-165) with every GPU's window IPC-mapped into every
+ * peer (one process per GPU).  Result semantics = allred_mem_2D: block b is
+ * owner b's copy + every other rank's copy in rank order, fp32, one rounding.
+ *   create -> handle (128 bytes, exchange with every rank) -> connect(all
+ *   handles in rank order) -> allreduce ... -> destroy.
+ * Barriers spin with a bound; allred_peer_status() reports bit 0 = timeout.
+ * ==================================================================== */
+#define ALLRED_PEER_HANDLE_BYTES 128
+typedef struct allred_peer allred_peer;
+int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, allred_peer** out);
+int allred_peer_handle(allred_peer* peer, uint8_t* handle /*[ALLRED_PEER_HANDLE_BYTES]*/);
+int allred_peer_connect(allred_peer* peer, const uint8_t* all_handles /*[nranks * 128]*/);
+/* elems % (8 * nranks) == 0, elems <= max_elems.  local_ranks > 1: `buf`
+ * holds local_ranks virtual ranks (stride elems) reduced on-GPU first
+ * (tree of local rank 0) into `workspace` (elems * 2 bytes), then broadcast. */
+int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
+                          int local_algo, void* workspace, void* stream);
+int allred_peer_status(allred_peer* peer, uint32_t* status);
+int allred_peer_destroy(allred_peer* peer);
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,7 +27,7 @@ __all__ = [
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
     "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
-    "dist_allreduce_host", "dist_workspace_bytes",
+    "dist_allreduce_host", "dist_workspace_bytes", "Peer",
 ]
 
 
@@ -269,3 +269,40 @@ def dist_allreduce_host(desc: DistDesc, rank: int, buf: np.ndarray, scratch: np.
     assert buf.dtype == np.uint16 and scratch.dtype == np.uint16
     check(lib.allred_dist_allreduce_host(C.byref(desc), rank, buf.ctypes.data, scratch.ctypes.data, cb, None),
           "dist_allreduce_host")
+
+
+class Peer:
+    """Peer-mapped one-shot allreduce across GPUs (allred_peer_*): the
+    allred_mem_2D variant over xGMI.  handle() -> exchange with every rank ->
+    connect(list of all ranks' handles in rank order)."""
+
+    def __init__(self, nranks: int, rank: int, device: int, max_elems: int):
+        h = C.c_void_p()
+        check(lib.allred_peer_create(nranks, rank, device, max_elems, C.byref(h)), "peer_create")
+        self._h = h
+        self.nranks, self.rank = nranks, rank
+
+    def handle(self) -> bytes:
+        buf = (C.c_uint8 * _lib.PEER_HANDLE_BYTES)()
+        check(lib.allred_peer_handle(self._h, buf), "peer_handle")
+        return bytes(buf)
+
+    def connect(self, handles: Sequence[bytes]) -> None:
+        blob = b"".join(handles)
+        arr = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
+        check(lib.allred_peer_connect(self._h, arr), "peer_connect")
+
+    def allreduce(self, buf_ptr: int, elems: int, stream=None, local_ranks: int = 1, local_side: int = 1,
+                  local_algo: int = SWING, workspace_ptr: int | None = None) -> None:
+        check(lib.allred_peer_allreduce(self._h, buf_ptr, elems, local_ranks, local_side, local_algo, workspace_ptr,
+                                        _stream_ptr(stream)), "peer_allreduce")
+
+    def status(self) -> int:
+        v = C.c_uint32(0)
+        check(lib.allred_peer_status(self._h, C.byref(v)), "peer_status")
+        return v.value
+
+    def close(self):
+        if self._h:
+            lib.allred_peer_destroy(self._h)
+            self._h = None

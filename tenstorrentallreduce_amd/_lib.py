@@ -139,7 +139,14 @@ SIGNATURES = [
     ("allred_dist_workspace_bytes", C.c_size_t, [C.POINTER(DistDesc)]),
     ("allred_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_dist_allreduce_host", C.c_int, [C.POINTER(DistDesc), C.c_int, _u16p, _u16p, EXCHANGE_FN, _P]),
+    ("allred_peer_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, C.POINTER(_P)]),
+    ("allred_peer_handle", C.c_int, [_P, _P]),
+    ("allred_peer_connect", C.c_int, [_P, _P]),
+    ("allred_peer_allreduce", C.c_int, [_P, _u16p, C.c_uint64, C.c_int, C.c_int, C.c_int, _P, _P]),
+    ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    ("allred_peer_destroy", C.c_int, [_P]),
 ]
+PEER_HANDLE_BYTES = 128
 
 for _name, _res, _args in SIGNATURES:
     _f = getattr(lib, _name)  # AttributeError here = the library lacks a declared symbol

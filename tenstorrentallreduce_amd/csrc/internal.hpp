@@ -61,6 +61,9 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
                       void* stream);
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream);
 
+int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
+                          size_t n, uint32_t epoch, uint32_t* status, void* stream);
+
 int hip_status(int hip_err);  // maps hipError_t -> ALLRED_*
 
 }  // namespace tsa

@@ -475,6 +475,81 @@ __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, ui
     }
 }
 
+// ---------------------------------------------------------------------------
+// Peer-mapped one-shot allreduce (allred_mem_2D over xGMI): every GPU's window
+// is IPC-mapped into every other GPU; flags live in fine-grained (uncached)
+// memory and are written / polled with system-scope atomics.  Kernel
+// boundaries on the stream carry the system-scope release / acquire of the
+// window bytes (HIP dispatch packets fence at system scope).
+// ---------------------------------------------------------------------------
+struct PeerPtrs {
+    uint16_t* win[ALLRED_MAX_NODES];     // window of rank q (this parity), as mapped here
+    uint32_t* flags[ALLRED_MAX_NODES];   // flag array of rank q, as mapped here
+};
+
+// one workgroup: tell every peer "rank `me` reached `epoch`", then wait for all.
+// Bounded: on timeout bit 0 of *status is set and the kernel returns.
+__global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, uint32_t* status) {
+    const int t = threadIdx.x;
+    if (t < nranks)
+        __hip_atomic_store(pp.flags[t] + me, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < nranks) {
+        uint32_t* mine = pp.flags[me] + t;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
+            if (spin > (1ull << 24)) {  // ~ seconds: a peer never arrived
+                atomicOr(status, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+}
+
+// reduce-scatter: block `me` of every window, owner first then ranks in order
+// (fp32, one rounding), written to my window (peers gather it) and to my bucket
+__global__ __launch_bounds__(kBlock) void k_peer_rs(PeerPtrs pp, int nranks, int me, uint16_t* __restrict__ bucket,
+                                                    uint64_t blk_vec) {
+    const uint64_t off = (uint64_t)me * blk_vec;
+    for (uint64_t v = gtid(); v < blk_vec; v += gthreads()) {
+        const uint4 s = ld_nt(reinterpret_cast<const uint4*>(pp.win[me]) + off + v);
+        float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
+        uint4 y[ALLRED_MAX_NODES > 8 ? 8 : ALLRED_MAX_NODES];
+        for (int q0 = 0; q0 < nranks; q0 += 8) {
+            const int q1 = q0 + 8 < nranks ? q0 + 8 : nranks;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (q0 + i < q1 && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(pp.win[q0 + i]) + off + v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (q0 + i >= q1 || q0 + i == me) continue;
+                a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+            }
+        }
+        uint4 o;
+        o.x = pack_rne(a[0], a[1]);
+        o.y = pack_rne(a[2], a[3]);
+        o.z = pack_rne(a[4], a[5]);
+        o.w = pack_rne(a[6], a[7]);
+        st_nt(reinterpret_cast<uint4*>(pp.win[me]) + off + v, o);
+        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, o);
+    }
+}
+
+// all-gather: bucket[block q] = window_q[block q] for every q != me (grid.y = q)
+__global__ __launch_bounds__(kBlock) void k_peer_ag(PeerPtrs pp, int me, uint16_t* __restrict__ bucket,
+                                                    uint64_t blk_vec) {
+    const int q = blockIdx.y;
+    if (q == me) return;
+    const uint64_t off = (uint64_t)q * blk_vec;
+    for (uint64_t v = gtid(); v < blk_vec; v += gthreads())
+        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + off + v));
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ALLRED_TREE=registers selects the register-only k_tree for the fused BO pass
@@ -525,6 +600,29 @@ int tree_dispatch(uint16_t* ranks, uint64_t stride, uint64_t n_vec, int total, c
 }
 
 }  // namespace
+
+int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
+                          size_t n, uint32_t epoch, uint32_t* status, void* stream) {
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    PeerPtrs pp{};
+    for (int q = 0; q < nranks; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+    }
+    const uint64_t nv = n / 8, bv = nv / nranks;
+    // 1. my bucket -> my window (the bytes peers will read)
+    hipLaunchKernelGGL(k_copy_ranks, dim3(grid_all(nv), 1), dim3(kBlock), 0, st, bucket, 0, wins[me], 0, nv);
+    // 2. everyone's window is written
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, st, pp, nranks, me, epoch, status);
+    // 3. reduce my block from every window
+    hipLaunchKernelGGL(k_peer_rs, dim3(grid_all(bv)), dim3(kBlock), 0, st, pp, nranks, me, bucket, bv);
+    // 4. every block is reduced
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, st, pp, nranks, me, epoch + 1, status);
+    // 5. gather the other blocks
+    hipLaunchKernelGGL(k_peer_ag, dim3(grid_all(bv), nranks), dim3(kBlock), 0, st, pp, me, bucket, bv);
+    return last_error();
+}
 
 int hip_status(int e) { return e == (int)hipSuccess ? ALLRED_OK : ALLRED_ERR_HIP; }
 

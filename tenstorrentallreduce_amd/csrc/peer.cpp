@@ -1,0 +1,151 @@
+// peer.cpp — the shared-memory variant (allred_mem_2D) across GPUs: a
+// peer-mapped one-shot reduce-scatter / all-gather over xGMI.
+//
+// The reference's SM variant (allred_mem_2D.cpp:4-165, kernels/*) has every
+// core dump its vector into one shared DRAM buffer, reduce its own block from
+// all copies, write it to the destination buffer and read everything back,
+// with node-to-node semaphore barriers between the phases (sync_nodes,
+// kernels/dataflow_kernel.cpp:201-230).  Across MI355X GPUs the "shared
+// buffer" is each GPU's window, IPC-mapped into every peer; the phases are
+//   copy bucket -> own window | barrier | reduce own block from all windows |
+//   barrier | gather every other block from its owner's window,
+// so every transfer reads from all N-1 peers at once (all xGMI links busy).
+// Barrier flags live in uncached device memory and are written / polled with
+// system-scope atomics (bounded spins set a status bit instead of hanging).
+// Windows are double-buffered by call parity: call k+2 can only overwrite a
+// window after every peer passed call k+1's first barrier, i.e. finished
+// reading call k's windows.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "internal.hpp"
+
+using namespace tsa;
+
+struct allred_peer {
+    int nranks = 0, rank = 0, device = 0;
+    uint64_t max_elems = 0;
+    uint16_t* win = nullptr;        // own window: 2 parities x max_elems
+    uint32_t* flags = nullptr;      // own flag array [64] (uncached)
+    uint32_t* status = nullptr;     // device status word
+    bool flags_uncached = false;
+    uint16_t* peer_win[ALLRED_MAX_NODES] = {};
+    uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
+    bool opened[ALLRED_MAX_NODES] = {};
+    uint32_t calls = 0;
+    bool connected = false;
+};
+
+extern "C" {
+
+int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, allred_peer** out) {
+    if (!out || nranks < 1 || nranks > ALLRED_MAX_NODES || rank < 0 || rank >= nranks || max_elems == 0)
+        return ALLRED_ERR_ARG;
+    *out = nullptr;
+    if (device >= 0 && hipSetDevice(device) != hipSuccess) return ALLRED_ERR_HIP;
+    auto* p = new allred_peer();
+    p->nranks = nranks;
+    p->rank = rank;
+    (void)hipGetDevice(&p->device);
+    p->max_elems = (max_elems + 63) / 64 * 64;
+    if (hipMalloc((void**)&p->win, 2 * p->max_elems * 2) != hipSuccess) { delete p; return ALLRED_ERR_NOMEM; }
+    if (hipExtMallocWithFlags((void**)&p->flags, 256, hipDeviceMallocUncached) == hipSuccess) {
+        p->flags_uncached = true;
+    } else if (hipMalloc((void**)&p->flags, 256) != hipSuccess) {
+        (void)hipFree(p->win);
+        delete p;
+        return ALLRED_ERR_NOMEM;
+    }
+    if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, 256) != hipSuccess ||
+        hipMemset(p->status, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p->win);
+        (void)hipFree(p->flags);
+        delete p;
+        return ALLRED_ERR_HIP;
+    }
+    *out = p;
+    return ALLRED_OK;
+}
+
+int allred_peer_handle(allred_peer* p, uint8_t* out) {
+    if (!p || !out) return ALLRED_ERR_ARG;
+    hipIpcMemHandle_t hw, hf;
+    if (hipIpcGetMemHandle(&hw, p->win) != hipSuccess) return ALLRED_ERR_HIP;
+    if (hipIpcGetMemHandle(&hf, p->flags) != hipSuccess) return ALLRED_ERR_HIP;
+    static_assert(sizeof(hipIpcMemHandle_t) * 2 <= ALLRED_PEER_HANDLE_BYTES, "handle size");
+    std::memset(out, 0, ALLRED_PEER_HANDLE_BYTES);
+    std::memcpy(out, &hw, sizeof(hw));
+    std::memcpy(out + ALLRED_PEER_HANDLE_BYTES / 2, &hf, sizeof(hf));
+    return ALLRED_OK;
+}
+
+int allred_peer_connect(allred_peer* p, const uint8_t* all) {
+    if (!p || !all) return ALLRED_ERR_ARG;
+    for (int q = 0; q < p->nranks; ++q) {
+        if (q == p->rank) {
+            p->peer_win[q] = p->win;
+            p->peer_flags[q] = p->flags;
+            continue;
+        }
+        hipIpcMemHandle_t hw, hf;
+        std::memcpy(&hw, all + (size_t)q * ALLRED_PEER_HANDLE_BYTES, sizeof(hw));
+        std::memcpy(&hf, all + (size_t)q * ALLRED_PEER_HANDLE_BYTES + ALLRED_PEER_HANDLE_BYTES / 2, sizeof(hf));
+        void* w = nullptr;
+        void* f = nullptr;
+        if (hipIpcOpenMemHandle(&w, hw, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ALLRED_ERR_HIP;
+        if (hipIpcOpenMemHandle(&f, hf, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ALLRED_ERR_HIP;
+        p->peer_win[q] = static_cast<uint16_t*>(w);
+        p->peer_flags[q] = static_cast<uint32_t*>(f);
+        p->opened[q] = true;
+    }
+    p->connected = true;
+    return ALLRED_OK;
+}
+
+int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
+                          int local_algo, void* workspace, void* stream) {
+    if (!p || !buf || !p->connected) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)elems;
+    if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
+    uint16_t* bucket = buf;
+    int st = ALLRED_OK;
+    if (local_ranks > 1) {
+        if (!workspace) return ALLRED_ERR_ARG;
+        bucket = static_cast<uint16_t*>(workspace);
+        st = allred_tree_reduce(buf, n, n, local_algo, local_side, local_ranks, bucket, stream);
+        if (st != ALLRED_OK) return st;
+    }
+    const size_t parity = p->calls & 1u;
+    uint16_t* wins[ALLRED_MAX_NODES];
+    for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q] + parity * p->max_elems;
+    const uint32_t epoch = 2u * p->calls + 1u;
+    st = launch_peer_allreduce(wins, p->peer_flags, p->nranks, p->rank, bucket, n, epoch, p->status, stream);
+    if (st != ALLRED_OK) return st;
+    ++p->calls;
+    if (local_ranks > 1) st = allred_broadcast(buf, n, n, local_ranks, bucket, stream);
+    return st;
+}
+
+int allred_peer_status(allred_peer* p, uint32_t* out) {
+    if (!p || !out) return ALLRED_ERR_ARG;
+    if (hipMemcpy(out, p->status, 4, hipMemcpyDeviceToHost) != hipSuccess) return ALLRED_ERR_HIP;
+    return ALLRED_OK;
+}
+
+int allred_peer_destroy(allred_peer* p) {
+    if (!p) return ALLRED_OK;
+    (void)hipDeviceSynchronize();
+    for (int q = 0; q < p->nranks; ++q) {
+        if (!p->opened[q]) continue;
+        (void)hipIpcCloseMemHandle(p->peer_win[q]);
+        (void)hipIpcCloseMemHandle(p->peer_flags[q]);
+    }
+    (void)hipFree(p->win);
+    (void)hipFree(p->flags);
+    (void)hipFree(p->status);
+    delete p;
+    return ALLRED_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,101 @@
+"""Peer-mapped one-shot allreduce (allred_peer_*, the mem_2D variant over
+IPC-mapped windows) with 2 and 4 processes sharing ONE MI355X: the same code
+path as across GPUs (IPC handles, uncached flag words, system-scope atomics,
+parity-double-buffered windows), with real cross-process concurrency.
+Results must equal the oracle's mem_2D semantics bit for bit, over several
+consecutive calls (epochs and window parities)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, world, port, q):
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import tenstorrentallreduce_amd as t
+        import oracle
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        n = 8 * world * 64 * 5
+        peer = t.Peer(world, rank, 0, n)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        fails = []
+        for call in range(5):
+            rng = [np.random.default_rng(1000 * call + r) for r in range(world)]
+            data = [g.integers(0x3F80, 0x42C8, n).astype(np.uint16) for g in rng]
+            buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
+            peer.allreduce(buf.data_ptr(), n, torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            want = [d.copy() for d in data]
+            oracle.allreduce("mem", 0, 1, want, world)
+            got = buf.cpu().numpy().view(np.uint16)
+            if not np.array_equal(got, want[rank]):
+                fails.append(("flat", call, int((got != want[rank]).sum())))
+            dist.barrier()
+        # hierarchical: 8 virtual ranks per process (4x2 Swing local grid)
+        local = 8
+        data = [np.random.default_rng(77 + r).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+                for r in range(world)]
+        buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
+        ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
+        peer.allreduce(buf.data_ptr(), n, torch.cuda.current_stream(), local, 4, t.SWING, ws.data_ptr())
+        torch.cuda.synchronize()
+        partials = []
+        for d in data:
+            loc = [x.copy() for x in d]
+            oracle.allreduce("lo", 1, 4, loc, local)   # tree of local rank 0
+            partials.append(loc[0])
+        oracle.allreduce("mem", 0, 1, partials, world)
+        got = buf.cpu().numpy().view(np.uint16)
+        if not all(np.array_equal(got[i], partials[rank]) for i in range(local)):
+            fails.append(("hier", 0, 1))
+        status = peer.status()
+        dist.barrier()
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_peer_one_shot_multi_process_one_gpu(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in procs:
+            results.append(q.get(timeout=240))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails, status in results:
+        assert fails == [], (rank, fails)
+        assert status == 0, (rank, status)
