@@ -212,6 +212,96 @@ def bench_single(args) -> dict:
     return out
 
 
+def timed_max(fn, reps, stream) -> float:
+    """ms per call on `stream`, max over ranks."""
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    dist.barrier()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    m = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return m.item()
+
+
+def peer_arms(rank, world, local_rank, dev, stream, comm, side, total) -> dict:
+    """The mem_2D variant across GPUs (allred_peer_*): one-shot reduce-scatter /
+    all-gather reading every peer's IPC-mapped window at once.  Verified first
+    against the RCCL Swing BO path on small-integer data (every order exact)."""
+    max_elems = (256 << 20) // 2
+    peer, mine = None, None
+    try:
+        peer = t.Peer(world, rank, local_rank, max_elems)
+        mine = peer.handle()
+    except Exception as e:  # every rank must learn of it, or the others block below
+        mine = None
+        print(f"[bench] peer create failed on rank {rank}: {e!r}", file=sys.stderr)
+    handles = [None] * world
+    dist.all_gather_object(handles, mine)
+
+    def agreed(ok: bool) -> bool:
+        v = torch.tensor([int(ok)], dtype=torch.int64)
+        dist.all_reduce(v, op=dist.ReduceOp.MIN)
+        return bool(v.item())
+
+    if not all(h is not None for h in handles):
+        if peer:
+            peer.close()
+        return {"peer_error": "create failed on some rank"}
+    try:
+        peer.connect(handles)
+        ok = True
+    except Exception as e:
+        print(f"[bench] peer connect failed on rank {rank}: {e!r}", file=sys.stderr)
+        ok = False
+    if not agreed(ok):
+        peer.close()
+        return {"peer_error": "connect failed on some rank"}
+    out = {}
+    n = ELEMS
+    g = torch.Generator().manual_seed(5 + rank)
+    vals = torch.randint(0, 8, (n,), generator=g).to(torch.bfloat16).view(torch.int16).to(dev)
+    a, b = vals.clone(), vals.clone()
+    peer.allreduce(a.data_ptr(), n, stream)
+    d = t.dist_desc(t.SWING, t.BO, side, total, n)
+    w = torch.empty(t.dist_workspace_bytes(d), dtype=torch.uint8, device=dev)
+    t.dist_allreduce(comm, d, b.data_ptr(), w.data_ptr(), stream)
+    torch.cuda.synchronize()
+    ok = torch.tensor([int(torch.equal(a, b))], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    out["peer_verified_vs_rccl"] = bool(ok.item())
+    if not agreed(peer.status() & t.PEER_TIMEOUT == 0):
+        out["peer_error"] = "barrier timeout"
+        peer.close()
+        return out
+    arms = [(f"peer_mem_{kb}kB", kb << 10, 200, 1) for kb in (2, 8, 32, 128)]
+    arms += [("peer_mem_640kB", ELEMS * 2, 100, 1), ("peer_mem_256MiB", 256 << 20, 5, 1),
+             ("hierarchical_peer", ELEMS * 2, 50, RANKS)]
+    for name, nbytes, reps, local in arms:
+        n = nbytes // 2
+        buf = torch.zeros((local, n), dtype=torch.int16, device=dev)
+        ws = torch.empty(n, dtype=torch.int16, device=dev)
+        ms = timed_max(lambda: peer.allreduce(buf.data_ptr(), n, stream, local, SIDE, t.SWING, ws.data_ptr()),
+                       reps, stream)
+        sec = ms * 1e-3
+        busbw = 2 * (world - 1) / world * nbytes / sec / 1e9
+        out[name] = {"ms": round(ms, 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
+                     "busbw_GBps": round(busbw, 3), "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
+        del buf, ws
+    st = torch.tensor([peer.status()], dtype=torch.int64)
+    dist.all_reduce(st, op=dist.ReduceOp.MAX)
+    out["peer_status"] = int(st.item())
+    dist.barrier()
+    peer.close()
+    return out
+
+
 def bench_multi(args, rank, world, local_rank) -> dict | None:
     dev = torch.device(f"cuda:{local_rank}")
     torch.cuda.set_device(dev)
@@ -296,6 +386,10 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
                             "busbw_GBps": round(busbw, 3), "channels": chans,
                             "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
             del b2, w2
+        try:
+            extras.update(peer_arms(rank, world, local_rank, dev, stream, comm, side, total))
+        except Exception as e:  # reported, never silently dropped
+            extras["peer_error"] = repr(e)
     comm.close()
     if rank != 0:
         return None

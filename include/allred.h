@@ -258,9 +258,14 @@ int allred_dist_allreduce_host(const allred_dist_desc* desc, int rank, uint16_t*
  * owner b's copy + every other rank's copy in rank order, fp32, one rounding.
  *   create -> handle (128 bytes, exchange with every rank) -> connect(all
  *   handles in rank order) -> allreduce ... -> destroy.
- * Barriers spin with a bound; allred_peer_status() reports bit 0 = timeout.
+ * Barriers spin with a bound; allred_peer_status() reports bit 0 = timeout,
+ * and the WIN/FLAGS_CACHED bits when uncached (fine-grained) device memory
+ * was unavailable and ordinary hipMalloc memory had to be used instead.
  * ==================================================================== */
 #define ALLRED_PEER_HANDLE_BYTES 128
+#define ALLRED_PEER_TIMEOUT 0x1u
+#define ALLRED_PEER_WIN_CACHED 0x100u
+#define ALLRED_PEER_FLAGS_CACHED 0x200u
 typedef struct allred_peer allred_peer;
 int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, allred_peer** out);
 int allred_peer_handle(allred_peer* peer, uint8_t* handle /*[ALLRED_PEER_HANDLE_BYTES]*/);

@@ -271,6 +271,9 @@ def dist_allreduce_host(desc: DistDesc, rank: int, buf: np.ndarray, scratch: np.
           "dist_allreduce_host")
 
 
+PEER_TIMEOUT, PEER_WIN_CACHED, PEER_FLAGS_CACHED = _lib.PEER_TIMEOUT, _lib.PEER_WIN_CACHED, _lib.PEER_FLAGS_CACHED
+
+
 class Peer:
     """Peer-mapped one-shot allreduce across GPUs (allred_peer_*): the
     allred_mem_2D variant over xGMI.  handle() -> exchange with every rank ->

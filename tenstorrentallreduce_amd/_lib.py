@@ -147,6 +147,7 @@ SIGNATURES = [
     ("allred_peer_destroy", C.c_int, [_P]),
 ]
 PEER_HANDLE_BYTES = 128
+PEER_TIMEOUT, PEER_WIN_CACHED, PEER_FLAGS_CACHED = 0x1, 0x100, 0x200   # allred_peer_status bits
 
 for _name, _res, _args in SIGNATURES:
     _f = getattr(lib, _name)  # AttributeError here = the library lacks a declared symbol

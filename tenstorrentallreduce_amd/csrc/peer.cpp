@@ -29,7 +29,7 @@ struct allred_peer {
     uint16_t* win = nullptr;        // own window: 2 parities x max_elems
     uint32_t* flags = nullptr;      // own flag array [64] (uncached)
     uint32_t* status = nullptr;     // device status word
-    bool flags_uncached = false;
+    bool flags_uncached = false, win_uncached = false;
     uint16_t* peer_win[ALLRED_MAX_NODES] = {};
     uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
     bool opened[ALLRED_MAX_NODES] = {};
@@ -49,7 +49,14 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     p->rank = rank;
     (void)hipGetDevice(&p->device);
     p->max_elems = (max_elems + 63) / 64 * 64;
-    if (hipMalloc((void**)&p->win, 2 * p->max_elems * 2) != hipSuccess) { delete p; return ALLRED_ERR_NOMEM; }
+    // windows are uncached too: peers read them over xGMI straight from HBM, so
+    // no write may linger in one of this GPU's eight per-XCD L2s
+    if (hipExtMallocWithFlags((void**)&p->win, 2 * p->max_elems * 2, hipDeviceMallocUncached) == hipSuccess) {
+        p->win_uncached = true;
+    } else if (hipMalloc((void**)&p->win, 2 * p->max_elems * 2) != hipSuccess) {
+        delete p;
+        return ALLRED_ERR_NOMEM;
+    }
     if (hipExtMallocWithFlags((void**)&p->flags, 256, hipDeviceMallocUncached) == hipSuccess) {
         p->flags_uncached = true;
     } else if (hipMalloc((void**)&p->flags, 256) != hipSuccess) {
@@ -130,6 +137,8 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
 int allred_peer_status(allred_peer* p, uint32_t* out) {
     if (!p || !out) return ALLRED_ERR_ARG;
     if (hipMemcpy(out, p->status, 4, hipMemcpyDeviceToHost) != hipSuccess) return ALLRED_ERR_HIP;
+    if (!p->win_uncached) *out |= ALLRED_PEER_WIN_CACHED;
+    if (!p->flags_uncached) *out |= ALLRED_PEER_FLAGS_CACHED;
     return ALLRED_OK;
 }
 
