@@ -280,11 +280,15 @@ def peer_arms(rank, world, local_rank, dev, stream, comm, side, total) -> dict:
         out["peer_error"] = "barrier timeout"
         peer.close()
         return out
-    arms = [(f"peer_mem_{kb}kB", kb << 10, 200, 1) for kb in (2, 8, 32, 128)]
-    arms += [("peer_mem_640kB", ELEMS * 2, 100, 1), ("peer_mem_256MiB", 256 << 20, 5, 1),
-             ("hierarchical_peer", ELEMS * 2, 50, RANKS)]
-    for name, nbytes, reps, local in arms:
+    one, multi = 1 << 40, 0   # one-kernel form / copy-barrier-RS-barrier-AG launches
+    arms = [(f"peer_oneshot_{kb}kB", kb << 10, 200, 1, one) for kb in (2, 8, 32, 128)]
+    arms += [("peer_oneshot_640kB", ELEMS * 2, 100, 1, one), ("peer_multi_640kB", ELEMS * 2, 100, 1, multi),
+             ("peer_multi_8kB", 8 << 10, 200, 1, multi), ("peer_oneshot_4MiB", 4 << 20, 50, 1, one),
+             ("peer_multi_4MiB", 4 << 20, 50, 1, multi), ("peer_multi_256MiB", 256 << 20, 5, 1, multi),
+             ("hierarchical_peer", ELEMS * 2, 50, RANKS, 1 << 20)]
+    for name, nbytes, reps, local, limit in arms:
         n = nbytes // 2
+        peer.set_oneshot_max(limit)
         buf = torch.zeros((local, n), dtype=torch.int16, device=dev)
         ws = torch.empty(n, dtype=torch.int16, device=dev)
         ms = timed_max(lambda: peer.allreduce(buf.data_ptr(), n, stream, local, SIDE, t.SWING, ws.data_ptr()),

@@ -275,6 +275,11 @@ int allred_peer_connect(allred_peer* peer, const uint8_t* all_handles /*[nranks 
  * (tree of local rank 0) into `workspace` (elems * 2 bytes), then broadcast. */
 int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream);
+/* Buckets of at most `bytes` (default 4 MiB) run as one kernel (per-workgroup
+ * flags, no kernel boundaries); larger ones as copy / barrier / reduce-scatter /
+ * barrier / all-gather launches.  Same result bits either way.  Every rank
+ * must use the same setting. */
+int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
 int allred_peer_status(allred_peer* peer, uint32_t* status);
 int allred_peer_destroy(allred_peer* peer);
 

@@ -300,6 +300,10 @@ class Peer:
         check(lib.allred_peer_allreduce(self._h, buf_ptr, elems, local_ranks, local_side, local_algo, workspace_ptr,
                                         _stream_ptr(stream)), "peer_allreduce")
 
+    def set_oneshot_max(self, nbytes: int) -> None:
+        """Buckets of at most nbytes run as one kernel (same bits either way)."""
+        check(lib.allred_peer_set_oneshot_max(self._h, nbytes), "peer_set_oneshot_max")
+
     def status(self) -> int:
         v = C.c_uint32(0)
         check(lib.allred_peer_status(self._h, C.byref(v)), "peer_status")

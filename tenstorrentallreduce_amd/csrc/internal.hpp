@@ -61,8 +61,17 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
                       void* stream);
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream);
 
+// peer flag area (uint32 words): [0, 64) the multi-kernel barrier, then the
+// one-kernel form's [2 phases][kPeerFusedMaxGroups][64 ranks] slots
+constexpr uint32_t kPeerFusedFlagOff = 64;
+constexpr uint32_t kPeerFusedMaxGroups = 128;
+constexpr size_t kPeerFlagBytes = 4 * (kPeerFusedFlagOff + 2 * kPeerFusedMaxGroups * 64);
+
 int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                           size_t n, uint32_t epoch, uint32_t* status, void* stream);
+// one launch; epoch must grow by >= 1 per call
+int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
+                        size_t n, uint32_t epoch, uint32_t* status, void* stream);
 
 int hip_status(int hip_err);  // maps hipError_t -> ALLRED_*
 

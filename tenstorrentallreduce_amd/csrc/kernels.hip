@@ -496,7 +496,7 @@ __global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, 
     if (t < nranks) {
         uint32_t* mine = pp.flags[me] + t;
         for (uint64_t spin = 0;; ++spin) {
-            if (__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
+            if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
             if (spin > (1ull << 24)) {  // ~ seconds: a peer never arrived
                 atomicOr(status, 1u);
                 break;
@@ -505,6 +505,7 @@ __global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, 
         }
     }
     __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
 // reduce-scatter: block `me` of every window, owner first then ranks in order
@@ -548,6 +549,96 @@ __global__ __launch_bounds__(kBlock) void k_peer_ag(PeerPtrs pp, int me, uint16_
     const uint64_t off = (uint64_t)q * blk_vec;
     for (uint64_t v = gtid(); v < blk_vec; v += gthreads())
         st_nt(reinterpret_cast<uint4*>(bucket) + off + v, ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + off + v));
+}
+
+// ---- one-kernel form (latency regime) --------------------------------------
+// Workgroup g owns sub-slice g of every block and only ever synchronises with
+// workgroup g of the other GPUs, so there is no grid-wide barrier:
+//   1. copy sub-slice g of every block but mine to my window, signal phase 0
+//   2. wait phase 0 from all ranks; reduce sub-slice g of my block (own copy
+//      from the bucket, then ranks in order), write it to window + bucket,
+//      signal phase 1
+//   3. wait phase 1; gather sub-slice g of every other block from its owner.
+// Flag slot [phase][g][q] of rank r's fused flag area is written only by
+// workgroup g of rank q.  Windows and flags are uncached (MTYPE UC) device
+// memory, so a store is in HBM once it is acknowledged: every wave waits for
+// its stores (s_waitcnt vmcnt(0)) before the workgroup barrier, then the flag
+// goes out as a system-scope store, and the poll reads memory directly (no
+// L2 writeback / invalidate, which cost ~20 us at 128 KiB).  allred_peer
+// only selects this form when both allocations really are uncached.
+__device__ inline void peer_signal_wait(const PeerPtrs& pp, int nranks, int me, uint32_t slot_base, uint32_t epoch,
+                                        uint32_t* status) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < nranks)
+        __hip_atomic_store(pp.flags[t] + slot_base + me, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < nranks) {
+        uint32_t* mine = pp.flags[me] + slot_base + t;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
+            if (spin > (1ull << 24)) {
+                atomicOr(status, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks, int me, uint16_t* __restrict__ bucket,
+                                                         uint64_t blk_vec, uint64_t chunk, uint32_t epoch,
+                                                         uint32_t* status) {
+    const int g = blockIdx.x;
+    const uint64_t lo = (uint64_t)g * chunk;
+    const uint64_t hi = lo + chunk < blk_vec ? lo + chunk : blk_vec;
+    const uint64_t len = hi > lo ? hi - lo : 0;
+    const uint4* src = reinterpret_cast<const uint4*>(bucket);
+    uint4* mywin = reinterpret_cast<uint4*>(pp.win[me]);
+    // 1. my copy of every block but mine -> my window
+    for (uint64_t i = threadIdx.x; i < (uint64_t)nranks * len; i += blockDim.x) {
+        const uint64_t q = i / len, v = q * blk_vec + lo + i % len;
+        if ((int)q != me) st_nt(mywin + v, ld_nt(src + v));
+    }
+    const uint32_t base0 = kPeerFusedFlagOff + (uint32_t)g * 64u;
+    const uint32_t base1 = kPeerFusedFlagOff + (uint32_t)(kPeerFusedMaxGroups + g) * 64u;
+    peer_signal_wait(pp, nranks, me, base0, epoch, status);
+    // 2. reduce my block's sub-slice g
+    const uint64_t off = (uint64_t)me * blk_vec;
+    for (uint64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+        const uint4 s = ld_nt(src + off + v);
+        float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
+        uint4 y[8];
+        for (int q0 = 0; q0 < nranks; q0 += 8) {
+            const int q1 = q0 + 8 < nranks ? q0 + 8 : nranks;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (q0 + i < q1 && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(pp.win[q0 + i]) + off + v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (q0 + i >= q1 || q0 + i == me) continue;
+                a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+            }
+        }
+        uint4 o;
+        o.x = pack_rne(a[0], a[1]);
+        o.y = pack_rne(a[2], a[3]);
+        o.z = pack_rne(a[4], a[5]);
+        o.w = pack_rne(a[6], a[7]);
+        st_nt(mywin + off + v, o);
+        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, o);
+    }
+    peer_signal_wait(pp, nranks, me, base1, epoch, status);
+    // 3. gather every other block's sub-slice g from its owner
+    for (uint64_t i = threadIdx.x; i < (uint64_t)nranks * len; i += blockDim.x) {
+        const uint64_t q = i / len, v = q * blk_vec + lo + i % len;
+        if ((int)q != me)
+            st_nt(reinterpret_cast<uint4*>(bucket) + v, ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + v));
+    }
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -621,6 +712,24 @@ int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nra
     hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, st, pp, nranks, me, epoch + 1, status);
     // 5. gather the other blocks
     hipLaunchKernelGGL(k_peer_ag, dim3(grid_all(bv), nranks), dim3(kBlock), 0, st, pp, me, bucket, bv);
+    return last_error();
+}
+
+int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
+                        size_t n, uint32_t epoch, uint32_t* status, void* stream) {
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    for (int q = 0; q < nranks; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+    }
+    const uint64_t bv = n / 8 / nranks;
+    uint64_t groups = (bv + 63) / 64;
+    if (groups > kPeerFusedMaxGroups) groups = kPeerFusedMaxGroups;
+    if (groups < 1) groups = 1;
+    const uint64_t chunk = (bv + groups - 1) / groups;
+    hipLaunchKernelGGL(k_peer_oneshot, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, pp, nranks, me,
+                       bucket, bv, chunk, epoch, status);
     return last_error();
 }
 

@@ -12,6 +12,9 @@
 // so every transfer reads from all N-1 peers at once (all xGMI links busy).
 // Barrier flags live in uncached device memory and are written / polled with
 // system-scope atomics (bounded spins set a status bit instead of hanging).
+// Buckets up to allred_peer_set_oneshot_max() bytes (default 4 MiB) run the
+// same three phases as ONE kernel (k_peer_oneshot): workgroup g syncs only
+// with workgroup g of the peers, through per-workgroup flag slots.
 // Windows are double-buffered by call parity: call k+2 can only overwrite a
 // window after every peer passed call k+1's first barrier, i.e. finished
 // reading call k's windows.
@@ -27,13 +30,14 @@ struct allred_peer {
     int nranks = 0, rank = 0, device = 0;
     uint64_t max_elems = 0;
     uint16_t* win = nullptr;        // own window: 2 parities x max_elems
-    uint32_t* flags = nullptr;      // own flag array [64] (uncached)
+    uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp
     uint32_t* status = nullptr;     // device status word
     bool flags_uncached = false, win_uncached = false;
     uint16_t* peer_win[ALLRED_MAX_NODES] = {};
     uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
     bool opened[ALLRED_MAX_NODES] = {};
     uint32_t calls = 0;
+    uint64_t oneshot_max = 4ull << 20;  // buckets up to this many bytes use the one-kernel form
     bool connected = false;
 };
 
@@ -57,14 +61,14 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
         delete p;
         return ALLRED_ERR_NOMEM;
     }
-    if (hipExtMallocWithFlags((void**)&p->flags, 256, hipDeviceMallocUncached) == hipSuccess) {
+    if (hipExtMallocWithFlags((void**)&p->flags, kPeerFlagBytes, hipDeviceMallocUncached) == hipSuccess) {
         p->flags_uncached = true;
-    } else if (hipMalloc((void**)&p->flags, 256) != hipSuccess) {
+    } else if (hipMalloc((void**)&p->flags, kPeerFlagBytes) != hipSuccess) {
         (void)hipFree(p->win);
         delete p;
         return ALLRED_ERR_NOMEM;
     }
-    if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, 256) != hipSuccess ||
+    if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, kPeerFlagBytes) != hipSuccess ||
         hipMemset(p->status, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(p->win);
         (void)hipFree(p->flags);
@@ -126,12 +130,21 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
     const size_t parity = p->calls & 1u;
     uint16_t* wins[ALLRED_MAX_NODES];
     for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q] + parity * p->max_elems;
-    const uint32_t epoch = 2u * p->calls + 1u;
-    st = launch_peer_allreduce(wins, p->peer_flags, p->nranks, p->rank, bucket, n, epoch, p->status, stream);
+    if (n * 2 <= p->oneshot_max && p->win_uncached && p->flags_uncached)
+        st = launch_peer_oneshot(wins, p->peer_flags, p->nranks, p->rank, bucket, n, p->calls + 1u, p->status, stream);
+    else
+        st = launch_peer_allreduce(wins, p->peer_flags, p->nranks, p->rank, bucket, n, 2u * p->calls + 1u, p->status,
+                                   stream);
     if (st != ALLRED_OK) return st;
     ++p->calls;
     if (local_ranks > 1) st = allred_broadcast(buf, n, n, local_ranks, bucket, stream);
     return st;
+}
+
+int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
+    if (!p) return ALLRED_ERR_ARG;
+    p->oneshot_max = bytes;
+    return ALLRED_OK;
 }
 
 int allred_peer_status(allred_peer* p, uint32_t* out) {

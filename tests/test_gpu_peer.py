@@ -33,24 +33,48 @@ def worker(rank, world, port, q):
         import tenstorrentallreduce_amd as t
         import oracle
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        n = 8 * world * 64 * 5
-        peer = t.Peer(world, rank, 0, n)
+        unit = 8 * world
+        sizes = [unit, unit * 64 * 5, unit * 3, unit * 8200, unit * 64 * 5]   # 8200 vectors: > 128 groups x 64
+        n = unit * 64 * 5
+        peer = t.Peer(world, rank, 0, max(sizes))
         handles = [None] * world
         dist.all_gather_object(handles, peer.handle())
         peer.connect(handles)
         fails = []
-        for call in range(5):
-            rng = [np.random.default_rng(1000 * call + r) for r in range(world)]
-            data = [g.integers(0x3F80, 0x42C8, n).astype(np.uint16) for g in rng]
-            buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
-            peer.allreduce(buf.data_ptr(), n, torch.cuda.current_stream())
-            torch.cuda.synchronize()
-            want = [d.copy() for d in data]
+        call = 0
+        for mode, limit in (("oneshot", 1 << 40), ("steps", 0), ("auto", 1 << 20)):
+            peer.set_oneshot_max(limit)
+            for m in sizes:
+                rng = [np.random.default_rng(1000 * call + r) for r in range(world)]
+                data = [g.integers(0x3F80, 0x42C8, m).astype(np.uint16) for g in rng]
+                buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
+                peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream())
+                torch.cuda.synchronize()
+                want = [d.copy() for d in data]
+                oracle.allreduce("mem", 0, 1, want, world)
+                got = buf.cpu().numpy().view(np.uint16)
+                if not np.array_equal(got, want[rank]):
+                    fails.append((mode, m, call, int((got != want[rank]).sum())))
+                call += 1
+                dist.barrier()
+        # back-to-back calls with no host sync in between (window parities, epochs)
+        bufs = []
+        for k in range(6):
+            d = np.random.default_rng(50 + k * world + rank).integers(0x3F80, 0x42C8, n).astype(np.uint16)
+            bufs.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
+        torch.cuda.synchronize()
+        dist.barrier()
+        for k, b in enumerate(bufs):
+            peer.set_oneshot_max(1 << 40 if k % 2 else 0)
+            peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        for k, b in enumerate(bufs):
+            want = [np.random.default_rng(50 + k * world + r).integers(0x3F80, 0x42C8, n).astype(np.uint16)
+                    for r in range(world)]
             oracle.allreduce("mem", 0, 1, want, world)
-            got = buf.cpu().numpy().view(np.uint16)
-            if not np.array_equal(got, want[rank]):
-                fails.append(("flat", call, int((got != want[rank]).sum())))
-            dist.barrier()
+            if not np.array_equal(b.cpu().numpy().view(np.uint16), want[rank]):
+                fails.append(("pipelined", k))
+        dist.barrier()
         # hierarchical: 8 virtual ranks per process (4x2 Swing local grid)
         local = 8
         data = [np.random.default_rng(77 + r).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
