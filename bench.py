@@ -230,30 +230,27 @@ def timed_max(fn, reps, stream) -> float:
     return m.item()
 
 
-def peer_arms(rank, world, local_rank, dev, stream, comm, side, total) -> dict:
-    """The mem_2D variant across GPUs (allred_peer_*): one-shot reduce-scatter /
-    all-gather reading every peer's IPC-mapped window at once.  Verified first
-    against the RCCL Swing BO path on small-integer data (every order exact)."""
-    max_elems = (256 << 20) // 2
+def agreed(ok: bool) -> bool:
+    v = torch.tensor([int(ok)], dtype=torch.int64)
+    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+    return bool(v.item())
+
+
+def open_peer(rank, world, local_rank, max_elems):
+    """Peer windows (allred_peer_*), IPC handles exchanged over gloo.  Returns
+    (peer, None) or (None, reason) — the same on every rank."""
     peer, mine = None, None
     try:
         peer = t.Peer(world, rank, local_rank, max_elems)
         mine = peer.handle()
     except Exception as e:  # every rank must learn of it, or the others block below
-        mine = None
         print(f"[bench] peer create failed on rank {rank}: {e!r}", file=sys.stderr)
     handles = [None] * world
     dist.all_gather_object(handles, mine)
-
-    def agreed(ok: bool) -> bool:
-        v = torch.tensor([int(ok)], dtype=torch.int64)
-        dist.all_reduce(v, op=dist.ReduceOp.MIN)
-        return bool(v.item())
-
     if not all(h is not None for h in handles):
         if peer:
             peer.close()
-        return {"peer_error": "create failed on some rank"}
+        return None, "create failed on some rank"
     try:
         peer.connect(handles)
         ok = True
@@ -262,47 +259,46 @@ def peer_arms(rank, world, local_rank, dev, stream, comm, side, total) -> dict:
         ok = False
     if not agreed(ok):
         peer.close()
-        return {"peer_error": "connect failed on some rank"}
+        return None, "connect failed on some rank"
+    return peer, None
+
+
+def arm_stats(ms, nbytes, world, lo=False) -> dict:
+    sec = ms * 1e-3
+    busbw = 2 * (world - 1) / world * nbytes / sec / 1e9   # nccl-tests convention
+    if lo:
+        busbw = nbytes / sec / 1e9   # LO moves the whole bucket every step: report algbw
+    return {"ms": round(ms, 4), "algbw_GBps": round(nbytes / sec / 1e9, 3), "busbw_GBps": round(busbw, 3),
+            "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
+
+
+def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
+    """Flat / hierarchical inter-GPU allreduces (BASELINE configs 3-5 regimes),
+    each through RCCL (allred_dist_allreduce) and through the peer windows
+    (allred_peer_dist_allreduce: same program, same bits, one kernel)."""
     out = {}
-    n = ELEMS
-    g = torch.Generator().manual_seed(5 + rank)
-    vals = torch.randint(0, 8, (n,), generator=g).to(torch.bfloat16).view(torch.int16).to(dev)
-    a, b = vals.clone(), vals.clone()
-    peer.allreduce(a.data_ptr(), n, stream)
-    d = t.dist_desc(t.SWING, t.BO, side, total, n)
-    w = torch.empty(t.dist_workspace_bytes(d), dtype=torch.uint8, device=dev)
-    t.dist_allreduce(comm, d, b.data_ptr(), w.data_ptr(), stream)
-    torch.cuda.synchronize()
-    ok = torch.tensor([int(torch.equal(a, b))], dtype=torch.int64)
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-    out["peer_verified_vs_rccl"] = bool(ok.item())
-    if not agreed(peer.status() & t.PEER_TIMEOUT == 0):
-        out["peer_error"] = "barrier timeout"
-        peer.close()
-        return out
-    one, multi = 1 << 40, 0   # one-kernel form / copy-barrier-RS-barrier-AG launches
-    arms = [(f"peer_oneshot_{kb}kB", kb << 10, 200, 1, one) for kb in (2, 8, 32, 128)]
-    arms += [("peer_oneshot_640kB", ELEMS * 2, 100, 1, one), ("peer_multi_640kB", ELEMS * 2, 100, 1, multi),
-             ("peer_multi_8kB", 8 << 10, 200, 1, multi), ("peer_oneshot_4MiB", 4 << 20, 50, 1, one),
-             ("peer_multi_4MiB", 4 << 20, 50, 1, multi), ("peer_multi_256MiB", 256 << 20, 5, 1, multi),
-             ("hierarchical_peer", ELEMS * 2, 50, RANKS, 1 << 20)]
-    for name, nbytes, reps, local, limit in arms:
+    arms = [("config4_swing_bo_256MiB_all_links", t.SWING, t.BO, 256 << 20, 5, 0, 1),
+            ("config4_swing_bo_256MiB_one_link", t.SWING, t.BO, 256 << 20, 3, 1, 1),
+            ("config3_recdub_bo_640kB", t.RECDUB, t.BO, ELEMS * 2, 50, 0, 1),
+            ("hierarchical_all_links", t.SWING, t.BO, ELEMS * 2, 50, world - 1, RANKS),
+            ("hierarchical_lo_partial", t.SWING, t.LO, ELEMS * 2, 50, 1, RANKS)]
+    # BASELINE config 5: flat 2D Swing LO, 2 kB .. 128 kB per GPU (latency regime)
+    arms += [(f"config5_swing_lo_{kb}kB", t.SWING, t.LO, kb << 10, 100, 1, 1) for kb in (2, 8, 32, 128)]
+    arms += [(f"mem_{kb}kB", t.SWING, t.MEM, kb << 10, 100, 1, 1) for kb in (2, 32)]
+    arms += [("mem_640kB", t.SWING, t.MEM, ELEMS * 2, 100, 1, 1), ("mem_256MiB", t.SWING, t.MEM, 256 << 20, 5, 1, 1)]
+    for name, algo, variant, nbytes, reps, chans, local in arms:
         n = nbytes // 2
-        peer.set_oneshot_max(limit)
-        buf = torch.zeros((local, n), dtype=torch.int16, device=dev)
-        ws = torch.empty(n, dtype=torch.int16, device=dev)
-        ms = timed_max(lambda: peer.allreduce(buf.data_ptr(), n, stream, local, SIDE, t.SWING, ws.data_ptr()),
-                       reps, stream)
-        sec = ms * 1e-3
-        busbw = 2 * (world - 1) / world * nbytes / sec / 1e9
-        out[name] = {"ms": round(ms, 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
-                     "busbw_GBps": round(busbw, 3), "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
-        del buf, ws
-    st = torch.tensor([peer.status()], dtype=torch.int64)
-    dist.all_reduce(st, op=dist.ReduceOp.MAX)
-    out["peer_status"] = int(st.item())
-    dist.barrier()
-    peer.close()
+        d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
+                         channels=chans)
+        b2 = torch.zeros((local, n), dtype=torch.int16, device=dev)
+        w2 = torch.empty(max(16, t.dist_workspace_bytes(d2)), dtype=torch.uint8, device=dev)
+        if variant != t.MEM:
+            ms = timed_max(lambda: t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+            out[name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+        if peer is not None:
+            ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+            out["peer_" + name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+        del b2, w2
     return out
 
 
@@ -313,6 +309,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     uid = [t.Comm.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     comm = t.Comm(uid[0], world, rank, local_rank)
+    peer, peer_err = open_peer(rank, world, local_rank, (256 << 20) // 2)
     stream = torch.cuda.Stream(device=dev)
     desc = t.dist_desc(t.SWING, t.BO, side, total, ELEMS, local_ranks=RANKS, local_side=SIDE, local_algo=t.SWING)
     buf = torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev)
@@ -320,8 +317,26 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)
     partial = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
+    # transport: the same Swing program through RCCL and through the peer windows
+    # must give identical bits on these inputs; the peer form is timed only then
+    transport, bits_equal = "rccl", None
+    if peer is not None:
+        a, b = buf.clone(), buf.clone()
+        t.dist_allreduce(comm, desc, a.data_ptr(), ws.data_ptr(), stream)
+        peer.dist_allreduce(desc, b.data_ptr(), ws.data_ptr(), stream)
+        torch.cuda.synchronize()
+        bits_equal = agreed(torch.equal(a, b) and (peer.status() & t.PEER_TIMEOUT) == 0)
+        del a, b
+        if bits_equal:
+            transport = "peer"
+        else:
+            peer_err = "peer result differs from RCCL (or barrier timeout): not used"
+
     def step():
-        t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr(), stream)
+        if transport == "peer":
+            peer.dist_allreduce(desc, buf.data_ptr(), ws.data_ptr(), stream)
+        else:
+            t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr(), stream)
 
     for _ in range(args.warmup):
         step()
@@ -352,54 +367,24 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     torch.cuda.synchronize()
     local_ms = e0.elapsed_time(e1) / args.steps
 
-    # flat xGMI allreduces (BASELINE configs 3/4 regimes): 2D Swing BO on a 256 MiB bucket with
-    # every link in use (link-spreading channels) and on one link (the plain schedule), 2D RecDub
-    # BO on 640 kB, and the hierarchical step with its partial spread over all links
-    extras = {}
+    extras = {"headline_transport": transport, "peer_bits_equal_rccl": bits_equal}
+    if peer_err:
+        extras["peer_error"] = peer_err
     if args.extras:
-        arms = [("config4_swing_bo_256MiB_all_links", t.SWING, 256 << 20, 5, 0, 1),
-                ("config4_swing_bo_256MiB_one_link", t.SWING, 256 << 20, 3, 1, 1),
-                ("config3_recdub_bo_640kB", t.RECDUB, ELEMS * 2, 50, 0, 1),
-                ("hierarchical_all_links", t.SWING, ELEMS * 2, 50, world - 1, RANKS),
-                ("hierarchical_lo_partial", t.SWING, ELEMS * 2, 50, 1, RANKS)]
-        # BASELINE config 5: flat 2D Swing LO, 2 kB .. 128 kB per GPU (latency regime)
-        arms += [(f"config5_swing_lo_{kb}kB", t.SWING, kb << 10, 100, 1, 1) for kb in (2, 8, 32, 128)]
-        for name, algo, nbytes, reps, chans, local in arms:
-            n = nbytes // 2
-            variant = t.LO if ("_lo_" in name) else t.BO
-            d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
-                             channels=chans)
-            b2 = torch.zeros((local, n), dtype=torch.int16, device=dev)
-            w2 = torch.empty(t.dist_workspace_bytes(d2), dtype=torch.uint8, device=dev)
-            for _ in range(2):
-                t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream)
-            torch.cuda.synchronize()
-            dist.barrier()
-            e0.record(stream)
-            for _ in range(reps):
-                t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            m = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64)
-            dist.all_reduce(m, op=dist.ReduceOp.MAX)
-            sec = m.item() * 1e-3
-            busbw = 2 * (world - 1) / world * nbytes / sec / 1e9  # nccl-tests convention
-            if variant == t.LO:
-                busbw = nbytes / sec / 1e9  # LO moves the whole bucket every step: report algbw
-            extras[name] = {"ms": round(m.item(), 4), "algbw_GBps": round(nbytes / sec / 1e9, 3),
-                            "busbw_GBps": round(busbw, 3), "channels": chans,
-                            "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
-            del b2, w2
-        try:
-            extras.update(peer_arms(rank, world, local_rank, dev, stream, comm, side, total))
-        except Exception as e:  # reported, never silently dropped
-            extras["peer_error"] = repr(e)
+        extras.update(xgmi_arms(comm, peer if transport == "peer" else None, world, dev, stream, side, total))
+    if peer is not None:
+        st = torch.tensor([peer.status()], dtype=torch.int64)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        extras["peer_status"] = int(st.item())
+        dist.barrier()
+        peer.close()
     comm.close()
     if rank != 0:
         return None
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
     achieved = local_bytes / (local_ms * 1e-3) / 1e9
+    via = "peer-mapped xGMI windows (one kernel)" if transport == "peer" else "RCCL/xGMI"
     return {
         "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
@@ -414,8 +399,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         "dtype": "bf16",
         "data": "synthetic (uniform [0,100) bf16, reference rank convention)",
         "config": {"workload": f"config 2 per GPU (64 virtual ranks x 655,360 B, 8x8 Swing) x {world} GPUs: "
-                               f"on-GPU tree reduce, 2D Swing BO over RCCL/xGMI on grid {GRIDS[world]}, broadcast",
-                   "ranks": RANKS * world, "bytes_per_rank": ELEMS * 2, "parallelism": f"dp{world}"},
+                               f"on-GPU tree reduce, 2D Swing BO over {via} on grid {GRIDS[world]}, broadcast",
+                   "ranks": RANKS * world, "bytes_per_rank": ELEMS * 2, "parallelism": f"dp{world}",
+                   "transport": transport},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
                      "kernel": "k_tree<64,false> + k_broadcast (local phases)",

@@ -280,6 +280,16 @@ int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int 
  * barrier / all-gather launches.  Same result bits either way.  Every rank
  * must use the same setting. */
 int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
+/* The allred_dist_allreduce program (same desc, same result bits: Swing /
+ * RecDub BO or LO, link-spreading channels, hierarchical local ranks) with
+ * RCCL replaced by direct reads of the partners' IPC-mapped windows: one
+ * kernel, each step waits only for its partner (allred_BO_2D
+ * dataflow_kernel.cpp:152-267 semaphore handshakes, over xGMI).
+ * desc->variant ALLRED_MEM runs allred_peer_allreduce.  desc->total_nodes
+ * must equal nranks; elems <= max_elems (BO) or max_elems / 2 (LO);
+ * workspace: allred_dist_workspace_bytes(desc) bytes when local_ranks > 1. */
+int allred_peer_dist_allreduce(allred_peer* peer, const allred_dist_desc* desc, uint16_t* buf, void* workspace,
+                               void* stream);
 int allred_peer_status(allred_peer* peer, uint32_t* status);
 int allred_peer_destroy(allred_peer* peer);
 

@@ -300,6 +300,11 @@ class Peer:
         check(lib.allred_peer_allreduce(self._h, buf_ptr, elems, local_ranks, local_side, local_algo, workspace_ptr,
                                         _stream_ptr(stream)), "peer_allreduce")
 
+    def dist_allreduce(self, desc: DistDesc, buf_ptr: int, workspace_ptr: int | None = None, stream=None) -> None:
+        """dist_allreduce's program (same desc, same bits) over the peer windows."""
+        check(lib.allred_peer_dist_allreduce(self._h, C.byref(desc), buf_ptr, workspace_ptr, _stream_ptr(stream)),
+              "peer_dist_allreduce")
+
     def set_oneshot_max(self, nbytes: int) -> None:
         """Buckets of at most nbytes run as one kernel (same bits either way)."""
         check(lib.allred_peer_set_oneshot_max(self._h, nbytes), "peer_set_oneshot_max")

@@ -250,6 +250,48 @@ int device_order(int algo, int side, int total, const uint8_t** out) {
 
 }  // namespace
 
+namespace tsa {
+
+// The RCCL program's exchanges, as tables for the peer-mapped kernel
+// (k_peer_sched): per channel, the step partner and this rank's block masks
+// in the channel's labels, plus the channel slice in 16-byte vectors.
+int peer_prog(const allred_dist_desc* d, int rank, PeerProg* out) {
+    allred_schedule s;
+    int st = check_desc(d, &s);
+    if (st != ALLRED_OK) return st;
+    if (rank < 0 || rank >= d->total_nodes || s.steps > kPeerMaxSteps) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)d->elems;
+    const int N = s.total, S = s.steps;
+    int C = channels_for(s, d->channels, n);
+    if (d->variant == ALLRED_LO && n % (8 * (size_t)N)) C = 1;
+    if (C > kPeerMaxChannels) C = kPeerMaxChannels;
+    *out = PeerProg{};
+    out->S = S;
+    out->C = C;
+    out->N = N;
+    out->lo = d->variant == ALLRED_LO;
+    auto id_of = [&](int c, int r) { return C == 1 ? r : gf_mul(gf_pow_alpha(c, S), r, S); };
+    for (int c = 0; c < C; ++c) {
+        size_t base = 0, len = n;
+        if (C > 1) slice_of(n, N, C, c, &base, &len);
+        out->base[c] = base / 8;
+        out->len[c] = len / 8;
+        const int x = id_of(c, rank);
+        for (int k = 0; k < S; ++k) {
+            const int px = s.partner[x][k];
+            int q = px;
+            if (C > 1)
+                for (q = 0; q < N && id_of(c, q) != px; ++q) {}
+            out->peer[c][k] = q;
+            out->recv[c][k] = s.recv[x][k];
+            out->send[c][k] = s.send[x][k];
+        }
+    }
+    return ALLRED_OK;
+}
+
+}  // namespace tsa
+
 extern "C" {
 
 int allred_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int algo, int side, int total,

@@ -62,13 +62,34 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream);
 
 // peer flag area (uint32 words): [0, 64) the multi-kernel barrier, then the
-// one-kernel form's [2 phases][kPeerFusedMaxGroups][64 ranks] slots
+// one-kernel form's [2 phases][kPeerFusedMaxGroups][64 ranks] slots, then the
+// scheduled (Swing / RecDub) form's progress slots [kPeerSchedMaxGroups][64 ranks]
 constexpr uint32_t kPeerFusedFlagOff = 64;
 constexpr uint32_t kPeerFusedMaxGroups = 128;
-constexpr size_t kPeerFlagBytes = 4 * (kPeerFusedFlagOff + 2 * kPeerFusedMaxGroups * 64);
+constexpr uint32_t kPeerSchedFlagOff = kPeerFusedFlagOff + 2 * kPeerFusedMaxGroups * 64;
+constexpr uint32_t kPeerSchedMaxGroups = 256;
+constexpr size_t kPeerFlagBytes = 4 * ((size_t)kPeerSchedFlagOff + kPeerSchedMaxGroups * 64);
+
+// One rank's BO / LO program over peer-mapped windows (dist.cpp builds it from
+// the same schedule + link-spreading channels as the RCCL program).
+constexpr int kPeerMaxChannels = 7;
+constexpr int kPeerMaxSteps = 6;
+struct PeerProg {
+    int S = 0, C = 1, N = 1, lo = 0;
+    int peer[kPeerMaxChannels][kPeerMaxSteps] = {};       // real rank, [channel][step]
+    uint64_t recv[kPeerMaxChannels][kPeerMaxSteps] = {};  // block masks in the channel's labels
+    uint64_t send[kPeerMaxChannels][kPeerMaxSteps] = {};
+    uint64_t base[kPeerMaxChannels] = {}, len[kPeerMaxChannels] = {};  // channel slice, 16-byte vectors
+};
+int peer_prog(const allred_dist_desc* d, int rank, PeerProg* out);
 
 int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                           size_t n, uint32_t epoch, uint32_t* status, void* stream);
+// full barrier of the peer set (flag region [0, 64))
+int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epoch, uint32_t* status, void* stream);
+// the scheduled form: one launch; flag values base_epoch + 1 .. base_epoch + 2S + 1
+int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
+                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, void* stream);
 // one launch; epoch must grow by >= 1 per call
 int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                         size_t n, uint32_t epoch, uint32_t* status, void* stream);

@@ -641,6 +641,114 @@ __global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks
     }
 }
 
+// ---- scheduled form: the Swing / RecDub BO or LO program over peer windows --
+// The RCCL program of dist.cpp with every exchange turned into a direct read
+// of the partner's IPC-mapped window: step k of rank r waits until its
+// partner p has finished step k-1 (p's progress slot in r's flag area), then
+// reads p's blocks straight over xGMI and adds them into its own window.
+// Workgroup g = channel g % C, sub-slice g / C of every block of the channel;
+// it only ever waits for workgroup g of its partners.  Progress values for a
+// call are base+1 (window filled) .. base+2S (all-gather step S-2 done).
+// Hazards (why no ack is needed in BO): at RS step k rank r writes only
+// recv_r[k], which no partner reads at step k or later; at AG step i it writes
+// send_r[i], whose only earlier reader is the same partner p_i, which has
+// finished its whole reduce-scatter before it can serve AG step i.
+// LO ping-pongs two halves of the window: step k reads half k&1 and writes
+// half (k+1)&1, after p_{k-1} (the previous reader of that half) finished k-1.
+__device__ inline void sched_signal(const PeerPtrs& pp, const PeerProg& pr, int c, int me, uint32_t slot,
+                                    uint32_t value) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < pr.S)
+        __hip_atomic_store(pp.flags[pr.peer[c][t]] + slot + me, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ inline void sched_wait(const PeerPtrs& pp, int me, uint32_t slot, int q0, int q1, uint32_t value,
+                                  uint32_t* status) {
+    const int t = threadIdx.x;
+    const int q = t == 0 ? q0 : (t == 1 ? q1 : -1);
+    if (q >= 0) {
+        uint32_t* f = pp.flags[me] + slot + q;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= value) break;
+            if (spin > (1ull << 24)) {
+                atomicOr(status, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
+                                                       uint64_t half_vec, uint32_t base, uint32_t* status) {
+    const int C = pr.C, S = pr.S, N = pr.N;
+    const int g = blockIdx.x, c = g % C, Gc = gridDim.x / C, j = g / C;
+    const uint32_t slot = kPeerSchedFlagOff + (uint32_t)g * 64u;
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint4* mine = reinterpret_cast<uint4*>(pp.win[me]);
+    const uint64_t cb = pr.base[c];
+    const int tid = threadIdx.x;
+    if (!pr.lo) {
+        const uint64_t blk = pr.len[c] / N;
+        const uint64_t chunk = (blk + Gc - 1) / Gc;
+        const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk < blk ? lo + chunk : blk;
+        for (int b = 0; b < N; ++b)
+            for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) st_nt(mine + v, ld_nt(bk + v));
+        sched_signal(pp, pr, c, me, slot, base + 1);
+        for (int k = 0; k < S; ++k) {  // reduce-scatter
+            const int p = pr.peer[c][k];
+            sched_wait(pp, me, slot, p, -1, base + 1 + k, status);
+            const uint4* theirs = reinterpret_cast<const uint4*>(pp.win[p]);
+            const bool last = k == S - 1;
+            for (uint64_t m = pr.recv[c][k]; m; m &= m - 1) {
+                const int b = __builtin_ctzll(m);
+                for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) {
+                    const uint4 o = add8(ld_nt(mine + v), ld_nt(theirs + v));
+                    st_nt(mine + v, o);
+                    if (last) st_nt(bk + v, o);
+                }
+            }
+            sched_signal(pp, pr, c, me, slot, base + 2 + k);
+        }
+        for (int t = 0; t < S; ++t) {  // all-gather, steps in reverse
+            const int i = S - 1 - t, pos = S + t;
+            const int p = pr.peer[c][i];
+            sched_wait(pp, me, slot, p, -1, base + 1 + pos, status);
+            const uint4* theirs = reinterpret_cast<const uint4*>(pp.win[p]);
+            const bool keep = t < S - 1;  // later partners read these blocks from my window
+            for (uint64_t m = pr.send[c][i]; m; m &= m - 1) {
+                const int b = __builtin_ctzll(m);
+                for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) {
+                    const uint4 y = ld_nt(theirs + v);
+                    if (keep) st_nt(mine + v, y);
+                    st_nt(bk + v, y);
+                }
+            }
+            if (keep) sched_signal(pp, pr, c, me, slot, base + 2 + pos);
+        }
+        return;
+    }
+    // LO: full exchange + add every step, two window halves
+    const uint64_t L = pr.len[c];
+    const uint64_t chunk = (L + Gc - 1) / Gc;
+    const uint64_t lo = cb + (uint64_t)j * chunk, hi = (uint64_t)j * chunk + chunk < L ? lo + chunk : cb + L;
+    for (uint64_t v = lo + tid; v < hi; v += kBlock) st_nt(mine + v, ld_nt(bk + v));
+    sched_signal(pp, pr, c, me, slot, base + 1);
+    for (int k = 0; k < S; ++k) {
+        const int p = pr.peer[c][k];
+        const bool last = k == S - 1;
+        sched_wait(pp, me, slot, p, (k >= 1 && !last) ? pr.peer[c][k - 1] : -1, base + 1 + k, status);
+        const uint4* a = mine + (k & 1) * half_vec;
+        const uint4* b = reinterpret_cast<const uint4*>(pp.win[p]) + (k & 1) * half_vec;
+        uint4* dst = last ? bk : mine + ((k + 1) & 1) * half_vec;
+        for (uint64_t v = lo + tid; v < hi; v += kBlock) st_nt(dst + v, add8(ld_nt(a + v), ld_nt(b + v)));
+        if (!last) sched_signal(pp, pr, c, me, slot, base + 2 + k);
+    }
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ALLRED_TREE=registers selects the register-only k_tree for the fused BO pass
@@ -712,6 +820,38 @@ int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nra
     hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, st, pp, nranks, me, epoch + 1, status);
     // 5. gather the other blocks
     hipLaunchKernelGGL(k_peer_ag, dim3(grid_all(bv), nranks), dim3(kBlock), 0, st, pp, me, bucket, bv);
+    return last_error();
+}
+
+int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epoch, uint32_t* status, void* stream) {
+    if (nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    for (int q = 0; q < nranks; ++q) pp.flags[q] = flags[q];
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, (hipStream_t)stream, pp, nranks, me, epoch, status);
+    return last_error();
+}
+
+int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
+                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, void* stream) {
+    if (!aligned16(bucket) || prog.N > ALLRED_MAX_NODES || prog.C < 1 || prog.C > kPeerMaxChannels ||
+        prog.S > kPeerMaxSteps)
+        return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    for (int q = 0; q < prog.N; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+    }
+    uint64_t per = 0;  // vectors per workgroup sub-slice unit (largest channel)
+    for (int c = 0; c < prog.C; ++c) {
+        const uint64_t u = prog.lo ? prog.len[c] : prog.len[c] / prog.N;
+        if (u > per) per = u;
+    }
+    uint64_t gc = (per + kBlock - 1) / kBlock;
+    const uint64_t gmax = kPeerSchedMaxGroups / prog.C;
+    if (gc > gmax) gc = gmax;
+    if (gc < 1) gc = 1;
+    hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
+                       bucket, half_vec, base_epoch, status);
     return last_error();
 }
 

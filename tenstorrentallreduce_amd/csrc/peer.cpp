@@ -37,6 +37,8 @@ struct allred_peer {
     uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
     bool opened[ALLRED_MAX_NODES] = {};
     uint32_t calls = 0;
+    uint32_t seq = 0;               // progress-flag base of the scheduled form
+    bool last_all_peer = false;     // previous call read every rank's window
     uint64_t oneshot_max = 4ull << 20;  // buckets up to this many bytes use the one-kernel form
     bool connected = false;
 };
@@ -52,7 +54,7 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     p->nranks = nranks;
     p->rank = rank;
     (void)hipGetDevice(&p->device);
-    p->max_elems = (max_elems + 63) / 64 * 64;
+    p->max_elems = (max_elems + 127) / 128 * 128;  // LO halves stay 64-element aligned
     // windows are uncached too: peers read them over xGMI straight from HBM, so
     // no write may linger in one of this GPU's eight per-XCD L2s
     if (hipExtMallocWithFlags((void**)&p->win, 2 * p->max_elems * 2, hipDeviceMallocUncached) == hipSuccess) {
@@ -114,6 +116,16 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
     return ALLRED_OK;
 }
 
+namespace {
+
+// windows of this call's parity, as mapped in this process
+void parity_windows(allred_peer* p, uint16_t** wins) {
+    const size_t parity = p->calls & 1u;
+    for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q] + parity * p->max_elems;
+}
+
+}  // namespace
+
 int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream) {
     if (!p || !buf || !p->connected) return ALLRED_ERR_ARG;
@@ -127,9 +139,8 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         st = allred_tree_reduce(buf, n, n, local_algo, local_side, local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
-    const size_t parity = p->calls & 1u;
     uint16_t* wins[ALLRED_MAX_NODES];
-    for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q] + parity * p->max_elems;
+    parity_windows(p, wins);
     if (n * 2 <= p->oneshot_max && p->win_uncached && p->flags_uncached)
         st = launch_peer_oneshot(wins, p->peer_flags, p->nranks, p->rank, bucket, n, p->calls + 1u, p->status, stream);
     else
@@ -137,7 +148,48 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
                                    stream);
     if (st != ALLRED_OK) return st;
     ++p->calls;
+    p->last_all_peer = true;
     if (local_ranks > 1) st = allred_broadcast(buf, n, n, local_ranks, bucket, stream);
+    return st;
+}
+
+int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16_t* buf, void* workspace,
+                               void* stream) {
+    if (!p || !d || !buf || !p->connected) return ALLRED_ERR_ARG;
+    if (d->total_nodes != p->nranks) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)d->elems;
+    if (d->variant == ALLRED_MEM) {
+        uint16_t* ws = workspace ? static_cast<uint16_t*>(workspace) + n : nullptr;  // dist workspace layout
+        return allred_peer_allreduce(p, buf, n, d->local_ranks, d->local_side, d->local_algo, ws, stream);
+    }
+    PeerProg prog;
+    int st = peer_prog(d, p->rank, &prog);
+    if (st != ALLRED_OK) return st;
+    if (n > (prog.lo ? p->max_elems / 2 : p->max_elems)) return ALLRED_ERR_ARG;
+    uint16_t* bucket = buf;
+    if (d->local_ranks > 1) {
+        if (!workspace) return ALLRED_ERR_ARG;
+        bucket = static_cast<uint16_t*>(workspace) + n;
+        st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
+        if (st != ALLRED_OK) return st;
+    }
+    if (prog.S > 0) {
+        uint16_t* wins[ALLRED_MAX_NODES];
+        parity_windows(p, wins);
+        if (p->last_all_peer) {
+            // the previous call read every rank's window, this one only waits for
+            // partners: one full barrier keeps call k+2 off windows still being read
+            st = launch_peer_barrier(p->peer_flags, p->nranks, p->rank, 2u * p->calls + 1u, p->status, stream);
+            if (st != ALLRED_OK) return st;
+        }
+        st = launch_peer_sched(wins, p->peer_flags, p->rank, bucket, prog, p->max_elems / 2 / 8, p->seq, p->status,
+                               stream);
+        if (st != ALLRED_OK) return st;
+        p->seq += 2u * (uint32_t)prog.S + 2u;
+        ++p->calls;
+        p->last_all_peer = false;
+    }
+    if (d->local_ranks > 1) st = allred_broadcast(buf, n, n, d->local_ranks, bucket, stream);
     return st;
 }
 

@@ -123,3 +123,76 @@ def test_peer_one_shot_multi_process_one_gpu(world):
     for rank, fails, status in results:
         assert fails == [], (rank, fails)
         assert status == 0, (rank, status)
+
+
+def dist_worker(rank, world, port, q):
+    """allred_peer_dist_allreduce: every case of the gloo-tested RCCL program
+    (tests/test_dist_host.py: Swing / RecDub / 1D schedules, BO and LO, flat and
+    hierarchical, link-spreading channels) over the peer windows, bit-exact with
+    the oracle; each case twice back to back, a mem_2D call in between."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import tenstorrentallreduce_amd as t
+        import test_dist_host as tdh
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        side, total = tdh.GRIDS[world]
+        n = 8 * total * 16 * 3
+        peer = t.Peer(world, rank, 0, 4 * n * 2)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        fails = []
+        for ci, (variant, algo, local, chans) in enumerate(tdh.cases(world)):
+            desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
+                               local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
+            ws = torch.empty(max(t.dist_workspace_bytes(desc), 16), dtype=torch.uint8, device="cuda:0")
+            runs = []
+            for rep in range(2):
+                data = tdh.inputs(world, local, n, seed=1000 * world + 10 * ci + rep)
+                buf = torch.from_numpy(np.concatenate(data[rank]).view(np.int16)).to("cuda:0")
+                peer.dist_allreduce(desc, buf.data_ptr(), ws.data_ptr(), torch.cuda.current_stream())
+                runs.append((data, buf))
+            torch.cuda.synchronize()
+            for rep, (data, buf) in enumerate(runs):
+                want = np.concatenate(tdh.expected(variant, algo, world, local, data, chans)[rank])
+                got = buf.cpu().numpy().view(np.uint16)
+                if not np.array_equal(got, want):
+                    fails.append((variant, algo, local, chans, rep, int((got != want).sum())))
+            # a mem_2D call (reads every window) between scheduled calls
+            m = torch.zeros(n, dtype=torch.int16, device="cuda:0")
+            peer.allreduce(m.data_ptr(), n, torch.cuda.current_stream())
+        torch.cuda.synchronize()
+        status = peer.status()
+        dist.barrier()
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_peer_scheduled_program_multi_process_one_gpu(world):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=dist_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in procs:
+            results.append(q.get(timeout=300))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails, status in results:
+        assert fails == [], (rank, fails)
+        assert status == 0, (rank, status)
