@@ -174,9 +174,20 @@ def bench_single(args) -> dict:
 
     # host-staged end to end (buckets start and end in pinned host memory): the
     # reference program surface, H2D of all 64 buckets + allreduce + D2H
-    rep = t.run(["allred_BO_2D", "1", "1", str(SIDE), "13", str(TILES), "32", "0", "1"], t.BO, False, t.EXEC_FUSED)
-    e2e = {"e2e_ms": round(rep.e2e_seconds * 1e3, 4), "device_ms": round(rep.device_seconds * 1e3, 4),
-           "value": round(bytes_all / rep.e2e_seconds / 1e9, 3), "mismatches": int(rep.mismatches)}
+    # reference program surface, H2D of all 64 buckets + allreduce + D2H (one DMA each way) ...
+    # ("dma") and the fused kernel reading / writing the pinned host buckets in place ("zerocopy")
+    argv = ["allred_BO_2D", "1", "1", str(SIDE), "13", str(TILES), "32", "0", "1"]
+    e2e = {}
+    for mode in ("zerocopy", "dma"):
+        os.environ["ALLRED_E2E"] = mode
+        try:
+            rep = t.run(argv, t.BO, False, t.EXEC_FUSED)
+            e2e[mode] = {"e2e_ms": round(rep.e2e_seconds * 1e3, 4), "device_ms": round(rep.device_seconds * 1e3, 4),
+                         "value": round(bytes_all / rep.e2e_seconds / 1e9, 3), "mismatches": int(rep.mismatches)}
+        except Exception as e:  # reported, never silently dropped
+            e2e[mode] = {"error": repr(e)}
+        finally:
+            del os.environ["ALLRED_E2E"]
 
     alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9

@@ -40,6 +40,8 @@ struct allred_plan {
     uint8_t* d_order = nullptr;
     size_t ws_bytes = 0;
     int launches = 0;
+    const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
+    bool last_host = false;
 };
 
 namespace {
@@ -153,7 +155,13 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
         if (p->desc.variant == ALLRED_LO) return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, stream);
-        return launch_tree_fused(ranks, stride, p->n, N, p->d_order, stream);
+        if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
+            hipPointerAttribute_t at{};
+            p->last_host = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;
+            (void)hipGetLastError();
+            p->last_ranks = ranks;
+        }
+        return launch_tree_fused(ranks, stride, p->n, N, p->d_order, stream, p->last_host);
     }
     if (p->desc.variant == ALLRED_BO) {
         for (int k = 0; k < steps && st == ALLRED_OK; ++k)
@@ -289,6 +297,13 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     const size_t stride = (size_t)allred_preferred_rank_stride(n);
     const size_t dev_bytes = (size_t)N * stride * 2;
     float ms = 0;
+    // end-to-end mode: "zerocopy" = the kernel reads / writes the pinned host
+    // buckets in place (both PCIe directions at once; the default for the
+    // fused BO pass, whose pipelined form is built for it), "dma" = one H2D
+    // and one D2H around the device-resident allreduce.  ALLRED_E2E overrides.
+    const char* e2e_mode = std::getenv("ALLRED_E2E");
+    const bool zero_copy = e2e_mode ? std::strcmp(e2e_mode, "zerocopy") == 0
+                                    : (variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED && N >= 8);
     if (a->seed < 0) {
         allred_constant_bf16_vector(bytes, 1.0f, src0.data());
         src1 = src0;
@@ -315,6 +330,19 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     ST(launch_copy_ranks(d_stage, n, d_scratch, stride, N, n, s));
     if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, stride, d_ws, s));
     HIPCK(hipStreamSynchronize(s));
+    if (zero_copy) {
+        // the kernels read and write the pinned host buckets in place over PCIe
+        // (both directions at once); no staging copies, no HBM round trip
+        uint16_t* h_dev = nullptr;
+        HIPCK(hipHostGetDevicePointer((void**)&h_dev, h_in, 0));
+        HIPCK(hipEventRecord(e0, s));
+        HIPCK(hipEventRecord(e1, s));
+        if (a->run_kernel) ST(allred_plan_execute(plan, h_dev, n, d_ws, s));
+        HIPCK(hipEventRecord(e2, s));
+        HIPCK(hipEventRecord(e3, s));
+        HIPCK(hipStreamSynchronize(s));
+        std::memcpy(h_out, h_in, all_bytes);  // (untimed) the result, for validation below
+    } else {
     // timed: H2D | allreduce | D2H
     HIPCK(hipEventRecord(e0, s));
     // the 64 host buckets are contiguous: one DMA each way (per-bucket copies pay ~70 us each),
@@ -328,6 +356,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     HIPCK(hipMemcpyAsync(h_out, d_stage, all_bytes, hipMemcpyDeviceToHost, s));
     HIPCK(hipEventRecord(e3, s));
     HIPCK(hipStreamSynchronize(s));
+    }
     HIPCK(hipEventElapsedTime(&ms, e1, e2));
     R->device_seconds = ms * 1e-3;
     HIPCK(hipEventElapsedTime(&ms, e0, e3));

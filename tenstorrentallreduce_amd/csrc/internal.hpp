@@ -41,8 +41,9 @@ struct RankTable;  // opaque device tables of a plan
 int launch_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream);
 int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* blocks, int nblocks,
                            size_t block_elems, void* stream);
-int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order,
-                      void* stream);
+// host_memory: the ranks live in pinned host memory (zero-copy) -> pipelined form
+int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
+                      bool host_memory = false);
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
                      void* stream);
 int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total,

@@ -240,6 +240,59 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ rank
 }
 
 // ---------------------------------------------------------------------------
+// k_tree_lds with a persistent grid and two LDS tile buffers, for buckets in
+// pinned HOST memory (zero-copy end to end): tile i+1's loads are issued
+// before tile i is reduced and stored, so the one s_waitcnt per tile waits on
+// PCIe reads (downstream) and writes (upstream) in flight together — the two
+// link directions overlap instead of all reads, then all writes.
+// ---------------------------------------------------------------------------
+template <int P>
+__global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                          const uint8_t* __restrict__ order, uint64_t block_vec,
+                                                          uint64_t ntiles) {
+    constexpr int TV = 32, RPW = P / 4, LPL = RPW / 2;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    auto issue = [&](uint64_t t, uint4* dst) {
+#pragma unroll
+        for (int k = 0; k < RPW / 2; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            __builtin_amdgcn_global_load_lds((global_u32*)src, (lds_u32*)&dst[(RPW * w + 2 * k) * TV], 16, 0, 2);
+        }
+    };
+    int cur = 0;
+    if (blockIdx.x < ntiles) issue(blockIdx.x, buf[0]);
+    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + gridDim.x < ntiles) issue(t + gridDim.x, buf[cur ^ 1]);
+        const uint4* tile = buf[cur];
+        const uint64_t v0 = t * TV;
+        const uint8_t* ord = order + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * h;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s = 1; s < LPL; s *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s) x[i] = add8(x[i], x[i + s]);
+        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+        if (h == 0) part[w * TV + c] = pw;
+        __syncthreads();
+        const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
+#pragma unroll
+        for (int k = 0; k < RPW / 2; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res);
+        }
+        cur ^= 1;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // LO allreduce of P ranks in one pass: the butterfly itself.  Rank x keeps
 // its own tree (for Swing the P results differ in bf16 rounding, exactly as
 // the reference's per-core LO results do).  Lane (q, x) = q * P + x holds
@@ -904,9 +957,28 @@ int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* bl
     return last_error();
 }
 
-int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream) {
+int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
+                      bool host_memory) {
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
-    return tree_dispatch<true>(ranks, stride, n / 8, total, order, n / 8 / total, nullptr, (hipStream_t)stream);
+    const uint64_t nv = n / 8, bv = nv / total;
+    if (host_memory && total >= 8 && nv % 32 == 0 && bv % 32 == 0) {
+        const uint64_t tiles = nv / 32;
+        static const uint64_t cap = [] {  // PCIe-bound: 32 workgroups keep both link directions busy (tools/pcie_probe.py)
+            const char* e = std::getenv("ALLRED_PIPE_GRID");
+            return e ? std::strtoull(e, nullptr, 10) : 32ull;
+        }();
+        const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
+        hipStream_t st = (hipStream_t)stream;
+        switch (total) {
+            case 8: hipLaunchKernelGGL((k_tree_lds_pipe<8>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
+            case 16: hipLaunchKernelGGL((k_tree_lds_pipe<16>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
+            case 32: hipLaunchKernelGGL((k_tree_lds_pipe<32>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
+            case 64: hipLaunchKernelGGL((k_tree_lds_pipe<64>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
+            default: return ALLRED_ERR_UNSUPPORTED;
+        }
+        return last_error();
+    }
+    return tree_dispatch<true>(ranks, stride, nv, total, order, bv, nullptr, (hipStream_t)stream);
 }
 
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,

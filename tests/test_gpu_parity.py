@@ -244,3 +244,22 @@ def test_linearity_and_idempotent_layout():
     torch.cuda.synchronize()
     assert torch.equal(buf, torch.full_like(buf, 192.0))
     plan.close()
+
+
+@pytest.mark.parametrize("grid", [(4, 16), (8, 64)])
+@pytest.mark.parametrize("tiles", [1, 5, 40])
+def test_fused_bo_on_pinned_host_buckets(grid, tiles):
+    """Zero-copy end to end: the fused BO pass on buckets in pinned host memory
+    takes the pipelined form (k_tree_lds_pipe: persistent grid, double-buffered
+    LDS tiles, looping over more tiles than workgroups at 40 tiles)."""
+    side, total = grid
+    n = t.normalize_tiles(tiles, total, True) * 1024
+    ranks = rand_ranks(total, n, 900 + tiles + total)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("bo", t.SWING, side, want, total)
+    host = torch.from_numpy(np.stack(ranks).view(np.int16)).pin_memory()
+    plan = t.Plan(t.SWING, t.BO, side, n, total, t.EXEC_FUSED)
+    plan.execute(host.data_ptr(), n, None, torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    plan.close()
+    assert np.array_equal(host.numpy().view(np.uint16), np.stack(want))
