@@ -72,7 +72,12 @@ def cpu_baseline() -> dict:
     argv = [1, 1, SIDE, 13, TILES, 32, 0, 1]
     probe = oracle.loopback("bo", argv, reps=3)
     reps = int(min(400, max(5, 10.0 / max(probe["median_s"], 1e-4))))
-    out = oracle.loopback("bo", argv, reps=reps, timeout=300)
+    log = os.path.join(ROOT, "gpurun_out", "cpu_baseline_profile_log.csv")
+    os.makedirs(os.path.dirname(log), exist_ok=True)
+    out = oracle.loopback("bo", argv, reps=reps, timeout=300, profile_log=log)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from profile_analyzer import analyze  # profiler_results_analyzer.py statistics over the 64 ranks
+    per_rank = analyze(log)
     bytes_all = RANKS * ELEMS * 2
     return {
         "value": round(bytes_all / out["median_s"] / 1e9, 4),
@@ -82,6 +87,8 @@ def cpu_baseline() -> dict:
         "sample": (f"oracle loopback (64 forked rank processes, shared-memory buffers, semaphore handshakes) "
                    f"of the full config-2 allreduce, {reps} reps, median {out['median_s'] * 1e3:.3f} ms "
                    f"(min {out['min_s'] * 1e3:.3f}, max {out['max_s'] * 1e3:.3f}); mismatches {out['mismatches']}"),
+        "online_cpus": os.sysconf("SC_NPROCESSORS_ONLN"),
+        "per_rank_last_rep_ns": per_rank,
     }
 
 

@@ -501,7 +501,9 @@ static void rank_mem(int r, const or_schedule* s, size_t n, uint16_t* local_all,
     memcpy(local, dst, n * 2);
 }
 
-long or_loopback_run(const or_loopback_args* a, double* seconds) {
+long or_loopback_run(const or_loopback_args* a, double* seconds) { return or_loopback_run_stamps(a, seconds, NULL); }
+
+long or_loopback_run_stamps(const or_loopback_args* a, double* seconds, double* stamps) {
     int side = or_highest_power_of_two(a->side);
     int N = a->total > 0 ? a->total : side * side;
     int mem = a->variant == 2;
@@ -523,7 +525,8 @@ long or_loopback_run(const or_loopback_args* a, double* seconds) {
         or_random_bf16_vector(bytes, 100, a->seed + 1, a->round_mode, src1);
     }
     int reps = a->reps < 1 ? 1 : a->reps;
-    size_t shm_bytes = 4096 + (size_t)N * sizeof(rank_ctl) + 2 * (size_t)N * bytes + bytes + 8 * (size_t)reps;
+    size_t shm_bytes = 4096 + (size_t)N * sizeof(rank_ctl) + 2 * (size_t)N * bytes + bytes + 8 * (size_t)reps +
+                       16 * (size_t)reps * (size_t)N;
     uint8_t* shm = (uint8_t*)mmap(NULL, shm_bytes, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (shm == MAP_FAILED) { free(src0); free(src1); return -4; }
     memset(shm, 0, 4096 + (size_t)N * sizeof(rank_ctl));
@@ -533,6 +536,7 @@ long or_loopback_run(const or_loopback_args* a, double* seconds) {
     uint16_t* recv_all = local_all + (size_t)N * n;   /* recv buffers, or the common buffer for mem */
     uint16_t* dst = recv_all + (size_t)N * n;
     double* times = (double*)(dst + n);
+    double* rank_stamps = times + reps;   /* [reps][N][2] absolute CLOCK_MONOTONIC seconds */
     pid_t* pids = (pid_t*)calloc((size_t)N, sizeof(pid_t));
     for (int r = 0; r < N; ++r) {
         pid_t pid = fork();
@@ -547,6 +551,8 @@ long or_loopback_run(const or_loopback_args* a, double* seconds) {
                 if (mem) rank_mem(r, &s, n, local_all, recv_all, dst, ctl, &sync_count);
                 else rank_bo_lo(r, &s, bo, n, local_all, recv_all, ctl, (uint32_t)rep);
                 ctl[r].t_end = now_s();
+                rank_stamps[((size_t)rep * N + r) * 2] = ctl[r].t_start;
+                rank_stamps[((size_t)rep * N + r) * 2 + 1] = ctl[r].t_end;
                 barrier_wait(bar, (uint32_t)N);
                 if (r == 0) {
                     double t0 = 1e300, t1 = 0;
@@ -571,6 +577,12 @@ long or_loopback_run(const or_loopback_args* a, double* seconds) {
     long bad = 0;
     if (seconds)
         for (int rep = 0; rep < reps; ++rep) seconds[rep] = times[rep];
+    if (stamps) {
+        double t0 = 1e300;
+        for (int r = 0; r < N; ++r)
+            if (rank_stamps[(size_t)r * 2] < t0) t0 = rank_stamps[(size_t)r * 2];
+        for (size_t i = 0; i < (size_t)reps * N * 2; ++i) stamps[i] = rank_stamps[i] - t0;
+    }
     int pc = (a->print_core >= 0 && a->print_core < N) ? a->print_core : 0;
     bad = or_validate((const uint32_t*)(local_all + (size_t)pc * n), src0, src1, bytes / 4, (float)a->error,
                       (uint32_t)N, a->round_mode, NULL);

@@ -12,6 +12,13 @@
  * ALL_RED_LOOP normalisation of python/profiler_results_analyzer*.py), the
  * summary statistics of profiler_results_analyzer.py:39-56, mismatch count
  * and the number of online cores.  Used by bench.py's cpu_baseline leg.
+ *
+ * ORACLE_PROFILE_LOG=<path> also writes every rank's ALL_RED_LOOP
+ * ZONE_START / ZONE_END of every rep in the layout of tt-metal's
+ * profile_log_device.csv (metadata line, then the columns
+ * python/profiler_results_analyzer.py:9-22 reads: core_x, core_y, RISC
+ * processor type, time[cycles since reset], zone name, type), with a 1000 MHz
+ * "chip" clock, i.e. one cycle = 1 ns of host time.
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -53,9 +60,27 @@ int main(int argc, char** argv) {
     a.round_mode = argc > 12 ? atoi(argv[12]) : 0;
     if (a.reps < 1) a.reps = 1;
     double* t = (double*)calloc((size_t)a.reps, sizeof(double));
-    long bad = or_loopback_run(&a, t);
     int side = or_highest_power_of_two(a.side);
     int total = a.total > 0 ? a.total : side * side;
+    const char* log_path = getenv("ORACLE_PROFILE_LOG");
+    double* stamps = log_path ? (double*)calloc((size_t)a.reps * (size_t)total * 2, sizeof(double)) : NULL;
+    long bad = or_loopback_run_stamps(&a, t, stamps);
+    if (stamps && bad >= 0) {
+        FILE* f = fopen(log_path, "w");
+        if (f) {
+            fprintf(f, "ARCH: cpu_loopback, CHIP_FREQ[MHz]: 1000\n");
+            fprintf(f, "PCIe slot, core_x, core_y, RISC processor type, timer_id, time[cycles since reset], stat value, "
+                       "run ID, run host ID,  zone name, type, source line, source file\n");
+            for (int rep = 0; rep < a.reps; ++rep)
+                for (int r = 0; r < total; ++r)
+                    for (int e = 0; e < 2; ++e)
+                        fprintf(f, "0,%d,%d,BRISC,%d,%llu,0,%d,%d,ALL_RED_LOOP,%s,0,allred_oracle.c\n", r % side,
+                                r / side, e, (unsigned long long)(stamps[((size_t)rep * total + r) * 2 + e] * 1e9),
+                                rep, rep, e ? "ZONE_END" : "ZONE_START");
+            fclose(f);
+        }
+    }
+    free(stamps);
     int nt = or_normalize_tiles(a.tiles_arg, total, a.variant == 2 ? 1 : a.bo);
     double* s = (double*)calloc((size_t)a.reps, sizeof(double));
     memcpy(s, t, sizeof(double) * (size_t)a.reps);

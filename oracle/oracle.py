@@ -133,14 +133,20 @@ def reference_inputs(side: int, total: int, n_elems: int, seed: int, round_mode:
     return s0, s1, ranks
 
 
-def loopback(variant: str, argv: list, reps: int = 5, total: int = 0, round_mode: int = 0, timeout: float = 600):
-    """Run the multi-process loopback restatement; returns its JSON summary."""
+def loopback(variant: str, argv: list, reps: int = 5, total: int = 0, round_mode: int = 0, timeout: float = 600,
+             profile_log: str | None = None):
+    """Run the multi-process loopback restatement; returns its JSON summary.
+    profile_log: also write per-rank ALL_RED_LOOP stamps there (tt-metal
+    profile_log_device.csv layout)."""
     import json
     args = [CLI, variant, *map(str, argv)]
     while len(args) < 10:
         args.append("0")
     args += [str(reps), str(total), str(round_mode)]
-    p = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    env = dict(os.environ)
+    if profile_log:
+        env["ORACLE_PROFILE_LOG"] = profile_log
+    p = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     if p.returncode != 0:
         raise RuntimeError(p.stderr)
     first = p.stdout.splitlines()[0]

@@ -108,3 +108,22 @@ def test_loopback_config1_known_answer():
 def test_loopback_multiprocess(variant, argv):
     out = oracle.loopback(variant, argv, reps=2)
     assert out["mismatches"] == 0 and out["ranks"] == 64
+
+
+def test_loopback_profile_log_per_rank_stats(tmp_path):
+    """Per-rank ALL_RED_LOOP stamps in the profile_log_device.csv layout, read
+    back with the reference analyzer's statistics (tools/profile_analyzer.py)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from profile_analyzer import analyze
+    log = str(tmp_path / "profile_log_device.csv")
+    out = oracle.loopback("bo", [1, 1, 4, 13, 1, 32, 0, 1], reps=3, total=8, profile_log=log)
+    assert out["mismatches"] == 0
+    lines = open(log).read().splitlines()
+    assert lines[0].startswith("ARCH:") and len(lines) == 2 + 3 * 8 * 2
+    r = analyze(log)
+    assert r["cores"] == 8
+    assert 0 < r["min"] <= r["q1"] <= r["median"] <= r["q3"] <= r["max"]
+    # the last rep's per-rank span never exceeds that rep's max-end - min-start
+    assert r["max"] <= out["seconds"][-1] * 1e9 + 1
