@@ -240,38 +240,85 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds(uint16_t* __restrict__ rank
 }
 
 // ---------------------------------------------------------------------------
-// k_tree_lds with a persistent grid and two LDS tile buffers, for buckets in
-// pinned HOST memory (zero-copy end to end): tile i+1's loads are issued
-// before tile i is reduced and stored, so the one s_waitcnt per tile waits on
-// PCIe reads (downstream) and writes (upstream) in flight together — the two
-// link directions overlap instead of all reads, then all writes.
+// k_tree_lds with a persistent grid and D+1 LDS tile buffers (prefetch depth
+// D): tile j+D's loads are issued before tile j is reduced and stored, and
+// the wait before tile j is an exact s_waitcnt vmcnt(n) that leaves every op
+// issued after tile j's loads in flight (CDNA3/4 count VMEM loads, LDS-DMA
+// loads and stores on one in-order vmcnt).  Loads of later tiles and stores
+// of earlier ones overlap: on pinned HOST buckets (zero-copy end to end) the
+// two PCIe directions run at once; on HBM it hides the per-tile ramp.
 // ---------------------------------------------------------------------------
-template <int P>
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int OPS, int D>
+__device__ __forceinline__ void wait_tile(int after) {  // after = tiles' worth of ops issued after this tile's loads
+    static_assert(2 * D * OPS <= 63, "vmcnt is 6 bits");
+    switch (after) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<OPS>(); break;
+        case 2: wait_vm<2 * OPS>(); break;
+        case 3: if constexpr (D >= 2) { wait_vm<3 * OPS>(); break; } else { wait_vm<0>(); break; }
+        default: wait_vm<0>(); break;
+    }
+}
+
+// LDS-DMA load issued as inline asm: the compiler's waitcnt pass then does
+// not see an LDS write in flight and does not put vmcnt(0) in front of every
+// LDS read (which would serialise the pipeline); wait_tile() is the only wait.
+// (m0 is reserved for the compiler; nothing else in the kernels that use this
+// reads it — checked in the ISA — so clobbering it here is safe.)
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_base) {
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off nt" ::"v"(src), "s"(lds_base) : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
+// workgroup barrier without the release fence of __syncthreads (which waits
+// vmcnt(0)); LDS traffic is ordered by the lgkmcnt wait
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int P, int D>
 __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                           const uint8_t* __restrict__ order, uint64_t block_vec,
                                                           uint64_t ntiles) {
-    constexpr int TV = 32, RPW = P / 4, LPL = RPW / 2;
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    constexpr int TV = 32, RPW = P / 4, LPL = RPW / 2, OPS = RPW / 2, NB = D + 1;
+    __shared__ __attribute__((aligned(16))) uint4 buf[NB][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[P * ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 31, h = lane >> 5;
-    auto issue = [&](uint64_t t, uint4* dst) {
+    // the order rows of all P blocks, once (plain loads, waited for here)
+    for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
+        reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
+    __syncthreads();
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] +
+        (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
 #pragma unroll
-        for (int k = 0; k < RPW / 2; ++k) {
+        for (int k = 0; k < OPS; ++k) {
             const int r = RPW * w + 2 * k + h;
             const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
-            __builtin_amdgcn_global_load_lds((global_u32*)src, (lds_u32*)&dst[(RPW * w + 2 * k) * TV], 16, 0, 2);
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
         }
     };
-    int cur = 0;
-    if (blockIdx.x < ntiles) issue(blockIdx.x, buf[0]);
-    for (uint64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t + gridDim.x < ntiles) issue(t + gridDim.x, buf[cur ^ 1]);
-        const uint4* tile = buf[cur];
-        const uint64_t v0 = t * TV;
-        const uint8_t* ord = order + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * h;
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;  // tiles of this WG
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+        if (d < mine) issue(blockIdx.x + d * G, d);
+    for (int j = 0; j < mine; ++j) {
+        const int rem = mine - 1 - j;
+        wait_tile<OPS, D>((j < D ? j : D) + (rem < D - 1 ? rem : D - 1));
+        lds_barrier();
+        if (j + D < mine) issue(blockIdx.x + (uint64_t)(j + D) * G, (j + D) % NB);
+        const uint4* tile = buf[j % NB];
+        const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
+        const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * h;
         uint4 x[LPL];
 #pragma unroll
         for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
@@ -281,14 +328,13 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
             for (int i = 0; i < LPL; i += 2 * s) x[i] = add8(x[i], x[i + s]);
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
         if (h == 0) part[w * TV + c] = pw;
-        __syncthreads();
+        lds_barrier();
         const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
 #pragma unroll
-        for (int k = 0; k < RPW / 2; ++k) {
+        for (int k = 0; k < OPS; ++k) {
             const int r = RPW * w + 2 * k + h;
             st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res);
         }
-        cur ^= 1;
     }
 }
 
@@ -392,6 +438,72 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64(uint16_t* __restrict
         const int r = 16 * w + 2 * k + h;
         st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (r & 31)),
               tile[(16 * w + 2 * k + h) * TV + l32]);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_butterfly_lds64 on a persistent grid with two LDS tiles: tile j+1's
+// LDS-DMA loads are in flight while tile j runs its butterfly and leaves;
+// the only vmcnt wait lets tile j-1's stores stay outstanding (see
+// k_tree_lds_pipe).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                                 const int16_t* __restrict__ partner, int steps,
+                                                                 uint64_t ntiles) {
+    constexpr int TV = 32, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][64 * TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int x = lane;
+    int src_lane[ALLRED_MAX_STEPS];
+#pragma unroll
+    for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(16 * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = 16 * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + (l32 ^ (r & 31));
+            lds_dma16(src, wbase + (uint32_t)(b * 64 * TV * 16 + 2 * k * TV * 16));
+        }
+    };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    if (mine > 0) issue(blockIdx.x, 0);
+    for (int j = 0; j < mine; ++j) {
+        wait_tile<OPS, 1>(j < 1 ? j : 1);
+        lds_barrier();
+        if (j + 1 < mine) issue(blockIdx.x + (uint64_t)(j + 1) * G, (j + 1) & 1);
+        uint4* tile = buf[j & 1];
+        const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
+        uint4 val[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) val[i] = tile[x * TV + ((8 * w + i) ^ (x & 31))];
+#pragma unroll
+        for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+            if (k >= steps) break;
+            const int sl = src_lane[k];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint4 o;
+                o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].x);
+                o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].y);
+                o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].z);
+                o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].w);
+                val[i] = add8(val[i], o);
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];  // own columns only
+        lds_barrier();
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = 16 * w + 2 * k + h;
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (r & 31)),
+                  tile[(16 * w + 2 * k + h) * TV + l32]);
+        }
     }
 }
 
@@ -814,6 +926,24 @@ bool tree_force_registers() {
     return v;
 }
 
+// ALLRED_TREE=pipe forces the persistent double-buffered forms on device
+// memory for every shape, ALLRED_TREE=lds the one-tile-per-workgroup forms (A/B)
+bool tree_force_pipe() {
+    static const bool v = [] {
+        const char* e = std::getenv("ALLRED_TREE");
+        return e && e[0] == 'p';
+    }();
+    return v;
+}
+
+bool tree_force_lds() {
+    static const bool v = [] {
+        const char* e = std::getenv("ALLRED_TREE");
+        return e && e[0] == 'l';
+    }();
+    return v;
+}
+
 int last_error() { return hip_status((int)hipGetLastError()); }
 
 template <bool WRITE_ALL>
@@ -961,21 +1091,45 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
                       bool host_memory) {
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, bv = nv / total;
-    if (host_memory && total >= 8 && nv % 32 == 0 && bv % 32 == 0) {
+    // persistent double-buffered form: host buckets always; HBM buckets of 64
+    // ranks with >= 1024 tiles (config 2: 15.2 vs 16.5 us for one tile per
+    // workgroup, 2 workgroups per CU = 512, each CU 5 tiles)
+    const bool pipe_hbm = total == 64 && nv / 32 >= 1024 && !tree_force_lds() && !tree_force_registers();
+    if ((host_memory || pipe_hbm || tree_force_pipe()) && total >= 8 && nv % 32 == 0 && bv % 32 == 0) {
         const uint64_t tiles = nv / 32;
-        static const uint64_t cap = [] {  // PCIe-bound: 32 workgroups keep both link directions busy (tools/pcie_probe.py)
+        // PCIe-bound host buckets: 32 workgroups keep both link directions busy (tools/pcie_probe.py);
+        // ALLRED_PIPE_GRID / ALLRED_PIPE_DEPTH override (A/B)
+        static const uint64_t cap_env = [] {
             const char* e = std::getenv("ALLRED_PIPE_GRID");
-            return e ? std::strtoull(e, nullptr, 10) : 32ull;
+            return e ? std::strtoull(e, nullptr, 10) : 0ull;
         }();
+        static const int depth = [] {
+            const char* e = std::getenv("ALLRED_PIPE_DEPTH");
+            return e ? std::atoi(e) : 1;
+        }();
+        const uint64_t cap = cap_env ? cap_env : (host_memory ? 32 : 512);
         const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
         hipStream_t st = (hipStream_t)stream;
-        switch (total) {
-            case 8: hipLaunchKernelGGL((k_tree_lds_pipe<8>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
-            case 16: hipLaunchKernelGGL((k_tree_lds_pipe<16>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
-            case 32: hipLaunchKernelGGL((k_tree_lds_pipe<32>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
-            case 64: hipLaunchKernelGGL((k_tree_lds_pipe<64>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles); break;
-            default: return ALLRED_ERR_UNSUPPORTED;
+#define TSA_PIPE(PP, DD) \
+    hipLaunchKernelGGL((k_tree_lds_pipe<PP, DD>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles)
+        if (depth >= 2) {
+            switch (total) {
+                case 8: TSA_PIPE(8, 2); break;
+                case 16: TSA_PIPE(16, 2); break;
+                case 32: TSA_PIPE(32, 2); break;
+                case 64: TSA_PIPE(64, 2); break;
+                default: return ALLRED_ERR_UNSUPPORTED;
+            }
+        } else {
+            switch (total) {
+                case 8: TSA_PIPE(8, 1); break;
+                case 16: TSA_PIPE(16, 1); break;
+                case 32: TSA_PIPE(32, 1); break;
+                case 64: TSA_PIPE(64, 1); break;
+                default: return ALLRED_ERR_UNSUPPORTED;
+            }
         }
+#undef TSA_PIPE
         return last_error();
     }
     return tree_dispatch<true>(ranks, stride, nv, total, order, bv, nullptr, (hipStream_t)stream);
@@ -986,6 +1140,17 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
     if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
     hipStream_t st = (hipStream_t)stream;
+    // persistent pipelined form for >= 1024 tiles (640 kB: 23.9 vs 25.2-26.0 us)
+    if (total == 64 && nv % 32 == 0 && nv >= 32 * 256 && (tree_force_pipe() || (nv >= 32 * 1024 && !tree_force_lds()))) {
+        static const uint64_t cap = [] {
+            const char* e = std::getenv("ALLRED_PIPE_GRID");
+            return e ? std::strtoull(e, nullptr, 10) : 512ull;
+        }();
+        const uint64_t tiles = nv / 32;
+        hipLaunchKernelGGL(k_butterfly_lds64_pipe, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0, st,
+                           ranks, stride, d_partner, steps, tiles);
+        return last_error();
+    }
     if (total == 64 && nv % 32 == 0 && nv >= 32 * 256) {  // >= 256 tiles: the LDS-staged form pays
         hipLaunchKernelGGL(k_butterfly_lds64, dim3((unsigned)(nv / 32)), dim3(kBlock), 0, st, ranks, stride, d_partner,
                            steps);
