@@ -281,16 +281,20 @@ __device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_base) {
 // vmcnt(0)); LDS traffic is ordered by the lgkmcnt wait
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-template <int P, int D>
+// TV = 16-byte vectors per rank row of a tile (32: 32 KiB tiles at P = 64, two
+// workgroups per CU; 16: 16 KiB tiles, four per CU).  A wave-instruction
+// stages RPI = 64 / TV rank rows (1 KiB contiguous per row group).
+template <int P, int D, int TV>
 __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                           const uint8_t* __restrict__ order, uint64_t block_vec,
                                                           uint64_t ntiles) {
-    constexpr int TV = 32, RPW = P / 4, LPL = RPW / 2, OPS = RPW / 2, NB = D + 1;
+    constexpr int RPI = 64 / TV, RPW = P / 4, OPS = RPW / RPI, LPL = OPS, NB = D + 1;
+    static_assert(OPS >= 1, "tile too narrow for this rank count");
     __shared__ __attribute__((aligned(16))) uint4 buf[NB][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[P * ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 31, h = lane >> 5;
+    const int c = lane % TV, q = lane / TV;
     // the order rows of all P blocks, once (plain loads, waited for here)
     for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
         reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
@@ -301,9 +305,9 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
     auto issue = [&](uint64_t t, int b) {
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
-            const int r = RPW * w + 2 * k + h;
+            const int r = RPW * w + RPI * k + q;
             const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
-            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
         }
     };
     const uint64_t G = gridDim.x;
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
         if (j + D < mine) issue(blockIdx.x + (uint64_t)(j + D) * G, (j + D) % NB);
         const uint4* tile = buf[j % NB];
         const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
-        const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * h;
+        const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * q;
         uint4 x[LPL];
 #pragma unroll
         for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
@@ -326,13 +330,15 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
         for (int s = 1; s < LPL; s *= 2)
 #pragma unroll
             for (int i = 0; i < LPL; i += 2 * s) x[i] = add8(x[i], x[i + s]);
-        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
-        if (h == 0) part[w * TV + c] = pw;
+        uint4 pw = x[0];
+#pragma unroll
+        for (int s = TV; s < 64; s *= 2) pw = add8(pw, shfl_xor4(pw, s));   // tree levels across lane groups
+        if (q == 0) part[w * TV + c] = pw;
         lds_barrier();
         const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
-            const int r = RPW * w + 2 * k + h;
+            const int r = RPW * w + RPI * k + q;
             st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res);
         }
     }
@@ -647,6 +653,11 @@ __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, ui
 // boundaries on the stream carry the system-scope release / acquire of the
 // window bytes (HIP dispatch packets fence at system scope).
 // ---------------------------------------------------------------------------
+// bounded waits: 2^22 polls of an uncached word (~1 us each) ~ 4 s, far above
+// any legitimate skew between ranks, short enough that a broken peer set
+// degrades to a status bit within seconds per wait instead of hanging
+constexpr uint64_t kPeerSpinLimit = 1ull << 22;
+
 struct PeerPtrs {
     uint16_t* win[ALLRED_MAX_NODES];     // window of rank q (this parity), as mapped here
     uint32_t* flags[ALLRED_MAX_NODES];   // flag array of rank q, as mapped here
@@ -662,7 +673,7 @@ __global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, 
         uint32_t* mine = pp.flags[me] + t;
         for (uint64_t spin = 0;; ++spin) {
             if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
-            if (spin > (1ull << 24)) {  // ~ seconds: a peer never arrived
+            if (spin > kPeerSpinLimit) {  // ~ seconds: a peer never arrived
                 atomicOr(status, 1u);
                 break;
             }
@@ -742,7 +753,7 @@ __device__ inline void peer_signal_wait(const PeerPtrs& pp, int nranks, int me, 
         uint32_t* mine = pp.flags[me] + slot_base + t;
         for (uint64_t spin = 0;; ++spin) {
             if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
-            if (spin > (1ull << 24)) {
+            if (spin > kPeerSpinLimit) {
                 atomicOr(status, 1u);
                 break;
             }
@@ -837,7 +848,7 @@ __device__ inline void sched_wait(const PeerPtrs& pp, int me, uint32_t slot, int
         uint32_t* f = pp.flags[me] + slot + q;
         for (uint64_t spin = 0;; ++spin) {
             if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= value) break;
-            if (spin > (1ull << 24)) {
+            if (spin > kPeerSpinLimit) {
                 atomicOr(status, 1u);
                 break;
             }
@@ -1096,7 +1107,6 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
     // workgroup, 2 workgroups per CU = 512, each CU 5 tiles)
     const bool pipe_hbm = total == 64 && nv / 32 >= 1024 && !tree_force_lds() && !tree_force_registers();
     if ((host_memory || pipe_hbm || tree_force_pipe()) && total >= 8 && nv % 32 == 0 && bv % 32 == 0) {
-        const uint64_t tiles = nv / 32;
         // PCIe-bound host buckets: 32 workgroups keep both link directions busy (tools/pcie_probe.py);
         // ALLRED_PIPE_GRID / ALLRED_PIPE_DEPTH override (A/B)
         static const uint64_t cap_env = [] {
@@ -1107,25 +1117,38 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
             const char* e = std::getenv("ALLRED_PIPE_DEPTH");
             return e ? std::atoi(e) : 1;
         }();
-        const uint64_t cap = cap_env ? cap_env : (host_memory ? 32 : 512);
+        static const int tvsel = [] {  // ALLRED_PIPE_TV=16 selects 16-vector tiles (A/B)
+            const char* e = std::getenv("ALLRED_PIPE_TV");
+            return e ? std::atoi(e) : 32;
+        }();
+        const int TVs = (tvsel == 16 && total >= 16 && bv % 16 == 0) ? 16 : 32;
+        const uint64_t tiles = nv / TVs;
+        const uint64_t cap = cap_env ? cap_env : (host_memory ? 32 : (TVs == 16 ? 1024 : 512));
         const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
         hipStream_t st = (hipStream_t)stream;
-#define TSA_PIPE(PP, DD) \
-    hipLaunchKernelGGL((k_tree_lds_pipe<PP, DD>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles)
-        if (depth >= 2) {
+#define TSA_PIPE(PP, DD, TT) \
+    hipLaunchKernelGGL((k_tree_lds_pipe<PP, DD, TT>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles)
+        if (TVs == 16) {
             switch (total) {
-                case 8: TSA_PIPE(8, 2); break;
-                case 16: TSA_PIPE(16, 2); break;
-                case 32: TSA_PIPE(32, 2); break;
-                case 64: TSA_PIPE(64, 2); break;
+                case 16: TSA_PIPE(16, 1, 16); break;
+                case 32: TSA_PIPE(32, 1, 16); break;
+                case 64: if (depth >= 2) TSA_PIPE(64, 2, 16); else TSA_PIPE(64, 1, 16); break;
+                default: return ALLRED_ERR_UNSUPPORTED;
+            }
+        } else if (depth >= 2) {
+            switch (total) {
+                case 8: TSA_PIPE(8, 2, 32); break;
+                case 16: TSA_PIPE(16, 2, 32); break;
+                case 32: TSA_PIPE(32, 2, 32); break;
+                case 64: TSA_PIPE(64, 2, 32); break;
                 default: return ALLRED_ERR_UNSUPPORTED;
             }
         } else {
             switch (total) {
-                case 8: TSA_PIPE(8, 1); break;
-                case 16: TSA_PIPE(16, 1); break;
-                case 32: TSA_PIPE(32, 1); break;
-                case 64: TSA_PIPE(64, 1); break;
+                case 8: TSA_PIPE(8, 1, 32); break;
+                case 16: TSA_PIPE(16, 1, 32); break;
+                case 32: TSA_PIPE(32, 1, 32); break;
+                case 64: TSA_PIPE(64, 1, 32); break;
                 default: return ALLRED_ERR_UNSUPPORTED;
             }
         }
