@@ -290,6 +290,40 @@ def arm_stats(ms, nbytes, world, lo=False) -> dict:
             "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
 
 
+def link_probe(rank, world, dev) -> dict:
+    """Measured per-direction xGMI link rate (the xGMI-fraction
+    denominator from an RCCL sendrecv microbench): ranks 2i <-> 2i+1 exchange
+    128 MiB both ways at once over torch.distributed's nccl (= RCCL) backend."""
+    pg = dist.new_group(backend="nccl")
+    nbytes = 128 << 20
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    peer_rank = rank ^ 1
+
+    def xchg():
+        if peer_rank >= world:
+            return
+        ops = [dist.P2POp(dist.isend, a, peer_rank, group=pg), dist.P2POp(dist.irecv, b, peer_rank, group=pg)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+
+    for _ in range(2):
+        xchg()
+    torch.cuda.synchronize()
+    dist.barrier()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        xchg()
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    gbps = nbytes * reps / dt.item() / 1e9
+    dist.destroy_process_group(pg)
+    return {"bytes": nbytes, "reps": reps, "GBps_per_direction": round(gbps, 2),
+            "spec_GBps_per_direction": XGMI_LINK_DIR_GBPS, "pairs": "2i<->2i+1, both directions at once"}
+
+
 def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
     """Flat / hierarchical inter-GPU allreduces (BASELINE configs 3-5 regimes),
     each through RCCL (allred_dist_allreduce) and through the peer windows
@@ -390,6 +424,15 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         extras["peer_error"] = peer_err
     if args.extras:
         extras.update(xgmi_arms(comm, peer if transport == "peer" else None, world, dev, stream, side, total))
+        if world > 1:
+            try:
+                extras["link_probe"] = link_probe(rank, world, dev)
+                mb = extras["link_probe"]["GBps_per_direction"]
+                for v in extras.values():  # the fraction again against the MEASURED link rate
+                    if isinstance(v, dict) and "busbw_GBps" in v:
+                        v["xgmi_frac_measured_link"] = round(v["busbw_GBps"] / (7 * mb), 4)
+            except Exception as e:  # reported, never silently dropped
+                extras["link_probe"] = {"error": repr(e)}
     if peer is not None:
         st = torch.tensor([peer.status()], dtype=torch.int64)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
