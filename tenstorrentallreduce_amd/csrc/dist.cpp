@@ -252,6 +252,8 @@ int device_order(int algo, int side, int total, const uint8_t** out) {
 
 namespace tsa {
 
+int local_tree_order(int algo, int side, int total, const uint8_t** out) { return device_order(algo, side, total, out); }
+
 // The RCCL program's exchanges, as tables for the peer-mapped kernel
 // (k_peer_sched): per channel, the step partner and this rank's block masks
 // in the channel's labels, plus the channel slice in 16-byte vectors.

@@ -83,6 +83,8 @@ struct PeerProg {
     uint64_t base[kPeerMaxChannels] = {}, len[kPeerMaxChannels] = {};  // channel slice, 16-byte vectors
 };
 int peer_prog(const allred_dist_desc* d, int rank, PeerProg* out);
+// device copy of tree_order[0] of a (algo, side, total) schedule (cached per device)
+int local_tree_order(int algo, int side, int total, const uint8_t** out);
 
 int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                           size_t n, uint32_t epoch, uint32_t* status, void* stream);
@@ -91,6 +93,11 @@ int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epo
 // the scheduled form: one launch; flag values base_epoch + 1 .. base_epoch + 2S + 1
 int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
                       uint64_t half_vec, uint32_t base_epoch, uint32_t* status, void* stream);
+// hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast.
+// wins[q] = GPU q's window for this parity ([partial n][result n]); hflags[q]: [tiles][nranks + 1]
+int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
+                        uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
+                        void* stream);
 // one launch; epoch must grow by >= 1 per call
 int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                         size_t n, uint32_t epoch, uint32_t* status, void* stream);

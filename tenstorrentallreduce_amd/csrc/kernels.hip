@@ -925,6 +925,177 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
     }
 }
 
+// ---- hierarchical one-kernel form: 64 local ranks per GPU -------------------
+// The whole hierarchical step (local tree of the 64 virtual ranks -> mem_2D
+// across the W GPUs -> broadcast back to the 64 ranks) as ONE persistent
+// launch with per-tile flags, so the xGMI latency of one tile hides behind
+// the HBM streaming of the others.  Tile = 256 elements (512 B per rank row);
+// owner(t) = t / (tiles / W), i.e. the block ownership of allred_mem_2D, so
+// the bits equal tree_reduce + allred_peer_allreduce + broadcast.
+//   A (all my tiles, double-buffered LDS as k_tree_lds_pipe): partial of tile
+//     t -> my window's partial region (local, uncached); flagA[t][me] -> owner.
+//   R (my tiles that I own): wait flagA[t][*]; read the W partials (remote
+//     loads), fp32 sum owner first then ascending, one rounding -> my result
+//     region; flagB[t] -> every GPU.
+//   B (all my tiles): wait flagB[t]; read the result from the owner's window;
+//     store it to the 64 rank rows.
+// A never waits, R waits only for A, B only for R: with the grid resident
+// (2 workgroups per CU) every wait is reached and satisfied.
+struct HierPtrs {
+    uint16_t* win[ALLRED_MAX_NODES];   // GPU q's window, this parity: [partial n][result n]
+    uint32_t* hfl[ALLRED_MAX_NODES];   // GPU q's per-tile flags: [tile][W + 1]
+};
+
+__device__ inline void hier_wait(const uint32_t* f, uint32_t epoch, uint32_t* status) {
+    for (uint64_t spin = 0;; ++spin) {
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) return;
+        if (spin > kPeerSpinLimit) {
+            atomicOr(status, 1u);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_hier_oneshot(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                         const uint8_t* __restrict__ order, HierPtrs hp, int W, int me,
+                                                         uint64_t n, uint64_t ntiles, uint64_t tiles_per_owner,
+                                                         uint32_t epoch, uint32_t* status) {
+    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    __syncthreads();
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+        }
+    };
+    const uint64_t G = gridDim.x, nvec = n / 8;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    const uint32_t F = (uint32_t)W + 1;
+    uint4* my_partial = reinterpret_cast<uint4*>(hp.win[me]);
+    uint4* my_result = my_partial + nvec;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    // ---- A: local trees, partials published.  Each iteration starts with
+    // vmcnt(0): tile j's LDS-DMA and tile j-1's partial store are then done, so
+    // tile j-1's flag goes out there, one iteration late, without draining the
+    // prefetch of tile j+1 (issued after that wait).  (Interleaving R and B
+    // into this loop measured slower: 22.6 vs 19.6 us at W = 1 — each
+    // uncached round trip is then paid once per tile instead of once per batch.)
+    auto publish = [&](uint64_t t) {
+        if (threadIdx.x == 0)
+            __hip_atomic_store(hp.hfl[owner_of(t)] + t * F + me, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    if (mine > 0) issue(tile_of(0), 0);
+    for (int j = 0; j < mine; ++j) {
+        wait_vm<0>();
+        lds_barrier();
+        if (j > 0) publish(tile_of(j - 1));
+        if (j + 1 < mine) issue(tile_of(j + 1), (j + 1) & 1);
+        const uint4* tile = buf[j & 1];
+        const uint64_t v0 = tile_of(j) * TV;
+        const uint8_t* ord = ord_lds + RPW * w + LPL * h;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+        if (h == 0) part[w * TV + c] = pw;
+        lds_barrier();
+        if (w == 0 && h == 0)
+            st_nt(my_partial + v0 + c,
+                  add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c])));
+    }
+    wait_vm<0>();
+    if (mine > 0) publish(tile_of(mine - 1));
+    // ---- R: the tiles I own, 8 at a time: every flag, then every remote load in flight at once
+    {
+        int owned[8];
+        int no = 0;
+        auto flush = [&]() {
+            for (int i = threadIdx.x; i < no * W; i += kBlock)
+                hier_wait(hp.hfl[me] + tile_of(owned[i / W]) * F + i % W, epoch, status);
+            lds_barrier();
+            const int b = threadIdx.x / TV;
+            if (b < no) {
+                const uint64_t v0 = tile_of(owned[b]) * TV;
+                const uint4 s0 = ld_nt(my_partial + v0 + c);
+                float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y),
+                              lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+                for (int q0 = 0; q0 < W; q0 += 8) {   // 8 remote partials in flight at once
+                    uint4 y[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (q0 + i < W && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(hp.win[q0 + i]) + v0 + c);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        if (q0 + i >= W || q0 + i == me) continue;
+                        a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                        a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                        a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                        a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+                    }
+                }
+                uint4 o;
+                o.x = pack_rne(a[0], a[1]);
+                o.y = pack_rne(a[2], a[3]);
+                o.z = pack_rne(a[4], a[5]);
+                o.w = pack_rne(a[6], a[7]);
+                st_nt(my_result + v0 + c, o);
+            }
+            wait_vm<0>();     // results are in HBM (uncached) before their flags
+            lds_barrier();
+            for (int i = threadIdx.x; i < no * W; i += kBlock)
+                __hip_atomic_store(hp.hfl[i % W] + tile_of(owned[i / W]) * F + W, epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            no = 0;
+        };
+        for (int j = 0; j < mine; ++j) {
+            if (owner_of(tile_of(j)) != me) continue;
+            owned[no++] = j;
+            if (no == 8) flush();
+        }
+        if (no) flush();
+    }
+    // ---- B: results back to the 64 rank rows, 4 tiles' remote loads in flight at once
+    constexpr int BB = 4;
+    for (int j0 = 0; j0 < mine; j0 += BB) {
+        const int nb = mine - j0 < BB ? mine - j0 : BB;
+        if (threadIdx.x < (unsigned)nb) hier_wait(hp.hfl[me] + tile_of(j0 + (int)threadIdx.x) * F + W, epoch, status);
+        lds_barrier();
+        uint4 res[BB];
+#pragma unroll
+        for (int b = 0; b < BB; ++b) {
+            if (b >= nb) break;
+            const uint64_t t = tile_of(j0 + b);
+            res[b] = ld_nt(reinterpret_cast<const uint4*>(hp.win[owner_of(t)]) + nvec + t * TV + c);
+        }
+#pragma unroll
+        for (int b = 0; b < BB; ++b) {
+            if (b >= nb) break;
+            const uint64_t v0 = tile_of(j0 + b) * TV;
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res[b]);
+            }
+        }
+    }
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ALLRED_TREE=registers selects the register-only k_tree for the fused BO pass
@@ -1046,6 +1217,23 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
     if (gc < 1) gc = 1;
     hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
                        bucket, half_vec, base_epoch, status);
+    return last_error();
+}
+
+int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
+                        uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
+                        void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > ALLRED_MAX_NODES || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks))
+        return ALLRED_ERR_ARG;
+    HierPtrs hp{};
+    for (int q = 0; q < nranks; ++q) {
+        hp.win[q] = wins[q];
+        hp.hfl[q] = hflags[q];
+    }
+    const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);   // 2 per CU: the whole grid resident
+    hipLaunchKernelGGL(k_hier_oneshot, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, hp,
+                       nranks, me, (uint64_t)n, ntiles, ntiles / nranks, epoch, status);
     return last_error();
 }
 

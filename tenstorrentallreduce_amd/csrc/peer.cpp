@@ -14,7 +14,9 @@
 // system-scope atomics (bounded spins set a status bit instead of hanging).
 // Buckets up to allred_peer_set_oneshot_max() bytes (default 4 MiB) run the
 // same three phases as ONE kernel (k_peer_oneshot): workgroup g syncs only
-// with workgroup g of the peers, through per-workgroup flag slots.
+// with workgroup g of the peers, through per-workgroup flag slots.  With 64
+// local ranks per GPU the local tree and the broadcast join that kernel too
+// (k_hier_oneshot, per-tile flags behind the window parities).
 // Windows are double-buffered by call parity: call k+2 can only overwrite a
 // window after every peer passed call k+1's first barrier, i.e. finished
 // reading call k's windows.
@@ -33,6 +35,9 @@ struct allred_peer {
     uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp
     uint32_t* status = nullptr;     // device status word
     bool flags_uncached = false, win_uncached = false;
+    size_t hfl_off = 0;             // byte offset of the per-tile flags behind the two window parities
+    size_t hfl_bytes = 0;
+    uint32_t* peer_hfl[ALLRED_MAX_NODES] = {};
     uint16_t* peer_win[ALLRED_MAX_NODES] = {};
     uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
     bool opened[ALLRED_MAX_NODES] = {};
@@ -56,10 +61,15 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     (void)hipGetDevice(&p->device);
     p->max_elems = (max_elems + 127) / 128 * 128;  // LO halves stay 64-element aligned
     // windows are uncached too: peers read them over xGMI straight from HBM, so
-    // no write may linger in one of this GPU's eight per-XCD L2s
-    if (hipExtMallocWithFlags((void**)&p->win, 2 * p->max_elems * 2, hipDeviceMallocUncached) == hipSuccess) {
+    // no write may linger in one of this GPU's eight per-XCD L2s.  Behind the
+    // two parities: the hierarchical form's per-tile flags, [tiles][nranks + 1]
+    // for up to max_elems / 2 elements per call (256-element tiles).
+    p->hfl_off = 2 * p->max_elems * 2;
+    p->hfl_bytes = 4 * (size_t)(nranks + 1) * (p->max_elems / 2 / 256 + 1);
+    const size_t win_bytes = p->hfl_off + p->hfl_bytes;
+    if (hipExtMallocWithFlags((void**)&p->win, win_bytes, hipDeviceMallocUncached) == hipSuccess) {
         p->win_uncached = true;
-    } else if (hipMalloc((void**)&p->win, 2 * p->max_elems * 2) != hipSuccess) {
+    } else if (hipMalloc((void**)&p->win, win_bytes) != hipSuccess) {
         delete p;
         return ALLRED_ERR_NOMEM;
     }
@@ -71,6 +81,7 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
         return ALLRED_ERR_NOMEM;
     }
     if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, kPeerFlagBytes) != hipSuccess ||
+        hipMemset(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off, 0, p->hfl_bytes) != hipSuccess ||
         hipMemset(p->status, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(p->win);
         (void)hipFree(p->flags);
@@ -99,6 +110,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
         if (q == p->rank) {
             p->peer_win[q] = p->win;
             p->peer_flags[q] = p->flags;
+            p->peer_hfl[q] = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off);
             continue;
         }
         hipIpcMemHandle_t hw, hf;
@@ -110,6 +122,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
         if (hipIpcOpenMemHandle(&f, hf, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ALLRED_ERR_HIP;
         p->peer_win[q] = static_cast<uint16_t*>(w);
         p->peer_flags[q] = static_cast<uint32_t*>(f);
+        p->peer_hfl[q] = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(w) + p->hfl_off);
         p->opened[q] = true;
     }
     p->connected = true;
@@ -133,6 +146,22 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
     if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     uint16_t* bucket = buf;
     int st = ALLRED_OK;
+    const bool one_kernel = n * 2 <= p->oneshot_max && p->win_uncached && p->flags_uncached;
+    if (one_kernel && local_ranks == 64 && n % (256 * (size_t)p->nranks) == 0 && 2 * n <= p->max_elems) {
+        // the whole hierarchical step in one launch (k_hier_oneshot): same bits as
+        // tree_reduce + the mem_2D exchange + broadcast below
+        const uint8_t* order = nullptr;
+        st = local_tree_order(local_algo, local_side, local_ranks, &order);
+        if (st != ALLRED_OK) return st;
+        uint16_t* wins[ALLRED_MAX_NODES];
+        parity_windows(p, wins);
+        st = launch_hier_oneshot(buf, n, order, wins, p->peer_hfl, p->nranks, p->rank, n, p->calls + 1u, p->status,
+                                 stream);
+        if (st != ALLRED_OK) return st;
+        ++p->calls;
+        p->last_all_peer = true;
+        return ALLRED_OK;
+    }
     if (local_ranks > 1) {
         if (!workspace) return ALLRED_ERR_ARG;
         bucket = static_cast<uint16_t*>(workspace);
@@ -141,7 +170,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
     }
     uint16_t* wins[ALLRED_MAX_NODES];
     parity_windows(p, wins);
-    if (n * 2 <= p->oneshot_max && p->win_uncached && p->flags_uncached)
+    if (one_kernel)
         st = launch_peer_oneshot(wins, p->peer_flags, p->nranks, p->rank, bucket, n, p->calls + 1u, p->status, stream);
     else
         st = launch_peer_allreduce(wins, p->peer_flags, p->nranks, p->rank, bucket, n, 2u * p->calls + 1u, p->status,

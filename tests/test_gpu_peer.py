@@ -92,6 +92,32 @@ def worker(rank, world, port, q):
         got = buf.cpu().numpy().view(np.uint16)
         if not all(np.array_equal(got[i], partials[rank]) for i in range(local)):
             fails.append(("hier", 0, 1))
+        # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form
+        # (k_hier_oneshot, per-tile flags) and the launch form, two calls back to back each
+        local, m = 64, 256 * world * 3
+        for mode, limit in (("hier_one_kernel", 1 << 40), ("hier_launches", 0)):
+            peer.set_oneshot_max(limit)
+            runs = []
+            for rep in range(2):
+                data = [np.random.default_rng(700 + 10 * rep + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
+                        for r in range(world)]
+                buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
+                ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
+                peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+                runs.append((data, buf, ws))
+            torch.cuda.synchronize()
+            for rep, (data, buf, _) in enumerate(runs):
+                partials = []
+                for d in data:
+                    loc = [x.copy() for x in d]
+                    oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+                    partials.append(loc[0])
+                oracle.allreduce("mem", 0, 1, partials, world)
+                got = buf.cpu().numpy().view(np.uint16)
+                bad = sum(int((got[i] != partials[rank]).sum()) for i in range(local))
+                if bad:
+                    fails.append((mode, rep, bad))
+            dist.barrier()
         status = peer.status()
         dist.barrier()
         peer.close()
