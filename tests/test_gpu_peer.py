@@ -128,7 +128,7 @@ def worker(rank, world, port, q):
         q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_peer_one_shot_multi_process_one_gpu(world):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
