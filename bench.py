@@ -329,8 +329,10 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
     each through RCCL (allred_dist_allreduce) and through the peer windows
     (allred_peer_dist_allreduce: same program, same bits, one kernel)."""
     out = {}
-    arms = [("config4_swing_bo_256MiB_all_links", t.SWING, t.BO, 256 << 20, 5, 0, 1),
-            ("config4_swing_bo_256MiB_one_link", t.SWING, t.BO, 256 << 20, 3, 1, 1),
+    # BASELINE config 4: 8-rank Swing BO, 1 GiB per rank (all links = link-spreading channels; one link = plain)
+    arms = [("config4_swing_bo_1GiB_all_links", t.SWING, t.BO, 1 << 30, 3, 0, 1),
+            ("config4_swing_bo_1GiB_one_link", t.SWING, t.BO, 1 << 30, 2, 1, 1),
+            ("swing_bo_256MiB_all_links", t.SWING, t.BO, 256 << 20, 5, 0, 1),
             ("config3_recdub_bo_640kB", t.RECDUB, t.BO, ELEMS * 2, 50, 0, 1),
             ("hierarchical_all_links", t.SWING, t.BO, ELEMS * 2, 50, world - 1, RANKS),
             ("hierarchical_lo_partial", t.SWING, t.LO, ELEMS * 2, 50, 1, RANKS)]
@@ -361,7 +363,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     uid = [t.Comm.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(uid, src=0)
     comm = t.Comm(uid[0], world, rank, local_rank)
-    peer, peer_err = open_peer(rank, world, local_rank, (256 << 20) // 2)
+    peer, peer_err = open_peer(rank, world, local_rank, (1 << 30) // 2)   # windows for 1 GiB buckets
     stream = torch.cuda.Stream(device=dev)
     desc = t.dist_desc(t.SWING, t.BO, side, total, ELEMS, local_ranks=RANKS, local_side=SIDE, local_algo=t.SWING)
     buf = torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev)
