@@ -265,6 +265,21 @@ __device__ __forceinline__ void wait_tile(int after) {  // after = tiles' worth 
     }
 }
 
+// vmcnt(k * OPS) for a run-time k in 0..7
+template <int OPS>
+__device__ __forceinline__ void wait_units(int k) {
+    switch (k) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<OPS>(); break;
+        case 2: wait_vm<(2 * OPS < 63 ? 2 * OPS : 63)>(); break;
+        case 3: wait_vm<(3 * OPS < 63 ? 3 * OPS : 63)>(); break;
+        case 4: wait_vm<(4 * OPS < 63 ? 4 * OPS : 63)>(); break;
+        case 5: wait_vm<(5 * OPS < 63 ? 5 * OPS : 63)>(); break;
+        case 6: wait_vm<(6 * OPS < 63 ? 6 * OPS : 63)>(); break;
+        default: wait_vm<(7 * OPS < 63 ? 7 * OPS : 63)>(); break;
+    }
+}
+
 // LDS-DMA load issued as inline asm: the compiler's waitcnt pass then does
 // not see an LDS write in flight and does not put vmcnt(0) in front of every
 // LDS read (which would serialise the pipeline); wait_tile() is the only wait.
@@ -284,21 +299,26 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 // TV = 16-byte vectors per rank row of a tile (32: 32 KiB tiles at P = 64, two
 // workgroups per CU; 16: 16 KiB tiles, four per CU).  A wave-instruction
 // stages RPI = 64 / TV rank rows (1 KiB contiguous per row group).
-template <int P, int D, int TV>
+// WRITE_ALL = false: the hierarchical partial — the tree of every tile goes to
+// `out` (one row; wave 0 issues its one store per tile, so its wait leaves
+// that one store in flight and the other waves wait for their loads alone).
+// REL (early release, two buffers): tile j+2's loads go into tile j's buffer
+// as soon as every wave has read tile j out of LDS (after the partials'
+// barrier), before tile j's stores and before the wait for tile j+1 — so two
+// tiles' loads are in flight per workgroup most of the time instead of one.
+template <int P, int D, int TV, bool WRITE_ALL = true, bool REL = false>
 __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                           const uint8_t* __restrict__ order, uint64_t block_vec,
-                                                          uint64_t ntiles) {
+                                                          uint64_t ntiles, uint16_t* __restrict__ out) {
     constexpr int RPI = 64 / TV, RPW = P / 4, OPS = RPW / RPI, LPL = OPS, NB = D + 1;
     static_assert(OPS >= 1, "tile too narrow for this rank count");
+    static_assert(WRITE_ALL || D == 1, "partial form is double-buffered only");
+    static_assert(!REL || (WRITE_ALL && (2 * NB - 1) * OPS <= 63), "early release: full form, vmcnt <= 63");
     __shared__ __attribute__((aligned(16))) uint4 buf[NB][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[P * ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
-    // the order rows of all P blocks, once (plain loads, waited for here)
-    for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
-        reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
-    __syncthreads();
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] +
         (uint32_t)(RPW * w * TV * 16));
@@ -312,14 +332,30 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
     };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;  // tiles of this WG
+    // the order rows of all P blocks, once, then the first tiles' loads
+    // (issuing those first measured slower: 15.65 vs 15.3 us at config 2)
+    for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
+        reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
+    __syncthreads();
 #pragma unroll
-    for (int d = 0; d < D; ++d)
+    for (int d = 0; d < (REL ? NB : D); ++d)
         if (d < mine) issue(blockIdx.x + d * G, d);
     for (int j = 0; j < mine; ++j) {
         const int rem = mine - 1 - j;
-        wait_tile<OPS, D>((j < D ? j : D) + (rem < D - 1 ? rem : D - 1));
+        if (REL && WRITE_ALL) {
+            // issued after tile j's loads (OPS ops each): the stores of tiles
+            // j-NB .. j-1 (those that exist) and the loads of tiles j+1 .. j+NB-1
+            // (prologue or earlier iterations, those that exist)
+            wait_units<OPS>((j < NB ? j : NB) + (rem < NB - 1 ? rem : NB - 1));
+        } else if (WRITE_ALL) {
+            wait_tile<OPS, D>((j < D ? j : D) + (rem < D - 1 ? rem : D - 1));
+        } else if (j > 0 && w == 0) {
+            wait_vm<1>();   // tile j-1's partial store may stay in flight
+        } else {
+            wait_vm<0>();
+        }
         lds_barrier();
-        if (j + D < mine) issue(blockIdx.x + (uint64_t)(j + D) * G, (j + D) % NB);
+        if (!REL && j + D < mine) issue(blockIdx.x + (uint64_t)(j + D) * G, (j + D) % NB);
         const uint4* tile = buf[j % NB];
         const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
         const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * q;
@@ -334,8 +370,13 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 #pragma unroll
         for (int s = TV; s < 64; s *= 2) pw = add8(pw, shfl_xor4(pw, s));   // tree levels across lane groups
         if (q == 0) part[w * TV + c] = pw;
-        lds_barrier();
+        lds_barrier();   // every wave has read tile j out of buf[j % NB]
+        if (REL && j + NB < mine) issue(blockIdx.x + (uint64_t)(j + NB) * G, j % NB);
         const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
+        if (!WRITE_ALL) {
+            if (w == 0 && q == 0) st_nt(reinterpret_cast<uint4*>(out) + v0 + c, res);
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             const int r = RPW * w + RPI * k + q;
@@ -461,10 +502,6 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int h = lane >> 5, l32 = lane & 31;
     const int x = lane;
-    int src_lane[ALLRED_MAX_STEPS];
-#pragma unroll
-    for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(16 * w * TV * 16));
     auto issue = [&](uint64_t t, int b) {
@@ -477,6 +514,12 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
     };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    // partner table first, then the first tile's loads (the other order
+    // measured slower: 24.0-24.3 vs 23.6-23.9 us at 640 kB)
+    int src_lane[ALLRED_MAX_STEPS];
+#pragma unroll
+    for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (mine > 0) issue(blockIdx.x, 0);
     for (int j = 0; j < mine; ++j) {
         wait_tile<OPS, 1>(j < 1 ? j : 1);
@@ -1126,11 +1169,31 @@ bool tree_force_lds() {
     return v;
 }
 
+// early-release pipelined tree forms (default; ALLRED_PIPE_REL=0 selects the
+// plain double-buffered form, 3 / 4 the one-workgroup-per-CU 3 / 4 buffer forms: A/B)
+int pipe_rel() {
+    static const int v = [] {
+        const char* e = std::getenv("ALLRED_PIPE_REL");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
 int last_error() { return hip_status((int)hipGetLastError()); }
 
 template <bool WRITE_ALL>
 int tree_dispatch(uint16_t* ranks, uint64_t stride, uint64_t n_vec, int total, const uint8_t* order,
                   uint64_t block_vec, uint16_t* out, hipStream_t st) {
+    // hierarchical partial of 64 ranks, >= 1024 tiles: the persistent
+    // double-buffered form (2 workgroups per CU), as the fused pass
+    if (!WRITE_ALL && total == 64 && n_vec % 32 == 0 && block_vec == 0 && !tree_force_lds() &&
+        !tree_force_registers() && (n_vec / 32 >= 1024 || tree_force_pipe())) {
+        const uint64_t tiles = n_vec / 32;
+        // (the early-release form measured slower here: 10.4 vs 9.6 us, read-only stream)
+        hipLaunchKernelGGL((k_tree_lds_pipe<64, 1, 32, false>), dim3((unsigned)(tiles < 512 ? tiles : 512)),
+                           dim3(kBlock), 0, st, ranks, stride, order, (uint64_t)0, tiles, out);
+        return last_error();
+    }
     // LDS-staged form: whole 32-vector tiles inside one block (any tile when block_vec == 0)
     if (total >= 8 && n_vec % 32 == 0 && (block_vec == 0 || block_vec % 32 == 0) && (block_vec || !WRITE_ALL) &&
         !tree_force_registers()) {
@@ -1309,13 +1372,14 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
             const char* e = std::getenv("ALLRED_PIPE_TV");
             return e ? std::atoi(e) : 32;
         }();
+        const int rel = pipe_rel();
         const int TVs = (tvsel == 16 && total >= 16 && bv % 16 == 0) ? 16 : 32;
         const uint64_t tiles = nv / TVs;
         const uint64_t cap = cap_env ? cap_env : (host_memory ? 32 : (TVs == 16 ? 1024 : 512));
         const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
         hipStream_t st = (hipStream_t)stream;
 #define TSA_PIPE(PP, DD, TT) \
-    hipLaunchKernelGGL((k_tree_lds_pipe<PP, DD, TT>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles)
+    hipLaunchKernelGGL((k_tree_lds_pipe<PP, DD, TT>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, tiles, nullptr)
         if (TVs == 16) {
             switch (total) {
                 case 16: TSA_PIPE(16, 1, 16); break;
@@ -1331,6 +1395,15 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
                 case 64: TSA_PIPE(64, 2, 32); break;
                 default: return ALLRED_ERR_UNSUPPORTED;
             }
+        } else if (rel && total == 64 && !host_memory) {
+            // REL: NB = rel buffers; NB >= 3 needs one workgroup per CU (grid <= 256)
+            const unsigned g1 = (unsigned)(tiles < 256 ? tiles : 256);
+            if (rel >= 4) hipLaunchKernelGGL((k_tree_lds_pipe<64, 3, 32, true, true>), dim3(cap_env ? grid : g1),
+                                             dim3(kBlock), 0, st, ranks, stride, order, bv, tiles, nullptr);
+            else if (rel == 3) hipLaunchKernelGGL((k_tree_lds_pipe<64, 2, 32, true, true>), dim3(cap_env ? grid : g1),
+                                                  dim3(kBlock), 0, st, ranks, stride, order, bv, tiles, nullptr);
+            else hipLaunchKernelGGL((k_tree_lds_pipe<64, 1, 32, true, true>), dim3(grid), dim3(kBlock), 0, st, ranks,
+                                    stride, order, bv, tiles, nullptr);
         } else {
             switch (total) {
                 case 8: TSA_PIPE(8, 1, 32); break;

@@ -14,8 +14,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
-def test_tree_reduce_and_broadcast_match_oracle():
-    side, total, n = 8, 64, 64 * 8 * 5
+# 2,560 elements: one tile per workgroup; 327,680 (config 2, 1,280 tiles) and
+# 1,061 tiles (ragged over the 512-workgroup persistent grid): the pipelined form
+@pytest.mark.parametrize("n", [64 * 8 * 5, 327680, 1061 * 256])
+def test_tree_reduce_and_broadcast_match_oracle(n):
+    side, total = 8, 64
     rng = np.random.default_rng(9)
     ranks = [rng.integers(0x3F80, 0x42C8, n).astype(np.uint16) for _ in range(total)]
     buf = torch.from_numpy(np.stack(ranks).view(np.int16)).to(DEV)

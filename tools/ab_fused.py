@@ -16,17 +16,18 @@ steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 P = 64
 n = t.normalize_tiles(tiles, P, variant != t.LO) * 1024
 stride = t.preferred_rank_stride(n)
-sets = [torch.randint(0x3F80, 0x42C8, (P, stride), dtype=torch.int16, device="cuda") for _ in range(8)]
+NS = int(os.environ.get("AB_SETS", "8"))
+sets = [torch.randint(0x3F80, 0x42C8, (P, stride), dtype=torch.int16, device="cuda") for _ in range(NS)]
 plan = t.Plan(t.SWING, variant, 8, n, P, t.EXEC_FUSED)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
     for i in range(10):
-        plan.execute(sets[i % 8].data_ptr(), stride, None, s)
+        plan.execute(sets[i % NS].data_ptr(), stride, None, s)
 torch.cuda.synchronize()
 g = torch.cuda.CUDAGraph()
 with torch.cuda.graph(g, stream=s):
     for i in range(steps):
-        plan.execute(sets[i % 8].data_ptr(), stride, None, s)
+        plan.execute(sets[i % NS].data_ptr(), stride, None, s)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(s)
@@ -38,5 +39,5 @@ us = e0.elapsed_time(e1) / steps * 1e3
 alg = 2 * P * n * 2
 print(json.dumps({"variant": sys.argv[1], "bytes_per_rank": n * 2, "us": round(us, 3),
                   "hbm_GBps": round(alg / us / 1e3, 1), "env": {k: v for k, v in os.environ.items()
-                                                               if k.startswith("ALLRED_")}}))
+                                                               if k.startswith(("ALLRED_", "AB_"))}}))
 plan.close()
