@@ -220,7 +220,7 @@ def bench_single(args) -> dict:
                    "exec": "fused", "launches_per_step": plan.launches, "hip_graph": graph is not None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic("k_tree_lds_pipe64"),
-                     "kernel": "k_tree_lds_pipe<64, 1, 32>", "algorithmic_bytes_per_launch": alg_bytes},
+                     "kernel": ("k_tree_lds_pipe<64, 1, 32, true, true>" if os.environ.get("ALLRED_PIPE_REL", "1") == "1" else "k_tree_lds_pipe<64, 1, 32, true, false>"), "algorithmic_bytes_per_launch": alg_bytes},
         "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
                               "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
@@ -491,7 +491,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         roof = {"kernel": "k_hier_oneshot (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
     else:
-        roof = {"kernel": "k_tree_lds<64,false> + k_broadcast (local phases)",
+        roof = {"kernel": "k_tree_lds_pipe<64, 1, 32, false> + k_broadcast (local phases)",
                 "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9}
     achieved = roof["achieved"]
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
