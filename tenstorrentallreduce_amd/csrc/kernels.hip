@@ -331,7 +331,12 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
         }
     };
     const uint64_t G = gridDim.x;
-    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;  // tiles of this WG
+    // tiles of this WG: blockIdx.x + j * G, so the workgroups in flight together
+    // read adjacent 512-byte segments of every rank row (a contiguous run per
+    // workgroup instead measured 18.8 vs 15.6 us: DRAM page locality across
+    // workgroups is what counts; 16-vector tiles, 256 B per row, 17.1-17.7)
+    const uint64_t first = blockIdx.x, step = G;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     // the order rows of all P blocks, once, then the first tiles' loads
     // (issuing those first measured slower: 15.65 vs 15.3 us at config 2)
     for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
@@ -339,7 +344,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
     __syncthreads();
 #pragma unroll
     for (int d = 0; d < (REL ? NB : D); ++d)
-        if (d < mine) issue(blockIdx.x + d * G, d);
+        if (d < mine) issue(first + d * step, d);
     for (int j = 0; j < mine; ++j) {
         const int rem = mine - 1 - j;
         if (REL && WRITE_ALL) {
@@ -355,9 +360,9 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
             wait_vm<0>();
         }
         lds_barrier();
-        if (!REL && j + D < mine) issue(blockIdx.x + (uint64_t)(j + D) * G, (j + D) % NB);
+        if (!REL && j + D < mine) issue(first + (uint64_t)(j + D) * step, (j + D) % NB);
         const uint4* tile = buf[j % NB];
-        const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
+        const uint64_t v0 = (first + (uint64_t)j * step) * TV;
         const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * q;
         uint4 x[LPL];
 #pragma unroll
@@ -371,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
         for (int s = TV; s < 64; s *= 2) pw = add8(pw, shfl_xor4(pw, s));   // tree levels across lane groups
         if (q == 0) part[w * TV + c] = pw;
         lds_barrier();   // every wave has read tile j out of buf[j % NB]
-        if (REL && j + NB < mine) issue(blockIdx.x + (uint64_t)(j + NB) * G, j % NB);
+        if (REL && j + NB < mine) issue(first + (uint64_t)(j + NB) * step, j % NB);
         const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
         if (!WRITE_ALL) {
             if (w == 0 && q == 0) st_nt(reinterpret_cast<uint4*>(out) + v0 + c, res);

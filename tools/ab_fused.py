@@ -15,7 +15,7 @@ tiles = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
 P = 64
 n = t.normalize_tiles(tiles, P, variant != t.LO) * 1024
-stride = t.preferred_rank_stride(n)
+stride = n + int(os.environ["AB_PAD"]) if "AB_PAD" in os.environ else t.preferred_rank_stride(n)
 NS = int(os.environ.get("AB_SETS", "8"))
 sets = [torch.randint(0x3F80, 0x42C8, (P, stride), dtype=torch.int16, device="cuda") for _ in range(NS)]
 plan = t.Plan(t.SWING, variant, 8, n, P, t.EXEC_FUSED)
