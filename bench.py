@@ -380,6 +380,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     #   rccl        tree -> 2D Swing BO over RCCL -> broadcast (3 launches + RCCL groups)
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
+    #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -395,7 +396,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
             peer.dist_allreduce(desc, b.data_ptr(), ws.data_ptr(), stream)
         else:
             peer.set_oneshot_max((4 << 20) if one_kernel else 0)
+            peer.set_hier_ll(kind == "peer_hier_ll")
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
+            peer.set_hier_ll(False)
             peer.set_oneshot_max(4 << 20)
 
     candidates, verify = ["rccl"], {}
@@ -404,7 +407,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         small[:4] = torch.randint(0, 2, (4, ELEMS), device=dev).to(torch.bfloat16).view(torch.int16)
         ref = small.clone()
         run("rccl", ref)
-        for kind in ("peer_swing", "peer_hier"):
+        for kind in ("peer_swing", "peer_hier", "peer_hier_ll"):
             x = small.clone()
             run(kind, x)
             torch.cuda.synchronize()
@@ -413,9 +416,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
             if kind == "peer_swing":
                 run("rccl", a)
                 run("peer_swing", b2)
-            else:
+            else:   # the one-kernel forms against the launch form of the same semantics
                 run("peer_hier", a, one_kernel=False)
-                run("peer_hier", b2, one_kernel=True)
+                run(kind, b2, one_kernel=True)
             torch.cuda.synchronize()
             ok = ok and torch.equal(a, b2) and (peer.status() & t.PEER_TIMEOUT) == 0
             verify[kind] = agreed(ok)
@@ -487,8 +490,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         return None
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    if transport == "peer_hier":   # the step IS one launch: its HBM bytes over its time
-        roof = {"kernel": "k_hier_oneshot (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
+    if transport in ("peer_hier", "peer_hier_ll"):   # the step IS one launch: its HBM bytes over its time
+        roof = {"kernel": "k_hier_oneshot (whole step)" if transport == "peer_hier" else "k_hier_ll (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
     else:
         roof = {"kernel": "k_tree_lds_pipe<64, 1, 32, false> + k_broadcast (local phases)",
@@ -497,7 +500,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
            "peer_swing": "on-GPU tree reduce, 2D Swing BO over peer-mapped xGMI windows (one kernel), broadcast",
            "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "
-                        "windows, broadcast (per-tile flags)"}[transport]
+                        "windows, broadcast (per-tile flags)",
+           "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
+                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     return {
         "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),

@@ -280,6 +280,15 @@ int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int 
  * barrier / all-gather launches.  Same result bits either way.  Every rank
  * must use the same setting. */
 int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
+/* enable != 0: with local_ranks == 64 and nranks <= 8, allred_peer_allreduce
+ * runs the hierarchical step as one kernel with LL hand-offs (each cross-GPU
+ * transfer a push of self-validating 8-byte data+epoch words into the
+ * consumer's own memory; no flags, no remote reads) for buckets of up to
+ * min(max_elems, 4 Mi) elements.  Same result bits as the default form
+ * (allred_mem_2D semantics over the per-GPU trees).  Every rank must use the
+ * same setting.  Replaces nothing in the reference (its mem_2D phases sync
+ * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
+int allred_peer_set_hier_ll(allred_peer* peer, int enable);
 /* The allred_dist_allreduce program (same desc, same result bits: Swing /
  * RecDub BO or LO, link-spreading channels, hierarchical local ranks) with
  * RCCL replaced by direct reads of the partners' IPC-mapped windows: one

@@ -309,6 +309,10 @@ class Peer:
         """Buckets of at most nbytes run as one kernel (same bits either way)."""
         check(lib.allred_peer_set_oneshot_max(self._h, nbytes), "peer_set_oneshot_max")
 
+    def set_hier_ll(self, enable: bool) -> None:
+        """64 local ranks: the hierarchical step with LL push hand-offs (k_hier_ll)."""
+        check(lib.allred_peer_set_hier_ll(self._h, int(bool(enable))), "peer_set_hier_ll")
+
     def status(self) -> int:
         v = C.c_uint32(0)
         check(lib.allred_peer_status(self._h, C.byref(v)), "peer_status")

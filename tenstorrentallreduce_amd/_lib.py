@@ -144,6 +144,7 @@ SIGNATURES = [
     ("allred_peer_connect", C.c_int, [_P, _P]),
     ("allred_peer_allreduce", C.c_int, [_P, _u16p, C.c_uint64, C.c_int, C.c_int, C.c_int, _P, _P]),
     ("allred_peer_set_oneshot_max", C.c_int, [_P, C.c_uint64]),
+    ("allred_peer_set_hier_ll", C.c_int, [_P, C.c_int]),
     ("allred_peer_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("allred_peer_destroy", C.c_int, [_P]),

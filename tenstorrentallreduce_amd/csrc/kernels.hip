@@ -1144,6 +1144,170 @@ __global__ __launch_bounds__(kBlock) void k_hier_oneshot(uint16_t* __restrict__ 
     }
 }
 
+// ---- hierarchical one-kernel form, LL (push) variant ------------------------
+// Same bits as k_hier_oneshot (local tree per tile -> mem_2D across the W GPUs,
+// fp32 owner first then ascending, one rounding -> every GPU's 64 rank rows),
+// but every cross-GPU transfer is a PUSH of self-validating 8-byte words
+// (4 bytes of data + the call's epoch, RCCL's "LL" idea): the producer's
+// relaxed system-scope stores go straight into the consumer's uncached LL
+// area and the consumer polls its OWN memory until every word carries the
+// epoch.  No flag follows the data and no remote load is ever waited for, so
+// each hand-off costs one one-way xGMI trip instead of a flag trip plus a
+// remote read round trip (k_hier_oneshot: A publish -> R remote loads -> B
+// remote loads).
+//   A (all my tiles, double-buffered LDS): tile t's partial -> owner o's inbox
+//     slot [t - o*tpo][me] (1 KiB of LL words per tile).
+//   R (my tiles that I own): poll the W slots, fp32 sum owner first then
+//     ascending, one rounding -> every GPU's result box [t].
+//   B (all my tiles): poll my result box [t], store to the 64 rank rows.
+// A never waits, R waits only for A, B only for R; the grid is resident (2
+// workgroups per CU), so every wait is reached and satisfied.  Epochs grow by
+// one per call and the LL areas alternate by call parity, so a word of an
+// earlier call never carries the awaited epoch.
+constexpr int kLLMaxGpus = 8;
+struct LLPtrs {
+    uint64_t* ll[kLLMaxGpus];   // GPU q's LL area, this parity: [inbox: tiles x 128 words][result box: same]
+};
+
+__device__ __forceinline__ void ll_put(uint64_t* dst, uint4 v, uint32_t e) {
+    const uint64_t hi = (uint64_t)e << 32;
+    __hip_atomic_store(dst + 0, hi | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1, hi | v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 2, hi | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 3, hi | v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// poll 4 LL words until all carry epoch e (bounded: status bit 0 on timeout)
+__device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_t* status) {
+    uint64_t w0, w1, w2, w3;
+    for (uint64_t spin = 0;; ++spin) {
+        w0 = __hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w2 = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w3 = __hip_atomic_load(src + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(w0 >> 32) == e && (uint32_t)(w1 >> 32) == e && (uint32_t)(w2 >> 32) == e &&
+            (uint32_t)(w3 >> 32) == e)
+            break;
+        if (spin > kPeerSpinLimit) {
+            atomicOr(status, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return make_uint4((uint32_t)w0, (uint32_t)w1, (uint32_t)w2, (uint32_t)w3);
+}
+
+__global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
+                                                    uint32_t epoch, uint32_t* status) {
+    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    __syncthreads();
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+        }
+    };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    uint64_t* const my_ll = lp.ll[me];
+    // ---- A: local trees, partials pushed to their owners
+    if (mine > 0) issue(tile_of(0), 0);
+    for (int j = 0; j < mine; ++j) {
+        // in flight after tile j's loads: wave 0's four LL stores of tile j-1
+        // (wave-uniform branch: vmcnt is per wave)
+        if (j > 0 && w == 0) wait_vm<4>(); else wait_vm<0>();
+        lds_barrier();
+        if (j + 1 < mine) issue(tile_of(j + 1), (j + 1) & 1);
+        const uint4* tile = buf[j & 1];
+        const uint64_t t = tile_of(j);
+        const uint8_t* ord = ord_lds + RPW * w + LPL * h;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+        if (h == 0) part[w * TV + c] = pw;
+        lds_barrier();
+        if (w == 0 && h == 0) {
+            const int o = owner_of(t);
+            const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
+            ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, res, epoch);
+        }
+    }
+    __syncthreads();   // every wave is past A: buf may be reused below
+    uint4* xs = buf[0];   // [8 GPUs][32 columns] partials, then [32] results / [4][32] B rows
+    // ---- R: the tiles I own: W partials from my inbox -> every GPU's result box
+    for (int j = 0; j < mine; ++j) {
+        const uint64_t t = tile_of(j);
+        if (owner_of(t) != me) continue;
+        const uint64_t li = t - (uint64_t)me * tiles_per_owner;
+        const int q = threadIdx.x >> 5;   // source GPU of this lane's slot
+        if (q < W) xs[q * 32 + c] = ll_get(my_ll + (li * W + q) * 128 + c * 4, epoch, status);
+        __syncthreads();
+        if (threadIdx.x < 32) {
+            const uint4 s0 = xs[me * 32 + c];
+            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+            for (int qq = 0; qq < W; ++qq) {
+                if (qq == me) continue;
+                const uint4 y = xs[qq * 32 + c];
+                a[0] += lo_f(y.x); a[1] += hi_f(y.x);
+                a[2] += lo_f(y.y); a[3] += hi_f(y.y);
+                a[4] += lo_f(y.z); a[5] += hi_f(y.z);
+                a[6] += lo_f(y.w); a[7] += hi_f(y.w);
+            }
+            uint4 o;
+            o.x = pack_rne(a[0], a[1]);
+            o.y = pack_rne(a[2], a[3]);
+            o.z = pack_rne(a[4], a[5]);
+            o.w = pack_rne(a[6], a[7]);
+            xs[8 * 32 + c] = o;
+        }
+        __syncthreads();
+        if (q < W) ll_put(lp.ll[q] + box_words + t * 128 + c * 4, xs[8 * 32 + c], epoch);
+        __syncthreads();   // xs is reused by the next owned tile
+    }
+    // ---- B: my result box -> the 64 rank rows, 4 tiles at a time
+    constexpr int BB = 4;
+    for (int j0 = 0; j0 < mine; j0 += BB) {
+        const int nb = mine - j0 < BB ? mine - j0 : BB;
+        const int b = threadIdx.x >> 5;
+        if (b < nb) xs[16 * 32 + b * 32 + c] = ll_get(my_ll + box_words + tile_of(j0 + b) * 128 + c * 4, epoch, status);
+        __syncthreads();
+        uint4 res[BB];
+#pragma unroll
+        for (int bb = 0; bb < BB; ++bb)
+            if (bb < nb) res[bb] = xs[16 * 32 + bb * 32 + c];
+        __syncthreads();   // xs is reused by the next batch
+#pragma unroll
+        for (int bb = 0; bb < BB; ++bb) {
+            if (bb >= nb) break;
+            const uint64_t v0 = tile_of(j0 + bb) * TV;
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res[bb]);
+            }
+        }
+    }
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ALLRED_TREE=registers selects the register-only k_tree for the fused BO pass
@@ -1302,6 +1466,20 @@ int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, 
     const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);   // 2 per CU: the whole grid resident
     hipLaunchKernelGGL(k_hier_oneshot, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, hp,
                        nranks, me, (uint64_t)n, ntiles, ntiles / nranks, epoch, status);
+    return last_error();
+}
+
+int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
+        ntiles * 128 > box_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);   // 2 per CU: the whole grid resident
+    hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
+                       me, ntiles, ntiles / nranks, box_words, epoch, status);
     return last_error();
 }
 

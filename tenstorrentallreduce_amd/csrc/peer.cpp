@@ -16,7 +16,8 @@
 // same three phases as ONE kernel (k_peer_oneshot): workgroup g syncs only
 // with workgroup g of the peers, through per-workgroup flag slots.  With 64
 // local ranks per GPU the local tree and the broadcast join that kernel too
-// (k_hier_oneshot, per-tile flags behind the window parities).
+// (k_hier_oneshot, per-tile flags behind the window parities; k_hier_ll, the
+// same step with LL push hand-offs, LL boxes behind the flags).
 // Windows are double-buffered by call parity: call k+2 can only overwrite a
 // window after every peer passed call k+1's first barrier, i.e. finished
 // reading call k's windows.
@@ -46,6 +47,12 @@ struct allred_peer {
     bool last_all_peer = false;     // previous call read every rank's window
     uint64_t oneshot_max = 4ull << 20;  // buckets up to this many bytes use the one-kernel form
     bool connected = false;
+    // LL (push) hierarchical form: behind the per-tile flags, 2 parities x
+    // [inbox ll_box_words][result box ll_box_words] 8-byte words, zeroed at create
+    size_t ll_off = 0;
+    uint64_t ll_box_words = 0;
+    uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
+    bool hier_ll = false;
 };
 
 extern "C" {
@@ -66,7 +73,12 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     // for up to max_elems / 2 elements per call (256-element tiles).
     p->hfl_off = 2 * p->max_elems * 2;
     p->hfl_bytes = 4 * (size_t)(nranks + 1) * (p->max_elems / 2 / 256 + 1);
-    const size_t win_bytes = p->hfl_off + p->hfl_bytes;
+    // LL boxes for buckets of up to min(max_elems, 4 Mi) elements: 128 words per 256-element tile
+    const uint64_t ll_elems = p->max_elems < (4ull << 20) ? p->max_elems : (4ull << 20);
+    p->ll_off = (p->hfl_off + p->hfl_bytes + 255) / 256 * 256;
+    p->ll_box_words = (ll_elems / 256) * 128;
+    const size_t ll_bytes = 2 * 2 * p->ll_box_words * 8;
+    const size_t win_bytes = p->ll_off + ll_bytes;
     if (hipExtMallocWithFlags((void**)&p->win, win_bytes, hipDeviceMallocUncached) == hipSuccess) {
         p->win_uncached = true;
     } else if (hipMalloc((void**)&p->win, win_bytes) != hipSuccess) {
@@ -81,7 +93,7 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
         return ALLRED_ERR_NOMEM;
     }
     if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, kPeerFlagBytes) != hipSuccess ||
-        hipMemset(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off, 0, p->hfl_bytes) != hipSuccess ||
+        hipMemset(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off, 0, win_bytes - p->hfl_off) != hipSuccess ||
         hipMemset(p->status, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
         (void)hipFree(p->win);
         (void)hipFree(p->flags);
@@ -111,6 +123,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
             p->peer_win[q] = p->win;
             p->peer_flags[q] = p->flags;
             p->peer_hfl[q] = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off);
+            p->peer_ll[q] = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(p->win) + p->ll_off);
             continue;
         }
         hipIpcMemHandle_t hw, hf;
@@ -123,6 +136,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
         p->peer_win[q] = static_cast<uint16_t*>(w);
         p->peer_flags[q] = static_cast<uint32_t*>(f);
         p->peer_hfl[q] = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(w) + p->hfl_off);
+        p->peer_ll[q] = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(w) + p->ll_off);
         p->opened[q] = true;
     }
     p->connected = true;
@@ -146,6 +160,21 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
     if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     uint16_t* bucket = buf;
     int st = ALLRED_OK;
+    if (p->hier_ll && local_ranks == 64 && p->nranks <= 8 && p->win_uncached && n % (256 * (size_t)p->nranks) == 0 &&
+        (n / 256) * 128 <= p->ll_box_words) {
+        // the hierarchical step in one launch with LL (push) hand-offs (k_hier_ll): same bits
+        const uint8_t* order = nullptr;
+        st = local_tree_order(local_algo, local_side, local_ranks, &order);
+        if (st != ALLRED_OK) return st;
+        uint64_t* ll[ALLRED_MAX_NODES];
+        for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
+        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
+                            stream);
+        if (st != ALLRED_OK) return st;
+        ++p->calls;
+        p->last_all_peer = true;
+        return ALLRED_OK;
+    }
     const bool one_kernel = n * 2 <= p->oneshot_max && p->win_uncached && p->flags_uncached;
     if (one_kernel && local_ranks == 64 && n % (256 * (size_t)p->nranks) == 0 && 2 * n <= p->max_elems) {
         // the whole hierarchical step in one launch (k_hier_oneshot): same bits as
@@ -225,6 +254,12 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
 int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
     if (!p) return ALLRED_ERR_ARG;
     p->oneshot_max = bytes;
+    return ALLRED_OK;
+}
+
+int allred_peer_set_hier_ll(allred_peer* p, int enable) {
+    if (!p) return ALLRED_ERR_ARG;
+    p->hier_ll = enable != 0;
     return ALLRED_OK;
 }
 

@@ -93,13 +93,17 @@ def worker(rank, world, port, q):
         if not all(np.array_equal(got[i], partials[rank]) for i in range(local)):
             fails.append(("hier", 0, 1))
         # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form
-        # (k_hier_oneshot, per-tile flags) and the launch form, two calls back to back each
+        # (k_hier_oneshot, per-tile flags), the LL push form (k_hier_ll) and the
+        # launch form, two calls back to back each (then LL once more after the
+        # launch form: its LL boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
-        for mode, limit in (("hier_one_kernel", 1 << 40), ("hier_launches", 0)):
+        for mi, (mode, limit, ll) in enumerate((("hier_one_kernel", 1 << 40, False), ("hier_ll", 1 << 40, True),
+                                                ("hier_launches", 0, False), ("hier_ll_again", 0, True))):
             peer.set_oneshot_max(limit)
+            peer.set_hier_ll(ll)
             runs = []
             for rep in range(2):
-                data = [np.random.default_rng(700 + 10 * rep + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
+                data = [np.random.default_rng(700 + 100 * mi + 10 * rep + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
                         for r in range(world)]
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
@@ -118,6 +122,7 @@ def worker(rank, world, port, q):
                 if bad:
                     fails.append((mode, rep, bad))
             dist.barrier()
+        peer.set_hier_ll(False)
         status = peer.status()
         dist.barrier()
         peer.close()
