@@ -250,6 +250,11 @@ def timed_max(fn, reps, stream) -> float:
     return m.item()
 
 
+def note(rank, msg):
+    """progress line on stderr (stdout carries only the JSON line)"""
+    print(f"[bench r{rank} {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def agreed(ok: bool) -> bool:
     v = torch.tensor([int(ok)], dtype=torch.int64)
     dist.all_reduce(v, op=dist.ReduceOp.MIN)
@@ -348,7 +353,7 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
                          channels=chans)
         b2 = torch.zeros((local, n), dtype=torch.int16, device=dev)
         w2 = torch.empty(max(16, t.dist_workspace_bytes(d2)), dtype=torch.uint8, device=dev)
-        if variant != t.MEM:
+        if variant != t.MEM and comm is not None:
             ms = timed_max(lambda: t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
             out[name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
         if peer is not None:
@@ -359,13 +364,22 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
 
 
 def bench_multi(args, rank, world, local_rank) -> dict | None:
-    dev = torch.device(f"cuda:{local_rank}")
+    # --share-gpu (rehearsal only): every rank on cuda:0 and no RCCL (it refuses two
+    # ranks on one device), so the whole N>1 path except RCCL runs on a 1-GPU box
+    dev_index = 0 if args.share_gpu else local_rank
+    dev = torch.device(f"cuda:{dev_index}")
     torch.cuda.set_device(dev)
     side, total = GRIDS[world]
-    uid = [t.Comm.unique_id() if rank == 0 else None]
-    dist.broadcast_object_list(uid, src=0)
-    comm = t.Comm(uid[0], world, rank, local_rank)
-    peer, peer_err = open_peer(rank, world, local_rank, (1 << 30) // 2)   # windows for 1 GiB buckets
+    comm = None
+    if not args.share_gpu:
+        uid = [t.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = t.Comm(uid[0], world, rank, local_rank)
+    note(rank, f"world {world}, device {dev_index}: opening peer windows")
+    peer, peer_err = open_peer(rank, world, dev_index, (1 << 30) // 2)   # windows for 1 GiB buckets
+    note(rank, f"peer windows: {'ok' if peer is not None else peer_err}")
+    if peer is not None and args.share_gpu:
+        peer.set_max_groups(512 // world)   # every rank's one-kernel grid resident at once
     stream = torch.cuda.Stream(device=dev)
     desc = t.dist_desc(t.SWING, t.BO, side, total, ELEMS, local_ranks=RANKS, local_side=SIDE, local_algo=t.SWING)
     # rotating bucket sets as at N = 1 (every step streams its 64 ranks from HBM)
@@ -373,6 +387,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     for i, b in enumerate(bufs):
         fill_reference_convention(b, 77 + rank + 1000 * i)
     buf = bufs[0]
+    torch.cuda.synchronize()
     ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)
     partial = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
@@ -389,38 +404,49 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     # timed briefly and the fastest is the headline transport.
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
-    def run(kind, b, one_kernel=True):
+    def run(kind, b, one_kernel=True, fresh=False):
+        if fresh:   # b was just written on torch's current stream
+            stream.wait_stream(torch.cuda.current_stream())
         if kind == "rccl":
             t.dist_allreduce(comm, desc, b.data_ptr(), ws.data_ptr(), stream)
         elif kind == "peer_swing":
             peer.dist_allreduce(desc, b.data_ptr(), ws.data_ptr(), stream)
         else:
+            one_kernel = one_kernel and kind != "peer_launches"
             peer.set_oneshot_max((4 << 20) if one_kernel else 0)
             peer.set_hier_ll(kind == "peer_hier_ll")
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
             peer.set_hier_ll(False)
             peer.set_oneshot_max(4 << 20)
 
-    candidates, verify = ["rccl"], {}
+    # the reference transport: RCCL, or (--share-gpu) the peer launch form
+    base = "rccl" if comm is not None else "peer_launches"
+    candidates, verify = [base], {}
+    if peer is None and comm is None:
+        raise RuntimeError("--share-gpu needs the peer windows")
     if peer is not None:
         small = torch.zeros_like(buf)
         small[:4] = torch.randint(0, 2, (4, ELEMS), device=dev).to(torch.bfloat16).view(torch.int16)
         ref = small.clone()
-        run("rccl", ref)
+        note(rank, f"verify: {base} on small integers")
+        run(base, ref, fresh=True)
         for kind in ("peer_swing", "peer_hier", "peer_hier_ll"):
             x = small.clone()
-            run(kind, x)
+            note(rank, f"verify: {kind}")
+            run(kind, x, fresh=True)
             torch.cuda.synchronize()
             ok = torch.equal(x, ref)
             a, b2 = buf.clone(), buf.clone()
-            if kind == "peer_swing":
-                run("rccl", a)
+            if kind == "peer_swing" and base == "rccl":
+                run("rccl", a, fresh=True)
                 run("peer_swing", b2)
+            elif kind == "peer_swing":   # --share-gpu: same semantics (Swing trees) only on small integers
+                a = b2 = None
             else:   # the one-kernel forms against the launch form of the same semantics
-                run("peer_hier", a, one_kernel=False)
-                run(kind, b2, one_kernel=True)
+                run("peer_launches", a, fresh=True)
+                run(kind, b2)
             torch.cuda.synchronize()
-            ok = ok and torch.equal(a, b2) and (peer.status() & t.PEER_TIMEOUT) == 0
+            ok = ok and (a is None or torch.equal(a, b2)) and (peer.status() & t.PEER_TIMEOUT) == 0
             verify[kind] = agreed(ok)
             if verify[kind]:
                 candidates.append(kind)
@@ -428,6 +454,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         del small, ref
     quick = {}
     for kind in candidates:
+        note(rank, f"quick timing: {kind}")
         it = iter(range(1 << 30))
         quick[kind] = round(timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), 20, stream), 4)
     transport = min(candidates, key=lambda k: quick[k])
@@ -435,6 +462,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     def step(i):
         run(transport, bufs[i % len(bufs)])
 
+    note(rank, f"timed: {transport}")
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -470,7 +498,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         extras["peer_error"] = peer_err
     if args.extras:
         extras.update(xgmi_arms(comm, peer if verify.get("peer_swing") else None, world, dev, stream, side, total))
-        if world > 1:
+        if world > 1 and comm is not None:
             try:
                 extras["link_probe"] = link_probe(rank, world, dev)
                 mb = extras["link_probe"]["GBps_per_direction"]
@@ -485,7 +513,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         extras["peer_status"] = int(st.item())
         dist.barrier()
         peer.close()
-    comm.close()
+    if comm is not None:
+        comm.close()
     if rank != 0:
         return None
     bytes_all = world * RANKS * ELEMS * 2
@@ -498,6 +527,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
                 "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9}
     achieved = roof["achieved"]
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
+           "peer_launches": "on-GPU tree reduce, mem_2D across GPUs over peer-mapped windows (launches), broadcast",
            "peer_swing": "on-GPU tree reduce, 2D Swing BO over peer-mapped xGMI windows (one kernel), broadcast",
            "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "
                         "windows, broadcast (per-tile flags)",
@@ -543,6 +573,8 @@ def main():
     ap.add_argument("--no-extras", dest="extras", action="store_false")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
     ap.add_argument("--force-dist", action="store_true", help="run the N>1 code path on one GPU (1-rank RCCL)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="rehearsal: every rank on cuda:0, peer transports only (no RCCL); not a measurement")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -256,20 +256,20 @@ int allred_dist_allreduce_host(const allred_dist_desc* desc, int rank, uint16_t*
  * (allred_mem_2D.cpp:4-165) with every GPU's window IPC-mapped into every
  * peer (one process per GPU).  Result semantics = allred_mem_2D: block b is
  * owner b's copy + every other rank's copy in rank order, fp32, one rounding.
- *   create -> handle (128 bytes, exchange with every rank) -> connect(all
+ *   create -> handle (192 bytes, exchange with every rank) -> connect(all
  *   handles in rank order) -> allreduce ... -> destroy.
  * Barriers spin with a bound; allred_peer_status() reports bit 0 = timeout,
  * and the WIN/FLAGS_CACHED bits when uncached (fine-grained) device memory
  * was unavailable and ordinary hipMalloc memory had to be used instead.
  * ==================================================================== */
-#define ALLRED_PEER_HANDLE_BYTES 128
+#define ALLRED_PEER_HANDLE_BYTES 192
 #define ALLRED_PEER_TIMEOUT 0x1u
 #define ALLRED_PEER_WIN_CACHED 0x100u
 #define ALLRED_PEER_FLAGS_CACHED 0x200u
 typedef struct allred_peer allred_peer;
 int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, allred_peer** out);
 int allred_peer_handle(allred_peer* peer, uint8_t* handle /*[ALLRED_PEER_HANDLE_BYTES]*/);
-int allred_peer_connect(allred_peer* peer, const uint8_t* all_handles /*[nranks * 128]*/);
+int allred_peer_connect(allred_peer* peer, const uint8_t* all_handles /*[nranks * ALLRED_PEER_HANDLE_BYTES]*/);
 /* elems % (8 * nranks) == 0, elems <= max_elems.  local_ranks > 1: `buf`
  * holds local_ranks virtual ranks (stride elems) reduced on-GPU first
  * (tree of local rank 0) into `workspace` (elems * 2 bytes), then broadcast. */
@@ -289,6 +289,12 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * same setting.  Replaces nothing in the reference (its mem_2D phases sync
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
+/* Caps the grid of the hierarchical one-kernel forms at `groups` workgroups
+ * (0 = default: 512, two per CU, the whole grid resident on a GPU of its own).
+ * Their workgroups wait for each other across processes, so when several
+ * processes share one GPU (rehearsals) the sum of their grids must fit at once:
+ * groups <= 512 / processes.  Same result bits at any cap. */
+int allred_peer_set_max_groups(allred_peer* peer, uint32_t groups);
 /* The allred_dist_allreduce program (same desc, same result bits: Swing /
  * RecDub BO or LO, link-spreading channels, hierarchical local ranks) with
  * RCCL replaced by direct reads of the partners' IPC-mapped windows: one

@@ -313,6 +313,11 @@ class Peer:
         """64 local ranks: the hierarchical step with LL push hand-offs (k_hier_ll)."""
         check(lib.allred_peer_set_hier_ll(self._h, int(bool(enable))), "peer_set_hier_ll")
 
+    def set_max_groups(self, groups: int) -> None:
+        """Grid cap of the hierarchical one-kernel forms (0 = one full grid per GPU);
+        processes sharing a GPU need groups <= 512 / processes."""
+        check(lib.allred_peer_set_max_groups(self._h, groups), "peer_set_max_groups")
+
     def status(self) -> int:
         v = C.c_uint32(0)
         check(lib.allred_peer_status(self._h, C.byref(v)), "peer_status")

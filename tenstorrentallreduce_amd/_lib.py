@@ -145,11 +145,12 @@ SIGNATURES = [
     ("allred_peer_allreduce", C.c_int, [_P, _u16p, C.c_uint64, C.c_int, C.c_int, C.c_int, _P, _P]),
     ("allred_peer_set_oneshot_max", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_set_hier_ll", C.c_int, [_P, C.c_int]),
+    ("allred_peer_set_max_groups", C.c_int, [_P, C.c_uint32]),
     ("allred_peer_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("allred_peer_destroy", C.c_int, [_P]),
 ]
-PEER_HANDLE_BYTES = 128
+PEER_HANDLE_BYTES = 192
 PEER_TIMEOUT, PEER_WIN_CACHED, PEER_FLAGS_CACHED = 0x1, 0x100, 0x200   # allred_peer_status bits
 
 for _name, _res, _args in SIGNATURES:

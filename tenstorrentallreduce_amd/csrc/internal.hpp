@@ -97,11 +97,12 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
 // wins[q] = GPU q's window for this parity ([partial n][result n]); hflags[q]: [tiles][nranks + 1]
 int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
                         uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
-                        void* stream);
+                        unsigned max_grid, void* stream);
 // the same step with LL (push) hand-offs: ll[q] = GPU q's LL area for this parity,
 // [inbox box_words words][result box box_words words]; nranks <= 8; epoch grows by 1 per call
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, void* stream);
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                   void* stream);
 // one launch; epoch must grow by >= 1 per call
 int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                         size_t n, uint32_t epoch, uint32_t* status, void* stream);

@@ -1454,7 +1454,7 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
 
 int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
                         uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
-                        void* stream) {
+                        unsigned max_grid, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > ALLRED_MAX_NODES || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks))
         return ALLRED_ERR_ARG;
@@ -1463,21 +1463,26 @@ int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, 
         hp.win[q] = wins[q];
         hp.hfl[q] = hflags[q];
     }
-    const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);   // 2 per CU: the whole grid resident
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_oneshot, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, hp,
                        nranks, me, (uint64_t)n, ntiles, ntiles / nranks, epoch, status);
     return last_error();
 }
 
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, void* stream) {
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                   void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
         ntiles * 128 > box_words)
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
-    const unsigned grid = (unsigned)(ntiles < 512 ? ntiles : 512);   // 2 per CU: the whole grid resident
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
                        me, ntiles, ntiles / nranks, box_words, epoch, status);
     return last_error();

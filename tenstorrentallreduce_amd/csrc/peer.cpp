@@ -16,8 +16,8 @@
 // same three phases as ONE kernel (k_peer_oneshot): workgroup g syncs only
 // with workgroup g of the peers, through per-workgroup flag slots.  With 64
 // local ranks per GPU the local tree and the broadcast join that kernel too
-// (k_hier_oneshot, per-tile flags behind the window parities; k_hier_ll, the
-// same step with LL push hand-offs, LL boxes behind the flags).
+// (k_hier_oneshot, per-tile flags; k_hier_ll, the same step with LL push
+// hand-offs, LL boxes; both live in the flag allocation behind the flags).
 // Windows are double-buffered by call parity: call k+2 can only overwrite a
 // window after every peer passed call k+1's first barrier, i.e. finished
 // reading call k's windows.
@@ -32,14 +32,17 @@ using namespace tsa;
 struct allred_peer {
     int nranks = 0, rank = 0, device = 0;
     uint64_t max_elems = 0;
-    uint16_t* win = nullptr;        // own window: 2 parities x max_elems
-    uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp
+    // own windows, one allocation per parity (max_elems each): every IPC-exported
+    // allocation stays <= 1 GiB + 256 B, since opening a ~2 GiB one in a peer
+    // process hung on the MI355X boxes (tools/peer_open_probe.py)
+    uint16_t* win[2] = {};
+    uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp, then hfl and LL
     uint32_t* status = nullptr;     // device status word
     bool flags_uncached = false, win_uncached = false;
-    size_t hfl_off = 0;             // byte offset of the per-tile flags behind the two window parities
+    size_t hfl_off = 0;             // byte offset of the per-tile flags in the flag allocation
     size_t hfl_bytes = 0;
     uint32_t* peer_hfl[ALLRED_MAX_NODES] = {};
-    uint16_t* peer_win[ALLRED_MAX_NODES] = {};
+    uint16_t* peer_win[ALLRED_MAX_NODES][2] = {};
     uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
     bool opened[ALLRED_MAX_NODES] = {};
     uint32_t calls = 0;
@@ -53,6 +56,7 @@ struct allred_peer {
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
     bool hier_ll = false;
+    uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
 };
 
 extern "C" {
@@ -68,36 +72,51 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     (void)hipGetDevice(&p->device);
     p->max_elems = (max_elems + 127) / 128 * 128;  // LO halves stay 64-element aligned
     // windows are uncached too: peers read them over xGMI straight from HBM, so
-    // no write may linger in one of this GPU's eight per-XCD L2s.  Behind the
-    // two parities: the hierarchical form's per-tile flags, [tiles][nranks + 1]
-    // for up to max_elems / 2 elements per call (256-element tiles).
-    p->hfl_off = 2 * p->max_elems * 2;
+    // no write may linger in one of this GPU's eight per-XCD L2s.  The flag
+    // allocation holds, behind the flags of internal.hpp: the hierarchical
+    // form's per-tile flags, [tiles][nranks + 1] for up to max_elems / 2
+    // elements per call (256-element tiles), and the LL boxes for buckets of up
+    // to min(max_elems, 4 Mi) elements (128 words per 256-element tile).
+    p->hfl_off = ((size_t)kPeerFlagBytes + 255) / 256 * 256;
     p->hfl_bytes = 4 * (size_t)(nranks + 1) * (p->max_elems / 2 / 256 + 1);
-    // LL boxes for buckets of up to min(max_elems, 4 Mi) elements: 128 words per 256-element tile
     const uint64_t ll_elems = p->max_elems < (4ull << 20) ? p->max_elems : (4ull << 20);
     p->ll_off = (p->hfl_off + p->hfl_bytes + 255) / 256 * 256;
     p->ll_box_words = (ll_elems / 256) * 128;
-    const size_t ll_bytes = 2 * 2 * p->ll_box_words * 8;
-    const size_t win_bytes = p->ll_off + ll_bytes;
-    if (hipExtMallocWithFlags((void**)&p->win, win_bytes, hipDeviceMallocUncached) == hipSuccess) {
-        p->win_uncached = true;
-    } else if (hipMalloc((void**)&p->win, win_bytes) != hipSuccess) {
-        delete p;
-        return ALLRED_ERR_NOMEM;
-    }
-    if (hipExtMallocWithFlags((void**)&p->flags, kPeerFlagBytes, hipDeviceMallocUncached) == hipSuccess) {
-        p->flags_uncached = true;
-    } else if (hipMalloc((void**)&p->flags, kPeerFlagBytes) != hipSuccess) {
-        (void)hipFree(p->win);
-        delete p;
-        return ALLRED_ERR_NOMEM;
-    }
-    if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, kPeerFlagBytes) != hipSuccess ||
-        hipMemset(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off, 0, win_bytes - p->hfl_off) != hipSuccess ||
-        hipMemset(p->status, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        (void)hipFree(p->win);
+    const size_t flag_bytes = p->ll_off + 2 * 2 * p->ll_box_words * 8;
+    const size_t win_bytes = p->max_elems * 2;
+    auto release = [p]() {
+        for (uint16_t* w : p->win) (void)hipFree(w);
         (void)hipFree(p->flags);
+        (void)hipFree(p->status);
         delete p;
+    };
+    p->win_uncached = true;
+    for (uint16_t*& w : p->win) {
+        if (hipExtMallocWithFlags((void**)&w, win_bytes, hipDeviceMallocUncached) != hipSuccess) {
+            w = nullptr;
+            p->win_uncached = false;
+        }
+    }
+    if (!p->win_uncached) {   // all cached or all uncached
+        for (uint16_t*& w : p->win) {
+            (void)hipFree(w);
+            if (hipMalloc((void**)&w, win_bytes) != hipSuccess) {
+                w = nullptr;
+                release();
+                return ALLRED_ERR_NOMEM;
+            }
+        }
+    }
+    if (hipExtMallocWithFlags((void**)&p->flags, flag_bytes, hipDeviceMallocUncached) == hipSuccess) {
+        p->flags_uncached = true;
+    } else if (hipMalloc((void**)&p->flags, flag_bytes) != hipSuccess) {
+        p->flags = nullptr;
+        release();
+        return ALLRED_ERR_NOMEM;
+    }
+    if (hipMalloc((void**)&p->status, 4) != hipSuccess || hipMemset(p->flags, 0, flag_bytes) != hipSuccess ||
+        hipMemset(p->status, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        release();
         return ALLRED_ERR_HIP;
     }
     *out = p;
@@ -106,38 +125,42 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
 
 int allred_peer_handle(allred_peer* p, uint8_t* out) {
     if (!p || !out) return ALLRED_ERR_ARG;
-    hipIpcMemHandle_t hw, hf;
-    if (hipIpcGetMemHandle(&hw, p->win) != hipSuccess) return ALLRED_ERR_HIP;
-    if (hipIpcGetMemHandle(&hf, p->flags) != hipSuccess) return ALLRED_ERR_HIP;
-    static_assert(sizeof(hipIpcMemHandle_t) * 2 <= ALLRED_PEER_HANDLE_BYTES, "handle size");
+    // [window parity 0][window parity 1][flags], 64 bytes each
+    static_assert(sizeof(hipIpcMemHandle_t) * 3 <= ALLRED_PEER_HANDLE_BYTES, "handle size");
+    hipIpcMemHandle_t h[3];
+    if (hipIpcGetMemHandle(&h[0], p->win[0]) != hipSuccess) return ALLRED_ERR_HIP;
+    if (hipIpcGetMemHandle(&h[1], p->win[1]) != hipSuccess) return ALLRED_ERR_HIP;
+    if (hipIpcGetMemHandle(&h[2], p->flags) != hipSuccess) return ALLRED_ERR_HIP;
     std::memset(out, 0, ALLRED_PEER_HANDLE_BYTES);
-    std::memcpy(out, &hw, sizeof(hw));
-    std::memcpy(out + ALLRED_PEER_HANDLE_BYTES / 2, &hf, sizeof(hf));
+    for (int i = 0; i < 3; ++i) std::memcpy(out + i * sizeof(hipIpcMemHandle_t), &h[i], sizeof(h[i]));
     return ALLRED_OK;
 }
 
 int allred_peer_connect(allred_peer* p, const uint8_t* all) {
-    if (!p || !all) return ALLRED_ERR_ARG;
+    if (!p || !all || p->connected) return ALLRED_ERR_ARG;
     for (int q = 0; q < p->nranks; ++q) {
         if (q == p->rank) {
-            p->peer_win[q] = p->win;
+            p->peer_win[q][0] = p->win[0];
+            p->peer_win[q][1] = p->win[1];
             p->peer_flags[q] = p->flags;
-            p->peer_hfl[q] = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(p->win) + p->hfl_off);
-            p->peer_ll[q] = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(p->win) + p->ll_off);
-            continue;
+        } else {
+            void* m[3] = {};
+            for (int i = 0; i < 3; ++i) {
+                hipIpcMemHandle_t h;
+                std::memcpy(&h, all + (size_t)q * ALLRED_PEER_HANDLE_BYTES + i * sizeof(h), sizeof(h));
+                if (hipIpcOpenMemHandle(&m[i], h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                    for (int k = 0; k < i; ++k) (void)hipIpcCloseMemHandle(m[k]);
+                    return ALLRED_ERR_HIP;   // peers opened so far stay in opened[] for destroy
+                }
+            }
+            p->peer_win[q][0] = static_cast<uint16_t*>(m[0]);
+            p->peer_win[q][1] = static_cast<uint16_t*>(m[1]);
+            p->peer_flags[q] = static_cast<uint32_t*>(m[2]);
+            p->opened[q] = true;
         }
-        hipIpcMemHandle_t hw, hf;
-        std::memcpy(&hw, all + (size_t)q * ALLRED_PEER_HANDLE_BYTES, sizeof(hw));
-        std::memcpy(&hf, all + (size_t)q * ALLRED_PEER_HANDLE_BYTES + ALLRED_PEER_HANDLE_BYTES / 2, sizeof(hf));
-        void* w = nullptr;
-        void* f = nullptr;
-        if (hipIpcOpenMemHandle(&w, hw, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ALLRED_ERR_HIP;
-        if (hipIpcOpenMemHandle(&f, hf, hipIpcMemLazyEnablePeerAccess) != hipSuccess) return ALLRED_ERR_HIP;
-        p->peer_win[q] = static_cast<uint16_t*>(w);
-        p->peer_flags[q] = static_cast<uint32_t*>(f);
-        p->peer_hfl[q] = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(w) + p->hfl_off);
-        p->peer_ll[q] = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(w) + p->ll_off);
-        p->opened[q] = true;
+        uint8_t* f = reinterpret_cast<uint8_t*>(p->peer_flags[q]);
+        p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + p->hfl_off);
+        p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + p->ll_off);
     }
     p->connected = true;
     return ALLRED_OK;
@@ -148,7 +171,7 @@ namespace {
 // windows of this call's parity, as mapped in this process
 void parity_windows(allred_peer* p, uint16_t** wins) {
     const size_t parity = p->calls & 1u;
-    for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q] + parity * p->max_elems;
+    for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q][parity];
 }
 
 }  // namespace
@@ -160,7 +183,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
     if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     uint16_t* bucket = buf;
     int st = ALLRED_OK;
-    if (p->hier_ll && local_ranks == 64 && p->nranks <= 8 && p->win_uncached && n % (256 * (size_t)p->nranks) == 0 &&
+    if (p->hier_ll && local_ranks == 64 && p->nranks <= 8 && p->flags_uncached && n % (256 * (size_t)p->nranks) == 0 &&
         (n / 256) * 128 <= p->ll_box_words) {
         // the hierarchical step in one launch with LL (push) hand-offs (k_hier_ll): same bits
         const uint8_t* order = nullptr;
@@ -169,7 +192,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
         st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
-                            stream);
+                            p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -185,7 +208,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         uint16_t* wins[ALLRED_MAX_NODES];
         parity_windows(p, wins);
         st = launch_hier_oneshot(buf, n, order, wins, p->peer_hfl, p->nranks, p->rank, n, p->calls + 1u, p->status,
-                                 stream);
+                                 p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -263,6 +286,12 @@ int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     return ALLRED_OK;
 }
 
+int allred_peer_set_max_groups(allred_peer* p, uint32_t groups) {
+    if (!p) return ALLRED_ERR_ARG;
+    p->max_groups = groups;
+    return ALLRED_OK;
+}
+
 int allred_peer_status(allred_peer* p, uint32_t* out) {
     if (!p || !out) return ALLRED_ERR_ARG;
     if (hipMemcpy(out, p->status, 4, hipMemcpyDeviceToHost) != hipSuccess) return ALLRED_ERR_HIP;
@@ -276,10 +305,11 @@ int allred_peer_destroy(allred_peer* p) {
     (void)hipDeviceSynchronize();
     for (int q = 0; q < p->nranks; ++q) {
         if (!p->opened[q]) continue;
-        (void)hipIpcCloseMemHandle(p->peer_win[q]);
+        (void)hipIpcCloseMemHandle(p->peer_win[q][0]);
+        (void)hipIpcCloseMemHandle(p->peer_win[q][1]);
         (void)hipIpcCloseMemHandle(p->peer_flags[q]);
     }
-    (void)hipFree(p->win);
+    for (uint16_t* w : p->win) (void)hipFree(w);
     (void)hipFree(p->flags);
     (void)hipFree(p->status);
     delete p;

@@ -35,6 +35,13 @@ def test_every_declared_symbol_is_exported_and_bound():
         assert re.search(rf"\bT {n}\b", nm), n
 
 
+def test_header_constants_match_python_bindings():
+    src = open(os.path.join(ROOT, "include", "allred.h")).read()
+    defines = dict(re.findall(r"#define\s+(ALLRED_\w+)\s+(0x[0-9a-fA-F]+|\d+)u?\b", src))
+    assert int(defines["ALLRED_PEER_HANDLE_BYTES"], 0) == _lib.PEER_HANDLE_BYTES
+    assert int(defines["ALLRED_PEER_TIMEOUT"], 0) == t.PEER_TIMEOUT
+
+
 def test_status_strings():
     assert _lib.lib.allred_abi_version() == 1
     for st in range(0, -8, -1):

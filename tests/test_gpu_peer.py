@@ -227,3 +227,66 @@ def test_peer_scheduled_program_multi_process_one_gpu(world):
     for rank, fails, status in results:
         assert fails == [], (rank, fails)
         assert status == 0, (rank, status)
+
+
+def big_window_worker(rank, world, port, q):
+    """allred_peer_create / connect with the bench's windows (1 GiB buckets,
+    2 parities): an IPC-exported allocation of ~2 GiB hung in the peer's
+    hipIpcOpenMemHandle on these boxes, so each parity is its own allocation.
+    One small allreduce afterwards proves the mapping is live."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        import tenstorrentallreduce_amd as t
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        peer = t.Peer(world, rank, 0, (1 << 30) // 2)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        fails = []
+        for call in range(2):   # both parities
+            buf = torch.full((8 * world * 64,), rank + 1, dtype=torch.bfloat16, device="cuda:0").view(torch.int16)
+            peer.allreduce(buf.data_ptr(), buf.numel(), torch.cuda.current_stream())
+            torch.cuda.synchronize()
+            want = float(world * (world + 1) // 2)
+            got = buf.view(torch.bfloat16).float()
+            if not bool((got == want).all()):
+                fails.append((call, got[:4].tolist(), want))
+            dist.barrier()
+        status = peer.status()
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+def test_peer_one_gib_windows_open_and_reduce():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    world = 2
+    procs = [ctx.Process(target=big_window_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in procs:
+            results.append(q.get(timeout=90))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails, status in results:
+        assert fails == [], (rank, fails)
+        assert status & t_timeout_bit() == 0, (rank, status)
+
+
+def t_timeout_bit():
+    sys.path.insert(0, ROOT)
+    import tenstorrentallreduce_amd as t
+    return t.PEER_TIMEOUT
