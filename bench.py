@@ -7,7 +7,7 @@
 A step is one allreduce of device-resident bf16 buckets:
   N = 1  BASELINE config 2: the 8x8 Swing BO allreduce of 64 virtual ranks x
          655,360 B (5 tiles per block) in one MI355X's HBM, executed as the
-         one-pass fused HIP kernel (k_tree_lds_pipe<64>, bit-exact with the
+         one-pass fused HIP kernel (k_tree_lds_lag<64>, bit-exact with the
          12-step schedule).  32 rotating bucket sets (1.3 GB, 5x the 256 MiB Infinity
          Cache) so every step streams from HBM; the K steps are replayed from
          a captured HIP graph.
@@ -92,6 +92,16 @@ def cpu_baseline() -> dict:
         "online_cpus": os.sysconf("SC_NPROCESSORS_ONLN"),
         "per_rank_last_rep_ns": per_rank,
     }
+
+
+# the fused BO kernel the engine launches at config 2 (kernels.hip launch_tree_fused;
+# ALLRED_PIPE_LAG=0 / ALLRED_PIPE_REL=0 select the earlier forms for A/B)
+if os.environ.get("ALLRED_PIPE_LAG", "1") != "0":
+    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_lag<64, 32, false>", "k_tree_lds_lag64"
+elif os.environ.get("ALLRED_PIPE_REL", "1") == "1":
+    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_pipe<64, 1, 32, true, true>", "k_tree_lds_pipe64"
+else:
+    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_pipe<64, 1, 32, true, false>", "k_tree_lds_pipe64"
 
 
 def pmc_traffic(kernel_key: str):
@@ -219,8 +229,8 @@ def bench_single(args) -> dict:
                    "ranks": RANKS, "bytes_per_rank": ELEMS * 2, "algo": "swing", "variant": "BO",
                    "exec": "fused", "launches_per_step": plan.launches, "hip_graph": graph is not None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic("k_tree_lds_pipe64"),
-                     "kernel": ("k_tree_lds_pipe<64, 1, 32, true, true>" if os.environ.get("ALLRED_PIPE_REL", "1") == "1" else "k_tree_lds_pipe<64, 1, 32, true, false>"), "algorithmic_bytes_per_launch": alg_bytes},
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(FUSED_KEY),
+                     "kernel": FUSED_KERNEL, "algorithmic_bytes_per_launch": alg_bytes},
         "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
                               "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
@@ -396,6 +406,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
     #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
+    #   peer_hier_ws  the same step pipelined per tile: rank-row stores overlap the
+    #                 local pass's loads, one LL wave per workgroup (k_hier_ws)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -414,9 +426,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         else:
             one_kernel = one_kernel and kind != "peer_launches"
             peer.set_oneshot_max((4 << 20) if one_kernel else 0)
-            peer.set_hier_ll(kind == "peer_hier_ll")
+            peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_ws": 2}.get(kind, 0))
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
-            peer.set_hier_ll(False)
+            peer.set_hier_ll(0)
             peer.set_oneshot_max(4 << 20)
 
     # the reference transport: RCCL, or (--share-gpu) the peer launch form
@@ -430,7 +442,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         ref = small.clone()
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
-        for kind in ("peer_swing", "peer_hier", "peer_hier_ll"):
+        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_ws"):
             x = small.clone()
             note(rank, f"verify: {kind}")
             run(kind, x, fresh=True)
@@ -519,8 +531,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         return None
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    if transport in ("peer_hier", "peer_hier_ll"):   # the step IS one launch: its HBM bytes over its time
-        roof = {"kernel": "k_hier_oneshot (whole step)" if transport == "peer_hier" else "k_hier_ll (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
+    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_ws": "k_hier_ws"}
+    if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
+        roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
     else:
         roof = {"kernel": "k_tree_lds_pipe<64, 1, 32, false> + k_broadcast (local phases)",
@@ -532,7 +545,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
            "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "
                         "windows, broadcast (per-tile flags)",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
-                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
+                           "(data+epoch words) into peer-mapped xGMI windows, broadcast",
+           "peer_hier_ws": "ONE kernel, pipelined per tile: on-GPU tree reduce overlapped with the rank-row "
+                           "stores, mem_2D one-shot across GPUs by one LL-push wave per workgroup"}[transport]
     return {
         "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),

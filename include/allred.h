@@ -280,7 +280,7 @@ int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int 
  * barrier / all-gather launches.  Same result bits either way.  Every rank
  * must use the same setting. */
 int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
-/* enable != 0: with local_ranks == 64 and nranks <= 8, allred_peer_allreduce
+/* enable = 1 or 2: with local_ranks == 64 and nranks <= 8, allred_peer_allreduce
  * runs the hierarchical step as one kernel with LL hand-offs (each cross-GPU
  * transfer a push of self-validating 8-byte data+epoch words into the
  * consumer's own memory; no flags, no remote reads) for buckets of up to
@@ -288,6 +288,9 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * (allred_mem_2D semantics over the per-GPU trees).  Every rank must use the
  * same setting.  Replaces nothing in the reference (its mem_2D phases sync
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
+/* enable = 2 runs the same step pipelined per tile (k_hier_ws): the local
+ * pass's loads and the rank-row stores overlap, and one specialised wave per
+ * workgroup carries the cross-GPU hand-offs; same result bits.  0 = off. */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
 /* Caps the grid of the hierarchical one-kernel forms at `groups` workgroups
  * (0 = default: 512, two per CU, the whole grid resident on a GPU of its own).

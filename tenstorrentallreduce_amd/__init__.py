@@ -309,9 +309,11 @@ class Peer:
         """Buckets of at most nbytes run as one kernel (same bits either way)."""
         check(lib.allred_peer_set_oneshot_max(self._h, nbytes), "peer_set_oneshot_max")
 
-    def set_hier_ll(self, enable: bool) -> None:
-        """64 local ranks: the hierarchical step with LL push hand-offs (k_hier_ll)."""
-        check(lib.allred_peer_set_hier_ll(self._h, int(bool(enable))), "peer_set_hier_ll")
+    def set_hier_ll(self, mode) -> None:
+        """64 local ranks: the hierarchical step with LL push hand-offs — 1 (or True)
+        phased (k_hier_ll), 2 pipelined per tile on specialised waves (k_hier_ws),
+        0 (or False) off.  Same result bits in every mode."""
+        check(lib.allred_peer_set_hier_ll(self._h, int(mode)), "peer_set_hier_ll")
 
     def set_max_groups(self, groups: int) -> None:
         """Grid cap of the hierarchical one-kernel forms (0 = one full grid per GPU);

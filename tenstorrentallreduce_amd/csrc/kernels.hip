@@ -391,6 +391,98 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// k_tree_lds_lag: the fused BO pass of k_tree_lds_pipe (same tree, same bits)
+// with every tile's stores one iteration late.  Iteration j: wait for tile j's
+// loads, reduce it out of LDS, issue tile j+2's loads into its buffer (early
+// release), then store tile j-1's result, kept in registers from the previous
+// iteration.  A tile's stores thus always queue behind the next tile's loads
+// (k_tree_lds_pipe issues them between two loads), and the waves never wait
+// for a store before a load.  Measured on the hierarchical step's data path
+// (tools/ubench/ws_trace.hip): 14.6 us vs 15.4 us with stores in iteration j.
+// SWBAR: the 4 waves sync through an LDS counter instead of s_barrier (A/B).
+// Issue order per wave: L0 L1 | L2 | L3 S0 | L4 S1 | ..., so after tile j's
+// loads come tile j+1's loads and the stores of tiles j-2 and j-3.
+// ---------------------------------------------------------------------------
+template <int P, int TV, bool SWBAR>
+__global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                         const uint8_t* __restrict__ order, uint64_t block_vec,
+                                                         uint64_t ntiles) {
+    constexpr int RPI = 64 / TV, RPW = P / 4, OPS = RPW / RPI, LPL = OPS;
+    static_assert(OPS >= 1 && 3 * OPS <= 63, "vmcnt is 6 bits");
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[P * ALLRED_MAX_NODES];
+    __shared__ uint32_t bar_ctr;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + RPI * k + q;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
+        }
+    };
+    auto store = [&](uint64_t t, uint4 res) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + RPI * k + q;
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + t * TV + c, res);
+        }
+    };
+    uint32_t bar = 0;
+    auto barrier = [&]() {
+        if (SWBAR) {
+            bar += 4;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) __hip_atomic_fetch_add(&bar_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            while (__hip_atomic_load(&bar_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < bar) {
+            }
+            asm volatile("" ::: "memory");
+        } else {
+            lds_barrier();
+        }
+    };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
+        reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
+    if (threadIdx.x == 0) bar_ctr = 0;
+    __syncthreads();
+    if (mine > 0) issue(tile_of(0), 0);
+    if (mine > 1) issue(tile_of(1), 1);
+    uint4 prev = make_uint4(0, 0, 0, 0);
+    for (int j = 0; j < mine; ++j) {
+        wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
+        barrier();   // every wave's rows of tile j are in LDS
+        const uint4* tile = buf[j & 1];
+        const uint64_t t = tile_of(j), v0 = t * TV;
+        const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * q;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s = 1; s < LPL; s *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s) x[i] = add8(x[i], x[i + s]);
+        uint4 pw = x[0];
+#pragma unroll
+        for (int s = TV; s < 64; s *= 2) pw = add8(pw, shfl_xor4(pw, s));   // tree levels across lane groups
+        if (q == 0) part[j & 1][w * TV + c] = pw;
+        barrier();   // every wave has read tile j out of buf[j & 1]; the partials are in
+        if (j + 2 < mine) issue(tile_of(j + 2), j & 1);
+        const uint4* pp = part[j & 1];
+        const uint4 res = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+        if (j >= 1) store(tile_of(j - 1), prev);
+        prev = res;
+    }
+    if (mine > 0) store(tile_of(mine - 1), prev);
+}
+
+// ---------------------------------------------------------------------------
 // LO allreduce of P ranks in one pass: the butterfly itself.  Rank x keeps
 // its own tree (for Swing the P results differ in bf16 rounding, exactly as
 // the reference's per-core LO results do).  Lane (q, x) = q * P + x holds
@@ -1308,6 +1400,334 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_hier_ws: the k_hier_ll step (same bits) with the local pass and the
+// cross-GPU hand-offs pipelined per tile on specialised waves.  k_hier_ll
+// runs its phases one after the other (all reads, then all writes), so HBM
+// reads and writes never overlap; here they do, as in the one-GPU pass.
+//   waves 0-3 (data): the double-buffered LDS tree of k_tree_lds_pipe with
+//     early release.  Iteration j: wait for tile j's loads, tree -> partial
+//     in LDS, issue tile j+2's loads into tile j's buffer, then store tile
+//     j-1's result to the 64 rank rows, behind the loads in flight.  Their
+//     only waits are exact vmcnt counts of their own loads and LDS counters.
+//   wave 4 (pusher): stores only, never waits on memory.  Sums tile j's four
+//     wave partials and pushes it to the owner's inbox (its own partial, when
+//     this GPU owns tile j, goes to the poller through LDS); pushes the result
+//     of every tile this GPU owns to the other GPUs' boxes.  It serves
+//     whichever is ready first, so a slow result never holds a partial back.
+//   wave 5 (poller): loads only, so each poll costs one load latency and never
+//     waits for a store's acknowledgement.  Owned tile: the W-1 other partials
+//     from the inbox + its own from LDS, fp32 owner first then ascending, one
+//     rounding; other tiles: the result from this GPU's box.  -> LDS.
+// Waves talk through monotonic LDS counters instead of s_barrier, so a
+// polling wave never holds the others at a barrier.  Deadlock-free with a
+// resident grid: workgroup g runs the same tile sequence on every GPU; the
+// data waves publish tile j's partial before they wait for tile j-1's
+// result, and a tile-j hand-off needs nothing of a later tile anywhere.
+// Same LL layout, epochs and parities as k_hier_ll.  With W = 1 every tile
+// is owned and nothing leaves LDS.
+// ---------------------------------------------------------------------------
+constexpr int kWsBlock = 384;   // 4 data waves, the pusher, the poller
+
+// ALLRED_WS_TRACE (tools/ubench only): per-workgroup s_memrealtime stamps (100 MHz)
+// kept in LDS (an extra store would upset the data waves' exact vmcnt counts)
+// and written out by each wave at its end: [0] start, [1+j] tile j's loads
+// landed, [4+j] tile j's result seen by the data waves, [7] data end, [8+j]
+// result j in LDS (poller), [11+j] partial j pushed (pusher), 3 tiles at most.
+#ifdef ALLRED_WS_TRACE
+__device__ uint64_t g_ws_trace[1024 * 16];
+#define WS_MARK(slot)                                                        \
+    do {                                                                     \
+        if ((slot) < 16 && lane == 0) ws_tr[slot] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define WS_FLUSH(lo, hi)                                                     \
+    do {                                                                     \
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                  \
+        if (lane >= (lo) && lane < (hi)) g_ws_trace[blockIdx.x * 16 + lane] = ws_tr[lane]; \
+    } while (0)
+#else
+#define WS_MARK(slot) do { } while (0)
+#define WS_FLUSH(lo, hi) do { } while (0)
+#endif
+
+#ifndef ALLRED_WS_NAP
+#define ALLRED_WS_NAP 1   // s_sleep argument of the waves' LDS waits (64-clock units; A/B knob)
+#endif
+__device__ __forceinline__ void ws_nap() {
+    if (ALLRED_WS_NAP > 0) __builtin_amdgcn_s_sleep(ALLRED_WS_NAP);
+}
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// spin until *p >= target (LDS; wave-uniform), then keep later LDS reads behind it.
+// Bounded like every peer wait: a counter that never arrives (a bug) sets status
+// bit 0 and lets the wave run to the end instead of hanging the GPU.
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t target, bool nap, uint32_t* status) {
+    for (uint64_t spin = 0; lds_ld(p) < target; ++spin) {
+        if (spin > kPeerSpinLimit) {
+            atomicOr(status, 1u);
+            break;
+        }
+        if (nap) ws_nap();
+    }
+    asm volatile("" ::: "memory");
+}
+// publish: this wave's earlier LDS accesses complete, then one lane bumps / sets the counter
+__device__ __forceinline__ void lds_signal_add(uint32_t* p, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_fetch_add(p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_signal_set(uint32_t* p, uint32_t v, int lane) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// MODE (A/B diagnostics, tools/ubench/ws_trace.hip; W = 1 only for 1 and 2):
+// 0 the product; 1 the data waves alone, storing tile j from the four wave
+// partials in iteration j; 2 the same with the stores one iteration late.
+template <int MODE = 0>
+__global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                      const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+                                                      uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
+                                                      uint32_t epoch, uint32_t* status) {
+    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
+    enum { kBar = 0, kPartReady, kPartFree, kOwnReady, kOwnFree, kResReady, kResFree, kPushDone, kCtrs };
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][4 * TV];
+    __shared__ __attribute__((aligned(16))) uint4 ownp[2][TV];
+    __shared__ __attribute__((aligned(16))) uint4 resb[2][TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    __shared__ uint32_t ctr[kCtrs];
+#ifdef ALLRED_WS_TRACE
+    __shared__ uint64_t ws_tr[16];
+#endif
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    if (threadIdx.x < kCtrs) ctr[threadIdx.x] = 0;
+    __syncthreads();   // the only s_barrier: from here on the waves sync through ctr[]
+    if (w == 0) WS_MARK(0);
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    if (w < 4) {
+        // ---------------- data waves
+        const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+        auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+                lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+            }
+        };
+        auto store_result = [&](int j) {   // tile j's result (poller) -> my 16 rank rows
+            lds_wait_ge(&ctr[kResReady], (uint32_t)j + 1u, true, status);
+            if (w == 0 && j < 3) WS_MARK(4 + j);
+            const uint4 res = resb[j & 1][c];
+            lds_signal_add(&ctr[kResFree], lane);
+            const uint64_t v0 = tile_of(j) * TV;
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res);
+            }
+        };
+        uint32_t bar = 0;
+        auto data_barrier = [&]() {   // the 4 data waves only
+            bar += 4;
+            lds_signal_add(&ctr[kBar], lane);
+            lds_wait_ge(&ctr[kBar], bar, false, status);
+        };
+        auto store_rows = [&](int j, uint4 res) {
+            const uint64_t v0 = tile_of(j) * TV;
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res);
+            }
+        };
+        uint4 res_prev = make_uint4(0, 0, 0, 0);
+        if (mine > 0) issue(tile_of(0), 0);
+        if (mine > 1) issue(tile_of(1), 1);
+        for (int j = 0; j < mine; ++j) {
+            // issued after tile j's loads: tile j+1's loads, and the stores of
+            // tiles j-2 and j-3 (issue order L0 L1 | L2 | L3 S0 | L4 S1 | ...)
+            if (MODE == 1)   // L0 L1 | L2 S0 | L3 S1 | ...
+                wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 1 ? 1 : 0) + (j >= 2 ? 1 : 0));
+            else
+                wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
+            data_barrier();   // every wave's rows of tile j are in LDS
+            if (w == 0 && j < 3) WS_MARK(1 + j);
+            const uint4* tile = buf[j & 1];
+            const uint8_t* ord = ord_lds + RPW * w + LPL * h;
+            uint4 x[LPL];
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+            for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+            if (MODE == 0 && j >= 2) lds_wait_ge(&ctr[kPartFree], (uint32_t)j - 1u, true, status);   // pusher took partial j-2
+            if (h == 0) part[j & 1][w * TV + c] = pw;
+            lds_signal_add(&ctr[kPartReady], lane);
+            data_barrier();   // every wave has read tile j out of buf[j & 1]
+            if (j + 2 < mine) issue(tile_of(j + 2), j & 1);
+            if (MODE == 0) {
+                if (j >= 1) store_result(j - 1);
+            } else {
+                const uint4* pp = part[j & 1];
+                const uint4 res = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+                if (MODE == 1) store_rows(j, res);
+                if (MODE >= 2 && j >= 1) store_rows(j - 1, res_prev);
+                res_prev = res;
+            }
+        }
+        if (MODE == 0 && mine > 0) store_result(mine - 1);
+        if (MODE >= 2 && mine > 0) store_rows(mine - 1, res_prev);
+        if (MODE == 3) lds_signal_add(&ctr[kPushDone], lane);
+        if (w == 0) {
+            WS_MARK(7);
+            WS_FLUSH(0, 8);
+        }
+        return;
+    }
+    if (MODE == 3) {   // the two extra waves only spin on LDS until the data waves are done
+        lds_wait_ge(&ctr[kPushDone], 4u, true, status);
+        return;
+    }
+    if (MODE != 0) return;
+    if (w == 4) {
+        // ---------------- pusher: partials to owners, owned results to every other GPU
+        uint64_t* box[4];   // lane (h, c) serves GPUs 4h .. 4h+3 (loaded once: a per-lane
+                            // kernarg index is a vector load, and its wait would take every store)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) box[k] = 4 * h + k < W ? lp.ll[4 * h + k] + box_words : nullptr;
+        int jp = 0, jr = 0;
+        for (uint64_t idle = 0; jr < mine;) {
+            bool moved = false;
+            if (jp < mine && lds_ld(&ctr[kPartReady]) >= 4u * (uint32_t)(jp + 1)) {
+                const uint64_t t = tile_of(jp);
+                const int o = owner_of(t);
+                if (o != me || jp < 2 || lds_ld(&ctr[kOwnFree]) >= (uint32_t)jp - 1u) {
+                    asm volatile("" ::: "memory");
+                    const uint4* pp = part[jp & 1];
+                    const uint4 pv =
+                        add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+                    if (o == me) {
+                        if (h == 0) ownp[jp & 1][c] = pv;
+                    } else if (h == 0) {
+                        ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, pv, epoch);
+                    }
+                    lds_signal_set(&ctr[kPartFree], (uint32_t)jp + 1u, lane);
+                    lds_signal_set(&ctr[kOwnReady], (uint32_t)jp + 1u, lane);
+                    if (jp < 3) WS_MARK(11 + jp);
+                    ++jp;
+                    moved = true;
+                }
+            }
+            if (jr < jp) {
+                const uint64_t t = tile_of(jr);
+                if (owner_of(t) != me) {
+                    lds_signal_set(&ctr[kPushDone], (uint32_t)jr + 1u, lane);
+                    ++jr;
+                    moved = true;
+                } else if (lds_ld(&ctr[kResReady]) >= (uint32_t)jr + 1u) {
+                    asm volatile("" ::: "memory");
+                    const uint4 r = resb[jr & 1][c];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                        if (4 * h + k < W && 4 * h + k != me) ll_put(box[k] + t * 128 + c * 4, r, epoch);
+                    lds_signal_set(&ctr[kPushDone], (uint32_t)jr + 1u, lane);
+                    ++jr;
+                    moved = true;
+                }
+            }
+            if (moved) {
+                idle = 0;
+            } else if (++idle > kPeerSpinLimit) {   // bounded like every wait (status bit 0)
+                atomicOr(status, 1u);
+                break;
+            } else {
+                ws_nap();
+            }
+        }
+        WS_FLUSH(11, 14);
+        return;
+    }
+    // ---------------- poller (wave 5)
+    uint64_t* const my_ll = lp.ll[me];
+    for (int j = 0; j < mine; ++j) {
+        const uint64_t t = tile_of(j);
+        uint4 r;
+        if (owner_of(t) == me) {
+            // lane (h, c) polls the slots of GPUs 4h .. 4h+3 except its own at once
+            const uint64_t* inbox = my_ll + (t - (uint64_t)me * tiles_per_owner) * W * 128 + c * 4;
+            uint4 y[4];
+            for (uint64_t spin = 0;; ++spin) {
+                uint64_t v[4][4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        v[k][e] = (4 * h + k < W && 4 * h + k != me)
+                                      ? __hip_atomic_load(inbox + (4 * h + k) * 128 + e, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM)
+                                      : (uint64_t)epoch << 32;
+                uint32_t bad = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) bad |= (uint32_t)(v[k][e] >> 32) ^ epoch;
+                    y[k] = make_uint4((uint32_t)v[k][0], (uint32_t)v[k][1], (uint32_t)v[k][2], (uint32_t)v[k][3]);
+                }
+                if (bad == 0) break;
+                if (spin > kPeerSpinLimit) {
+                    atomicOr(status, 1u);
+                    break;
+                }
+                ws_nap();
+            }
+            if (j == 0) WS_MARK(14);
+            lds_wait_ge(&ctr[kOwnReady], (uint32_t)j + 1u, true, status);
+            if (j == 0) WS_MARK(15);
+            const uint4 own = ownp[j & 1][c];
+            lds_signal_set(&ctr[kOwnFree], (uint32_t)j + 1u, lane);
+            uint4 yo[4];   // the other half's slots
+#pragma unroll
+            for (int k = 0; k < 4; ++k) yo[k] = shfl_xor4(y[k], 32);
+            auto slot = [&](int q) { return q == me ? own : ((q >> 2) == h) ? y[q & 3] : yo[q & 3]; };
+            float a[8] = {lo_f(own.x), hi_f(own.x), lo_f(own.y), hi_f(own.y),
+                          lo_f(own.z), hi_f(own.z), lo_f(own.w), hi_f(own.w)};
+#pragma unroll
+            for (int q = 0; q < kLLMaxGpus; ++q) {
+                if (q >= W || q == me) continue;
+                const uint4 yq = slot(q);
+                a[0] += lo_f(yq.x); a[1] += hi_f(yq.x);
+                a[2] += lo_f(yq.y); a[3] += hi_f(yq.y);
+                a[4] += lo_f(yq.z); a[5] += hi_f(yq.z);
+                a[6] += lo_f(yq.w); a[7] += hi_f(yq.w);
+            }
+            r = make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
+        } else {
+            r = ll_get(my_ll + box_words + t * 128 + c * 4, epoch, status);
+            lds_signal_set(&ctr[kOwnFree], (uint32_t)j + 1u, lane);   // in tile order, owned or not
+        }
+        if (j >= 2) {   // slot j & 1 free: the data waves and the pusher are done with tile j-2
+            lds_wait_ge(&ctr[kResFree], 4u * (uint32_t)(j - 1), true, status);
+            lds_wait_ge(&ctr[kPushDone], (uint32_t)j - 1u, true, status);
+        }
+        if (h == 0) resb[j & 1][c] = r;
+        lds_signal_set(&ctr[kResReady], (uint32_t)j + 1u, lane);
+        if (j < 3) WS_MARK(8 + j);
+    }
+    WS_FLUSH(8, 11);
+    WS_FLUSH(14, 16);
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 // ALLRED_TREE=registers selects the register-only k_tree for the fused BO pass
@@ -1344,6 +1764,16 @@ int pipe_rel() {
     static const int v = [] {
         const char* e = std::getenv("ALLRED_PIPE_REL");
         return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
+
+// ALLRED_PIPE_LAG=0 selects the round-1 k_tree_lds_pipe (stores in the tile's own
+// iteration) for the fused BO pass on HBM; default: k_tree_lds_lag (A/B)
+bool pipe_lag() {
+    static const bool v = [] {
+        const char* e = std::getenv("ALLRED_PIPE_LAG");
+        return !(e && e[0] == '0');
     }();
     return v;
 }
@@ -1488,6 +1918,23 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     return last_error();
 }
 
+int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                   void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
+        ntiles * 128 > box_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    // 2 per CU (70 KiB of LDS each): the whole grid resident
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
+    hipLaunchKernelGGL(k_hier_ws<0>, dim3(grid), dim3(kWsBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
+                       me, ntiles, ntiles / nranks, box_words, epoch, status);
+    return last_error();
+}
+
 int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
                         size_t n, uint32_t epoch, uint32_t* status, void* stream) {
     if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
@@ -1583,6 +2030,11 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
                 case 64: TSA_PIPE(64, 2, 32); break;
                 default: return ALLRED_ERR_UNSUPPORTED;
             }
+        } else if (pipe_lag() && total == 64 && !host_memory && !cap_env) {
+            // stores one iteration late, behind the next tile's loads (config 2:
+            // 14.44 vs 15.30 us for k_tree_lds_pipe, tools/ubench/fused_ab.hip)
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, false>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order,
+                               bv, tiles);
         } else if (rel && total == 64 && !host_memory) {
             // REL: NB = rel buffers; NB >= 3 needs one workgroup per CU (grid <= 256)
             const unsigned g1 = (unsigned)(tiles < 256 ? tiles : 256);

@@ -55,7 +55,7 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
-    bool hier_ll = false;
+    int hier_ll = 0;                // 0 off, 1 k_hier_ll (phased), 2 k_hier_ws (pipelined)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
 };
 
@@ -191,8 +191,9 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
-        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
-                            p->max_groups, stream);
+        st = (p->hier_ll == 2 ? launch_hier_ws : launch_hier_ll)(buf, n, order, ll, p->nranks, p->rank, n,
+                                                                 p->ll_box_words, p->calls + 1u, p->status,
+                                                                 p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -282,7 +283,8 @@ int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
 
 int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
-    p->hier_ll = enable != 0;
+    if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
+    p->hier_ll = enable;
     return ALLRED_OK;
 }
 

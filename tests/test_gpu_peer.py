@@ -97,10 +97,15 @@ def worker(rank, world, port, q):
         # launch form, two calls back to back each (then LL once more after the
         # launch form: its LL boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
-        for mi, (mode, limit, ll) in enumerate((("hier_one_kernel", 1 << 40, False), ("hier_ll", 1 << 40, True),
-                                                ("hier_launches", 0, False), ("hier_ll_again", 0, True))):
+        # k_hier_ws (pipelined, specialised waves) in full and capped grids (a
+        # capped grid gives every workgroup many tiles: the whole pipeline)
+        for mi, (mode, limit, ll, cap) in enumerate((("hier_one_kernel", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
+                                                     ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
+                                                     ("hier_ws", 0, 2, 0), ("hier_ws_capped", 0, 2, 2),
+                                                     ("hier_ws_one_group", 0, 2, 1))):
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
+            peer.set_max_groups(cap)
             runs = []
             for rep in range(2):
                 data = [np.random.default_rng(700 + 100 * mi + 10 * rep + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
@@ -122,7 +127,8 @@ def worker(rank, world, port, q):
                 if bad:
                     fails.append((mode, rep, bad))
             dist.barrier()
-        peer.set_hier_ll(False)
+        peer.set_hier_ll(0)
+        peer.set_max_groups(0)
         status = peer.status()
         dist.barrier()
         peer.close()
@@ -290,3 +296,44 @@ def t_timeout_bit():
     sys.path.insert(0, ROOT)
     import tenstorrentallreduce_amd as t
     return t.PEER_TIMEOUT
+
+
+@pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
+def test_hier_forms_single_gpu_bit_exact(n, cap):
+    """One GPU (W = 1), 64 local ranks: the pipelined k_hier_ws, the phased
+    k_hier_ll, the flag form k_hier_oneshot and the launch form give the same
+    bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
+    mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
+    (both LL parities).  Config-2 size full grid and with capped grids (many
+    tiles per workgroup)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import tenstorrentallreduce_amd as t
+    import oracle
+    local = 64
+    peer = t.Peer(1, 0, 0, 2 * n)
+    peer.connect([peer.handle()])
+    try:
+        peer.set_max_groups(cap)
+        cases = []
+        for rep in range(2):
+            data = np.random.default_rng(900 + rep).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+            loc = [x.copy() for x in data]
+            oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+            cases.append((data, loc[0]))
+        ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
+        for ll, limit in ((2, 0), (1, 0), (0, 1 << 40), (0, 0), (2, 0)):
+            peer.set_hier_ll(ll)
+            peer.set_oneshot_max(limit)
+            bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
+            torch.cuda.synchronize()
+            for b in bufs:   # back to back: both LL parities / epochs
+                peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+            torch.cuda.synchronize()
+            for rep, (b, (_, want)) in enumerate(zip(bufs, cases)):
+                bad = int((b.cpu().numpy().view(np.uint16) != want[None, :]).sum())
+                assert bad == 0, (ll, limit, rep, bad)
+        assert peer.status() & t.PEER_TIMEOUT == 0
+    finally:
+        peer.set_hier_ll(0)
+        peer.close()

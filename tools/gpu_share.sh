@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-share}
 mkdir -p $OUT
-for n in 2 4; do
+for n in ${NS:-2 4}; do
   timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n \
       --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus $n --share-gpu \
       ${EXTRAS:---no-extras} --steps 50 --warmup 5 > $OUT/bench_share$n.json 2> $OUT/bench_share$n.err
