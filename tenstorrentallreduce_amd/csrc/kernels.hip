@@ -698,6 +698,69 @@ __global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, u
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_mem_lds_lag: the fused mem_2D pass of k_mem_lds (same bits: per element
+// fp32 owner first, then every other rank ascending, one rounding) as a
+// persistent double-buffered pipeline with the k_tree_lds_lag schedule, 64
+// ranks: one thread per element of a 256-element tile, results through a
+// small LDS row, each tile's 64 row stores one iteration late, behind tile
+// j+2's loads.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_mem_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                        uint64_t block_vec, uint64_t ntiles) {
+    constexpr int P = 64, TV = 32, RPW = 16, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 resb[2][TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+        }
+    };
+    auto store = [&](uint64_t t, uint4 res) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + t * TV + c, res);
+        }
+    };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    if (mine > 0) issue(tile_of(0), 0);
+    if (mine > 1) issue(tile_of(1), 1);
+    uint4 prev = make_uint4(0, 0, 0, 0);
+    const int e = threadIdx.x;   // element of the tile (0..255)
+    for (int j = 0; j < mine; ++j) {
+        wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
+        lds_barrier();
+        const uint64_t t = tile_of(j);
+        const int own = (int)(t * TV / block_vec);
+        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(buf[j & 1]);
+        float a = __uint_as_float((uint32_t)t16[own * TV * 8 + e] << 16);
+        for (int r = 0; r < P; ++r) {
+            if (r == own) continue;
+            a += __uint_as_float((uint32_t)t16[r * TV * 8 + e] << 16);
+        }
+        // one rounding; pairs of threads pack their two elements
+        const float b = __shfl_xor(a, 1);
+        if ((e & 1) == 0) reinterpret_cast<uint32_t*>(resb[j & 1])[e >> 1] = pack_rne(a, b);
+        lds_barrier();   // the tile is read out of buf[j & 1]; resb[j & 1] is complete
+        const uint4 res = resb[j & 1][c];
+        if (j + 2 < mine) issue(tile_of(j + 2), j & 1);
+        if (j >= 1) store(tile_of(j - 1), prev);
+        prev = res;
+    }
+    if (mine > 0) store(tile_of(mine - 1), prev);
+}
+
+
 // ranks[r] = src for every r (all-gather of a reduced vector)
 // grid.y picks a group of up to 8 ranks, so even a 640 kB vector fills the chip
 __global__ __launch_bounds__(kBlock) void k_broadcast(uint16_t* __restrict__ ranks, uint64_t stride, int total,
@@ -2071,6 +2134,8 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
             return e ? std::strtoull(e, nullptr, 10) : 512ull;
         }();
         const uint64_t tiles = nv / 32;
+        // (the k_tree_lds_lag schedule — stores one iteration late — measured slower
+        // here: 26.6 vs 24.1 us at 640 kB; the butterfly is not bound by HBM order)
         hipLaunchKernelGGL(k_butterfly_lds64_pipe, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0, st,
                            ranks, stride, d_partner, steps, tiles);
         return last_error();
@@ -2178,6 +2243,13 @@ int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
     const uint64_t bv = nv / total;
+    if (bv % 32 == 0 && total == 64 && nv / 32 >= 1024 && pipe_lag()) {
+        // persistent, stores one iteration late (640 kB: ALLRED_PIPE_LAG=0 gives k_mem_lds)
+        const uint64_t tiles = nv / 32;
+        hipLaunchKernelGGL(k_mem_lds_lag, dim3((unsigned)(tiles < 512 ? tiles : 512)), dim3(kBlock), 0,
+                           (hipStream_t)stream, ranks, stride, bv, tiles);
+        return last_error();
+    }
     if (bv % 32 == 0 && total >= 4) {
         const dim3 grid((unsigned)(nv / 32)), blk(128);
         hipStream_t st = (hipStream_t)stream;

@@ -153,6 +153,21 @@ def test_fused_lds_forms_bit_exact(grid, algo, variant):
     assert (got == np.stack(want)).all()
 
 
+@pytest.mark.parametrize("variant", ["bo", "lo", "mem"])
+@pytest.mark.parametrize("algo", [t.SWING, t.RECDUB])
+def test_fused_persistent_forms_bit_exact_config2_size(algo, variant):
+    """64 ranks x 327,680 bf16 (1280 tiles): the persistent double-buffered
+    fused kernels (k_tree_lds_lag, k_butterfly_lds64_pipe,
+    k_mem_lds_lag) on random bf16, against the oracle."""
+    side, total, n = 8, 64, 327680
+    ranks = rand_ranks(total, n, seed=17 + algo)
+    got = run_plan(algo, {"bo": t.BO, "lo": t.LO, "mem": t.MEM}[variant], side, total, ranks, t.EXEC_FUSED,
+                   stride=t.preferred_rank_stride(n))
+    want = [r.copy() for r in ranks]
+    oracle.allreduce(variant, algo, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
 @pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
 def test_plan_padded_stride(exec_mode):
     side, total, n = 8, 64, 64 * 8 * 3
