@@ -1651,7 +1651,8 @@ __global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ran
         }
         if (MODE == 0 && mine > 0) store_result(mine - 1);
         if (MODE >= 2 && mine > 0) store_rows(mine - 1, res_prev);
-        if (MODE == 3) lds_signal_add(&ctr[kPushDone], lane);
+        if (MODE >= 3) lds_signal_add(&ctr[kPushDone], lane);
+        if (MODE == 4) asm volatile("s_wakeup" ::: "memory");
         if (w == 0) {
             WS_MARK(7);
             WS_FLUSH(0, 8);
@@ -1660,6 +1661,11 @@ __global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ran
     }
     if (MODE == 3) {   // the two extra waves only spin on LDS until the data waves are done
         lds_wait_ge(&ctr[kPushDone], 4u, true, status);
+        return;
+    }
+    if (MODE == 4) {   // the same, sleeping 127 x 64 clocks per check, woken by the data waves' s_wakeup
+        for (uint64_t spin = 0; lds_ld(&ctr[kPushDone]) < 4u && spin < kPeerSpinLimit; ++spin)
+            __builtin_amdgcn_s_sleep(127);
         return;
     }
     if (MODE != 0) return;

@@ -56,6 +56,9 @@ int main(int argc, char** argv) {
             if (form == 3)
                 hipLaunchKernelGGL(k_hier_ws<1>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
                                    0, ntiles, ntiles, box_words, epoch, status);
+            else if (form == 6)
+                hipLaunchKernelGGL(k_hier_ws<4>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
+                                   0, ntiles, ntiles, box_words, epoch, status);
             else if (form == 5)
                 hipLaunchKernelGGL(k_hier_ws<3>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
                                    0, ntiles, ntiles, box_words, epoch, status);
@@ -65,13 +68,13 @@ int main(int argc, char** argv) {
         }
         if (rc) { std::printf("launch rc %d\n", rc); std::exit(1); }
     };
-    const char* names_f[6] = {"", "k_hier_ll", "k_hier_ws", "ws<1> data only", "ws<2> data only lag 1",
-                              "ws<3> lag 1 + 2 spinning waves"};
+    const char* names_f[7] = {"", "k_hier_ll", "k_hier_ws", "ws<1> data only", "ws<2> data only lag 1",
+                              "ws<3> lag 1 + 2 spinning waves", "ws<4> lag 1 + 2 sleeping waves, s_wakeup"};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int round = 0; round < 3; ++round) {
-        for (int form : {1, 2, 3, 4, 5}) {
+        for (int form : {4, 5, 6}) {
             for (int i = 0; i < 20; ++i) run(form, i);
             CK(hipEventRecord(e0, st));
             for (int i = 0; i < REPS; ++i) run(form, i);
@@ -83,6 +86,9 @@ int main(int argc, char** argv) {
                         ms * 1e3 / REPS);
         }
     }
+#ifndef ALLRED_WS_TRACE
+    return 0;
+#else
     // one traced launch
     std::vector<uint64_t> tr(1024 * 16);
     const int traced = argc > 3 ? std::atoi(argv[3]) : 2;
@@ -109,4 +115,5 @@ int main(int argc, char** argv) {
         std::printf("  %-10s min %6.2f  med %6.2f  max %6.2f\n", names[s], v.front(), v[v.size() / 2], v.back());
     }
     return 0;
+#endif
 }
