@@ -2099,7 +2099,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
                 case 64: TSA_PIPE(64, 2, 32); break;
                 default: return ALLRED_ERR_UNSUPPORTED;
             }
-        } else if (pipe_lag() && total == 64 && !host_memory && !cap_env) {
+        } else if (pipe_lag() && total == 64 && !host_memory) {
             // stores one iteration late, behind the next tile's loads (config 2:
             // 14.44 vs 15.30 us for k_tree_lds_pipe, tools/ubench/fused_ab.hip)
             hipLaunchKernelGGL((k_tree_lds_lag<64, 32, false>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order,
