@@ -399,11 +399,15 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 // (k_tree_lds_pipe issues them between two loads), and the waves never wait
 // for a store before a load.  Measured on the hierarchical step's data path
 // (tools/ubench/ws_trace.hip): 14.6 us vs 15.4 us with stores in iteration j.
-// SWBAR: the 4 waves sync through an LDS counter instead of s_barrier (A/B).
+// VAR (A/B arms, tools/ubench/fused_ab.hip, profiles/r01_fused_ab_arms.txt):
+// 2 the product: the first two tiles' loads issued before the 4 KiB tree-order
+// table is staged (14.23-14.29 vs 14.39-14.40 us); 0 the table first; 1 = 0
+// with an LDS-counter barrier instead of s_barrier (no gain); 3 no table at
+// all (leaf order = rank order: timing only, wrong bits for Swing; no faster).
 // Issue order per wave: L0 L1 | L2 | L3 S0 | L4 S1 | ..., so after tile j's
 // loads come tile j+1's loads and the stores of tiles j-2 and j-3.
 // ---------------------------------------------------------------------------
-template <int P, int TV, bool SWBAR>
+template <int P, int TV, int VAR>
 __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ order, uint64_t block_vec,
                                                          uint64_t ntiles) {
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
     };
     uint32_t bar = 0;
     auto barrier = [&]() {
-        if (SWBAR) {
+        if (VAR == 1) {
             bar += 4;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) __hip_atomic_fetch_add(&bar_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -448,12 +452,19 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
-        reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
+    if (VAR == 2) {
+        if (mine > 0) issue(tile_of(0), 0);
+        if (mine > 1) issue(tile_of(1), 1);
+    }
+    if (VAR != 3)
+        for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
+            reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
     if (threadIdx.x == 0) bar_ctr = 0;
     __syncthreads();
-    if (mine > 0) issue(tile_of(0), 0);
-    if (mine > 1) issue(tile_of(1), 1);
+    if (VAR != 2) {
+        if (mine > 0) issue(tile_of(0), 0);
+        if (mine > 1) issue(tile_of(1), 1);
+    }
     uint4 prev = make_uint4(0, 0, 0, 0);
     for (int j = 0; j < mine; ++j) {
         wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
@@ -463,7 +474,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
         const uint8_t* ord = ord_lds + (block_vec ? v0 / block_vec : 0) * ALLRED_MAX_NODES + RPW * w + LPL * q;
         uint4 x[LPL];
 #pragma unroll
-        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(VAR == 3 ? RPW * w + LPL * q + i : (int)ord[i]) * TV + c];
 #pragma unroll
         for (int s = 1; s < LPL; s *= 2)
 #pragma unroll
@@ -2102,7 +2113,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
         } else if (pipe_lag() && total == 64 && !host_memory) {
             // stores one iteration late, behind the next tile's loads (config 2:
             // 14.44 vs 15.30 us for k_tree_lds_pipe, tools/ubench/fused_ab.hip)
-            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, false>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order,
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 2>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order,
                                bv, tiles);
         } else if (rel && total == 64 && !host_memory) {
             // REL: NB = rel buffers; NB >= 3 needs one workgroup per CU (grid <= 256)

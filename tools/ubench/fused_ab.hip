@@ -1,8 +1,7 @@
 // fused_ab.hip — A/B of the fused BO pass forms at config 2 (64 ranks x
 // 327,680 bf16, stride n + 64) in ONE process, interleaved rounds, 32 rotating
 // bucket sets: k_tree_lds_pipe<64,1,32,true,true> (the round-1 product),
-// k_tree_lds_lag<64,32,false> (s_barrier), k_tree_lds_lag<64,32,true> (LDS
-// counter barrier).  First checks that all forms give identical bits on random
+// and the k_tree_lds_lag<64,32,VAR> arms (kernels.hip).  First checks that all forms give identical bits on random
 // bf16 with a random per-block tree order table.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I../../include \
 //         -I../../tenstorrentallreduce_amd/csrc fused_ab.hip -o fused_ab
@@ -48,25 +47,29 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(order, ord.data(), ord.size(), hipMemcpyHostToDevice));
     hipStream_t st;
     CK(hipStreamCreate(&st));
+    constexpr int NF = 5;
     auto run = [&](int form, uint16_t* r) {
         if (form == 0)
             hipLaunchKernelGGL((k_tree_lds_pipe<64, 1, 32, true, true>), dim3(grid), dim3(kBlock), 0, st, r, stride,
                                order, bv, tiles, nullptr);
         else if (form == 1)
-            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, false>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv,
-                               tiles);
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 0>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
+        else if (form == 2)
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 1>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
+        else if (form == 3)
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 2>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
         else
-            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, true>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv,
-                               tiles);
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 3>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
     };
-    const char* names[3] = {"k_tree_lds_pipe<64,1,32,true,true>", "k_tree_lds_lag<64,32,s_barrier>",
-                            "k_tree_lds_lag<64,32,lds_counter>"};
+    const char* names[NF] = {"k_tree_lds_pipe<64,1,32,true,true>", "k_tree_lds_lag<64,32,0> table first",
+                             "k_tree_lds_lag<64,32,1> lds-counter barrier", "k_tree_lds_lag<64,32,2> loads before table (product)",
+                             "k_tree_lds_lag<64,32,3> no table (timing only)"};
     // bits: every form on a copy of set 0
     const size_t bytes = (size_t)P * stride * 2;
     std::vector<uint16_t> ref(P * stride), got(P * stride);
     uint16_t* tmp;
     CK(hipMalloc(&tmp, bytes));
-    for (int form = 0; form < 3; ++form) {
+    for (int form = 0; form < NF; ++form) {
         CK(hipMemcpy(tmp, sets[0], bytes, hipMemcpyDeviceToDevice));
         run(form, tmp);
         CK(hipStreamSynchronize(st));
@@ -82,7 +85,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int round = 0; round < 3; ++round) {
-        for (int form = 0; form < 3; ++form) {
+        for (int form = 0; form < NF; ++form) {
             for (int i = 0; i < 20; ++i) run(form, sets[i % SETS]);
             CK(hipEventRecord(e0, st));
             for (int i = 0; i < REPS; ++i) run(form, sets[i % SETS]);
