@@ -369,6 +369,11 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
         if peer is not None:
             ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
             out["peer_" + name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+            if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
+                peer.set_lo_ll_max(0)
+                ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+                peer.set_lo_ll_max(256 << 10)
+                out["peer_sched_" + name] = {**arm_stats(ms, nbytes, world, True), "channels": chans}
         del b2, w2
     return out
 

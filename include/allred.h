@@ -298,6 +298,13 @@ int allred_peer_set_hier_ll(allred_peer* peer, int enable);
  * processes share one GPU (rehearsals) the sum of their grids must fit at once:
  * groups <= 512 / processes.  Same result bits at any cap. */
 int allred_peer_set_max_groups(allred_peer* peer, uint32_t groups);
+/* allred_peer_dist_allreduce runs one-channel LO buckets of at most `bytes`
+ * (default 256 KiB; 0 = never) with LL hand-offs (k_peer_lo_ll: each step
+ * pushes data+epoch words into the partner's memory and polls its own — one
+ * one-way xGMI trip per step instead of a flag and a remote read).  Same
+ * result bits.  Every rank must use the same setting.  Replaces the semaphore
+ * handshake + NoC write of allred_LOO_2D/kernels/dataflow_kernel.cpp:127-175. */
+int allred_peer_set_lo_ll_max(allred_peer* peer, uint64_t bytes);
 /* The allred_dist_allreduce program (same desc, same result bits: Swing /
  * RecDub BO or LO, link-spreading channels, hierarchical local ranks) with
  * RCCL replaced by direct reads of the partners' IPC-mapped windows: one

@@ -1475,6 +1475,33 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
 }
 
 // ---------------------------------------------------------------------------
+// k_peer_lo_ll: the LO program of allred_peer_dist_allreduce (one channel)
+// for small buckets with LL hand-offs: step k, every lane pushes its 16 bytes
+// as four self-validating 8-byte words (4 data bytes + the call's epoch) into
+// partner p_k's step-k slot, then polls its OWN step-k slot until the four
+// words of p_k carry the epoch, and adds (one bf16 rounding, the same add as
+// every LO form).  Per step one one-way xGMI trip instead of k_peer_sched's
+// progress flag + remote read round trip; no window, no flag area.  Slots
+// [step][vector][4 words] in the LL area of the call's parity; call k+2 may
+// reuse a parity because finishing call k+1 needs every rank to have started
+// it (the partners of all steps reach every rank of the schedule).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
+                                                       uint64_t nv, uint32_t epoch, uint32_t* status) {
+    const uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (v >= nv) return;
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint4 cur = ld_nt(bk + v);
+    const uint64_t* mine = lp.ll[me];
+    for (int k = 0; k < pr.S; ++k) {
+        const int p = pr.peer[0][k];
+        ll_put(lp.ll[p] + ((uint64_t)k * nv + v) * 4, cur, epoch);
+        cur = add8(cur, ll_get(mine + ((uint64_t)k * nv + v) * 4, epoch, status));
+    }
+    st_nt(bk + v, cur);
+}
+
+// ---------------------------------------------------------------------------
 // k_hier_ws: the k_hier_ll step (same bits) with the local pass and the
 // cross-GPU hand-offs pipelined per tile on specialised waves.  k_hier_ll
 // runs its phases one after the other (all reads, then all writes), so HBM
@@ -1959,6 +1986,19 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
     if (gc < 1) gc = 1;
     hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
                        bucket, half_vec, base_epoch, status);
+    return last_error();
+}
+
+int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, const PeerProg& prog, size_t n,
+                      uint64_t area_words, uint32_t epoch, uint32_t* status, void* stream) {
+    const uint64_t nv = n / 8;
+    if (n % 8 || !aligned16(bucket) || nranks > kLLMaxGpus || !prog.lo || prog.C != 1 ||
+        nv * 4 * (uint64_t)prog.S > area_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    hipLaunchKernelGGL(k_peer_lo_ll, dim3((unsigned)((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, lp, prog, me, bucket, nv, epoch, status);
     return last_error();
 }
 

@@ -57,6 +57,7 @@ struct allred_peer {
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
     int hier_ll = 0;                // 0 off, 1 k_hier_ll (phased), 2 k_hier_ws (pipelined)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
+    uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
 };
 
 extern "C" {
@@ -255,7 +256,17 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
         st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
-    if (prog.S > 0) {
+    const uint64_t ll_area = 2 * p->ll_box_words;   // LL words of one parity
+    if (prog.S > 0 && prog.lo && prog.C == 1 && p->lo_ll_max && n * 2 <= p->lo_ll_max && p->nranks <= 8 &&
+        p->flags_uncached && (n / 8) * 4 * (uint64_t)prog.S <= ll_area) {
+        // small LO buckets: LL pushes, one one-way trip per step (k_peer_lo_ll); same bits
+        uint64_t* ll[ALLRED_MAX_NODES];
+        for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * ll_area;
+        st = launch_peer_lo_ll(ll, p->nranks, p->rank, bucket, prog, n, ll_area, p->calls + 1u, p->status, stream);
+        if (st != ALLRED_OK) return st;
+        ++p->calls;
+        p->last_all_peer = false;   // no window was touched; every rank finished the call before
+    } else if (prog.S > 0) {
         uint16_t* wins[ALLRED_MAX_NODES];
         parity_windows(p, wins);
         if (p->last_all_peer) {
@@ -285,6 +296,12 @@ int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
     if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
+    return ALLRED_OK;
+}
+
+int allred_peer_set_lo_ll_max(allred_peer* p, uint64_t bytes) {
+    if (!p) return ALLRED_ERR_ARG;
+    p->lo_ll_max = bytes;
     return ALLRED_OK;
 }
 

@@ -182,7 +182,11 @@ def dist_worker(rank, world, port, q):
         dist.all_gather_object(handles, peer.handle())
         peer.connect(handles)
         fails = []
-        for ci, (variant, algo, local, chans) in enumerate(tdh.cases(world)):
+        # LO buckets this small take the LL-push program by default (k_peer_lo_ll);
+        # the second pass forces the scheduled form (k_peer_sched) for every case
+        for ci, (variant, algo, local, chans, ll_max) in enumerate(
+                [c + (256 << 10,) for c in tdh.cases(world)] + [c + (0,) for c in tdh.cases(world)]):
+            peer.set_lo_ll_max(ll_max)
             desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
                                local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
             ws = torch.empty(max(t.dist_workspace_bytes(desc), 16), dtype=torch.uint8, device="cuda:0")
@@ -197,7 +201,7 @@ def dist_worker(rank, world, port, q):
                 want = np.concatenate(tdh.expected(variant, algo, world, local, data, chans)[rank])
                 got = buf.cpu().numpy().view(np.uint16)
                 if not np.array_equal(got, want):
-                    fails.append((variant, algo, local, chans, rep, int((got != want).sum())))
+                    fails.append((variant, algo, local, chans, ll_max, rep, int((got != want).sum())))
             # a mem_2D call (reads every window) between scheduled calls
             m = torch.zeros(n, dtype=torch.int16, device="cuda:0")
             peer.allreduce(m.data_ptr(), n, torch.cuda.current_stream())
