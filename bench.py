@@ -374,6 +374,11 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
                 ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
                 peer.set_lo_ll_max(256 << 10)
                 out["peer_sched_" + name] = {**arm_stats(ms, nbytes, world, True), "channels": chans}
+            if variant == t.MEM and nbytes <= (256 << 10):   # mem_2D without LL hand-offs (k_peer_oneshot)
+                peer.set_mem_ll_max(0)
+                ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+                peer.set_mem_ll_max(256 << 10)
+                out["peer_oneshot_" + name] = {**arm_stats(ms, nbytes, world, False), "channels": chans}
         del b2, w2
     return out
 

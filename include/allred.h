@@ -305,6 +305,12 @@ int allred_peer_set_max_groups(allred_peer* peer, uint32_t groups);
  * result bits.  Every rank must use the same setting.  Replaces the semaphore
  * handshake + NoC write of allred_LOO_2D/kernels/dataflow_kernel.cpp:127-175. */
 int allred_peer_set_lo_ll_max(allred_peer* peer, uint64_t bytes);
+/* allred_peer_allreduce (mem_2D) runs buckets of at most `bytes` (default
+ * 256 KiB; 0 = never) with LL hand-offs (k_peer_mem_ll: block copies pushed to
+ * their owners, owners push the sums; two one-way xGMI trips, no flags, no
+ * remote reads), larger ones as before.  Same result bits.  Every rank must
+ * use the same setting. */
+int allred_peer_set_mem_ll_max(allred_peer* peer, uint64_t bytes);
 /* The allred_dist_allreduce program (same desc, same result bits: Swing /
  * RecDub BO or LO, link-spreading channels, hierarchical local ranks) with
  * RCCL replaced by direct reads of the partners' IPC-mapped windows: one

@@ -319,6 +319,10 @@ class Peer:
         """One-channel LO buckets up to nbytes take the LL-push program (same bits; 0 = never)."""
         check(lib.allred_peer_set_lo_ll_max(self._h, nbytes), "peer_set_lo_ll_max")
 
+    def set_mem_ll_max(self, nbytes: int) -> None:
+        """mem_2D buckets up to nbytes take the LL-push form (same bits; 0 = never)."""
+        check(lib.allred_peer_set_mem_ll_max(self._h, nbytes), "peer_set_mem_ll_max")
+
     def set_max_groups(self, groups: int) -> None:
         """Grid cap of the hierarchical one-kernel forms (0 = one full grid per GPU);
         processes sharing a GPU need groups <= 512 / processes."""

@@ -147,6 +147,7 @@ SIGNATURES = [
     ("allred_peer_set_hier_ll", C.c_int, [_P, C.c_int]),
     ("allred_peer_set_max_groups", C.c_int, [_P, C.c_uint32]),
     ("allred_peer_set_lo_ll_max", C.c_int, [_P, C.c_uint64]),
+    ("allred_peer_set_mem_ll_max", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("allred_peer_destroy", C.c_int, [_P]),

@@ -107,6 +107,9 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
 int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream);
+// allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * n / 8
+int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
+                       uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream);
 // the one-channel LO program with LL pushes (k_peer_lo_ll): ll[q] = GPU q's LL area of this
 // parity (area_words 8-byte words >= steps * n / 2)
 int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, const PeerProg& prog, size_t n,

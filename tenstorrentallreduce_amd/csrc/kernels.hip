@@ -1475,6 +1475,81 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
 }
 
 // ---------------------------------------------------------------------------
+// k_peer_mem_ll: allred_mem_2D across GPUs for small buckets with LL hand-offs
+// (the flat counterpart of k_hier_ll).  A: every vector is pushed as four
+// data+epoch words to its block owner's inbox; R: the owner polls the W
+// copies of each of its vectors (all loads in flight at once), sums them in
+// fp32 owner first then ascending, one rounding (allred_mem_2D semantics, the
+// bits of k_peer_oneshot), and pushes the result into every GPU's box; B:
+// every GPU polls its box and writes its bucket.  Two one-way trips, no flag,
+// no remote read.  A never waits and the grid is resident (<= 128 groups), so
+// every wait of R and B is reached.  LL layout of the call's parity:
+// [inbox: owned vectors][W][4 words], then [box: vectors][4 words].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me, uint16_t* __restrict__ bucket,
+                                                        uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status) {
+    const uint64_t gt = gtid(), GT = gthreads();
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint64_t* const my_ll = lp.ll[me];
+    const uint64_t box = nv * 4;
+    for (uint64_t v = gt; v < nv; v += GT) {   // A
+        const int o = (int)(v / bv);
+        // the owner's area by an unrolled select over the (scalar) kernarg pointers: a
+        // per-lane index into lp.ll would be a vector load waiting behind every store
+        uint64_t* dst = lp.ll[0];
+#pragma unroll
+        for (int q = 1; q < kLLMaxGpus; ++q)
+            if (o == q) dst = lp.ll[q];
+        ll_put(dst + ((v - (uint64_t)o * bv) * W + me) * 4, ld_nt(bk + v), epoch);
+    }
+    for (uint64_t u = gt; u < bv; u += GT) {   // R: my block
+        const uint64_t* slots = my_ll + u * W * 4;
+        uint4 y[kLLMaxGpus];
+        for (uint64_t spin = 0;; ++spin) {
+            uint64_t wv[kLLMaxGpus][4];
+#pragma unroll
+            for (int q = 0; q < kLLMaxGpus; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    wv[q][e] = q < W ? __hip_atomic_load(slots + q * 4 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                     : (uint64_t)epoch << 32;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int q = 0; q < kLLMaxGpus; ++q) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bad |= (uint32_t)(wv[q][e] >> 32) ^ epoch;
+                y[q] = make_uint4((uint32_t)wv[q][0], (uint32_t)wv[q][1], (uint32_t)wv[q][2], (uint32_t)wv[q][3]);
+            }
+            if (bad == 0) break;
+            if (spin > kPeerSpinLimit) {
+                atomicOr(status, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        float a[8];
+#pragma unroll
+        for (int q = 0; q < kLLMaxGpus; ++q) {
+            if (q != me) continue;
+            a[0] = lo_f(y[q].x); a[1] = hi_f(y[q].x); a[2] = lo_f(y[q].y); a[3] = hi_f(y[q].y);
+            a[4] = lo_f(y[q].z); a[5] = hi_f(y[q].z); a[6] = lo_f(y[q].w); a[7] = hi_f(y[q].w);
+        }
+#pragma unroll
+        for (int q = 0; q < kLLMaxGpus; ++q) {
+            if (q >= W || q == me) continue;
+            a[0] += lo_f(y[q].x); a[1] += hi_f(y[q].x);
+            a[2] += lo_f(y[q].y); a[3] += hi_f(y[q].y);
+            a[4] += lo_f(y[q].z); a[5] += hi_f(y[q].z);
+            a[6] += lo_f(y[q].w); a[7] += hi_f(y[q].w);
+        }
+        const uint4 r = make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
+        const uint64_t v = (uint64_t)me * bv + u;
+        for (int q = 0; q < W; ++q) ll_put(lp.ll[q] + box + v * 4, r, epoch);
+    }
+    for (uint64_t v = gt; v < nv; v += GT) st_nt(bk + v, ll_get(my_ll + box + v * 4, epoch, status));   // B
+}
+
+// ---------------------------------------------------------------------------
 // k_peer_lo_ll: the LO program of allred_peer_dist_allreduce (one channel)
 // for small buckets with LL hand-offs: step k, every lane pushes its 16 bytes
 // as four self-validating 8-byte words (4 data bytes + the call's epoch) into
@@ -1986,6 +2061,21 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
     if (gc < 1) gc = 1;
     hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
                        bucket, half_vec, base_epoch, status);
+    return last_error();
+}
+
+int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
+                       uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream) {
+    const uint64_t nv = n / 8;
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > kLLMaxGpus || 8 * nv > area_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    uint64_t groups = (nv + kBlock - 1) / kBlock;
+    const uint64_t cap = max_groups && max_groups < kPeerFusedMaxGroups ? max_groups : kPeerFusedMaxGroups;
+    if (groups > cap) groups = cap;   // resident: every wait is reached
+    hipLaunchKernelGGL(k_peer_mem_ll, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, lp, nranks, me,
+                       bucket, nv, nv / nranks, epoch, status);
     return last_error();
 }
 

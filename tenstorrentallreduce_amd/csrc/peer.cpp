@@ -58,6 +58,7 @@ struct allred_peer {
     int hier_ll = 0;                // 0 off, 1 k_hier_ll (phased), 2 k_hier_ws (pipelined)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
+    uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
 };
 
 extern "C" {
@@ -222,6 +223,19 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         st = allred_tree_reduce(buf, n, n, local_algo, local_side, local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
+    const uint64_t ll_area = 2 * p->ll_box_words;   // LL words of one parity
+    if (p->mem_ll_max && n * 2 <= p->mem_ll_max && p->nranks <= 8 && p->flags_uncached && (n / 8) * 8 <= ll_area) {
+        // small buckets: LL pushes, two one-way trips (k_peer_mem_ll); same bits
+        uint64_t* ll[ALLRED_MAX_NODES];
+        for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * ll_area;
+        st = launch_peer_mem_ll(ll, p->nranks, p->rank, bucket, n, ll_area, p->calls + 1u, p->status, p->max_groups,
+                                stream);
+        if (st != ALLRED_OK) return st;
+        ++p->calls;
+        p->last_all_peer = false;   // no window was read; every rank finished the call before
+        if (local_ranks > 1) st = allred_broadcast(buf, n, n, local_ranks, bucket, stream);
+        return st;
+    }
     uint16_t* wins[ALLRED_MAX_NODES];
     parity_windows(p, wins);
     if (one_kernel)
@@ -302,6 +316,12 @@ int allred_peer_set_hier_ll(allred_peer* p, int enable) {
 int allred_peer_set_lo_ll_max(allred_peer* p, uint64_t bytes) {
     if (!p) return ALLRED_ERR_ARG;
     p->lo_ll_max = bytes;
+    return ALLRED_OK;
+}
+
+int allred_peer_set_mem_ll_max(allred_peer* p, uint64_t bytes) {
+    if (!p) return ALLRED_ERR_ARG;
+    p->mem_ll_max = bytes;
     return ALLRED_OK;
 }
 

@@ -42,8 +42,10 @@ def worker(rank, world, port, q):
         peer.connect(handles)
         fails = []
         call = 0
-        for mode, limit in (("oneshot", 1 << 40), ("steps", 0), ("auto", 1 << 20)):
+        for mode, limit, ll_max in (("oneshot", 1 << 40, 0), ("steps", 0, 0), ("auto", 1 << 20, 256 << 10),
+                                    ("ll", 0, 1 << 40)):
             peer.set_oneshot_max(limit)
+            peer.set_mem_ll_max(ll_max)   # k_peer_mem_ll where the LL area holds the bucket
             for m in sizes:
                 rng = [np.random.default_rng(1000 * call + r) for r in range(world)]
                 data = [g.integers(0x3F80, 0x42C8, m).astype(np.uint16) for g in rng]
@@ -64,8 +66,9 @@ def worker(rank, world, port, q):
             bufs.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
         torch.cuda.synchronize()
         dist.barrier()
-        for k, b in enumerate(bufs):
+        for k, b in enumerate(bufs):   # launches / one kernel / LL pushes, interleaved
             peer.set_oneshot_max(1 << 40 if k % 2 else 0)
+            peer.set_mem_ll_max(1 << 40 if k % 3 == 2 else 0)
             peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream())
         torch.cuda.synchronize()
         for k, b in enumerate(bufs):
@@ -75,6 +78,7 @@ def worker(rank, world, port, q):
             if not np.array_equal(b.cpu().numpy().view(np.uint16), want[rank]):
                 fails.append(("pipelined", k))
         dist.barrier()
+        peer.set_mem_ll_max(0)   # the forms below as before (LL mem_2D is covered above)
         # hierarchical: 8 virtual ranks per process (4x2 Swing local grid)
         local = 8
         data = [np.random.default_rng(77 + r).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
