@@ -81,6 +81,9 @@ def cpu_baseline() -> dict:
     from profile_analyzer import analyze  # profiler_results_analyzer.py statistics over the 64 ranks
     per_rank = analyze(log)
     bytes_all = RANKS * ELEMS * 2
+    # BASELINE config 1 on the CPU: the reference's own CPU-runnable case
+    # (allred_BO_2D 0 1 2 -1 1 32 0 0: 2x2 RecDub LO, 1 tile, all ones), 4 rank processes
+    c1 = oracle.loopback("bo", [0, 1, 2, -1, 1, 32, 0, 0], reps=200, timeout=120)
     return {
         "value": round(bytes_all / out["median_s"] / 1e9, 4),
         "unit": "GB/s",
@@ -91,6 +94,8 @@ def cpu_baseline() -> dict:
                    f"(min {out['min_s'] * 1e3:.3f}, max {out['max_s'] * 1e3:.3f}); mismatches {out['mismatches']}"),
         "online_cpus": os.sysconf("SC_NPROCESSORS_ONLN"),
         "per_rank_last_rep_ns": per_rank,
+        "config1": {"us_per_allreduce_median": round(c1["median_s"] * 1e6, 3), "cores": min(4, cpu_cores()),
+                    "sample": f"oracle loopback, 4 rank processes, 200 reps; mismatches {c1['mismatches']}"},
     }
 
 
@@ -208,6 +213,28 @@ def bench_single(args) -> dict:
         finally:
             del os.environ["ALLRED_E2E"]
 
+    # BASELINE config 1: 2x2 RecDub LO, 1 tile (2 kB per rank), seed -1 (all ones) —
+    # latency-bound (no roofline): the fused one-launch plan, us per allreduce
+    c1 = torch.full((4, 1024), 0x3F80, dtype=torch.int16, device=dev)   # bf16 1.0
+    c1_plan = t.Plan(t.RECDUB, t.LO, 2, 1024, 4, t.EXEC_FUSED)
+    with torch.cuda.stream(stream):
+        for _ in range(20):
+            c1.fill_(0x3F80)
+            c1_plan.execute(c1.data_ptr(), 1024, None, stream)
+    torch.cuda.synchronize()
+    c1_ok = bool((c1 == 0x4080).all())   # every element = 4.0 (the known answer)
+    with torch.cuda.stream(stream):
+        e0.record(stream)
+        for _ in range(args.steps):
+            c1_plan.execute(c1.data_ptr(), 1024, None, stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    c1_us = e0.elapsed_time(e1) / args.steps * 1e3
+    c1_plan.close()
+    config1 = {"workload": "2x2 RecDub LO, 1 tile (4 ranks x 2,048 B), seed -1; fused one-launch plan",
+               "us_per_allreduce": round(c1_us, 3), "known_answer_ok": c1_ok,
+               "note": "back-to-back launches on one stream: launch-bound, no roofline"}
+
     alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
     out = {
@@ -235,6 +262,7 @@ def bench_single(args) -> dict:
                               "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
         "host_staged": e2e,
+        "config1": config1,
         "host_wall_s": round(wall, 6),
     }
     plan.close()

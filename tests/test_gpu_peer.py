@@ -40,6 +40,9 @@ def worker(rank, world, port, q):
         handles = [None] * world
         dist.all_gather_object(handles, peer.handle())
         peer.connect(handles)
+        # the one-kernel forms wait across processes: every process's grid must be
+        # resident at once on the shared GPU (one GPU per process needs no cap)
+        peer.set_max_groups(256 // world)
         fails = []
         call = 0
         for mode, limit, ll_max in (("oneshot", 1 << 40, 0), ("steps", 0, 0), ("auto", 1 << 20, 256 << 10),
@@ -56,7 +59,7 @@ def worker(rank, world, port, q):
                 oracle.allreduce("mem", 0, 1, want, world)
                 got = buf.cpu().numpy().view(np.uint16)
                 if not np.array_equal(got, want[rank]):
-                    fails.append((mode, m, call, int((got != want[rank]).sum())))
+                    fails.append((mode, m, call, int((got != want[rank]).sum()), peer.status()))
                 call += 1
                 dist.barrier()
         # back-to-back calls with no host sync in between (window parities, epochs)
