@@ -223,17 +223,35 @@ def bench_single(args) -> dict:
             c1_plan.execute(c1.data_ptr(), 1024, None, stream)
     torch.cuda.synchronize()
     c1_ok = bool((c1 == 0x4080).all())   # every element = 4.0 (the known answer)
-    with torch.cuda.stream(stream):
-        e0.record(stream)
-        for _ in range(args.steps):
-            c1_plan.execute(c1.data_ptr(), 1024, None, stream)
-        e1.record(stream)
-    torch.cuda.synchronize()
-    c1_us = e0.elapsed_time(e1) / args.steps * 1e3
+    c1_graph = None
+    if graph is not None:   # the same launches replayed from a HIP graph, as the main workload
+        try:
+            c1_graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(c1_graph, stream=stream):
+                for _ in range(args.steps):
+                    c1_plan.execute(c1.data_ptr(), 1024, None, stream)
+            torch.cuda.synchronize()
+        except Exception as e:
+            print(f"[bench] config-1 graph capture failed ({e}); eager", file=sys.stderr)
+            c1_graph = None
+    c1_us = {}
+    for mode in ("eager", "graph"):
+        if mode == "graph" and c1_graph is None:
+            continue
+        with torch.cuda.stream(stream):
+            e0.record(stream)
+            if mode == "graph":
+                c1_graph.replay()
+            else:
+                for _ in range(args.steps):
+                    c1_plan.execute(c1.data_ptr(), 1024, None, stream)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        c1_us[mode] = round(e0.elapsed_time(e1) / args.steps * 1e3, 3)
     c1_plan.close()
     config1 = {"workload": "2x2 RecDub LO, 1 tile (4 ranks x 2,048 B), seed -1; fused one-launch plan",
-               "us_per_allreduce": round(c1_us, 3), "known_answer_ok": c1_ok,
-               "note": "back-to-back launches on one stream: launch-bound, no roofline"}
+               "us_per_allreduce": c1_us.get("graph", c1_us["eager"]), "us_eager_launches": c1_us["eager"],
+               "known_answer_ok": c1_ok, "note": "back-to-back allreduces on one stream: launch-bound, no roofline"}
 
     alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
