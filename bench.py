@@ -526,7 +526,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     for kind in candidates:
         note(rank, f"quick timing: {kind}")
         it = iter(range(1 << 30))
-        quick[kind] = round(timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), 20, stream), 4)
+        quick[kind] = round(timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), 50, stream), 4)
     transport = min(candidates, key=lambda k: quick[k])
 
     def step(i):
