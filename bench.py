@@ -472,7 +472,9 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     # timed briefly and the fastest is the headline transport.
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
-    def run(kind, b, one_kernel=True, fresh=False):
+    mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
+
+    def run(kind, b, fresh=False):
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
         if kind == "rccl":
@@ -480,12 +482,11 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         elif kind == "peer_swing":
             peer.dist_allreduce(desc, b.data_ptr(), ws.data_ptr(), stream)
         else:
-            one_kernel = one_kernel and kind != "peer_launches"
-            peer.set_oneshot_max((4 << 20) if one_kernel else 0)
-            peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_ws": 2}.get(kind, 0))
+            if mode[0] != kind:
+                peer.set_oneshot_max(0 if kind == "peer_launches" else (4 << 20))
+                peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_ws": 2}.get(kind, 0))
+                mode[0] = kind
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
-            peer.set_hier_ll(0)
-            peer.set_oneshot_max(4 << 20)
 
     # the reference transport: RCCL, or (--share-gpu) the peer launch form
     base = "rccl" if comm is not None else "peer_launches"
@@ -551,6 +552,10 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
     ms_per_step = ms.item() / args.steps
+    if peer is not None:   # defaults again for the extras below
+        peer.set_oneshot_max(4 << 20)
+        peer.set_hier_ll(0)
+        mode[0] = None
 
     # local phases alone (tree reduce of 64 ranks + broadcast): the HBM kernels
     torch.cuda.synchronize()
