@@ -38,6 +38,7 @@ import torch.distributed as dist  # noqa: E402
 import tenstorrentallreduce_amd as t  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0        # MI355X_MICROARCH.md chip table (spec)
+METRIC = "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak"   # BASELINE.json
 XGMI_LINK_DIR_GBPS = 76.8     # 153.6 GB/s per link quoted bidirectional -> per direction
 SIDE, RANKS, TILES = 8, 64, 5
 ELEMS = t.normalize_tiles(TILES, RANKS, True) * 1024   # 327,680 bf16 = 655,360 B per rank
@@ -256,7 +257,7 @@ def bench_single(args) -> dict:
     alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
     out = {
-        "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
+        "metric": METRIC,
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
         "unit": "GB/s",
         "n_gpus": 1,
@@ -612,7 +613,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
            "peer_hier_ws": "ONE kernel, pipelined per tile: on-GPU tree reduce overlapped with the rank-row "
                            "stores, mem_2D one-shot across GPUs by one LL-push wave per workgroup"}[transport]
     return {
-        "metric": "allreduce GB/s (device-resident bf16 buckets) at 1/2/4/8 MI355X; % xGMI peak",
+        "metric": METRIC,
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
         "unit": "GB/s",
         "n_gpus": world,
