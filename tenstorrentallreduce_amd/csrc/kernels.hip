@@ -1689,6 +1689,9 @@ __global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ran
     auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
     if (w < 4) {
         // ---------------- data waves
+#ifdef ALLRED_WS_PRIO
+        __builtin_amdgcn_s_setprio(ALLRED_WS_PRIO);   // A/B: issue priority over the helper waves
+#endif
         const uint32_t wbase = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
         auto issue = [&](uint64_t t, int b) {
@@ -1764,7 +1767,7 @@ __global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ran
         }
         if (MODE == 0 && mine > 0) store_result(mine - 1);
         if (MODE >= 2 && mine > 0) store_rows(mine - 1, res_prev);
-        if (MODE >= 3) lds_signal_add(&ctr[kPushDone], lane);
+        if (MODE >= 3) lds_signal_add(&ctr[kPushDone], lane);   // (5: nobody waits for it)
         if (MODE == 4) asm volatile("s_wakeup" ::: "memory");
         if (w == 0) {
             WS_MARK(7);
@@ -1774,6 +1777,21 @@ __global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ran
     }
     if (MODE == 3) {   // the two extra waves only spin on LDS until the data waves are done
         lds_wait_ge(&ctr[kPushDone], 4u, true, status);
+        return;
+    }
+    if (MODE == 6) {   // the helpers sleep without touching LDS, then leave
+#ifndef ALLRED_WS_SLEEPS
+#define ALLRED_WS_SLEEPS 110
+#endif
+#ifdef ALLRED_WS_NOPS
+        for (int i = 0; i < ALLRED_WS_NOPS; ++i) asm volatile("s_nop 7");   // busy, not asleep
+#else
+        for (int i = 0; i < ALLRED_WS_SLEEPS; ++i) __builtin_amdgcn_s_sleep(1);
+#endif
+        return;
+    }
+    if (MODE == 5) {   // 3, but the helpers leave once tile 0's partial is published (alive ~1/3 of the kernel)
+        lds_wait_ge(&ctr[kPartReady], 4u, true, status);
         return;
     }
     if (MODE == 4) {   // the same, sleeping 127 x 64 clocks per check, woken by the data waves' s_wakeup

@@ -56,6 +56,12 @@ int main(int argc, char** argv) {
             if (form == 3)
                 hipLaunchKernelGGL(k_hier_ws<1>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
                                    0, ntiles, ntiles, box_words, epoch, status);
+            else if (form == 7)
+                hipLaunchKernelGGL(k_hier_ws<6>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
+                                   0, ntiles, ntiles, box_words, epoch, status);
+            else if (form == 8)
+                hipLaunchKernelGGL(k_hier_ws<5>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
+                                   0, ntiles, ntiles, box_words, epoch, status);
             else if (form == 6)
                 hipLaunchKernelGGL(k_hier_ws<4>, dim3(grid), dim3(kWsBlock), 0, st, sets[i % SETS], stride, order, lp, 1,
                                    0, ntiles, ntiles, box_words, epoch, status);
@@ -68,13 +74,14 @@ int main(int argc, char** argv) {
         }
         if (rc) { std::printf("launch rc %d\n", rc); std::exit(1); }
     };
-    const char* names_f[7] = {"", "k_hier_ll", "k_hier_ws", "ws<1> data only", "ws<2> data only lag 1",
-                              "ws<3> lag 1 + 2 spinning waves", "ws<4> lag 1 + 2 sleeping waves, s_wakeup"};
+    const char* names_f[9] = {"", "k_hier_ll", "k_hier_ws", "ws<1> data only", "ws<2> data only lag 1",
+                              "ws<3> lag 1 + 2 spinning waves", "ws<4> lag 1 + 2 sleeping waves, s_wakeup", "ws<6> helpers sleep 3 us, no LDS",
+                              "ws<5> helpers leave after tile 0"};
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     for (int round = 0; round < 3; ++round) {
-        for (int form : {4, 5, 6}) {
+        for (int form : {4, 7}) {
             for (int i = 0; i < 20; ++i) run(form, i);
             CK(hipEventRecord(e0, st));
             for (int i = 0; i < REPS; ++i) run(form, i);
