@@ -407,14 +407,15 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 // Issue order per wave: L0 L1 | L2 | L3 S0 | L4 S1 | ..., so after tile j's
 // loads come tile j+1's loads and the stores of tiles j-2 and j-3.
 // ---------------------------------------------------------------------------
-template <int P, int TV, int VAR>
-__global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
+template <int P, int TV, int VAR, int NW = 4>   // NW waves per workgroup (A/B: 2)
+__global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ order, uint64_t block_vec,
                                                          uint64_t ntiles) {
-    constexpr int RPI = 64 / TV, RPW = P / 4, OPS = RPW / RPI, LPL = OPS;
+    constexpr int RPI = 64 / TV, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    static_assert(NW == 2 || NW == 4 || NW == 8, "2, 4 or 8 waves");
     static_assert(OPS >= 1 && 3 * OPS <= 63, "vmcnt is 6 bits");
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[2][4 * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[P * ALLRED_MAX_NODES];
     __shared__ uint32_t bar_ctr;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -439,7 +440,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
     uint32_t bar = 0;
     auto barrier = [&]() {
         if (VAR == 1) {
-            bar += 4;
+            bar += NW;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             if (lane == 0) __hip_atomic_fetch_add(&bar_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             while (__hip_atomic_load(&bar_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < bar) {
@@ -457,7 +458,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
         if (mine > 1) issue(tile_of(1), 1);
     }
     if (VAR != 3)
-        for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += kBlock)
+        for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += 64 * NW)
             reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
     if (threadIdx.x == 0) bar_ctr = 0;
     __syncthreads();
@@ -486,7 +487,15 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
         barrier();   // every wave has read tile j out of buf[j & 1]; the partials are in
         if (j + 2 < mine) issue(tile_of(j + 2), j & 1);
         const uint4* pp = part[j & 1];
-        const uint4 res = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+        uint4 res;
+        if (NW == 2) {
+            res = add8(pp[0 * TV + c], pp[1 * TV + c]);
+        } else if (NW == 4) {
+            res = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+        } else {
+            res = add8(add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c])),
+                       add8(add8(pp[4 * TV + c], pp[5 * TV + c]), add8(pp[6 * TV + c], pp[7 * TV + c])));
+        }
         if (j >= 1) store(tile_of(j - 1), prev);
         prev = res;
     }
