@@ -136,6 +136,7 @@ def bench_single(args) -> dict:
         p.execute(sets[i % nsets].data_ptr(), stride, None, stream)
 
     with torch.cuda.stream(stream):
+        prewarm_s = prewarm(step, args.prewarm_ms)
         for i in range(args.warmup):
             step(i)
     torch.cuda.synchronize()
@@ -154,9 +155,17 @@ def bench_single(args) -> dict:
 
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    if graph is not None:   # the first replay uploads the graph: untimed
+        with torch.cuda.stream(stream):
+            graph.replay()
     torch.cuda.synchronize()
-    e0.record(stream)
     t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        # a ~0.1 ms spin kernel ahead of e0 keeps the GPU busy while the host
+        # submits the K steps, so e0 -> e1 times the K steps themselves, not the
+        # host's launch latency (host_wall_s below includes everything)
+        torch.cuda._sleep(200000)
+    e0.record(stream)
     with torch.cuda.stream(stream):  # the graph launches on the current stream
         if graph is not None:
             graph.replay()
@@ -282,6 +291,7 @@ def bench_single(args) -> dict:
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
         "host_staged": e2e,
         "config1": config1,
+        "prewarm_ms": round(prewarm_s * 1e3, 1),
         "host_wall_s": round(wall, 6),
     }
     plan.close()
@@ -305,6 +315,22 @@ def timed_max(fn, reps, stream) -> float:
     m = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64)
     dist.all_reduce(m, op=dist.ReduceOp.MAX)
     return m.item()
+
+
+def prewarm(step, ms: float) -> float:
+    """Untimed: run the workload for >= ms of wall time before the W warmup steps.
+    A cold MI355X needs a few ms of sustained load to reach its steady clocks
+    (config 2 measured 14.80-14.86 us per step after 20 warmup steps, 14.49-14.53
+    after 1000); this makes the timed K steps measure the steady state whatever
+    W the caller passes.  No timed step is skipped or shortened."""
+    t0 = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t0 < ms * 1e-3:
+        for _ in range(50):
+            step(i)
+            i += 1
+        torch.cuda.synchronize()
+    return time.perf_counter() - t0
 
 
 def note(rank, msg):
@@ -535,6 +561,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         run(transport, bufs[i % len(bufs)])
 
     note(rank, f"timed: {transport}")
+    prewarm(step, args.prewarm_ms)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -543,6 +570,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(200000)   # GPU busy while the host submits the steps (as at N = 1)
     e0.record(stream)
     for i in range(args.steps):
         step(i)
@@ -646,6 +675,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--prewarm-ms", type=float, default=50.0,
+                    help="untimed sustained load before the warmup steps (steady clocks); 0 = none")
     ap.add_argument("--sets", type=int, default=32, help="rotating bucket sets (1.3 GB per GPU: far past the 256 MiB MALL)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
