@@ -561,7 +561,12 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         run(transport, bufs[i % len(bufs)])
 
     note(rank, f"timed: {transport}")
-    prewarm(step, args.prewarm_ms)
+    # untimed prewarm (steady clocks): the SAME number of steps on every rank — the
+    # ranks' calls must pair up (RCCL collectives, peer epochs) — derived from the
+    # max-over-ranks quick timing, identical everywhere
+    pre_steps = int(min(20000, args.prewarm_ms / max(quick[transport], 1e-3)))
+    for i in range(pre_steps):
+        step(i)
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
