@@ -51,11 +51,15 @@ def main():
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     rows = []
     for run in range(args.runs):
+        print(f"[timing_taker] run {run + 1}/{args.runs}", file=sys.stderr, flush=True)   # progress (long sweeps)
         for mode, binary, algos, sizes, bo in plan():
             for swing in algos:
                 for size in sizes:
                     argv = [str(swing), "1", "8", "13", str(size), "32"] + (["0", bo] if bo is not None else [])
-                    p = t.run_cli(binary, argv, env={"ALLRED_REPORT": "1", "ALLRED_EXEC": args.exec})
+                    # device_ns = the allreduce on device-resident buckets (the reference's
+                    # ALL_RED_LOOP zone), so the host buckets move by DMA before and after it
+                    p = t.run_cli(binary, argv, env={"ALLRED_REPORT": "1", "ALLRED_EXEC": args.exec,
+                                                     "ALLRED_E2E": "dma"})
                     rep = json.loads(p.stderr.strip().splitlines()[-1])
                     rows.append([mode, swing, size, run, round(rep["device_s"] * 1e9), round(rep["e2e_s"] * 1e9),
                                  rep["mismatches"]])
