@@ -348,3 +348,28 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
     finally:
         peer.set_hier_ll(0)
         peer.close()
+
+
+def test_peer_knob_argument_errors():
+    """The peer knobs reject what they cannot honour (ALLRED_ERR_ARG), like the
+    rest of the C-ABI; a one-rank peer set needs no second process."""
+    sys.path.insert(0, ROOT)
+    import tenstorrentallreduce_amd as t
+    from tenstorrentallreduce_amd import _lib
+    peer = t.Peer(1, 0, 0, 1 << 16)
+    peer.connect([peer.handle()])
+    try:
+        with pytest.raises(_lib.AllredError):
+            peer.set_hier_ll(3)            # 0, 1 or 2 only
+        with pytest.raises(_lib.AllredError):
+            peer.set_hier_ll(-1)
+        peer.set_lo_ll_max(0)
+        peer.set_mem_ll_max(0)
+        peer.set_max_groups(0)
+        buf = torch.zeros(1 << 17, dtype=torch.int16, device="cuda:0")
+        with pytest.raises(_lib.AllredError):   # larger than the windows
+            peer.allreduce(buf.data_ptr(), 1 << 17, torch.cuda.current_stream())
+        with pytest.raises(_lib.AllredError):   # not a multiple of 8 elements per rank
+            peer.allreduce(buf.data_ptr(), 12, torch.cuda.current_stream())
+    finally:
+        peer.close()
