@@ -103,7 +103,7 @@ def cpu_baseline() -> dict:
 # the fused BO kernel the engine launches at config 2 (kernels.hip launch_tree_fused;
 # ALLRED_PIPE_LAG=0 / ALLRED_PIPE_REL=0 select the earlier forms for A/B)
 if os.environ.get("ALLRED_PIPE_LAG", "1") != "0":
-    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_lag<64, 32, 2, 4>", "k_tree_lds_lag64"
+    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_lag<64, 32, 7, 4>", "k_tree_lds_lag64"
 elif os.environ.get("ALLRED_PIPE_REL", "1") == "1":
     FUSED_KERNEL, FUSED_KEY = "k_tree_lds_pipe<64, 1, 32, true, true>", "k_tree_lds_pipe64"
 else:

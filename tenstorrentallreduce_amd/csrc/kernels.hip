@@ -280,6 +280,77 @@ __device__ __forceinline__ void wait_units(int k) {
     }
 }
 
+// vmcnt(n) for a run-time n in 0..63 (larger n waits for 63: conservative)
+__device__ __forceinline__ void wait_any(int n) {
+    switch (n) {
+        case 0: wait_vm<0>(); break;
+        case 1: wait_vm<1>(); break;
+        case 2: wait_vm<2>(); break;
+        case 3: wait_vm<3>(); break;
+        case 4: wait_vm<4>(); break;
+        case 5: wait_vm<5>(); break;
+        case 6: wait_vm<6>(); break;
+        case 7: wait_vm<7>(); break;
+        case 8: wait_vm<8>(); break;
+        case 9: wait_vm<9>(); break;
+        case 10: wait_vm<10>(); break;
+        case 11: wait_vm<11>(); break;
+        case 12: wait_vm<12>(); break;
+        case 13: wait_vm<13>(); break;
+        case 14: wait_vm<14>(); break;
+        case 15: wait_vm<15>(); break;
+        case 16: wait_vm<16>(); break;
+        case 17: wait_vm<17>(); break;
+        case 18: wait_vm<18>(); break;
+        case 19: wait_vm<19>(); break;
+        case 20: wait_vm<20>(); break;
+        case 21: wait_vm<21>(); break;
+        case 22: wait_vm<22>(); break;
+        case 23: wait_vm<23>(); break;
+        case 24: wait_vm<24>(); break;
+        case 25: wait_vm<25>(); break;
+        case 26: wait_vm<26>(); break;
+        case 27: wait_vm<27>(); break;
+        case 28: wait_vm<28>(); break;
+        case 29: wait_vm<29>(); break;
+        case 30: wait_vm<30>(); break;
+        case 31: wait_vm<31>(); break;
+        case 32: wait_vm<32>(); break;
+        case 33: wait_vm<33>(); break;
+        case 34: wait_vm<34>(); break;
+        case 35: wait_vm<35>(); break;
+        case 36: wait_vm<36>(); break;
+        case 37: wait_vm<37>(); break;
+        case 38: wait_vm<38>(); break;
+        case 39: wait_vm<39>(); break;
+        case 40: wait_vm<40>(); break;
+        case 41: wait_vm<41>(); break;
+        case 42: wait_vm<42>(); break;
+        case 43: wait_vm<43>(); break;
+        case 44: wait_vm<44>(); break;
+        case 45: wait_vm<45>(); break;
+        case 46: wait_vm<46>(); break;
+        case 47: wait_vm<47>(); break;
+        case 48: wait_vm<48>(); break;
+        case 49: wait_vm<49>(); break;
+        case 50: wait_vm<50>(); break;
+        case 51: wait_vm<51>(); break;
+        case 52: wait_vm<52>(); break;
+        case 53: wait_vm<53>(); break;
+        case 54: wait_vm<54>(); break;
+        case 55: wait_vm<55>(); break;
+        case 56: wait_vm<56>(); break;
+        case 57: wait_vm<57>(); break;
+        case 58: wait_vm<58>(); break;
+        case 59: wait_vm<59>(); break;
+        case 60: wait_vm<60>(); break;
+        case 61: wait_vm<61>(); break;
+        case 62: wait_vm<62>(); break;
+        case 63: wait_vm<63>(); break;
+        default: wait_vm<63>(); break;
+    }
+}
+
 // LDS-DMA load issued as inline asm: the compiler's waitcnt pass then does
 // not see an LDS write in flight and does not put vmcnt(0) in front of every
 // LDS read (which would serialise the pipeline); wait_tile() is the only wait.
@@ -400,10 +471,13 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 // for a store before a load.  Measured on the hierarchical step's data path
 // (tools/ubench/ws_trace.hip): 14.6 us vs 15.4 us with stores in iteration j.
 // VAR (A/B arms, tools/ubench/fused_ab.hip, profiles/r01_fused_ab_arms.txt):
-// 2 the product: the first two tiles' loads issued before the 4 KiB tree-order
+// 7 the product = 2 with tile j+2's loads and tile j-1's stores interleaved op
+// by op (14.22-14.26 vs 14.32-14.36 us, profiles/r01_fused_ab_interleave.txt);
+// 2: the first two tiles' loads issued before the 4 KiB tree-order
 // table is staged (14.23-14.29 vs 14.39-14.40 us); 0 the table first; 1 = 0
 // with an LDS-counter barrier instead of s_barrier (no gain); 3 no table at
-// all (leaf order = rank order: timing only, wrong bits for Swing; no faster).
+// all (leaf order = rank order: timing only, wrong bits for Swing; no faster);
+// 7 = 2 with tile j+2's loads and tile j-1's stores interleaved op by op.
 // Issue order per wave: L0 L1 | L2 | L3 S0 | L4 S1 | ..., so after tile j's
 // loads come tile j+1's loads and the stores of tiles j-2 and j-3.
 // ---------------------------------------------------------------------------
@@ -453,7 +527,7 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    if (VAR == 2) {
+    if (VAR == 2 || VAR == 7) {
         if (mine > 0) issue(tile_of(0), 0);
         if (mine > 1) issue(tile_of(1), 1);
     }
@@ -462,13 +536,16 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
             reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
     if (threadIdx.x == 0) bar_ctr = 0;
     __syncthreads();
-    if (VAR != 2) {
+    if (VAR != 2 && VAR != 7) {
         if (mine > 0) issue(tile_of(0), 0);
         if (mine > 1) issue(tile_of(1), 1);
     }
     uint4 prev = make_uint4(0, 0, 0, 0);
     for (int j = 0; j < mine; ++j) {
-        wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
+        if (VAR == 7)   // after L(j): the last op of S(j-3) (interleaved with L(j)), L(j+1), S(j-2)
+            wait_any((j >= 3 ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 2 ? OPS : 0));
+        else
+            wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
         barrier();   // every wave's rows of tile j are in LDS
         const uint4* tile = buf[j & 1];
         const uint64_t t = tile_of(j), v0 = t * TV;
@@ -485,7 +562,20 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
         for (int s = TV; s < 64; s *= 2) pw = add8(pw, shfl_xor4(pw, s));   // tree levels across lane groups
         if (q == 0) part[j & 1][w * TV + c] = pw;
         barrier();   // every wave has read tile j out of buf[j & 1]; the partials are in
-        if (j + 2 < mine) issue(tile_of(j + 2), j & 1);
+        if (VAR == 7) {   // tile j+2's loads and tile j-1's stores interleaved op by op
+            const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 1);
+            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + RPI * k + q;
+                if (j + 2 < mine)
+                    lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + tl * TV + c,
+                              bl + (uint32_t)(RPI * k * TV * 16));
+                if (j >= 1) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + ts * TV + c, prev);
+            }
+        } else if (j + 2 < mine) {
+            issue(tile_of(j + 2), j & 1);
+        }
         const uint4* pp = part[j & 1];
         uint4 res;
         if (NW == 2) {
@@ -496,7 +586,7 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
             res = add8(add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c])),
                        add8(add8(pp[4 * TV + c], pp[5 * TV + c]), add8(pp[6 * TV + c], pp[7 * TV + c])));
         }
-        if (j >= 1) store(tile_of(j - 1), prev);
+        if (VAR != 7 && j >= 1) store(tile_of(j - 1), prev);
         prev = res;
     }
     if (mine > 0) store(tile_of(mine - 1), prev);
@@ -2270,7 +2360,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
         } else if (pipe_lag() && total == 64 && !host_memory) {
             // stores one iteration late, behind the next tile's loads (config 2:
             // 14.44 vs 15.30 us for k_tree_lds_pipe, tools/ubench/fused_ab.hip)
-            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 2>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order,
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 7>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order,
                                bv, tiles);
         } else if (rel && total == 64 && !host_memory) {
             // REL: NB = rel buffers; NB >= 3 needs one workgroup per CU (grid <= 256)
