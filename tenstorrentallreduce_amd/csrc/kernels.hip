@@ -848,7 +848,8 @@ __global__ __launch_bounds__(kBlock) void k_mem_lds_lag(uint16_t* __restrict__ r
     uint4 prev = make_uint4(0, 0, 0, 0);
     const int e = threadIdx.x;   // element of the tile (0..255)
     for (int j = 0; j < mine; ++j) {
-        wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
+        // after L(j): the last op of S(j-3) (interleaved with L(j)), L(j+1), S(j-2)
+        wait_any((j >= 3 ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 2 ? OPS : 0));
         lds_barrier();
         const uint64_t t = tile_of(j);
         const int own = (int)(t * TV / block_vec);
@@ -863,8 +864,18 @@ __global__ __launch_bounds__(kBlock) void k_mem_lds_lag(uint16_t* __restrict__ r
         if ((e & 1) == 0) reinterpret_cast<uint32_t*>(resb[j & 1])[e >> 1] = pack_rne(a, b);
         lds_barrier();   // the tile is read out of buf[j & 1]; resb[j & 1] is complete
         const uint4 res = resb[j & 1][c];
-        if (j + 2 < mine) issue(tile_of(j + 2), j & 1);
-        if (j >= 1) store(tile_of(j - 1), prev);
+        {   // tile j+2's loads and tile j-1's stores interleaved op by op (k_tree_lds_lag VAR 7)
+            const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 1);
+            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                if (j + 2 < mine)
+                    lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + tl * TV + c,
+                              bl + (uint32_t)(2 * k * TV * 16));
+                if (j >= 1) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + ts * TV + c, prev);
+            }
+        }
         prev = res;
     }
     if (mine > 0) store(tile_of(mine - 1), prev);
