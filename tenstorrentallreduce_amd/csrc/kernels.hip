@@ -527,7 +527,7 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    if (VAR == 2 || VAR == 7) {
+    if (VAR == 2 || VAR >= 7) {
         if (mine > 0) issue(tile_of(0), 0);
         if (mine > 1) issue(tile_of(1), 1);
     }
@@ -536,7 +536,7 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
             reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
     if (threadIdx.x == 0) bar_ctr = 0;
     __syncthreads();
-    if (VAR != 2 && VAR != 7) {
+    if (VAR != 2 && VAR < 7) {
         if (mine > 0) issue(tile_of(0), 0);
         if (mine > 1) issue(tile_of(1), 1);
     }
@@ -544,6 +544,10 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
     for (int j = 0; j < mine; ++j) {
         if (VAR == 7)   // after L(j): the last op of S(j-3) (interleaved with L(j)), L(j+1), S(j-2)
             wait_any((j >= 3 ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 2 ? OPS : 0));
+        else if (VAR == 8)   // S(k) before L(k): nothing of S(j-3) after L(j)'s last op
+            wait_any((j + 1 < mine ? OPS : 0) + (j >= 2 ? OPS : 0));
+        else if (VAR == 9)   // pairs L L S S: S(j-3)'s last two ops after L(j)'s last op
+            wait_any((j >= 3 ? 2 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 2 ? OPS : 0));
         else
             wait_units<OPS>((j + 1 < mine ? 1 : 0) + (j >= 2 ? 1 : 0) + (j >= 3 ? 1 : 0));
         barrier();   // every wave's rows of tile j are in LDS
@@ -562,16 +566,34 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
         for (int s = TV; s < 64; s *= 2) pw = add8(pw, shfl_xor4(pw, s));   // tree levels across lane groups
         if (q == 0) part[j & 1][w * TV + c] = pw;
         barrier();   // every wave has read tile j out of buf[j & 1]; the partials are in
-        if (VAR == 7) {   // tile j+2's loads and tile j-1's stores interleaved op by op
+        if (VAR >= 7) {   // tile j+2's loads and tile j-1's stores interleaved (7: L S, 8: S L, 9: L L S S)
             const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 1);
             const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                const int r = RPW * w + RPI * k + q;
+            auto ld = [&](int k) {
                 if (j + 2 < mine)
-                    lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + tl * TV + c,
+                    lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)(RPW * w + RPI * k + q) * stride) +
+                                  tl * TV + c,
                               bl + (uint32_t)(RPI * k * TV * 16));
-                if (j >= 1) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + ts * TV + c, prev);
+            };
+            auto sv = [&](int k) {
+                if (j >= 1) st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPW * w + RPI * k + q) * stride) +
+                                      ts * TV + c, prev);
+            };
+            if (VAR == 9) {
+#pragma unroll
+                for (int k = 0; k < OPS; k += 2) {
+                    ld(k);
+                    ld(k + 1);
+                    sv(k);
+                    sv(k + 1);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < OPS; ++k) {
+                    if (VAR == 8) sv(k);
+                    ld(k);
+                    if (VAR == 7) sv(k);
+                }
             }
         } else if (j + 2 < mine) {
             issue(tile_of(j + 2), j & 1);
@@ -586,7 +608,7 @@ __global__ __launch_bounds__(64 * NW) void k_tree_lds_lag(uint16_t* __restrict__
             res = add8(add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c])),
                        add8(add8(pp[4 * TV + c], pp[5 * TV + c]), add8(pp[6 * TV + c], pp[7 * TV + c])));
         }
-        if (VAR != 7 && j >= 1) store(tile_of(j - 1), prev);
+        if (VAR < 7 && j >= 1) store(tile_of(j - 1), prev);
         prev = res;
     }
     if (mine > 0) store(tile_of(mine - 1), prev);

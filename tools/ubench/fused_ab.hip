@@ -47,7 +47,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(order, ord.data(), ord.size(), hipMemcpyHostToDevice));
     hipStream_t st;
     CK(hipStreamCreate(&st));
-    constexpr int NF = 9;
+    constexpr int NF = 11;
     auto run = [&](int form, uint16_t* r) {
         if (form == 0)
             hipLaunchKernelGGL((k_tree_lds_pipe<64, 1, 32, true, true>), dim3(grid), dim3(kBlock), 0, st, r, stride,
@@ -67,14 +67,19 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 2, 2>), dim3(grid), dim3(128), 0, st, r, stride, order, bv, tiles);
         else if (form == 7)   // eight waves per workgroup (8 rank rows each)
             hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 2, 8>), dim3(grid), dim3(512), 0, st, r, stride, order, bv, tiles);
-        else   // loads and stores interleaved
+        else if (form == 8)   // loads and stores interleaved
             hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 7>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
+        else if (form == 9)
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 8>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
+        else
+            hipLaunchKernelGGL((k_tree_lds_lag<64, 32, 9>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
     };
     const char* names[NF] = {"k_tree_lds_pipe<64,1,32,true,true>", "k_tree_lds_lag<64,32,0> table first",
                              "k_tree_lds_lag<64,32,1> lds-counter barrier", "k_tree_lds_lag<64,32,2> loads before table",
                              "k_tree_lds_lag<64,32,3> no table (timing only)",
                              "k_tree_lds_lag<64,64,2> 1 KiB rows, grid 256", "k_tree_lds_lag<64,32,2,2> two waves",
-                             "k_tree_lds_lag<64,32,2,8> eight waves", "k_tree_lds_lag<64,32,7> interleaved (product)"};
+                             "k_tree_lds_lag<64,32,2,8> eight waves", "k_tree_lds_lag<64,32,7> interleaved (product)",
+                             "k_tree_lds_lag<64,32,8> interleaved S L", "k_tree_lds_lag<64,32,9> interleaved L L S S"};
     // bits: every form on a copy of set 0
     const size_t bytes = (size_t)P * stride * 2;
     std::vector<uint16_t> ref(P * stride), got(P * stride);
