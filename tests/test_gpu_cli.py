@@ -80,3 +80,13 @@ def test_mismatch_report_when_kernel_not_run():
 def test_bad_argument_fails_like_stoi():
     p = t.run_cli("allred_BO_2D", ["x"])
     assert p.returncode != 0 and "stoi" in p.stderr
+
+
+@pytest.mark.parametrize("e2e", ["zerocopy", "dma"])
+def test_config2_fused_both_end_to_end_modes(e2e):
+    """BASELINE config 2 through the reference CLI with the fused pass, the buckets
+    starting and ending in pinned host memory: read in place over PCIe
+    (zero-copy, the default) and staged by one DMA each way."""
+    out, rep = run("allred_BO_2D", ["1", "1", "8", "13", "5", "32", "0", "1"], ALLRED_EXEC="fused", ALLRED_E2E=e2e)
+    assert "All values match!" in out
+    assert rep["mismatches"] == 0
