@@ -10,14 +10,18 @@
 //         (allred_mem_2D/kernels/*)
 // ALLRED_EXEC_STEPS keeps the reference's step structure (one launch per
 // schedule step, all ranks at once); ALLRED_EXEC_FUSED does the identical
-// arithmetic in one HBM pass (BO/LO: k_tree, MEM: k_mem<true>).
+// arithmetic in one HBM pass (BO: k_tree*, LO: the butterfly k_butterfly*, or
+// the BO tree pass when every rank's tree is the same (lo_rank_uniform),
+// MEM: k_mem*).
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "internal.hpp"
@@ -42,6 +46,7 @@ struct allred_plan {
     int launches = 0;
     const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
     bool last_host = false;
+    bool lo_tree = false;  // fused LO runs as the BO tree pass (lo_rank_uniform)
 };
 
 namespace {
@@ -64,6 +69,32 @@ int upload(T** dst, const std::vector<T>& host) {
     if (hipMemcpy(*dst, host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
         return ALLRED_ERR_HIP;
     return ALLRED_OK;
+}
+
+// True when every rank's LO tree is the same tree up to swapping children:
+// then the butterfly leaves the same bits on every rank (the fp32 add of two
+// bf16 is commutative), and rank r's LO result — its own tree T(r), leaves
+// tree_order[r] — is BO block r's result, which is T(r) too (the BO partial of
+// block r at step k is exactly the LO value of its holder).  So the fused LO
+// is the fused BO pass, one tree per column instead of one per rank: every
+// RecDub schedule, Swing up to 16 ranks (tests/test_gpu_parity.py holds both
+// against the oracle's butterfly).
+bool lo_rank_uniform(const allred_schedule& s, int total) {
+    std::map<std::pair<int, int>, int> ids;  // interned unordered pairs of subtrees
+    std::vector<int> cur(total), nxt(total);
+    for (int r = 0; r < total; ++r) cur[r] = r;
+    for (int k = 0; k < s.steps; ++k) {
+        for (int r = 0; r < total; ++r) {
+            const int a = cur[r], b = cur[s.partner[r][k]];
+            const auto key = a < b ? std::make_pair(a, b) : std::make_pair(b, a);
+            const auto it = ids.emplace(key, total + (int)ids.size()).first;
+            nxt[r] = it->second;
+        }
+        cur.swap(nxt);
+    }
+    for (int r = 1; r < total; ++r)
+        if (cur[r] != cur[0]) return false;
+    return true;
 }
 
 bool env_is(const char* name, const char* value) {
@@ -113,6 +144,8 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
             }
         }
     }
+    p->lo_tree = desc->variant == ALLRED_LO && n % (8 * (size_t)total) == 0 && !env_is("ALLRED_LO_TREE", "0") &&
+                 lo_rank_uniform(p->sched, total);
     std::vector<uint8_t> order(&p->sched.tree_order[0][0],
                                &p->sched.tree_order[0][0] + ALLRED_MAX_NODES * ALLRED_MAX_NODES);
     if ((st = upload(&p->d_partner, partner)) || (st = upload(&p->d_rs_blocks, rs)) ||
@@ -154,7 +187,8 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
     int st = ALLRED_OK;
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
-        if (p->desc.variant == ALLRED_LO) return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, stream);
+        if (p->desc.variant == ALLRED_LO && !p->lo_tree)
+            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, stream);
         if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
             hipPointerAttribute_t at{};
             p->last_host = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;

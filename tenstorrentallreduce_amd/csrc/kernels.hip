@@ -723,6 +723,49 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64(uint16_t* __restrict
 // the only vmcnt wait lets tile j-1's stores stay outstanding (see
 // k_tree_lds_pipe).
 // ---------------------------------------------------------------------------
+// Cross-lane exchanges of the XOR steps without the LDS pipe (EX = 2 below):
+// DPP moves for lane ^ 1, 2, 4, 8 (xor 4 = row_half_mirror then quad xor 3),
+// and v_permlane16/32_swap for lane ^ 16, 32 — a swap of a register with a copy
+// of itself leaves {own, partner} in the pair in some order, and the bf16 add
+// (fp32 sum, one rounding) is commutative, so their sum is own + partner.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
+}
+template <int MASK>
+__device__ __forceinline__ uint32_t xor_add2(uint32_t v) {
+    if constexpr (MASK == 1) return add2(v, dpp_mov<0xB1>(v));        // quad_perm [1,0,3,2]
+    else if constexpr (MASK == 2) return add2(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
+    else if constexpr (MASK == 4) return add2(v, dpp_mov<0x1B>(dpp_mov<0x141>(v)));  // half_mirror, [3,2,1,0]
+    else if constexpr (MASK == 8) return add2(v, dpp_mov<0x128>(v));  // row_ror:8
+    else if constexpr (MASK == 16) {
+        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return add2(r[0], r[1]);
+    } else {
+        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return add2(r[0], r[1]);
+    }
+}
+template <int MASK>
+__device__ __forceinline__ void xor_step8(uint4 (&val)[8]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        val[i].x = xor_add2<MASK>(val[i].x);
+        val[i].y = xor_add2<MASK>(val[i].y);
+        val[i].z = xor_add2<MASK>(val[i].z);
+        val[i].w = xor_add2<MASK>(val[i].w);
+    }
+}
+
+// EX = 0: the butterfly in registers (ds_bpermute, 4 per 16-byte vector per
+// step); EX = 1: through the LDS tile itself — each step a lane reads its
+// partner's 16-byte vector of the same column (one ds_read_b128) and writes
+// its sum back (one ds_write_b128).  A wave owns its 8 columns of all 64 rows,
+// so no other wave touches them, and a wave's LDS ops execute in order, so the
+// step-k reads see the step-(k-1) writes and precede the step-k writes;
+// EX = 2: steps whose partner is lane ^ m for one m (every RecDub step, Swing's
+// first two) by DPP / permlane swaps (xor_step8), the others by ds_bpermute.
+template <int EX>
 __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                                  const int16_t* __restrict__ partner, int steps,
                                                                  uint64_t ntiles) {
@@ -748,6 +791,13 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
     int src_lane[ALLRED_MAX_STEPS];
 #pragma unroll
     for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
+    int xmask[ALLRED_MAX_STEPS];  // m when step k's partner is lane ^ m on every lane, else 0
+#pragma unroll
+    for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+        const int m = (src_lane[k] >> 2) ^ x;
+        const int m0 = __builtin_amdgcn_readfirstlane(m);
+        xmask[k] = (k < steps && __all(m == m0)) ? m0 : 0;
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (mine > 0) issue(blockIdx.x, 0);
     for (int j = 0; j < mine; ++j) {
@@ -759,22 +809,48 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
         uint4 val[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) val[i] = tile[x * TV + ((8 * w + i) ^ (x & 31))];
+        if constexpr (EX == 0 || EX == 2) {
 #pragma unroll
-        for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-            if (k >= steps) break;
-            const int sl = src_lane[k];
+            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+                if (k >= steps) break;
+                if constexpr (EX == 2) {
+                    const int m = xmask[k];
+                    if (m == 1) { xor_step8<1>(val); continue; }
+                    if (m == 2) { xor_step8<2>(val); continue; }
+                    if (m == 4) { xor_step8<4>(val); continue; }
+                    if (m == 8) { xor_step8<8>(val); continue; }
+                    if (m == 16) { xor_step8<16>(val); continue; }
+                    if (m == 32) { xor_step8<32>(val); continue; }
+                }
+                const int sl = src_lane[k];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                uint4 o;
-                o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].x);
-                o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].y);
-                o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].z);
-                o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].w);
-                val[i] = add8(val[i], o);
+                for (int i = 0; i < 8; ++i) {
+                    uint4 o;
+                    o.x = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].x);
+                    o.y = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].y);
+                    o.z = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].z);
+                    o.w = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)val[i].w);
+                    val[i] = add8(val[i], o);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];  // own columns only
+        } else {
+#pragma unroll
+            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+                if (k >= steps) break;
+                const int p = src_lane[k] >> 2;
+                uint4 o[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) o[i] = tile[p * TV + ((8 * w + i) ^ (p & 31))];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    val[i] = add8(val[i], o[i]);
+                    tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];
+                }
+                __builtin_amdgcn_wave_barrier();
             }
         }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];  // own columns only
         lds_barrier();
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
@@ -2433,8 +2509,19 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
         const uint64_t tiles = nv / 32;
         // (the k_tree_lds_lag schedule — stores one iteration late — measured slower
         // here: 26.6 vs 24.1 us at 640 kB; the butterfly is not bound by HBM order)
-        hipLaunchKernelGGL(k_butterfly_lds64_pipe, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0, st,
-                           ranks, stride, d_partner, steps, tiles);
+        static const int ex = [] {
+            const char* e = std::getenv("ALLRED_BFLY_EX");
+            return e ? std::atoi(e) : 0;
+        }();
+        if (ex == 1)
+            hipLaunchKernelGGL(k_butterfly_lds64_pipe<1>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
+                               st, ranks, stride, d_partner, steps, tiles);
+        else if (ex == 2)
+            hipLaunchKernelGGL(k_butterfly_lds64_pipe<2>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
+                               st, ranks, stride, d_partner, steps, tiles);
+        else
+            hipLaunchKernelGGL(k_butterfly_lds64_pipe<0>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
+                               st, ranks, stride, d_partner, steps, tiles);
         return last_error();
     }
     if (total == 64 && nv % 32 == 0 && nv >= 32 * 256) {  // >= 256 tiles: the LDS-staged form pays

@@ -206,6 +206,26 @@ def test_lo_sizes_reference_inputs(tiles, exec_mode):
     assert (got == np.stack(want)).all()
 
 
+@pytest.mark.parametrize("lo_tree", ["1", "0"])
+@pytest.mark.parametrize("algo,grid,n", [
+    (t.RECDUB, (8, 64), 327680), (t.RECDUB, (8, 64), 1024 * 16), (t.RECDUB, (4, 16), 1024 * 64),
+    (t.RECDUB, (2, 4), 1024), (t.SWING, (4, 16), 1024 * 64), (t.SWING, (2, 4), 1024),
+    (t.RECDUB_1D, (8, 64), 1024 * 64), (t.SWING_1D, (2, 4), 1024 * 8)])
+def test_fused_lo_rank_uniform_tree_route(algo, grid, n, lo_tree, monkeypatch):
+    """Schedules whose LO trees are all the same up to child swaps (every RecDub,
+    Swing up to 16 ranks) run the fused LO as the BO tree pass (engine.cpp
+    lo_rank_uniform); ALLRED_LO_TREE=0 keeps the butterfly.  Both against the
+    oracle's butterfly, bit-exact."""
+    monkeypatch.setenv("ALLRED_LO_TREE", lo_tree)
+    side, total = grid
+    ranks = rand_ranks(total, n, seed=29 + total + algo)
+    got = run_plan(algo, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("lo", algo, side, want, total)
+    assert (got == np.stack(want)).all()
+    assert (got == got[0]).all()
+
+
 def test_config1_known_answer():
     s0, s1, ranks = oracle.reference_inputs(2, 4, 1024, -1)
     for exec_mode in (t.EXEC_STEPS, t.EXEC_FUSED):

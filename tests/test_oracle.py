@@ -91,6 +91,8 @@ def test_bo_block_equals_lo_tree_of_owner():
             assert (bo[0][r * blk:(r + 1) * blk] == lo[r][r * blk:(r + 1) * blk]).all()
         same = all((lo[r] == lo[0]).all() for r in range(total))
         assert same == (algo == oracle.RECDUB)
+        if same:  # rank-uniform LO is the BO result (the engine's fused LO route, engine.cpp lo_rank_uniform)
+            assert all((lo[r] == bo[r]).all() for r in range(total))
 
 
 def test_loopback_config1_known_answer():

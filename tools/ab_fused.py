@@ -13,12 +13,14 @@ import tenstorrentallreduce_amd as t  # noqa: E402
 variant = {"bo": t.BO, "lo": t.LO, "mem": t.MEM}[sys.argv[1]]
 tiles = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 200
-P = 64
+P = int(os.environ.get("AB_P", "64"))
+SIDE = int(os.environ.get("AB_SIDE", "8"))
 n = t.normalize_tiles(tiles, P, variant != t.LO) * 1024
 stride = n + int(os.environ["AB_PAD"]) if "AB_PAD" in os.environ else t.preferred_rank_stride(n)
 NS = int(os.environ.get("AB_SETS", "8"))
 sets = [torch.randint(0x3F80, 0x42C8, (P, stride), dtype=torch.int16, device="cuda") for _ in range(NS)]
-plan = t.Plan(t.SWING, variant, 8, n, P, t.EXEC_FUSED)
+algo = {"swing": t.SWING, "recdub": t.RECDUB}[os.environ.get("AB_ALGO", "swing")]
+plan = t.Plan(algo, variant, SIDE, n, P, t.EXEC_FUSED)
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
     for i in range(10):
@@ -37,7 +39,7 @@ e1.record(s)
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / steps * 1e3
 alg = 2 * P * n * 2
-print(json.dumps({"variant": sys.argv[1], "bytes_per_rank": n * 2, "us": round(us, 3),
+print(json.dumps({"variant": sys.argv[1], "algo": os.environ.get("AB_ALGO", "swing"), "bytes_per_rank": n * 2, "us": round(us, 3),
                   "hbm_GBps": round(alg / us / 1e3, 1), "env": {k: v for k, v in os.environ.items()
                                                                if k.startswith(("ALLRED_", "AB_"))}}))
 plan.close()
