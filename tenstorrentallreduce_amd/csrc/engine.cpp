@@ -42,11 +42,13 @@ struct allred_plan {
     std::vector<size_t> blk_off;            // offset of step k in the block tables
     std::vector<int> blk_per_rank;          // m_k
     uint8_t* d_order = nullptr;
+    uint8_t* d_dag = nullptr;               // LO: interned DAG (lo_dag), 64 ranks only
     size_t ws_bytes = 0;
     int launches = 0;
     const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
     bool last_host = false;
     bool lo_tree = false;  // fused LO runs as the BO tree pass (lo_rank_uniform)
+    bool paired = false;   // every step's partners are an involution without fixed points
 };
 
 namespace {
@@ -59,6 +61,7 @@ void free_plan(allred_plan* p) {
     if (p->d_rs_blocks) (void)hipFree(p->d_rs_blocks);
     if (p->d_ag_blocks) (void)hipFree(p->d_ag_blocks);
     if (p->d_order) (void)hipFree(p->d_order);
+    if (p->d_dag) (void)hipFree(p->d_dag);
     delete p;
 }
 
@@ -95,6 +98,40 @@ bool lo_rank_uniform(const allred_schedule& s, int total) {
     for (int r = 1; r < total; ++r)
         if (cur[r] != cur[0]) return false;
     return true;
+}
+
+// The LO butterfly as a DAG of its distinct sums, for the LDS pass of 64 ranks
+// (k_butterfly_lds64_pipe<4>): step k's nodes are the distinct unordered pairs
+// (value of r, value of partner_k(r)) of step-(k-1) values, numbered in order
+// of first appearance; node q is kept in tile row q.  Layout: [k*64 + 2q],
+// [k*64 + 2q + 1] = input rows of node q, [384 + r] = final row of rank r,
+// [448 + k] = d_k.  Empty when a step would have more than 32 nodes (a
+// kernel lane group serves at most 4 x 8).
+std::vector<uint8_t> lo_dag(const allred_schedule& s, int total) {
+    if (total != 64) return {};
+    std::vector<uint8_t> dag(456, 0);
+    std::vector<int> cur(total), nxt(total);
+    for (int r = 0; r < total; ++r) cur[r] = r;  // leaves: tile rows
+    for (int k = 0; k < s.steps; ++k) {
+        std::map<std::pair<int, int>, int> nodes;
+        for (int r = 0; r < total; ++r) {
+            const int a = cur[r], b = cur[s.partner[r][k]];
+            const auto key = a < b ? std::make_pair(a, b) : std::make_pair(b, a);
+            auto it = nodes.find(key);
+            if (it == nodes.end()) {
+                const int q = (int)nodes.size();
+                if (q >= 32) return {};
+                dag[(size_t)k * 64 + 2 * q] = (uint8_t)key.first;
+                dag[(size_t)k * 64 + 2 * q + 1] = (uint8_t)key.second;
+                it = nodes.emplace(key, q).first;
+            }
+            nxt[r] = it->second;
+        }
+        dag[448 + k] = (uint8_t)nodes.size();
+        cur.swap(nxt);
+    }
+    for (int r = 0; r < total; ++r) dag[384 + r] = (uint8_t)cur[r];
+    return dag;
 }
 
 bool env_is(const char* name, const char* value) {
@@ -144,10 +181,20 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
             }
         }
     }
+    p->paired = true;
+    for (int k = 0; k < steps; ++k)
+        for (int r = 0; r < total; ++r) {
+            const int q = p->sched.partner[r][k];
+            if (q == r || q < 0 || q >= total || p->sched.partner[q][k] != r) p->paired = false;
+        }
     p->lo_tree = desc->variant == ALLRED_LO && n % (8 * (size_t)total) == 0 && !env_is("ALLRED_LO_TREE", "0") &&
                  lo_rank_uniform(p->sched, total);
     std::vector<uint8_t> order(&p->sched.tree_order[0][0],
                                &p->sched.tree_order[0][0] + ALLRED_MAX_NODES * ALLRED_MAX_NODES);
+    if (desc->variant == ALLRED_LO && desc->exec == ALLRED_EXEC_FUSED && (st = upload(&p->d_dag, lo_dag(p->sched, total)))) {
+        free_plan(p);
+        return st;
+    }
     if ((st = upload(&p->d_partner, partner)) || (st = upload(&p->d_rs_blocks, rs)) ||
         (st = upload(&p->d_ag_blocks, ag)) || (st = upload(&p->d_order, order))) {
         free_plan(p);
@@ -188,7 +235,7 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
         if (p->desc.variant == ALLRED_LO && !p->lo_tree)
-            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, stream);
+            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->paired, p->d_dag, stream);
         if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
             hipPointerAttribute_t at{};
             p->last_host = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;

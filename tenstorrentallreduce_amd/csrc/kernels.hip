@@ -764,11 +764,30 @@ __device__ __forceinline__ void xor_step8(uint4 (&val)[8]) {
 // so no other wave touches them, and a wave's LDS ops execute in order, so the
 // step-k reads see the step-(k-1) writes and precede the step-k writes;
 // EX = 2: steps whose partner is lane ^ m for one m (every RecDub step, Swing's
-// first two) by DPP / permlane swaps (xor_step8), the others by ds_bpermute.
+// first two) by DPP / permlane swaps (xor_step8), the others by ds_bpermute;
+// EX = 3 (partners an involution, checked by the host): the two ranks of a
+// pair compute the same sum, so each (pair, column) is added once — lane
+// (q, h) of a wave sums pair q's two rows in the wave's column half h and
+// writes the sum to both rows, in the LDS tile.  Per step a lane reads and
+// writes only its own pair's rows in its own columns, so a step has no
+// hazards inside the wave; the next step's reads follow in wave order.  Half
+// the adds of EX = 0..2 (the butterfly there is bound by its adds, not by
+// the exchange: profiles/r01_lo_exchange_arms.txt);
+// EX = 4 (dag != nullptr): each step adds only the DISTINCT sums.  Ranks whose
+// step-k values come from the same pair of step-(k-1) values hold the same
+// bits, so the host interns them (engine.cpp lo_dag): step k has d_k distinct
+// nodes (Swing 8x8: 32, 16, 16, 16, 8, 4 — 92 adds per column instead of the
+// butterfly's 384), node q of step k lives in tile row q, its inputs are rows
+// of step k-1 (the leaves at step 0).  Lane group g = lane >> 3 takes nodes
+// g, g + 8, g + 16, g + 24 in column 8w + (lane & 7); a step issues all its
+// reads before its writes, so overwriting rows of step k-1 is safe in wave
+// order.  Rank r's result is row fin[r], stored to rank r's bucket.
+// dag layout (uint8): [k*64 + 2q] / [+1] = input rows of node q of step k,
+// [384 + r] = final row of rank r, [448 + k] = d_k.
 template <int EX>
 __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                                  const int16_t* __restrict__ partner, int steps,
-                                                                 uint64_t ntiles) {
+                                                                 uint64_t ntiles, const uint8_t* __restrict__ dag) {
     constexpr int TV = 32, OPS = 8;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][64 * TV];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -791,6 +810,46 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
     int src_lane[ALLRED_MAX_STEPS];
 #pragma unroll
     for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
+    // EX = 4: node operands (a | b << 8, or -1) of this lane's items, final rows
+    int nab[ALLRED_MAX_STEPS][4], fin[OPS];
+    if constexpr (EX == 4) {
+#pragma unroll
+        for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+            const int dk = k < steps ? dag[448 + k] : 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int q = 8 * i + (lane >> 3);
+                nab[k][i] = q < dk ? (int)dag[k * 64 + 2 * q] | ((int)dag[k * 64 + 2 * q + 1] << 8) : -1;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) fin[k] = dag[384 + 16 * w + 2 * k + h];
+    }
+    // EX = 3: pair q of step k = the q-th rank y (ascending) with y < partner(y)
+    int pa[ALLRED_MAX_STEPS], pb[ALLRED_MAX_STEPS];
+    if constexpr (EX == 3) {
+        __shared__ uint8_t pairs[ALLRED_MAX_STEPS][2][32];
+        if (w == 0) {
+#pragma unroll
+            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+                if (k >= steps) break;
+                const int p = src_lane[k] >> 2;
+                const bool lead = x < p;
+                const uint64_t m = __ballot(lead);
+                const int q = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (lead && q < 32) {
+                    pairs[k][0][q] = (uint8_t)x;
+                    pairs[k][1][q] = (uint8_t)p;
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+            pa[k] = k < steps ? pairs[k][0][lane & 31] : 0;
+            pb[k] = k < steps ? pairs[k][1][lane & 31] : 0;
+        }
+    }
     int xmask[ALLRED_MAX_STEPS];  // m when step k's partner is lane ^ m on every lane, else 0
 #pragma unroll
     for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
@@ -807,8 +866,10 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
         uint4* tile = buf[j & 1];
         const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
         uint4 val[8];
+        if constexpr (EX != 3) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) val[i] = tile[x * TV + ((8 * w + i) ^ (x & 31))];
+            for (int i = 0; i < 8; ++i) val[i] = tile[x * TV + ((8 * w + i) ^ (x & 31))];
+        }
         if constexpr (EX == 0 || EX == 2) {
 #pragma unroll
             for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
@@ -835,6 +896,49 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];  // own columns only
+        } else if constexpr (EX == 4) {
+            const int c = 8 * w + (lane & 7);
+#pragma unroll
+            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+                if (k >= steps) break;
+                uint4 A[4], B[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (nab[k][i] >= 0) {
+                        const int a = nab[k][i] & 255, b = nab[k][i] >> 8;
+                        A[i] = tile[a * TV + (c ^ (a & 31))];
+                        B[i] = tile[b * TV + (c ^ (b & 31))];
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (nab[k][i] >= 0) {
+                        const int q = 8 * i + (lane >> 3);
+                        tile[q * TV + (c ^ (q & 31))] = add8(A[i], B[i]);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        } else if constexpr (EX == 3) {
+            const int c0 = 8 * w + 4 * (lane >> 5);
+#pragma unroll
+            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
+                if (k >= steps) break;
+                const int a = pa[k], b = pb[k];
+                uint4 A[4], B[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    A[i] = tile[a * TV + ((c0 + i) ^ (a & 31))];
+                    B[i] = tile[b * TV + ((c0 + i) ^ (b & 31))];
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const uint4 sum = add8(A[i], B[i]);
+                    tile[a * TV + ((c0 + i) ^ (a & 31))] = sum;
+                    tile[b * TV + ((c0 + i) ^ (b & 31))] = sum;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
@@ -855,8 +959,8 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             const int r = 16 * w + 2 * k + h;
-            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (r & 31)),
-                  tile[(16 * w + 2 * k + h) * TV + l32]);
+            const int fr = EX == 4 ? fin[k] : r;  // LDS row holding rank r's result
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (fr & 31)), tile[fr * TV + l32]);
         }
     }
 }
@@ -2496,7 +2600,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
 }
 
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
-                     void* stream) {
+                     bool paired, const uint8_t* dag, void* stream) {
     if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
     hipStream_t st = (hipStream_t)stream;
@@ -2510,18 +2614,27 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
         // (the k_tree_lds_lag schedule — stores one iteration late — measured slower
         // here: 26.6 vs 24.1 us at 640 kB; the butterfly is not bound by HBM order)
         static const int ex = [] {
-            const char* e = std::getenv("ALLRED_BFLY_EX");
-            return e ? std::atoi(e) : 0;
+            const char* e = std::getenv("ALLRED_BFLY_EX");  // A/B arms; 4 (default) = the DAG form
+            return e ? std::atoi(e) : 4;
         }();
+        const dim3 grid((unsigned)(tiles < cap ? tiles : cap));
+        if (dag && ex != 0 && ex != 1 && ex != 2 && ex != 3) {
+            hipLaunchKernelGGL(k_butterfly_lds64_pipe<4>, grid, dim3(kBlock), 0, st, ranks, stride, d_partner, steps,
+                               tiles, dag);
+            return last_error();
+        }
         if (ex == 1)
             hipLaunchKernelGGL(k_butterfly_lds64_pipe<1>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles);
+                               st, ranks, stride, d_partner, steps, tiles, nullptr);
         else if (ex == 2)
             hipLaunchKernelGGL(k_butterfly_lds64_pipe<2>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles);
+                               st, ranks, stride, d_partner, steps, tiles, nullptr);
+        else if (ex == 3 && paired)
+            hipLaunchKernelGGL(k_butterfly_lds64_pipe<3>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
+                               st, ranks, stride, d_partner, steps, tiles, nullptr);
         else
             hipLaunchKernelGGL(k_butterfly_lds64_pipe<0>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles);
+                               st, ranks, stride, d_partner, steps, tiles, nullptr);
         return last_error();
     }
     if (total == 64 && nv % 32 == 0 && nv >= 32 * 256) {  // >= 256 tiles: the LDS-staged form pays

@@ -9,7 +9,7 @@ OUT=gpurun_out/${TAG:-abbfly}
 mkdir -p $OUT
 ARMS=${ARMS:-"0 1"}
 for ex in $ARMS; do
-  ALLRED_BFLY_EX=$ex timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "persistent or lo_sizes or lds_forms" -x -q --timeout 100 --timeout-method thread > $OUT/pytest_ex$ex.log 2>&1
+  ALLRED_LO_TREE=0 ALLRED_BFLY_EX=$ex timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "persistent or lo_sizes or lds_forms or rank_uniform" -x -q --timeout 100 --timeout-method thread > $OUT/pytest_ex$ex.log 2>&1
   rc=$?
   echo "PYTEST_EXIT $rc" >> $OUT/pytest_ex$ex.log
   [ $rc -eq 0 ] || exit 1
@@ -17,7 +17,7 @@ done
 for i in 1 2 3; do
   for ex in $ARMS; do
     for algo in swing recdub; do
-      AB_ALGO=$algo ALLRED_BFLY_EX=$ex AB_SETS=32 timeout -k 10 120 python tools/ab_fused.py lo 320 400 >> $OUT/ab.jsonl || exit 1
+      ALLRED_LO_TREE=0 AB_ALGO=$algo ALLRED_BFLY_EX=$ex AB_SETS=32 timeout -k 10 120 python tools/ab_fused.py lo 320 400 >> $OUT/ab.jsonl || exit 1
     done
   done
 done
