@@ -2604,8 +2604,15 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
     if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
     hipStream_t st = (hipStream_t)stream;
-    // persistent pipelined form for >= 1024 tiles (640 kB: 23.9 vs 25.2-26.0 us)
-    if (total == 64 && nv % 32 == 0 && nv >= 32 * 256 && (tree_force_pipe() || (nv >= 32 * 1024 && !tree_force_lds()))) {
+    // persistent pipelined form for >= 1024 tiles (640 kB: 23.9 vs 25.2-26.0 us);
+    // its DAG form (dag != null) from ALLRED_BFLY_DAG_MIN tiles (default 256)
+    static const uint64_t dag_min = [] {
+        const char* e = std::getenv("ALLRED_BFLY_DAG_MIN");
+        return e ? std::strtoull(e, nullptr, 10) : 256ull;
+    }();
+    const bool dag_pipe = dag && !tree_force_lds() && nv / 32 >= dag_min;
+    if (total == 64 && nv % 32 == 0 && nv >= 32 &&
+        (dag_pipe || (nv >= 32 * 256 && (tree_force_pipe() || (nv >= 32 * 1024 && !tree_force_lds()))))) {
         static const uint64_t cap = [] {
             const char* e = std::getenv("ALLRED_PIPE_GRID");
             return e ? std::strtoull(e, nullptr, 10) : 512ull;
