@@ -48,7 +48,6 @@ struct allred_plan {
     const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
     bool last_host = false;
     bool lo_tree = false;  // fused LO runs as the BO tree pass (lo_rank_uniform)
-    bool paired = false;   // every step's partners are an involution without fixed points
 };
 
 namespace {
@@ -181,12 +180,6 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
             }
         }
     }
-    p->paired = true;
-    for (int k = 0; k < steps; ++k)
-        for (int r = 0; r < total; ++r) {
-            const int q = p->sched.partner[r][k];
-            if (q == r || q < 0 || q >= total || p->sched.partner[q][k] != r) p->paired = false;
-        }
     p->lo_tree = desc->variant == ALLRED_LO && n % (8 * (size_t)total) == 0 && !env_is("ALLRED_LO_TREE", "0") &&
                  lo_rank_uniform(p->sched, total);
     std::vector<uint8_t> order(&p->sched.tree_order[0][0],
@@ -235,7 +228,7 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
         if (p->desc.variant == ALLRED_LO && !p->lo_tree)
-            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->paired, p->d_dag, stream);
+            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->d_dag, stream);
         if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
             hipPointerAttribute_t at{};
             p->last_host = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;

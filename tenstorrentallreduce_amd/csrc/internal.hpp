@@ -44,10 +44,9 @@ int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* bl
 // host_memory: the ranks live in pinned host memory (zero-copy) -> pipelined form
 int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
                       bool host_memory = false);
-// paired: every step's partners form an involution without fixed points;
 // dag: the interned LO DAG of a 64-rank schedule (engine.cpp lo_dag), or null
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
-                     bool paired, const uint8_t* dag, void* stream);
+                     const uint8_t* dag, void* stream);
 int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total,
                        const uint8_t* order, uint16_t* out, void* stream);
 int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src,

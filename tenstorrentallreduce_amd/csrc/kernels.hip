@@ -723,57 +723,12 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64(uint16_t* __restrict
 // the only vmcnt wait lets tile j-1's stores stay outstanding (see
 // k_tree_lds_pipe).
 // ---------------------------------------------------------------------------
-// Cross-lane exchanges of the XOR steps without the LDS pipe (EX = 2 below):
-// DPP moves for lane ^ 1, 2, 4, 8 (xor 4 = row_half_mirror then quad xor 3),
-// and v_permlane16/32_swap for lane ^ 16, 32 — a swap of a register with a copy
-// of itself leaves {own, partner} in the pair in some order, and the bf16 add
-// (fp32 sum, one rounding) is commutative, so their sum is own + partner.
-template <int CTRL>
-__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, true);
-}
-template <int MASK>
-__device__ __forceinline__ uint32_t xor_add2(uint32_t v) {
-    if constexpr (MASK == 1) return add2(v, dpp_mov<0xB1>(v));        // quad_perm [1,0,3,2]
-    else if constexpr (MASK == 2) return add2(v, dpp_mov<0x4E>(v));   // quad_perm [2,3,0,1]
-    else if constexpr (MASK == 4) return add2(v, dpp_mov<0x1B>(dpp_mov<0x141>(v)));  // half_mirror, [3,2,1,0]
-    else if constexpr (MASK == 8) return add2(v, dpp_mov<0x128>(v));  // row_ror:8
-    else if constexpr (MASK == 16) {
-        const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-        return add2(r[0], r[1]);
-    } else {
-        const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-        return add2(r[0], r[1]);
-    }
-}
-template <int MASK>
-__device__ __forceinline__ void xor_step8(uint4 (&val)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        val[i].x = xor_add2<MASK>(val[i].x);
-        val[i].y = xor_add2<MASK>(val[i].y);
-        val[i].z = xor_add2<MASK>(val[i].z);
-        val[i].w = xor_add2<MASK>(val[i].w);
-    }
-}
-
 // EX = 0: the butterfly in registers (ds_bpermute, 4 per 16-byte vector per
-// step); EX = 1: through the LDS tile itself — each step a lane reads its
-// partner's 16-byte vector of the same column (one ds_read_b128) and writes
-// its sum back (one ds_write_b128).  A wave owns its 8 columns of all 64 rows,
-// so no other wave touches them, and a wave's LDS ops execute in order, so the
-// step-k reads see the step-(k-1) writes and precede the step-k writes;
-// EX = 2: steps whose partner is lane ^ m for one m (every RecDub step, Swing's
-// first two) by DPP / permlane swaps (xor_step8), the others by ds_bpermute;
-// EX = 3 (partners an involution, checked by the host): the two ranks of a
-// pair compute the same sum, so each (pair, column) is added once — lane
-// (q, h) of a wave sums pair q's two rows in the wave's column half h and
-// writes the sum to both rows, in the LDS tile.  Per step a lane reads and
-// writes only its own pair's rows in its own columns, so a step has no
-// hazards inside the wave; the next step's reads follow in wave order.  Half
-// the adds of EX = 0..2 (the butterfly there is bound by its adds, not by
-// the exchange: profiles/r01_lo_exchange_arms.txt);
-// EX = 4 (dag != nullptr): each step adds only the DISTINCT sums.  Ranks whose
+// step, one add per rank and step).  It is bound by its adds, not by the
+// exchange: exchanging through the LDS tile, or by DPP / v_permlane16/32_swap
+// on the XOR steps, ran as fast or slower; one add per partner pair 19.3 us
+// (profiles/r01_lo_exchange_arms.txt; those arms were removed).
+// EX = 4 (dag != nullptr, the default): each step adds only the DISTINCT sums.  Ranks whose
 // step-k values come from the same pair of step-(k-1) values hold the same
 // bits, so the host interns them (engine.cpp lo_dag): step k has d_k distinct
 // nodes (Swing 8x8: 32, 16, 16, 16, 8, 4 — 92 adds per column instead of the
@@ -784,7 +739,7 @@ __device__ __forceinline__ void xor_step8(uint4 (&val)[8]) {
 // order.  Rank r's result is row fin[r], stored to rank r's bucket.
 // dag layout (uint8): [k*64 + 2q] / [+1] = input rows of node q of step k,
 // [384 + r] = final row of rank r, [448 + k] = d_k.
-template <int EX>
+template <int EX>   // 0 or 4
 __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                                  const int16_t* __restrict__ partner, int steps,
                                                                  uint64_t ntiles, const uint8_t* __restrict__ dag) {
@@ -825,38 +780,6 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 #pragma unroll
         for (int k = 0; k < OPS; ++k) fin[k] = dag[384 + 16 * w + 2 * k + h];
     }
-    // EX = 3: pair q of step k = the q-th rank y (ascending) with y < partner(y)
-    int pa[ALLRED_MAX_STEPS], pb[ALLRED_MAX_STEPS];
-    if constexpr (EX == 3) {
-        __shared__ uint8_t pairs[ALLRED_MAX_STEPS][2][32];
-        if (w == 0) {
-#pragma unroll
-            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-                if (k >= steps) break;
-                const int p = src_lane[k] >> 2;
-                const bool lead = x < p;
-                const uint64_t m = __ballot(lead);
-                const int q = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-                if (lead && q < 32) {
-                    pairs[k][0][q] = (uint8_t)x;
-                    pairs[k][1][q] = (uint8_t)p;
-                }
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-            pa[k] = k < steps ? pairs[k][0][lane & 31] : 0;
-            pb[k] = k < steps ? pairs[k][1][lane & 31] : 0;
-        }
-    }
-    int xmask[ALLRED_MAX_STEPS];  // m when step k's partner is lane ^ m on every lane, else 0
-#pragma unroll
-    for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-        const int m = (src_lane[k] >> 2) ^ x;
-        const int m0 = __builtin_amdgcn_readfirstlane(m);
-        xmask[k] = (k < steps && __all(m == m0)) ? m0 : 0;
-    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (mine > 0) issue(blockIdx.x, 0);
     for (int j = 0; j < mine; ++j) {
@@ -865,24 +788,13 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
         if (j + 1 < mine) issue(blockIdx.x + (uint64_t)(j + 1) * G, (j + 1) & 1);
         uint4* tile = buf[j & 1];
         const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
-        uint4 val[8];
-        if constexpr (EX != 3) {
+        if constexpr (EX == 0) {
+            uint4 val[8];
 #pragma unroll
             for (int i = 0; i < 8; ++i) val[i] = tile[x * TV + ((8 * w + i) ^ (x & 31))];
-        }
-        if constexpr (EX == 0 || EX == 2) {
 #pragma unroll
             for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
                 if (k >= steps) break;
-                if constexpr (EX == 2) {
-                    const int m = xmask[k];
-                    if (m == 1) { xor_step8<1>(val); continue; }
-                    if (m == 2) { xor_step8<2>(val); continue; }
-                    if (m == 4) { xor_step8<4>(val); continue; }
-                    if (m == 8) { xor_step8<8>(val); continue; }
-                    if (m == 16) { xor_step8<16>(val); continue; }
-                    if (m == 32) { xor_step8<32>(val); continue; }
-                }
                 const int sl = src_lane[k];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -896,7 +808,7 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
             }
 #pragma unroll
             for (int i = 0; i < 8; ++i) tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];  // own columns only
-        } else if constexpr (EX == 4) {
+        } else {
             const int c = 8 * w + (lane & 7);
 #pragma unroll
             for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
@@ -916,41 +828,6 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
                         const int q = 8 * i + (lane >> 3);
                         tile[q * TV + (c ^ (q & 31))] = add8(A[i], B[i]);
                     }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        } else if constexpr (EX == 3) {
-            const int c0 = 8 * w + 4 * (lane >> 5);
-#pragma unroll
-            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-                if (k >= steps) break;
-                const int a = pa[k], b = pb[k];
-                uint4 A[4], B[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    A[i] = tile[a * TV + ((c0 + i) ^ (a & 31))];
-                    B[i] = tile[b * TV + ((c0 + i) ^ (b & 31))];
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const uint4 sum = add8(A[i], B[i]);
-                    tile[a * TV + ((c0 + i) ^ (a & 31))] = sum;
-                    tile[b * TV + ((c0 + i) ^ (b & 31))] = sum;
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-                if (k >= steps) break;
-                const int p = src_lane[k] >> 2;
-                uint4 o[8];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) o[i] = tile[p * TV + ((8 * w + i) ^ (p & 31))];
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    val[i] = add8(val[i], o[i]);
-                    tile[x * TV + ((8 * w + i) ^ (x & 31))] = val[i];
                 }
                 __builtin_amdgcn_wave_barrier();
             }
@@ -2600,7 +2477,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
 }
 
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
-                     bool paired, const uint8_t* dag, void* stream) {
+                     const uint8_t* dag, void* stream) {
     if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
     hipStream_t st = (hipStream_t)stream;
@@ -2620,28 +2497,17 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
         const uint64_t tiles = nv / 32;
         // (the k_tree_lds_lag schedule — stores one iteration late — measured slower
         // here: 26.6 vs 24.1 us at 640 kB; the butterfly is not bound by HBM order)
-        static const int ex = [] {
-            const char* e = std::getenv("ALLRED_BFLY_EX");  // A/B arms; 4 (default) = the DAG form
-            return e ? std::atoi(e) : 4;
+        static const bool force_bpermute = [] {  // ALLRED_BFLY_EX=0: the register butterfly (A/B)
+            const char* e = std::getenv("ALLRED_BFLY_EX");
+            return e && std::atoi(e) == 0;
         }();
         const dim3 grid((unsigned)(tiles < cap ? tiles : cap));
-        if (dag && ex != 0 && ex != 1 && ex != 2 && ex != 3) {
+        if (dag && !force_bpermute)
             hipLaunchKernelGGL(k_butterfly_lds64_pipe<4>, grid, dim3(kBlock), 0, st, ranks, stride, d_partner, steps,
                                tiles, dag);
-            return last_error();
-        }
-        if (ex == 1)
-            hipLaunchKernelGGL(k_butterfly_lds64_pipe<1>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles, nullptr);
-        else if (ex == 2)
-            hipLaunchKernelGGL(k_butterfly_lds64_pipe<2>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles, nullptr);
-        else if (ex == 3 && paired)
-            hipLaunchKernelGGL(k_butterfly_lds64_pipe<3>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles, nullptr);
         else
-            hipLaunchKernelGGL(k_butterfly_lds64_pipe<0>, dim3((unsigned)(tiles < cap ? tiles : cap)), dim3(kBlock), 0,
-                               st, ranks, stride, d_partner, steps, tiles, nullptr);
+            hipLaunchKernelGGL(k_butterfly_lds64_pipe<0>, grid, dim3(kBlock), 0, st, ranks, stride, d_partner, steps,
+                               tiles, nullptr);
         return last_error();
     }
     if (total == 64 && nv % 32 == 0 && nv >= 32 * 256) {  // >= 256 tiles: the LDS-staged form pays
