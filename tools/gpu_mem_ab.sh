@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU session: mem_2D parity (every test naming mem / MEM / oneshot / persistent),
+# then the fused mem_2D pass at 640 kB x 64 ranks (tools/ab_fused.py, 32 sets),
+# and at 128 / 256 kB (k_mem_lds one tile per workgroup).
+cd "$(dirname "$0")/.." || exit 1
+export TMPDIR=/tmp
+OUT=gpurun_out/${TAG:-memab}
+mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_cli.py -k "mem or MEM or persistent or lds_forms" -x -q --timeout 100 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?
+echo "PYTEST_EXIT $rc" >> $OUT/pytest.log
+[ $rc -eq 0 ] || exit 1
+for i in 1 2 3; do
+  for tiles in 5 1 2; do
+    AB_SETS=32 timeout -k 10 120 python tools/ab_fused.py mem $tiles 400 >> $OUT/ab.jsonl || exit 1
+  done
+done
+echo DONE > $OUT/done
