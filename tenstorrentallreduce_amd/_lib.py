@@ -20,7 +20,8 @@ except Exception:  # pragma: no cover - torch is always present in this image
     torch = None
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "liballred.so")
+# ALLRED_LIB_PATH: another build of the same ABI (A/B timing of a change, tools/gpu_mem_ab.sh)
+LIB_PATH = os.environ.get("ALLRED_LIB_PATH") or os.path.join(HERE, "lib", "liballred.so")
 BIN_DIR = os.path.join(HERE, "bin")
 
 if not os.path.exists(LIB_PATH):

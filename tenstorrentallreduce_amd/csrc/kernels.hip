@@ -1032,13 +1032,23 @@ __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, ui
         const int own = (int)(v / block_vec);
         const uint4 s = reinterpret_cast<const uint4*>(ranks + (uint64_t)own * stride)[v];
         float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
-        for (int r = 0; r < total; ++r) {
-            if (r == own) continue;
-            const uint4 y = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride)[v];
-            a[0] += lo_f(y.x); a[1] += hi_f(y.x);
-            a[2] += lo_f(y.y); a[3] += hi_f(y.y);
-            a[4] += lo_f(y.z); a[5] += hi_f(y.z);
-            a[6] += lo_f(y.w); a[7] += hi_f(y.w);
+        // eight ranks' loads in flight before their adds; the owner's slot and
+        // ranks past `total` contribute -0.0 (x + -0.0 == x for every x)
+        for (int r0 = 0; r0 < total; r0 += 8) {
+            uint4 y[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int r = r0 + i;
+                y[i] = (r < total && r != own) ? reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride)[v]
+                                               : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+            }
         }
         uint4 o;
         o.x = pack_rne(a[0], a[1]);

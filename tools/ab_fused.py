@@ -20,16 +20,18 @@ stride = n + int(os.environ["AB_PAD"]) if "AB_PAD" in os.environ else t.preferre
 NS = int(os.environ.get("AB_SETS", "8"))
 sets = [torch.randint(0x3F80, 0x42C8, (P, stride), dtype=torch.int16, device="cuda") for _ in range(NS)]
 algo = {"swing": t.SWING, "recdub": t.RECDUB}[os.environ.get("AB_ALGO", "swing")]
-plan = t.Plan(algo, variant, SIDE, n, P, t.EXEC_FUSED)
+exec_mode = t.EXEC_STEPS if os.environ.get("AB_EXEC") == "steps" else t.EXEC_FUSED
+plan = t.Plan(algo, variant, SIDE, n, P, exec_mode)
+ws = torch.empty(max(plan.workspace_bytes, 16), dtype=torch.uint8, device="cuda")
 s = torch.cuda.Stream()
 with torch.cuda.stream(s):
     for i in range(10):
-        plan.execute(sets[i % NS].data_ptr(), stride, None, s)
+        plan.execute(sets[i % NS].data_ptr(), stride, ws.data_ptr(), s)
 torch.cuda.synchronize()
 g = torch.cuda.CUDAGraph()
 with torch.cuda.graph(g, stream=s):
     for i in range(steps):
-        plan.execute(sets[i % NS].data_ptr(), stride, None, s)
+        plan.execute(sets[i % NS].data_ptr(), stride, ws.data_ptr(), s)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(s)
@@ -39,7 +41,7 @@ e1.record(s)
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / steps * 1e3
 alg = 2 * P * n * 2
-print(json.dumps({"variant": sys.argv[1], "algo": os.environ.get("AB_ALGO", "swing"), "bytes_per_rank": n * 2, "us": round(us, 3),
+print(json.dumps({"variant": sys.argv[1], "P": P, "exec": os.environ.get("AB_EXEC", "fused"), "lib": os.environ.get("ALLRED_LIB_PATH", ""), "algo": os.environ.get("AB_ALGO", "swing"), "bytes_per_rank": n * 2, "us": round(us, 3),
                   "hbm_GBps": round(alg / us / 1e3, 1), "env": {k: v for k, v in os.environ.items()
                                                                if k.startswith(("ALLRED_", "AB_"))}}))
 plan.close()
