@@ -104,6 +104,15 @@ typedef struct {
     uint8_t tree_order[ALLRED_MAX_NODES][ALLRED_MAX_NODES];
 } allred_schedule;
 int allred_schedule_build(int algo, int side_length, int total_nodes, allred_schedule* out);
+/* The fused LO pass's DAG of distinct sums (64 ranks; no reference
+ * counterpart — the per-core butterfly of allred_BO_2D/kernels/
+ * dataflow_kernel.cpp:19-29 evaluated once per distinct value).  Writes the
+ * layout k_butterfly_lds64_pipe reads (kernels.hip) into out[cap]; returns
+ * the bytes written, 0 when the schedule has no DAG form (not 64 ranks, a
+ * step with more than 32 distinct sums), or a negative status.
+ * *read_conflicts = extra LDS bank cycles of its reads per column group and
+ * tile (0 once placed; ALLRED_DAG_PLACE=0 keeps first-appearance order). */
+int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size_t cap, int* read_conflicts);
 
 /* ======================================================================
  * Host data — tt-metal bfloat16 helpers the reference calls

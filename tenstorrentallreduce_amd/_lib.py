@@ -118,6 +118,7 @@ SIGNATURES = [
     ("allred_get_comm_partner_swing_1d", C.c_int, [C.c_int, C.c_int, C.c_int]),
     ("allred_get_comm_partner_recdub_1d", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint32)]),
     ("allred_schedule_build", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(Schedule)]),
+    ("allred_lo_dag", C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_int)]),
     ("allred_random_bf16_vector", None, [C.c_size_t, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_constant_bf16_vector", None, [C.c_size_t, C.c_float, _P]),
     ("allred_validate_result_vector", C.c_long,
@@ -157,6 +158,8 @@ PEER_HANDLE_BYTES = 192
 PEER_TIMEOUT, PEER_WIN_CACHED, PEER_FLAGS_CACHED = 0x1, 0x100, 0x200   # allred_peer_status bits
 
 for _name, _res, _args in SIGNATURES:
+    if "ALLRED_LIB_PATH" in os.environ and not hasattr(lib, _name):
+        continue  # an older build under A/B may predate a later entry point
     _f = getattr(lib, _name)  # AttributeError here = the library lacks a declared symbol
     _f.restype = _res
     _f.argtypes = _args

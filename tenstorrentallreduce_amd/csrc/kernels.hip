@@ -732,13 +732,16 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64(uint16_t* __restrict
 // step-k values come from the same pair of step-(k-1) values hold the same
 // bits, so the host interns them (engine.cpp lo_dag): step k has d_k distinct
 // nodes (Swing 8x8: 32, 16, 16, 16, 8, 4 — 92 adds per column instead of the
-// butterfly's 384), node q of step k lives in tile row q, its inputs are rows
-// of step k-1 (the leaves at step 0).  Lane group g = lane >> 3 takes nodes
-// g, g + 8, g + 16, g + 24 in column 8w + (lane & 7); a step issues all its
-// reads before its writes, so overwriting rows of step k-1 is safe in wave
-// order.  Rank r's result is row fin[r], stored to rank r's bucket.
-// dag layout (uint8): [k*64 + 2q] / [+1] = input rows of node q of step k,
-// [384 + r] = final row of rank r, [448 + k] = d_k.
+// butterfly's 384); its inputs are rows of step k-1 (the leaves at step 0).
+// Lane group g = lane >> 3 takes the nodes in slots g, g + 8, g + 16, g + 24
+// in column 8w + (lane & 7); the host chooses each node's slot and tile row
+// so that every operand read (ds_read_b128, four 16-lane bank groups) is
+// bank-conflict free (engine.cpp lo_dag_place; Swing 8x8: 92 extra LDS cycles
+// per column group and tile with row = slot = first appearance, 0 placed).  A
+// step issues all its reads before its writes, so overwriting rows of step
+// k-1 is safe in wave order.  Rank r's result is row fin[r], stored to rank
+// r's bucket.  dag: the lane-group form of allred_lo_dag's table
+// (engine.cpp lo_dag_lanes).
 template <int EX>   // 0, 4 or 5 (below)
 __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                                  const int16_t* __restrict__ partner, int steps,
@@ -765,20 +768,21 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
     int src_lane[ALLRED_MAX_STEPS];
 #pragma unroll
     for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
-    // EX = 4: node operands (a | b << 8, or -1) of this lane's items, final rows
+    // EX >= 4: this lane's node of each step and item as a | b << 8 | dest << 16
+    // (input rows, output row; -1: empty slot) and the final rows, from the
+    // lane-group form of the table (engine.cpp lo_dag_lanes): six 16-byte loads
     int nab[ALLRED_MAX_STEPS][4], fin[OPS];
     if constexpr (EX >= 4) {
+        const uint4* tab = reinterpret_cast<const uint4*>(dag) + (lane >> 3) * 6;
 #pragma unroll
         for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-            const int dk = k < steps ? dag[448 + k] : 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const int q = 8 * i + (lane >> 3);
-                nab[k][i] = q < dk ? (int)dag[k * 64 + 2 * q] | ((int)dag[k * 64 + 2 * q + 1] << 8) : -1;
-            }
+            const uint4 t = tab[k];
+            nab[k][0] = (int)t.x, nab[k][1] = (int)t.y, nab[k][2] = (int)t.z, nab[k][3] = (int)t.w;
         }
+        const uint4 fv = reinterpret_cast<const uint4*>(dag + 768)[w];   // ranks 16w .. 16w+15
+        const uint32_t fw[4] = {fv.x, fv.y, fv.z, fv.w};
 #pragma unroll
-        for (int k = 0; k < OPS; ++k) fin[k] = dag[384 + 16 * w + 2 * k + h];
+        for (int k = 0; k < OPS; ++k) fin[k] = (int)(fw[k >> 1] >> (8 * (2 * (k & 1) + h))) & 255;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (EX == 5) {
@@ -809,7 +813,7 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (nab[k][i] >= 0) {
-                        const int a = nab[k][i] & 255, b = nab[k][i] >> 8;
+                        const int a = nab[k][i] & 255, b = (nab[k][i] >> 8) & 255;
                         A[i] = tile[a * TV + (c ^ (a & 31))];
                         B[i] = tile[b * TV + (c ^ (b & 31))];
                     }
@@ -817,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (nab[k][i] >= 0) {
-                        const int q = 8 * i + (lane >> 3);
+                        const int q = nab[k][i] >> 16;   // row; the last step's rows are 0..d_last-1
                         if (last) out[q * TV + c] = add8(A[i], B[i]);   // q < d_last <= 8
                         else tile[q * TV + (c ^ (q & 31))] = add8(A[i], B[i]);
                     }
@@ -877,7 +881,7 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (nab[k][i] >= 0) {
-                        const int a = nab[k][i] & 255, b = nab[k][i] >> 8;
+                        const int a = nab[k][i] & 255, b = (nab[k][i] >> 8) & 255;
                         A[i] = tile[a * TV + (c ^ (a & 31))];
                         B[i] = tile[b * TV + (c ^ (b & 31))];
                     }
@@ -885,7 +889,7 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (nab[k][i] >= 0) {
-                        const int q = 8 * i + (lane >> 3);
+                        const int q = nab[k][i] >> 16;
                         tile[q * TV + (c ^ (q & 31))] = add8(A[i], B[i]);
                     }
                 }

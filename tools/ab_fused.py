@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of one fused plan (64 ranks, config-2 size by default) with
 rotating bucket sets, HIP graph replay — the bench.py method for any variant.
-  python tools/ab_fused.py <bo|lo|mem> [tiles] [steps]   (env knobs pass through)"""
+  python tools/ab_fused.py <bo|lo|mem> [tiles] [steps]   (env knobs pass through); AB_EAGER=1: plain launches"""
 import json
 import os
 import sys
@@ -28,15 +28,21 @@ with torch.cuda.stream(s):
     for i in range(10):
         plan.execute(sets[i % NS].data_ptr(), stride, ws.data_ptr(), s)
 torch.cuda.synchronize()
-g = torch.cuda.CUDAGraph()
-with torch.cuda.graph(g, stream=s):
-    for i in range(steps):
-        plan.execute(sets[i % NS].data_ptr(), stride, ws.data_ptr(), s)
-torch.cuda.synchronize()
+eager = os.environ.get("AB_EAGER") == "1"   # plain launches (PMC passes)
+if not eager:
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for i in range(steps):
+            plan.execute(sets[i % NS].data_ptr(), stride, ws.data_ptr(), s)
+    torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record(s)
 with torch.cuda.stream(s):
-    g.replay()
+    if eager:
+        for i in range(steps):
+            plan.execute(sets[i % NS].data_ptr(), stride, ws.data_ptr(), s)
+    else:
+        g.replay()
 e1.record(s)
 torch.cuda.synchronize()
 us = e0.elapsed_time(e1) / steps * 1e3
