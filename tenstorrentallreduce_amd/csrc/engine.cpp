@@ -44,7 +44,6 @@ struct allred_plan {
     std::vector<int> blk_per_rank;          // m_k
     uint8_t* d_order = nullptr;
     uint8_t* d_dag = nullptr;               // LO: interned DAG (lo_dag_lanes form), 64 ranks only
-    int dag_last = 0;                       // LO: distinct final sums of the DAG (Swing 8x8: 4)
     size_t ws_bytes = 0;
     int launches = 0;
     const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
@@ -329,7 +328,6 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
                                &p->sched.tree_order[0][0] + ALLRED_MAX_NODES * ALLRED_MAX_NODES);
     if (desc->variant == ALLRED_LO && desc->exec == ALLRED_EXEC_FUSED) {
         const std::vector<uint8_t> dag = lo_dag(p->sched, total);
-        if (!dag.empty() && p->sched.steps > 0) p->dag_last = dag[448 + p->sched.steps - 1];
         if ((st = upload(&p->d_dag, lo_dag_lanes(dag, p->sched.steps)))) {
             free_plan(p);
             return st;
@@ -389,7 +387,7 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
         if (p->desc.variant == ALLRED_LO && !p->lo_tree)
-            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->d_dag, p->dag_last, stream);
+            return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->d_dag, stream);
         if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
             hipPointerAttribute_t at{};
             p->last_host = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;

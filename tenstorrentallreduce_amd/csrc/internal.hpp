@@ -46,7 +46,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
                       bool host_memory = false);
 // dag: the interned LO DAG of a 64-rank schedule (engine.cpp lo_dag), or null
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
-                     const uint8_t* dag, int dag_last, void* stream);
+                     const uint8_t* dag, void* stream);
 int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total,
                        const uint8_t* order, uint16_t* out, void* stream);
 int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src,

@@ -742,7 +742,7 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64(uint16_t* __restrict
 // k-1 is safe in wave order.  Rank r's result is row fin[r], stored to rank
 // r's bucket.  dag: the lane-group form of allred_lo_dag's table
 // (engine.cpp lo_dag_lanes).
-template <int EX>   // 0, 4 or 5 (below)
+template <int EX>   // 0 or 4
 __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                                  const int16_t* __restrict__ partner, int steps,
                                                                  uint64_t ntiles, const uint8_t* __restrict__ dag) {
@@ -768,11 +768,11 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
     int src_lane[ALLRED_MAX_STEPS];
 #pragma unroll
     for (int k = 0; k < ALLRED_MAX_STEPS; ++k) src_lane[k] = k < steps ? (int)partner[k * 64 + x] * 4 : 0;
-    // EX >= 4: this lane's node of each step and item as a | b << 8 | dest << 16
+    // EX = 4: this lane's node of each step and item as a | b << 8 | dest << 16
     // (input rows, output row; -1: empty slot) and the final rows, from the
     // lane-group form of the table (engine.cpp lo_dag_lanes): six 16-byte loads
     int nab[ALLRED_MAX_STEPS][4], fin[OPS];
-    if constexpr (EX >= 4) {
+    if constexpr (EX == 4) {
         const uint4* tab = reinterpret_cast<const uint4*>(dag) + (lane >> 3) * 6;
 #pragma unroll
         for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
@@ -785,66 +785,6 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
         for (int k = 0; k < OPS; ++k) fin[k] = (int)(fw[k >> 1] >> (8 * (2 * (k & 1) + h))) & 255;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (EX == 5) {
-        // EX = 5 (A/B arm, measured slower than EX = 4: see launch_butterfly):
-        // the DAG with loads two tiles ahead (as k_tree_lds_lag).  The last
-        // step's d_last <= 8 distinct sums go to a small LDS row set (res), not
-        // back into the tile, so tile j's buffer is free for tile j+2's loads as
-        // soon as the DAG has read it, and tile j's 64 row stores (each rank's row
-        // is res[fin[r]], unswizzled) leave interleaved op by op with those loads.
-        // Issue order per wave: L0 L1 | L2 S0 | L3 S1 | ..., so after tile j's
-        // loads come the last op of S(j-2), then L(j+1) and S(j-1).
-        __shared__ __attribute__((aligned(16))) uint4 res[2][8 * TV];
-        if (mine > 0) issue(blockIdx.x, 0);
-        if (mine > 1) issue(blockIdx.x + G, 1);
-        const int c = 8 * w + (lane & 7);
-        for (int j = 0; j < mine; ++j) {
-            wait_any(j == 0 ? (mine > 1 ? OPS : 0)
-                            : (j >= 2 ? 1 : 0) + (j + 1 < mine ? OPS : 0) + OPS);
-            lds_barrier();   // every wave's rows of tile j are in LDS
-            uint4* tile = buf[j & 1];
-            uint4* out = res[j & 1];
-            const uint64_t v0 = (blockIdx.x + (uint64_t)j * G) * TV;
-#pragma unroll
-            for (int k = 0; k < ALLRED_MAX_STEPS; ++k) {
-                if (k >= steps) break;
-                const bool last = k == steps - 1;
-                uint4 A[4], B[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (nab[k][i] >= 0) {
-                        const int a = nab[k][i] & 255, b = (nab[k][i] >> 8) & 255;
-                        A[i] = tile[a * TV + (c ^ (a & 31))];
-                        B[i] = tile[b * TV + (c ^ (b & 31))];
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (nab[k][i] >= 0) {
-                        const int q = nab[k][i] >> 16;   // row; the last step's rows are 0..d_last-1
-                        if (last) out[q * TV + c] = add8(A[i], B[i]);   // q < d_last <= 8
-                        else tile[q * TV + (c ^ (q & 31))] = add8(A[i], B[i]);
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-            lds_barrier();   // every wave has read tile j; the final rows are in res
-            uint4 o[OPS];
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) o[k] = out[fin[k] * TV + l32];
-            const uint64_t tl = blockIdx.x + (uint64_t)(j + 2) * G;
-            const uint32_t bl = wbase + (uint32_t)((j & 1) * 64 * TV * 16);
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                const int r = 16 * w + 2 * k + h;
-                if (j + 2 < mine)
-                    lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + tl * TV + (l32 ^ (r & 31)),
-                              bl + (uint32_t)(2 * k * TV * 16));
-                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + l32, o[k]);
-            }
-        }
-        return;
-    }
     if (mine > 0) issue(blockIdx.x, 0);
     for (int j = 0; j < mine; ++j) {
         wait_tile<OPS, 1>(j < 1 ? j : 1);
@@ -2555,7 +2495,7 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
 }
 
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
-                     const uint8_t* dag, int dag_last, void* stream) {
+                     const uint8_t* dag, void* stream) {
     if (n % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
     hipStream_t st = (hipStream_t)stream;
@@ -2575,19 +2515,15 @@ int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
         const uint64_t tiles = nv / 32;
         // (the k_tree_lds_lag schedule — stores one iteration late — measured slower
         // here: 26.6 vs 24.1 us at 640 kB; the butterfly is not bound by HBM order)
-        // ALLRED_BFLY_EX (A/B): 0 the register butterfly, 4 the DAG one tile ahead (default),
-        // 5 the DAG two tiles ahead with interleaved stores: slower, 19.0 vs 17.0 us at
-        // 640 kB, 7.9 vs 7.5 at 128 kB (profiles/r01_lo_lag_ab.txt)
-        static const int ex_env = [] {
+        // ALLRED_BFLY_EX=0: the register butterfly (A/B).  Measured and removed: the
+        // DAG with loads two tiles ahead, final rows in a small LDS set and stores
+        // interleaved with those loads, 19.0 vs 17.0 us at 640 kB (profiles/r01_lo_lag_ab.txt)
+        static const bool force_bpermute = [] {
             const char* e = std::getenv("ALLRED_BFLY_EX");
-            return e ? std::atoi(e) : 4;
+            return e && std::atoi(e) == 0;
         }();
-        const bool force_bpermute = ex_env == 0;
         const dim3 grid((unsigned)(tiles < cap ? tiles : cap));
-        if (dag && ex_env == 5 && dag_last >= 1 && dag_last <= 8)
-            hipLaunchKernelGGL(k_butterfly_lds64_pipe<5>, grid, dim3(kBlock), 0, st, ranks, stride, d_partner, steps,
-                               tiles, dag);
-        else if (dag && !force_bpermute)
+        if (dag && !force_bpermute)
             hipLaunchKernelGGL(k_butterfly_lds64_pipe<4>, grid, dim3(kBlock), 0, st, ranks, stride, d_partner, steps,
                                tiles, dag);
         else

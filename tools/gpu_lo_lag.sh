@@ -1,12 +1,12 @@
 #!/bin/bash
-# GPU session: the fused LO DAG pass with loads two tiles ahead (EX = 5, the
+# GPU session (historical: the EX = 5 arm is removed): the fused LO DAG pass with loads two tiles ahead (EX = 5, the
 # arm) vs one tile ahead (EX = 4, the default): LO parity with the DAG pipe forced from
 # 1 tile, then Swing LO 128 kB..640 kB x 64 ranks, arms alternated.
 cd "$(dirname "$0")/.." || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-lolag}
 mkdir -p $OUT
-ALLRED_BFLY_EX=5 ALLRED_BFLY_DAG_MIN=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "lo or LO" -x -q --timeout 100 --timeout-method thread > $OUT/pytest.log 2>&1
+ALLRED_BFLY_DAG_MIN=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -k "lo or LO" -x -q --timeout 100 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?
 echo "PYTEST_EXIT $rc" >> $OUT/pytest.log
 [ $rc -eq 0 ] || exit 1
