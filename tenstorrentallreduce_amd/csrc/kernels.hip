@@ -1029,25 +1029,26 @@ __global__ __launch_bounds__(kBlock) void k_copy_ranks(const uint16_t* __restric
 // seed).  WRITE_ALL: store to every rank (fused one-shot form);
 // else store to `out` (the shared dst buffer, allred_mem_2D dataflow :169-174).
 // ---------------------------------------------------------------------------
-template <bool WRITE_ALL>
+template <bool WRITE_ALL, int B = 8>   // B ranks' loads in flight per thread before their adds
 __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, uint64_t stride, int total,
                                                 uint64_t n_vec, uint64_t block_vec, uint16_t* __restrict__ out) {
     for (uint64_t v = gtid(); v < n_vec; v += gthreads()) {
         const int own = (int)(v / block_vec);
         const uint4 s = reinterpret_cast<const uint4*>(ranks + (uint64_t)own * stride)[v];
         float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
-        // eight ranks' loads in flight before their adds; the owner's slot and
-        // ranks past `total` contribute -0.0 (x + -0.0 == x for every x)
-        for (int r0 = 0; r0 < total; r0 += 8) {
-            uint4 y[8];
+        // B ranks' loads in flight before their adds (in rank order: the sum's
+        // order does not change); the owner's slot and ranks past `total`
+        // contribute -0.0 (x + -0.0 == x for every x)
+        for (int r0 = 0; r0 < total; r0 += B) {
+            uint4 y[B];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < B; ++i) {
                 const int r = r0 + i;
                 y[i] = (r < total && r != own) ? reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride)[v]
                                                : make_uint4(0x80008000u, 0x80008000u, 0x80008000u, 0x80008000u);
             }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < B; ++i) {
                 a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
                 a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
                 a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
@@ -2625,8 +2626,33 @@ int launch_copy_ranks(const uint16_t* src, uint64_t src_stride, uint16_t* dst, u
 int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, uint16_t* dst, void* stream) {
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks) || !aligned16(dst)) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8;
-    hipLaunchKernelGGL(k_mem<false>, dim3(grid_for(nv)), dim3(kBlock), 0, (hipStream_t)stream,
-                       const_cast<uint16_t*>(ranks), stride, total, nv, nv / total, dst);
+    // one column per thread reads all `total` ranks: a 640 kB bucket has only 40,960
+    // columns (160 workgroups), so bytes in flight come from loads per thread:
+    // 16 (default) vs 8 ranks' loads before their adds, 256 threads: 640 kB 22.1-22.3
+    // vs 22.7 us, 256 kB 15.9 vs 17.1, 128 kB 11.9 vs 13.1; one-wave workgroups
+    // (640 of them, every CU busy) were slower: 29.8 us at 640 kB
+    // (profiles/r01_mem_batch_ab.txt).  ALLRED_MEM_BATCH (8/16/32), ALLRED_MEM_BLOCK (A/B)
+    static const int batch = [] {
+        const char* e = std::getenv("ALLRED_MEM_BATCH");
+        return e ? std::atoi(e) : 16;
+    }();
+    static const unsigned block = [] {
+        const char* e = std::getenv("ALLRED_MEM_BLOCK");
+        const unsigned b = e ? (unsigned)std::atoi(e) : (unsigned)kBlock;
+        return b == 64 || b == 128 ? b : (unsigned)kBlock;
+    }();
+    uint64_t g = (nv + block - 1) / block;
+    if (g > (uint64_t)kMaxGrid) g = kMaxGrid;
+    uint16_t* r = const_cast<uint16_t*>(ranks);
+    if (batch == 32)
+        hipLaunchKernelGGL((k_mem<false, 32>), dim3((unsigned)g), dim3(block), 0, (hipStream_t)stream, r, stride, total,
+                           nv, nv / total, dst);
+    else if (batch == 16)
+        hipLaunchKernelGGL((k_mem<false, 16>), dim3((unsigned)g), dim3(block), 0, (hipStream_t)stream, r, stride, total,
+                           nv, nv / total, dst);
+    else
+        hipLaunchKernelGGL((k_mem<false, 8>), dim3((unsigned)g), dim3(block), 0, (hipStream_t)stream, r, stride, total,
+                           nv, nv / total, dst);
     return last_error();
 }
 
