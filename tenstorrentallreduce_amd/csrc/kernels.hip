@@ -854,7 +854,8 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
 // wave-instruction).  128 threads: 2 waves.
 // ---------------------------------------------------------------------------
 template <int P>
-__global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, uint64_t stride, uint64_t block_vec) {
+__global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, uint64_t stride, uint64_t block_vec,
+                                                 uint16_t* __restrict__ out = nullptr) {   // out: reduce only (schedule form)
     constexpr int TV = 32;                      // 16-byte vectors per rank row
     constexpr int RPW = P / 2;                  // rank rows staged per wave
     __shared__ __attribute__((aligned(16))) uint4 tile[P * TV];
@@ -880,6 +881,10 @@ __global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, u
         y = t32[r * TV * 4 + d];
         a0 += lo_f(y);
         a1 += hi_f(y);
+    }
+    if (out) {   // the schedule form's reduce: the block's sum goes to `out` (k_broadcast reads it back)
+        reinterpret_cast<uint32_t*>(out + v0 * 8)[d] = pack_rne(a0, a1);
+        return;
     }
     __syncthreads();
     reinterpret_cast<uint32_t*>(tile)[d] = pack_rne(a0, a1);
@@ -2641,9 +2646,31 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
         const unsigned b = e ? (unsigned)std::atoi(e) : (unsigned)kBlock;
         return b == 64 || b == 128 ? b : (unsigned)kBlock;
     }();
+    uint16_t* r = const_cast<uint16_t*>(ranks);
+    // block rows in whole 256-element tiles: the fused pass's LDS form (every rank's
+    // tile staged by LDS-DMA, one thread per dword sums from LDS in the same order),
+    // one workgroup per tile, result to dst only: 640 kB 13.6 us for k_mem<false, 16>
+    // (3.1 TB/s of reads; 160 workgroups) -> see profiles/r01_mem_reduce_ab.txt.
+    // ALLRED_MEM_REDUCE_LDS=0: k_mem<false, B> (A/B)
+    static const bool lds_form = [] {
+        const char* e = std::getenv("ALLRED_MEM_REDUCE_LDS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    const uint64_t bv = nv / total;
+    if (lds_form && bv % 32 == 0 && total >= 4 && total <= 64 && (total & (total - 1)) == 0) {
+        const dim3 grid((unsigned)(nv / 32)), blk(128);
+        hipStream_t st = (hipStream_t)stream;
+        switch (total) {
+            case 4: hipLaunchKernelGGL(k_mem_lds<4>, grid, blk, 0, st, r, stride, bv, dst); break;
+            case 8: hipLaunchKernelGGL(k_mem_lds<8>, grid, blk, 0, st, r, stride, bv, dst); break;
+            case 16: hipLaunchKernelGGL(k_mem_lds<16>, grid, blk, 0, st, r, stride, bv, dst); break;
+            case 32: hipLaunchKernelGGL(k_mem_lds<32>, grid, blk, 0, st, r, stride, bv, dst); break;
+            default: hipLaunchKernelGGL(k_mem_lds<64>, grid, blk, 0, st, r, stride, bv, dst); break;
+        }
+        return last_error();
+    }
     uint64_t g = (nv + block - 1) / block;
     if (g > (uint64_t)kMaxGrid) g = kMaxGrid;
-    uint16_t* r = const_cast<uint16_t*>(ranks);
     if (batch == 32)
         hipLaunchKernelGGL((k_mem<false, 32>), dim3((unsigned)g), dim3(block), 0, (hipStream_t)stream, r, stride, total,
                            nv, nv / total, dst);
