@@ -993,6 +993,37 @@ __global__ __launch_bounds__(kBlock) void k_broadcast(uint16_t* __restrict__ ran
 // AG: ranks[r][b]  = ranks[p][b] for b in send_mask_k(r) (= recv_mask_k(p))
 // grid.y = rank * blocks_per_rank + j
 // ---------------------------------------------------------------------------
+// k_step with one wave per (rank, block) and U vectors' loads in flight per
+// lane (the default step kernel; k_step below with ALLRED_STEP_FORM=0).
+template <bool ADD, int U>
+__global__ __launch_bounds__(64) void k_step_w(uint16_t* __restrict__ ranks, uint64_t stride,
+                                               const int16_t* __restrict__ partner,
+                                               const int16_t* __restrict__ blocks, int blocks_per_rank,
+                                               uint64_t block_vec) {
+    const int t = blockIdx.x;
+    const int r = t / blocks_per_rank;
+    const int p = partner[r];
+    const uint64_t off = (uint64_t)blocks[t] * block_vec;
+    uint4* L = reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + off;
+    const uint4* R = reinterpret_cast<const uint4*>(ranks + (uint64_t)p * stride) + off;
+    for (uint64_t v0 = threadIdx.x; v0 < block_vec; v0 += 64 * U) {
+        uint4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t v = v0 + 64 * u;
+            if (v < block_vec) {
+                b[u] = ld_nt(R + v);
+                if (ADD) a[u] = ld_nt(L + v);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t v = v0 + 64 * u;
+            if (v < block_vec) st_nt(L + v, ADD ? add8(a[u], b[u]) : b[u]);
+        }
+    }
+}
+
 template <bool ADD>
 __global__ __launch_bounds__(kBlock) void k_step(uint16_t* __restrict__ ranks, uint64_t stride,
                                                  const int16_t* __restrict__ partner,
@@ -2587,6 +2618,24 @@ static int launch_step(bool add, uint16_t* ranks, uint64_t stride, int total, co
                        const int16_t* d_blocks, int blocks_per_rank, size_t block_elems, void* stream) {
     if (block_elems % 8 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8;
+    // one wave per rank block, 8 vectors' loads in flight per lane (default) vs one
+    // thread per vector over a grid covering the block (ALLRED_STEP_FORM=0, A/B):
+    // the 12-launch config-2 program 67.8 vs 71.7 us, 256 kB 39.9 vs 45.5, 128 kB
+    // 34.0 vs 38.6 (profiles/r01_step_form_ab.txt)
+    static const int form = [] {
+        const char* e = std::getenv("ALLRED_STEP_FORM");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (form == 1) {
+        const dim3 g((unsigned)(total * blocks_per_rank));
+        if (add)
+            hipLaunchKernelGGL((k_step_w<true, 8>), g, dim3(64), 0, (hipStream_t)stream, ranks, stride, d_partner,
+                               d_blocks, blocks_per_rank, bv);
+        else
+            hipLaunchKernelGGL((k_step_w<false, 8>), g, dim3(64), 0, (hipStream_t)stream, ranks, stride, d_partner,
+                               d_blocks, blocks_per_rank, bv);
+        return last_error();
+    }
     const unsigned gx = grid_all(bv);
     const dim3 grid(gx, (unsigned)(total * blocks_per_rank));
     if (add)
