@@ -206,6 +206,22 @@ def test_lo_sizes_reference_inputs(tiles, exec_mode):
     assert (got == np.stack(want)).all()
 
 
+@pytest.mark.parametrize("place", ["1", "0"])
+@pytest.mark.parametrize("n", [1024 * 64, 327680])
+def test_fused_lo_dag_placement(n, place, monkeypatch):
+    """The fused Swing 8x8 LO DAG pass (k_butterfly_lds64_pipe<4>) with its
+    bank-conflict-free node placement (engine.cpp lo_dag_place) and with
+    first-appearance rows and slots (ALLRED_DAG_PLACE=0): both bit-exact vs the
+    oracle's per-rank butterfly (allred_BO_2D/kernels/dataflow_kernel.cpp:19-29)."""
+    monkeypatch.setenv("ALLRED_DAG_PLACE", place)
+    side, total = 8, 64
+    ranks = rand_ranks(total, n, seed=71 + n % 97)
+    got = run_plan(t.SWING, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("lo", t.SWING, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
 @pytest.mark.parametrize("lo_tree", ["1", "0"])
 @pytest.mark.parametrize("algo,grid,n", [
     (t.RECDUB, (8, 64), 327680), (t.RECDUB, (8, 64), 1024 * 16), (t.RECDUB, (4, 16), 1024 * 64),
