@@ -100,22 +100,20 @@ def cpu_baseline() -> dict:
     }
 
 
-# the fused BO kernel the engine launches at config 2 (kernels.hip launch_tree_fused;
-# ALLRED_PIPE_LAG=0 / ALLRED_PIPE_REL=0 select the earlier forms for A/B)
-if os.environ.get("ALLRED_PIPE_LAG", "1") != "0":
-    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_lag<64, 32, 7, 4>", "k_tree_lds_lag64"
-elif os.environ.get("ALLRED_PIPE_REL", "1") == "1":
-    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_pipe<64, 1, 32, true, true>", "k_tree_lds_pipe64"
-else:
-    FUSED_KERNEL, FUSED_KEY = "k_tree_lds_pipe<64, 1, 32, true, false>", "k_tree_lds_pipe64"
+# the fused BO kernel the engine launches at config 2 (kernels.hip launch_tree_fused)
+FUSED_KERNEL = "k_tree_lds_lag<64>"
 
 
-def pmc_traffic(kernel_key: str):
-    """HBM bytes per launch from the committed PMC summary (tools/pmc_traffic.py)."""
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (tools/pmc_traffic.py: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 --pmc
+    passes of bench.py --main-only, gfx950 FETCH_SIZE x2 correction), only when
+    that summary was taken on the same kernel template this bench launches."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         d = json.load(open(path))
-        return d["kernels"][kernel_key]["hbm_bytes_per_launch"]
+        e = d["kernels"][kernel]
+        return e["hbm_bytes_per_launch"] if e.get("template") == kernel else None
     except Exception:
         return None
 
@@ -135,12 +133,10 @@ def bench_single(args) -> dict:
     def step(i, p=plan):
         p.execute(sets[i % nsets].data_ptr(), stride, None, stream)
 
-    with torch.cuda.stream(stream):
-        prewarm_s = prewarm(step, args.prewarm_ms)
-        for i in range(args.warmup):
-            step(i)
-    torch.cuda.synchronize()
-
+    # the K timed steps as one HIP graph, captured BEFORE the prewarm so that no
+    # host-only phase (capture) sits between the steady-clock prewarm and the
+    # timed replays (a capture gap after the prewarm measured 14.8 us per step at
+    # K = 20 vs 14.2-14.3 at K = 200: the clocks had dropped)
     graph = None
     if not args.eager:
         try:
@@ -153,30 +149,42 @@ def bench_single(args) -> dict:
             print(f"[bench] graph capture failed ({e}); eager launches", file=sys.stderr)
             graph = None
 
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    if graph is not None:   # the first replay uploads the graph: untimed
+    def k_steps():   # one pass over the K timed steps
         with torch.cuda.stream(stream):
-            graph.replay()
+            if graph is not None:
+                graph.replay()
+            else:
+                for i in range(args.steps):
+                    step(i)
+
+    with torch.cuda.stream(stream):
+        prewarm_s = prewarm(lambda i: k_steps() if graph is not None else step(i), args.prewarm_ms,
+                            batch=max(1, 200 // args.steps) if graph is not None else 50)
+        for i in range(args.warmup):
+            step(i)
+    torch.cuda.synchronize()
+
+    # R back-to-back replays of the K steps, an event between consecutive ones;
+    # ms_per_step = the median replay / K (each interval is exactly K steps; the
+    # GPU never idles between them).  The whole R x K region is bracketed by
+    # synchronize on both sides.
+    reps = max(1, args.reps)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
-        # a ~0.1 ms spin kernel ahead of e0 keeps the GPU busy while the host
-        # submits the K steps, so e0 -> e1 times the K steps themselves, not the
-        # host's launch latency (host_wall_s below includes everything)
+        # a ~0.1 ms spin kernel ahead of the first event keeps the GPU busy while
+        # the host submits the replays (host_wall_s below includes everything)
         torch.cuda._sleep(200000)
-    e0.record(stream)
-    with torch.cuda.stream(stream):  # the graph launches on the current stream
-        if graph is not None:
-            graph.replay()
-        else:
-            for i in range(args.steps):
-                step(i)
-    e1.record(stream)
+    ev[0].record(stream)
+    for r in range(reps):
+        k_steps()
+        ev[r + 1].record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ms = e0.elapsed_time(e1)
-    ms_per_step = ms / args.steps
+    rep_ms = [ev[r].elapsed_time(ev[r + 1]) for r in range(reps)]
+    ms_per_step = statistics.median(rep_ms) / args.steps
+    e0, e1 = ev[0], ev[1]
 
     bytes_all = RANKS * ELEMS * 2
     steps_ms = hot_ms = float("nan")
@@ -248,6 +256,13 @@ def bench_single(args) -> dict:
     for mode in ("eager", "graph"):
         if mode == "graph" and c1_graph is None:
             continue
+        with torch.cuda.stream(stream):   # untimed pass first: the graph's first replay uploads it
+            if mode == "graph":
+                c1_graph.replay()
+            else:
+                for _ in range(args.steps):
+                    c1_plan.execute(c1.data_ptr(), 1024, None, stream)
+        torch.cuda.synchronize()
         with torch.cuda.stream(stream):
             e0.record(stream)
             if mode == "graph":
@@ -279,12 +294,14 @@ def bench_single(args) -> dict:
         "dtype": "bf16",
         "data": "synthetic (uniform [0,100) bf16, reference rank convention); 32 rotating bucket sets in HBM (1.3 GB), "
                 "rank rows 655,360 B + 128 B skew",
+        "timing": {"replays": reps, "ms_per_replay": [round(x, 5) for x in rep_ms],
+                   "ms_per_step": "median replay / steps (each replay = the K steps, back to back)"},
         "config": {"workload": "BASELINE config 2: 8x8 Swing BO allreduce, 64 virtual ranks x 655,360 B bf16 "
                                "(5 tiles/block) on one MI355X, fused one-pass HIP kernel, no RCCL",
                    "ranks": RANKS, "bytes_per_rank": ELEMS * 2, "algo": "swing", "variant": "BO",
                    "exec": "fused", "launches_per_step": plan.launches, "hip_graph": graph is not None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(FUSED_KEY),
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(FUSED_KERNEL),
                      "kernel": FUSED_KERNEL, "algorithmic_bytes_per_launch": alg_bytes},
         "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
                               "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
@@ -317,7 +334,7 @@ def timed_max(fn, reps, stream) -> float:
     return m.item()
 
 
-def prewarm(step, ms: float) -> float:
+def prewarm(step, ms: float, batch: int = 50) -> float:
     """Untimed: run the workload for >= ms of wall time before the W warmup steps.
     A cold MI355X needs a few ms of sustained load to reach its steady clocks
     (config 2 measured 14.80-14.86 us per step after 20 warmup steps, 14.49-14.53
@@ -326,7 +343,7 @@ def prewarm(step, ms: float) -> float:
     t0 = time.perf_counter()
     i = 0
     while time.perf_counter() - t0 < ms * 1e-3:
-        for _ in range(50):
+        for _ in range(batch):
             step(i)
             i += 1
         torch.cuda.synchronize()
@@ -372,12 +389,38 @@ def open_peer(rank, world, local_rank, max_elems):
 
 
 def arm_stats(ms, nbytes, world, lo=False) -> dict:
+    """busbw = 2(p-1)/p * n / t (nccl-tests); xgmi_frac = busbw over this GPU's
+    egress to its p-1 peers (one xGMI link each on the full mesh) at the spec
+    per-direction link rate."""
     sec = ms * 1e-3
     busbw = 2 * (world - 1) / world * nbytes / sec / 1e9   # nccl-tests convention
     if lo:
         busbw = nbytes / sec / 1e9   # LO moves the whole bucket every step: report algbw
     return {"ms": round(ms, 4), "algbw_GBps": round(nbytes / sec / 1e9, 3), "busbw_GBps": round(busbw, 3),
-            "xgmi_frac": round(busbw / (7 * XGMI_LINK_DIR_GBPS), 4)}
+            "xgmi_frac": round(busbw / (max(1, world - 1) * XGMI_LINK_DIR_GBPS), 4)}
+
+
+def roofline_xgmi(extras: dict, world: int) -> dict | None:
+    """The N > 1 xGMI roofline (north_star's >= 80 % target): the
+    BASELINE config-4 arm (8-rank-grid Swing BO, 1 GiB of real bf16 per GPU, all
+    links), the faster of its RCCL and peer-window transports, busbw over the
+    GPU's egress = (p - 1) links x the MEASURED per-direction link rate
+    (link_probe), with the spec rate (76.8 GB/s per direction) beside it."""
+    arms = {k: v for k, v in extras.items() if "config4_swing_bo_1GiB_all_links" in k and isinstance(v, dict)
+            and "busbw_GBps" in v}
+    if not arms or world < 2:
+        return None
+    name = max(arms, key=lambda k: arms[k]["busbw_GBps"])
+    bus = arms[name]["busbw_GBps"]
+    probe = extras.get("link_probe", {})
+    link = probe.get("GBps_per_direction") if isinstance(probe, dict) else None
+    peak_spec = (world - 1) * XGMI_LINK_DIR_GBPS
+    peak = (world - 1) * link if link else peak_spec
+    return {"bound": "xgmi", "achieved": bus, "peak": round(peak, 2), "unit": "GB/s", "frac": round(bus / peak, 4),
+            "traffic": None, "arm": name, "bytes_per_gpu": 1 << 30, "links": world - 1,
+            "peak_source": "measured link_probe" if link else "spec (no RCCL link probe: --share-gpu)",
+            "peak_spec": peak_spec, "frac_spec": round(bus / peak_spec, 4),
+            "achieved_def": "busbw = 2(p-1)/p * bytes_per_gpu / t"}
 
 
 def link_probe(rank, world, dev) -> dict:
@@ -434,7 +477,10 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
         n = nbytes // 2
         d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
                          channels=chans)
-        b2 = torch.zeros((local, n), dtype=torch.int16, device=dev)
+        b2 = torch.empty((local, n), dtype=torch.int16, device=dev)   # real data: uniform [0,100) bf16
+        g = torch.Generator(device=dev).manual_seed(4000 + 17 * len(out) + torch.distributed.get_rank())
+        for r in range(local):
+            b2[r].copy_((torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16).view(torch.int16))
         w2 = torch.empty(max(16, t.dist_workspace_bytes(d2)), dtype=torch.uint8, device=dev)
         if variant != t.MEM and comm is not None:
             ms = timed_max(lambda: t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
@@ -489,8 +535,6 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
     #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
-    #   peer_hier_ws  the same step pipelined per tile: rank-row stores overlap the
-    #                 local pass's loads, one LL wave per workgroup (k_hier_ws)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -511,7 +555,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         else:
             if mode[0] != kind:
                 peer.set_oneshot_max(0 if kind == "peer_launches" else (4 << 20))
-                peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_ws": 2}.get(kind, 0))
+                peer.set_hier_ll(1 if kind == "peer_hier_ll" else 0)
                 mode[0] = kind
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
@@ -526,8 +570,6 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         ref = small.clone()
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
-        # (peer_hier_ws, the pipelined form, is not a candidate: 27-38 us at W = 1 vs
-        # 18 us for peer_hier_ll; tests/test_gpu_peer.py keeps it exact)
         for kind in ("peer_swing", "peer_hier", "peer_hier_ll"):
             x = small.clone()
             note(rank, f"verify: {kind}")
@@ -587,6 +629,30 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
     dist.all_reduce(ms, op=dist.ReduceOp.MAX)
     ms_per_step = ms.item() / args.steps
+    peer_timeout = False
+    if transport != "rccl" and peer is not None:
+        # a timed-out peer wait means wrong bytes: such a number is never the headline
+        st0 = torch.tensor([peer.status() & t.PEER_TIMEOUT], dtype=torch.int64)
+        dist.all_reduce(st0, op=dist.ReduceOp.MAX)
+        peer_timeout = bool(st0.item())
+        if peer_timeout:
+            if comm is None:
+                raise RuntimeError(f"peer transport {transport} timed out during the timed steps: no valid number")
+            note(rank, f"{transport} timed out in the timed loop: timing the RCCL transport instead")
+            transport = "rccl"
+            for i in range(args.warmup):
+                step(i)
+            torch.cuda.synchronize()
+            dist.barrier()
+            e0.record(stream)
+            for i in range(args.steps):
+                step(i)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            dist.barrier()
+            ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
+            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+            ms_per_step = ms.item() / args.steps
     if peer is not None:   # defaults again for the extras below
         peer.set_oneshot_max(4 << 20)
         peer.set_hier_ll(0)
@@ -603,7 +669,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     torch.cuda.synchronize()
     local_ms = e0.elapsed_time(e1) / args.steps
 
-    extras = {"headline_transport": transport, "peer_verified": verify, "transport_quick_ms": quick}
+    extras = {"headline_transport": transport, "peer_verified": verify, "transport_quick_ms": quick,
+              "peer_timeout_in_timed_loop": peer_timeout}
     if peer_err:
         extras["peer_error"] = peer_err
     if args.extras:
@@ -614,7 +681,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
                 mb = extras["link_probe"]["GBps_per_direction"]
                 for v in extras.values():  # the fraction again against the MEASURED link rate
                     if isinstance(v, dict) and "busbw_GBps" in v:
-                        v["xgmi_frac_measured_link"] = round(v["busbw_GBps"] / (7 * mb), 4)
+                        v["xgmi_frac_measured_link"] = round(v["busbw_GBps"] / ((world - 1) * mb), 4)
             except Exception as e:  # reported, never silently dropped
                 extras["link_probe"] = {"error": repr(e)}
     if peer is not None:
@@ -629,12 +696,12 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         return None
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_ws": "k_hier_ws"}
+    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll"}
     if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
         roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
     else:
-        roof = {"kernel": "k_tree_lds_pipe<64, 1, 32, false> + k_broadcast (local phases)",
+        roof = {"kernel": "k_tree_lds_pipe<64, false> + k_broadcast (local phases)",
                 "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9}
     achieved = roof["achieved"]
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
@@ -643,9 +710,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
            "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "
                         "windows, broadcast (per-tile flags)",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
-                           "(data+epoch words) into peer-mapped xGMI windows, broadcast",
-           "peer_hier_ws": "ONE kernel, pipelined per tile: on-GPU tree reduce overlapped with the rank-row "
-                           "stores, mem_2D one-shot across GPUs by one LL-push wave per workgroup"}[transport]
+                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     return {
         "metric": METRIC,
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
@@ -667,6 +732,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": roof["kernel"],
                      "algorithmic_bytes_per_launch": roof["algorithmic_bytes_per_launch"],
                      "local_phases_ms": round(local_ms, 6)},
+        "roofline_xgmi": roofline_xgmi(extras, world),
         "xgmi": extras,
         "host_wall_s": round(wall, 6),
     }
@@ -684,6 +750,8 @@ def main():
                     help="untimed sustained load before the warmup steps (steady clocks); 0 = none")
     ap.add_argument("--sets", type=int, default=32, help="rotating bucket sets (1.3 GB per GPU: far past the 256 MiB MALL)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph capture")
+    ap.add_argument("--reps", type=int, default=5,
+                    help="N = 1: back-to-back replays of the K timed steps; ms_per_step = median replay / K")
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     ap.add_argument("--no-extras", dest="extras", action="store_false")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")

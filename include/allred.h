@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ALLRED_ABI_VERSION 1
+#define ALLRED_ABI_VERSION 2
 
 /* ---- status codes ---------------------------------------------------- */
 #define ALLRED_OK 0
@@ -46,8 +46,12 @@ extern "C" {
 #define ALLRED_LO 1
 #define ALLRED_MEM 2
 /* execution form of a virtual-rank plan */
-#define ALLRED_EXEC_STEPS 0  /* one launch per schedule step (the reference's step structure) */
-#define ALLRED_EXEC_FUSED 1  /* one launch for the whole allreduce, same arithmetic */
+#define ALLRED_EXEC_STEPS 0  /* the reference's step structure: every step's result stored to the buckets */
+#define ALLRED_EXEC_FUSED 1  /* one HBM pass for the whole allreduce, same arithmetic, same bits */
+/* mem_2D accumulation (allred_mem_2D/kernels/compute_kernel.cpp:44-67) */
+#define ALLRED_ACC_FP32 0    /* fp32 sum, rounded to bf16 once (default) */
+#define ALLRED_ACC_BF16 1    /* the reference's bf16 dest register (fp32_dest_acc_en = false,
+                                allred_helper.cpp:331-335): every add rounded to bf16 */
 
 #define ALLRED_MAX_NODES 64
 #define ALLRED_MAX_STEPS 6
@@ -165,6 +169,7 @@ typedef struct {
     int32_t total_nodes;   /* 0 = side*side                                     */
     int32_t device;        /* HIP device ordinal (-1 = current)                 */
     uint64_t elems_per_rank; /* bf16 elements; BO/MEM need a multiple of 8*total, LO of 8 */
+    int32_t mem_accum;     /* MEM only: ALLRED_ACC_FP32 (default) / ALLRED_ACC_BF16 */
 } allred_plan_desc;
 int allred_plan_create(const allred_plan_desc* desc, allred_plan** out);
 /* HBM layout helper: the rank stride (elements) this engine lays virtual ranks
@@ -179,6 +184,38 @@ int allred_plan_execute(allred_plan* plan, uint16_t* ranks, uint64_t rank_stride
                         void* workspace, void* stream);
 /* number of kernel launches one execute enqueues (for per-launch accounting) */
 int allred_plan_launches(const allred_plan* plan);
+/* Device-side profiling of the schedule form (the reference's DeviceZoneScopedN
+ * "ALL_RED_LOOP", allred_BO_2D/kernels/dataflow_kernel.cpp:147, dumped by
+ * DumpDeviceProfileResults, allred_helper.hpp:88).  stamp_words: the uint64
+ * words of device memory execute_profiled writes (0: this plan's form has no
+ * stamps — only ALLRED_EXEC_STEPS BO / LO do).  rank_zones: from the stamps
+ * copied to the host, each rank's zone start / end (s_memrealtime, 100 MHz):
+ * start = its first load, end = the end of the step of its last store. */
+uint64_t allred_plan_stamp_words(const allred_plan* plan);
+int allred_plan_execute_profiled(allred_plan* plan, uint16_t* ranks, uint64_t rank_stride, void* workspace,
+                                 uint64_t* device_stamps, void* stream);
+int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps, uint64_t* zone_start /*[total]*/,
+                           uint64_t* zone_end /*[total]*/);
+
+/* ======================================================================
+ * Tuning: the one entry point for switching between kernel forms that give
+ * bit-identical results (A/B measurements).  The defaults are the measured
+ * product forms; nothing needs setting.  Initial values may come from
+ * ALLRED_TUNE="key=value,key=value" (read once at load).  Keys:
+ *   fused_form        0 auto | 1 register tree | 2 one tile per workgroup | 3 persistent pipe
+ *   lo_tree           1: fused LO of rank-uniform schedules through the BO tree pass
+ *   lo_dag            1: fused 64-rank LO as the DAG of distinct sums (0 = per-rank butterfly)
+ *   lo_dag_place      1: bank-conflict-free DAG placement (0 = first-appearance order)
+ *   lo_dag_min_tiles  256: smallest bucket (256-element tiles) for the DAG pass
+ *   mem_reduce_lds    1: mem_2D schedule-form reduce staged through LDS
+ *   steps_form        0: schedule form as one persistent launch | 1: one launch per step
+ *   pipe_grid         0: auto grid of the persistent passes
+ * Plans read the keys when they are created (lo_*, steps_form) or launched.
+ * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
+ * counterpart (the reference picks its kernel directory by string,
+ * allred_BO_2D.cpp:203-211). */
+int allred_tune_set(const char* key, int64_t value);
+int allred_tune_get(const char* key, int64_t* value);
 
 /* ======================================================================
  * Reference program surface: AllredConfig (allred_helper.hpp:47-97) +
@@ -196,9 +233,12 @@ typedef struct {
     int32_t print_core;      /* argv[7]                                          */
     int32_t bandwidth_optimal; /* argv[8]                                        */
     int32_t total_nodes;     /* extension (ALLRED_NODES env / argv[9]); 0 = side^2 */
-    int32_t exec;            /* extension (ALLRED_EXEC env): steps (default) / fused */
+    int32_t exec;            /* extension (ALLRED_EXEC env): fused (default) / steps */
     int32_t round_mode;      /* extension (ALLRED_BF16_ROUND env): 0 trunc, 1 rne */
     int32_t num_tiles;       /* derived: normalised NUM_TILES                    */
+    int32_t device;          /* HIP device ordinal, -1 = current (ALLRED_DEVICE env); the
+                                reference's CreateDevice(0) / IDevice*, allred_BO_2D.cpp:8 */
+    int32_t mem_accum;       /* extension (ALLRED_MEM_ACC=bf16): ALLRED_ACC_FP32 / ALLRED_ACC_BF16 */
 } allred_args;
 /* Parses argv exactly like AllredConfig's ctor (std::stoi semantics: leading
  * integer, junk -> ALLRED_ERR_ARG where the reference would throw).          */
@@ -214,7 +254,10 @@ typedef struct {
     int32_t launches;
 } allred_report;
 /* Generate inputs, H2D, run (if run_kernel), D2H of print_core, validate
- * (printing like the reference when verbose), report timing.               */
+ * (printing like the reference when verbose), report timing, on args->device.
+ * ALLRED_PROFILE_LOG=<path> also writes every rank's ALL_RED_LOOP zone in the
+ * layout of tt-metal's profile_log_device.csv (the reference's
+ * TT_METAL_DEVICE_PROFILER=1 run, python/timing_taker.py:60-65).            */
 int allred_run(const allred_args* args, int verbose, allred_report* report);
 
 /* ======================================================================
@@ -247,6 +290,13 @@ size_t allred_dist_workspace_bytes(const allred_dist_desc* desc);
 int allred_dist_allreduce(allred_comm* comm, const allred_dist_desc* desc, uint16_t* buf,
                           void* workspace, void* stream);
 
+/* The per-rank program allred_dist_allreduce (and its host twin) runs for
+ * `desc`: steps = exchange steps (one RCCL group each), add_launches = add
+ * kernels it enqueues over all steps (one per reduce-scatter / LO step,
+ * whatever the channel count), segments = send + receive segments.  Programs
+ * are built once per (desc, rank) and cached. */
+int allred_dist_program_stats(const allred_dist_desc* desc, int rank, int* steps, int* add_launches, int* segments);
+
 /* Host-memory twin of allred_dist_allreduce for CPU tests and loopback
  * checks: the same per-rank step program, exchanges done by a callback.     */
 typedef struct {
@@ -270,8 +320,15 @@ int allred_dist_allreduce_host(const allred_dist_desc* desc, int rank, uint16_t*
  * Barriers spin with a bound; allred_peer_status() reports bit 0 = timeout,
  * and the WIN/FLAGS_CACHED bits when uncached (fine-grained) device memory
  * was unavailable and ordinary hipMalloc memory had to be used instead.
+ * A timed-out call has produced wrong bytes: callers must check the status
+ * (allred_peer_status after the stream, or allred_peer_check) before using
+ * results; the first timeout makes every later wait of that launch give up.
  * ==================================================================== */
 #define ALLRED_PEER_HANDLE_BYTES 192
+/* largest IPC-exported window: a peer's hipIpcOpenMemHandle of a ~2 GiB
+ * allocation never returned on the MI355X boxes (profiles/r01_peer_open_probe_2gib_hang.txt),
+ * so allred_peer_create rejects max_elems * 2 > 1 GiB (ALLRED_ERR_ARG) */
+#define ALLRED_PEER_MAX_WINDOW_BYTES (1ull << 30)
 #define ALLRED_PEER_TIMEOUT 0x1u
 #define ALLRED_PEER_WIN_CACHED 0x100u
 #define ALLRED_PEER_FLAGS_CACHED 0x200u
@@ -289,7 +346,7 @@ int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int 
  * barrier / all-gather launches.  Same result bits either way.  Every rank
  * must use the same setting. */
 int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
-/* enable = 1 or 2: with local_ranks == 64 and nranks <= 8, allred_peer_allreduce
+/* enable = 1: with local_ranks == 64 and nranks <= 8, allred_peer_allreduce
  * runs the hierarchical step as one kernel with LL hand-offs (each cross-GPU
  * transfer a push of self-validating 8-byte data+epoch words into the
  * consumer's own memory; no flags, no remote reads) for buckets of up to
@@ -297,9 +354,8 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * (allred_mem_2D semantics over the per-GPU trees).  Every rank must use the
  * same setting.  Replaces nothing in the reference (its mem_2D phases sync
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
-/* enable = 2 runs the same step pipelined per tile (k_hier_ws): the local
- * pass's loads and the rank-row stores overlap, and one specialised wave per
- * workgroup carries the cross-GPU hand-offs; same result bits.  0 = off. */
+/* 0 = off.  (The pipelined specialised-wave form of round 1 lives in
+ * tools/ubench/ws_trace.hip: 27-38 us vs 18 at W = 1, never a candidate.) */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
 /* Caps the grid of the hierarchical one-kernel forms at `groups` workgroups
  * (0 = default: 512, two per CU, the whole grid resident on a GPU of its own).
@@ -331,6 +387,9 @@ int allred_peer_set_mem_ll_max(allred_peer* peer, uint64_t bytes);
 int allred_peer_dist_allreduce(allred_peer* peer, const allred_dist_desc* desc, uint16_t* buf, void* workspace,
                                void* stream);
 int allred_peer_status(allred_peer* peer, uint32_t* status);
+/* Synchronises `stream` and returns ALLRED_ERR_TRANSPORT if any call so far
+ * timed out (ALLRED_PEER_TIMEOUT), else ALLRED_OK. */
+int allred_peer_check(allred_peer* peer, void* stream);
 int allred_peer_destroy(allred_peer* peer);
 
 #ifdef __cplusplus

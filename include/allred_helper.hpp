@@ -6,8 +6,10 @@
 // schedule code written against the reference compile unchanged.  The
 // tt-metal-typed parts (CreateComputeKernel / CreateDataflowKernel, the
 // IDevice / CommandQueue / Program ctor of AllredConfig) have no MI355X
-// meaning: AllredConfig takes (argc, argv, device ordinal, SIDE_LENGTH,
-// large_buffer) and RunProgram() runs the HIP engine (see include/allred.h).
+// meaning: AllredConfig takes (argc, argv, variant, device ordinal) — the
+// variant stands for the calling main (allred_BO_2D / _LO_2D / _mem_2D, whose
+// large_buffer flag it implies), the ordinal for the IDevice* — and
+// RunProgram() runs the HIP engine on that device (see include/allred.h).
 // Everything is a thin inline layer over liballred.so's C-ABI.
 #pragma once
 
@@ -84,10 +86,13 @@ public:
 
     // allred_helper.cpp:194-289 (argv parsing, NUM_TILES normalisation, inputs).
     // `variant`: ALLRED_BO for allred_BO_2D (arg 8 picks BO/LO), ALLRED_LO,
-    // ALLRED_MEM (large_buffer = true in allred_mem_2D.cpp:15).
-    AllredConfig(int argc, char** argv, int variant) {
+    // ALLRED_MEM (large_buffer = true in allred_mem_2D.cpp:15).  `device`: the
+    // HIP device ordinal the program runs on (the reference's IDevice*,
+    // allred_helper.hpp:75-82); -1 = ALLRED_DEVICE or the current device.
+    AllredConfig(int argc, char** argv, int variant, int device = -1) {
         status = allred_args_parse(argc, const_cast<const char* const*>(argv), variant, &args);
         if (status != ALLRED_OK) return;
+        if (device >= 0) args.device = device;
         SWING_VERSION = args.swing != 0;
         RUN_KERNEL = args.run_kernel != 0;
         RND_SRC = args.seed;

@@ -320,21 +320,30 @@ int or_allreduce_lo(const or_schedule* s, uint16_t** ranks, size_t n) {
  * the other ranks' copies of block b in rank order; the accumulation is kept
  * in fp32 and rounded once (the MI355X design).  Then every
  * rank reads the whole reduced vector back. */
-int or_allreduce_mem(int N, uint16_t** ranks, size_t n) {
+/* acc16 = 1: the reference's own accumulation register instead — the Tensix
+ * dest holds bf16 (fp32_dest_acc_en = false, allred_helper.cpp:331-335), so
+ * every binary_dest_reuse_tiles add (allred_mem_2D/kernels/compute_kernel.cpp:51-60)
+ * rounds the running sum to bf16 (nearest even here, like every other add). */
+int or_allreduce_mem_acc(int N, uint16_t** ranks, size_t n, int acc16) {
     if (n % (size_t)N) return -1;
     size_t blk = n / (size_t)N;
     uint16_t* dst = (uint16_t*)malloc(n * 2);
     for (int b = 0; b < N; ++b)
         for (size_t e = b * blk; e < (b + 1) * blk; ++e) {
             volatile float acc = or_bf16_to_float(ranks[b][e]);
-            for (int r = 0; r < N; ++r)
-                if (r != b) acc = acc + or_bf16_to_float(ranks[r][e]);
+            for (int r = 0; r < N; ++r) {
+                if (r == b) continue;
+                acc = acc + or_bf16_to_float(ranks[r][e]);
+                if (acc16) acc = or_bf16_to_float(or_bf16_rne(acc));
+            }
             dst[e] = or_bf16_rne(acc);
         }
     for (int r = 0; r < N; ++r) memcpy(ranks[r], dst, n * 2);
     free(dst);
     return 0;
 }
+
+int or_allreduce_mem(int N, uint16_t** ranks, size_t n) { return or_allreduce_mem_acc(N, ranks, n, 0); }
 
 /* ===================================================================== */
 /* validation (allred_helper.cpp:18-120)                                  */

@@ -50,6 +50,7 @@ _o.or_step_directions.argtypes = [C.c_int, C.c_int]
 for f in ("or_allreduce_bo", "or_allreduce_lo"):
     getattr(_o, f).argtypes = [C.POINTER(Schedule), C.POINTER(C.c_void_p), C.c_size_t]
 _o.or_allreduce_mem.argtypes = [C.c_int, C.POINTER(C.c_void_p), C.c_size_t]
+_o.or_allreduce_mem_acc.argtypes = [C.c_int, C.POINTER(C.c_void_p), C.c_size_t, C.c_int]
 _o.or_validate.restype = C.c_long
 _o.or_validate.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_float, C.c_uint32, C.c_int,
                            C.POINTER(C.c_float)]
@@ -96,12 +97,14 @@ def _ptrs(ranks):
     return (C.c_void_p * len(ranks))(*[r.ctypes.data for r in ranks])
 
 
-def allreduce(variant: str, swing: int, side: int, ranks: list[np.ndarray], total: int | None = None) -> None:
-    """In-place allreduce of uint16 bf16 rank vectors: variant bo | lo | mem."""
+def allreduce(variant: str, swing: int, side: int, ranks: list[np.ndarray], total: int | None = None,
+              acc16: bool = False) -> None:
+    """In-place allreduce of uint16 bf16 rank vectors: variant bo | lo | mem
+    (acc16: mem with the reference's bf16 accumulation, every add rounded)."""
     total = len(ranks) if total is None else total
     n = ranks[0].size
     if variant == "mem":
-        st = _o.or_allreduce_mem(total, _ptrs(ranks), n)
+        st = _o.or_allreduce_mem_acc(total, _ptrs(ranks), n, int(acc16))
     else:
         rc, s = schedule(swing, side, total)
         assert rc == 0, "invalid grid"

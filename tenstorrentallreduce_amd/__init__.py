@@ -17,8 +17,8 @@ from typing import Callable, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, RECDUB, RECDUB_1D, SWING, SWING_1D, AllredError, Args, DistDesc,  # noqa: F401
-                   PlanDesc, Report, Schedule, Seg, check, lib)
+from ._lib import (ACC_BF16, ACC_FP32, BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, RECDUB, RECDUB_1D, SWING, SWING_1D,  # noqa: F401
+                   AllredError, Args, DistDesc, PlanDesc, Report, Schedule, Seg, check, lib)
 
 __all__ = [
     "BO", "LO", "MEM", "SWING", "RECDUB", "SWING_1D", "RECDUB_1D", "get_comm_partner_swing_1D",
@@ -27,8 +27,36 @@ __all__ = [
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
     "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
-    "dist_allreduce_host", "dist_workspace_bytes", "Peer",
+    "dist_allreduce_host", "dist_workspace_bytes", "dist_program_stats", "Peer", "tune", "tuned", "ACC_FP32",
+    "ACC_BF16",
 ]
+
+
+# ---------------------------------------------------------------- tuning
+def tune(key: str, value: int | None = None) -> int:
+    """allred_tune_set / allred_tune_get: switch between bit-identical kernel
+    forms (A/B); returns the previous value.  Keys: allred.h §Tuning."""
+    old = C.c_int64(0)
+    check(lib.allred_tune_get(key.encode(), C.byref(old)), f"tune_get({key})")
+    if value is not None:
+        check(lib.allred_tune_set(key.encode(), int(value)), f"tune_set({key}={value})")
+    return old.value
+
+
+class tuned:
+    """with tuned(key=value, ...): the keys set for the block, restored after."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = tune(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            tune(k, v)
 
 
 # ---------------------------------------------------------------- schedule
@@ -153,11 +181,13 @@ def preferred_rank_stride(elems: int) -> int:
 
 
 class Plan:
-    """N virtual ranks in one GPU's HBM (allred_plan_*)."""
+    """N virtual ranks in one GPU's HBM (allred_plan_*).  exec_mode: EXEC_FUSED
+    (default, one HBM pass) or EXEC_STEPS (the reference's step structure);
+    mem_accum (MEM): ACC_FP32 or ACC_BF16 (the reference's bf16 dest)."""
 
     def __init__(self, algo: int, variant: int, side: int, elems_per_rank: int, total: int = 0,
-                 exec_mode: int = EXEC_STEPS, device: int = -1):
-        d = PlanDesc(algo, variant, exec_mode, side, total, device, elems_per_rank)
+                 exec_mode: int = EXEC_FUSED, device: int = -1, mem_accum: int = ACC_FP32):
+        d = PlanDesc(algo, variant, exec_mode, side, total, device, elems_per_rank, mem_accum)
         h = C.c_void_p()
         check(lib.allred_plan_create(C.byref(d), C.byref(h)), "plan_create")
         self._h = h
@@ -165,10 +195,21 @@ class Plan:
         self.elems = elems_per_rank
         self.workspace_bytes = lib.allred_plan_workspace_bytes(h)
         self.launches = lib.allred_plan_launches(h)
+        self.stamp_words = lib.allred_plan_stamp_words(h)
 
-    def execute(self, ranks_ptr: int, stride: int, workspace_ptr: int | None = None, stream=None) -> None:
-        check(lib.allred_plan_execute(self._h, ranks_ptr, stride, workspace_ptr, _stream_ptr(stream)),
-              "plan_execute")
+    def execute(self, ranks_ptr: int, stride: int, workspace_ptr: int | None = None, stream=None,
+                stamps_ptr: int | None = None) -> None:
+        """stamps_ptr: device memory of stamp_words uint64 (schedule form only)."""
+        check(lib.allred_plan_execute_profiled(self._h, ranks_ptr, stride, workspace_ptr, stamps_ptr,
+                                               _stream_ptr(stream)), "plan_execute")
+
+    def rank_zones(self, stamps: np.ndarray):
+        """Per-rank ALL_RED_LOOP (start, end) in 100 MHz ticks from host stamps."""
+        st = np.ascontiguousarray(stamps, dtype=np.uint64)
+        zs = np.zeros(self.total, dtype=np.uint64)
+        ze = np.zeros(self.total, dtype=np.uint64)
+        check(lib.allred_plan_rank_zones(self._h, st.ctypes.data, zs.ctypes.data, ze.ctypes.data), "plan_rank_zones")
+        return zs, ze
 
     def close(self):
         if self._h:
@@ -240,6 +281,13 @@ def dist_workspace_bytes(desc: DistDesc) -> int:
     return lib.allred_dist_workspace_bytes(C.byref(desc))
 
 
+def dist_program_stats(desc: DistDesc, rank: int) -> dict:
+    """The cached per-rank program: exchange steps, add launches, send+recv segments."""
+    k, a, g = C.c_int(0), C.c_int(0), C.c_int(0)
+    check(lib.allred_dist_program_stats(C.byref(desc), rank, C.byref(k), C.byref(a), C.byref(g)), "dist_program_stats")
+    return {"steps": k.value, "add_launches": a.value, "segments": g.value}
+
+
 def dist_allreduce(comm: Comm, desc: DistDesc, buf_ptr: int, workspace_ptr: int, stream=None) -> None:
     check(lib.allred_dist_allreduce(comm._h, C.byref(desc), buf_ptr, workspace_ptr, _stream_ptr(stream)),
           "dist_allreduce")
@@ -296,23 +344,34 @@ class Peer:
         check(lib.allred_peer_connect(self._h, arr), "peer_connect")
 
     def allreduce(self, buf_ptr: int, elems: int, stream=None, local_ranks: int = 1, local_side: int = 1,
-                  local_algo: int = SWING, workspace_ptr: int | None = None) -> None:
+                  local_algo: int = SWING, workspace_ptr: int | None = None, check_status: bool = False) -> None:
+        """check_status: synchronise the stream and raise AllredError(ERR_TRANSPORT)
+        if a peer wait timed out (the bytes are then wrong).  Without it the
+        caller must call check() (or status()) before using the result."""
         check(lib.allred_peer_allreduce(self._h, buf_ptr, elems, local_ranks, local_side, local_algo, workspace_ptr,
                                         _stream_ptr(stream)), "peer_allreduce")
+        if check_status:
+            self.check(stream)
 
-    def dist_allreduce(self, desc: DistDesc, buf_ptr: int, workspace_ptr: int | None = None, stream=None) -> None:
+    def dist_allreduce(self, desc: DistDesc, buf_ptr: int, workspace_ptr: int | None = None, stream=None,
+                       check_status: bool = False) -> None:
         """dist_allreduce's program (same desc, same bits) over the peer windows."""
         check(lib.allred_peer_dist_allreduce(self._h, C.byref(desc), buf_ptr, workspace_ptr, _stream_ptr(stream)),
               "peer_dist_allreduce")
+        if check_status:
+            self.check(stream)
+
+    def check(self, stream=None) -> None:
+        """allred_peer_check: sync `stream`, raise if any call so far timed out."""
+        check(lib.allred_peer_check(self._h, _stream_ptr(stream)), "peer timeout (a peer never arrived)")
 
     def set_oneshot_max(self, nbytes: int) -> None:
         """Buckets of at most nbytes run as one kernel (same bits either way)."""
         check(lib.allred_peer_set_oneshot_max(self._h, nbytes), "peer_set_oneshot_max")
 
     def set_hier_ll(self, mode) -> None:
-        """64 local ranks: the hierarchical step with LL push hand-offs — 1 (or True)
-        phased (k_hier_ll), 2 pipelined per tile on specialised waves (k_hier_ws),
-        0 (or False) off.  Same result bits in every mode."""
+        """64 local ranks: the hierarchical step with LL push hand-offs (k_hier_ll)
+        — 1 (or True) on, 0 (or False) off.  Same result bits either way."""
         check(lib.allred_peer_set_hier_ll(self._h, int(mode)), "peer_set_hier_ll")
 
     def set_lo_ll_max(self, nbytes: int) -> None:

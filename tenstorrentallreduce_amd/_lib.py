@@ -36,6 +36,8 @@ OK, ERR_ARG, ERR_SCHEDULE, ERR_HIP, ERR_RCCL, ERR_NOMEM, ERR_UNSUPPORTED, ERR_TR
 RECDUB, SWING, RECDUB_1D, SWING_1D = 0, 1, 2, 3
 BO, LO, MEM = 0, 1, 2
 EXEC_STEPS, EXEC_FUSED = 0, 1
+ACC_FP32, ACC_BF16 = 0, 1
+ABI_VERSION = 2
 MAX_NODES, MAX_STEPS = 64, 6
 UNIQUE_ID_BYTES = 128
 
@@ -68,13 +70,14 @@ class PlanDesc(C.Structure):
     _fields_ = [
         ("algo", C.c_int32), ("variant", C.c_int32), ("exec", C.c_int32), ("side_length", C.c_int32),
         ("total_nodes", C.c_int32), ("device", C.c_int32), ("elems_per_rank", C.c_uint64),
+        ("mem_accum", C.c_int32),
     ]
 
 
 class Args(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "variant", "swing", "run_kernel", "side_length", "seed", "tiles", "error", "print_core",
-        "bandwidth_optimal", "total_nodes", "exec", "round_mode", "num_tiles")]
+        "bandwidth_optimal", "total_nodes", "exec", "round_mode", "num_tiles", "device", "mem_accum")]
 
 
 class Report(C.Structure):
@@ -133,6 +136,11 @@ SIGNATURES = [
     ("allred_plan_workspace_bytes", C.c_size_t, [_P]),
     ("allred_plan_execute", C.c_int, [_P, _u16p, C.c_uint64, _P, _P]),
     ("allred_plan_launches", C.c_int, [_P]),
+    ("allred_plan_stamp_words", C.c_uint64, [_P]),
+    ("allred_plan_execute_profiled", C.c_int, [_P, _u16p, C.c_uint64, _P, _P, _P]),
+    ("allred_plan_rank_zones", C.c_int, [_P, _P, _P, _P]),
+    ("allred_tune_set", C.c_int, [C.c_char_p, C.c_int64]),
+    ("allred_tune_get", C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
     ("allred_args_parse", C.c_int, [C.c_int, C.POINTER(C.c_char_p), C.c_int, C.POINTER(Args)]),
     ("allred_run", C.c_int, [C.POINTER(Args), C.c_int, C.POINTER(Report)]),
     ("allred_comm_get_unique_id", C.c_int, [_P]),
@@ -140,6 +148,8 @@ SIGNATURES = [
     ("allred_comm_destroy", C.c_int, [_P]),
     ("allred_dist_workspace_bytes", C.c_size_t, [C.POINTER(DistDesc)]),
     ("allred_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
+    ("allred_dist_program_stats", C.c_int,
+     [C.POINTER(DistDesc), C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("allred_dist_allreduce_host", C.c_int, [C.POINTER(DistDesc), C.c_int, _u16p, _u16p, EXCHANGE_FN, _P]),
     ("allred_peer_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, C.POINTER(_P)]),
     ("allred_peer_handle", C.c_int, [_P, _P]),
@@ -152,14 +162,19 @@ SIGNATURES = [
     ("allred_peer_set_mem_ll_max", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    ("allred_peer_check", C.c_int, [_P, _P]),
     ("allred_peer_destroy", C.c_int, [_P]),
 ]
 PEER_HANDLE_BYTES = 192
+PEER_MAX_WINDOW_BYTES = 1 << 30   # allred_peer_create rejects larger windows (allred.h)
 PEER_TIMEOUT, PEER_WIN_CACHED, PEER_FLAGS_CACHED = 0x1, 0x100, 0x200   # allred_peer_status bits
 
-for _name, _res, _args in SIGNATURES:
+for _name, _res, _args in SIGNATURES:  # noqa: E305
     if "ALLRED_LIB_PATH" in os.environ and not hasattr(lib, _name):
         continue  # an older build under A/B may predate a later entry point
     _f = getattr(lib, _name)  # AttributeError here = the library lacks a declared symbol
     _f.restype = _res
     _f.argtypes = _args
+
+if "ALLRED_LIB_PATH" not in os.environ and lib.allred_abi_version() != ABI_VERSION:
+    raise ImportError(f"{LIB_PATH}: ABI {lib.allred_abi_version()}, this package expects {ABI_VERSION}: rebuild it")

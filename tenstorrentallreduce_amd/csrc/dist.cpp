@@ -10,14 +10,19 @@
 //   LO (shouldSendBlock with bandwidth_optimal = 0, :19-29): full-vector
 //     exchange + add every step.
 // A step's blocks go out as one ncclSend/ncclRecv per contiguous run of set
-// bits, inside one ncclGroupStart/End, on the caller's stream; the add is the
-// HIP kernel of kernels.hip on the same stream.  The identical program also
+// bits, inside one ncclGroupStart/End, on the caller's stream; the add of every
+// received run of every channel is ONE HIP kernel launch (k_add_segs) on the
+// same stream.  A rank's program is built once per (desc, rank) and cached
+// (the 2-128 kB latency regime of BASELINE config 5 pays no host rebuild per
+// call).  The identical program also
 // runs on host memory with a caller-supplied exchange (allred_dist_allreduce_host)
 // so CPU tests (gloo) cover every step of it.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -48,9 +53,11 @@ struct Exch {
     size_t base = 0;                // channel slice start (elements)
 };
 
-// A step = the exchanges of every channel, issued as one RCCL group.
+// A step = the exchanges of every channel, issued as one RCCL group, then one
+// add launch over every received segment (elements) of every channel.
 struct Step {
     std::vector<Exch> ex;
+    std::vector<uint64_t> add_off, add_len;
 };
 
 void runs(uint64_t mask, int total, size_t blk, size_t base, std::vector<Seg>* out) {
@@ -149,6 +156,8 @@ std::vector<Step> program(const allred_schedule& s, int rank, int variant, size_
                 e.add = true;
                 e.base = base;
                 e.blk = len;
+                st.add_off.push_back(base);
+                st.add_len.push_back(len);
                 st.ex.push_back(e);
             }
             prog.push_back(st);
@@ -169,6 +178,10 @@ std::vector<Step> program(const allred_schedule& s, int rank, int variant, size_
             runs(s.send[x][k], N, e.blk, base, &e.send);
             runs(s.recv[x][k], N, e.blk, base, &e.recv);
             e.add = true;
+            for (const Seg& g : e.recv) {
+                st.add_off.push_back(g.off);
+                st.add_len.push_back(g.len);
+            }
             st.ex.push_back(e);
         }
         prog.push_back(st);
@@ -193,6 +206,25 @@ std::vector<Step> program(const allred_schedule& s, int rank, int variant, size_
     }
     return prog;
 }
+
+// the rank's program for desc, built once and cached (key: every desc field that
+// shapes it, the channel count actually used, the rank)
+using ProgKey = std::tuple<int, int, int, int, uint64_t, int, int>;
+std::mutex g_prog_mu;
+std::map<ProgKey, std::shared_ptr<const std::vector<Step>>> g_progs;
+
+std::shared_ptr<const std::vector<Step>> cached_program(const allred_dist_desc* d, const allred_schedule& s, int rank,
+                                                        int C) {
+    const ProgKey key{d->algo, d->variant, d->side_length, d->total_nodes, d->elems, C, rank};
+    std::lock_guard<std::mutex> g(g_prog_mu);
+    auto it = g_progs.find(key);
+    if (it == g_progs.end())
+        it = g_progs.emplace(key, std::make_shared<const std::vector<Step>>(
+                                      program(s, rank, d->variant, (size_t)d->elems, C))).first;
+    return it->second;
+}
+
+int add_launches(const Step& st) { return ((int)st.add_off.size() + kMaxAddSegs - 1) / kMaxAddSegs; }
 
 int check_desc(const allred_dist_desc* d, allred_schedule* s) {
     if (!d) return ALLRED_ERR_ARG;
@@ -365,36 +397,46 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
         if (st != ALLRED_OK) return st;
     }
     const int C = channels_for(s, d->channels, n);
-    const std::vector<Step> prog = program(s, c->rank, d->variant, n, C);
-    for (const Step& step : prog) {
+    const auto prog = cached_program(d, s, c->rank, C);
+    for (const Step& step : *prog) {
         if (ncclGroupStart() != ncclSuccess) return ALLRED_ERR_RCCL;
+        bool ok = true;
         for (const Exch& e : step.ex) {
             for (const Seg& g : e.send)
-                if (ncclSend(bucket + g.off, g.len * 2, ncclUint8, e.peer, c->comm, hs) != ncclSuccess)
-                    return ALLRED_ERR_RCCL;
+                ok = ok && ncclSend(bucket + g.off, g.len * 2, ncclUint8, e.peer, c->comm, hs) == ncclSuccess;
             for (const Seg& g : e.recv)
-                if (ncclRecv((e.recv_to_bucket ? bucket : staging) + g.off, g.len * 2, ncclUint8, e.peer, c->comm,
-                             hs) != ncclSuccess)
-                    return ALLRED_ERR_RCCL;
+                ok = ok && ncclRecv((e.recv_to_bucket ? bucket : staging) + g.off, g.len * 2, ncclUint8, e.peer,
+                                    c->comm, hs) == ncclSuccess;
         }
-        if (ncclGroupEnd() != ncclSuccess) return ALLRED_ERR_RCCL;
-        for (const Exch& e : step.ex) {
-            if (!e.add) continue;
-            if (d->variant == ALLRED_LO) {
-                st = launch_bf16_add(bucket + e.base, staging + e.base, e.blk, stream);
-            } else {
-                uint8_t blocks[ALLRED_MAX_NODES];
-                int nb = 0;
-                for (const Seg& g : e.recv)
-                    for (size_t b = (g.off - e.base) / e.blk; b < (g.off - e.base + g.len) / e.blk; ++b)
-                        blocks[nb++] = (uint8_t)b;
-                st = launch_bf16_add_blocks(bucket + e.base, staging + e.base, blocks, nb, e.blk, stream);
-            }
+        // the group is always closed, also after a failed send / recv, so the
+        // next call does not start inside a dangling group
+        if (ncclGroupEnd() != ncclSuccess || !ok) return ALLRED_ERR_RCCL;
+        for (size_t i = 0; i < step.add_off.size(); i += kMaxAddSegs) {   // one launch per step (<= 64 segments)
+            const int ns = (int)std::min<size_t>(kMaxAddSegs, step.add_off.size() - i);
+            st = launch_bf16_add_segs(bucket, staging, step.add_off.data() + i, step.add_len.data() + i, ns, stream);
             if (st != ALLRED_OK) return st;
         }
     }
     if (d->local_ranks > 1) st = launch_broadcast(buf, n, n, d->local_ranks, bucket, stream);
     return st;
+}
+
+int allred_dist_program_stats(const allred_dist_desc* d, int rank, int* steps, int* launches, int* segments) {
+    allred_schedule s;
+    int st = check_desc(d, &s);
+    if (st != ALLRED_OK) return st;
+    if (rank < 0 || rank >= d->total_nodes) return ALLRED_ERR_ARG;
+    const auto prog = cached_program(d, s, rank, channels_for(s, d->channels, (size_t)d->elems));
+    int k = 0, l = 0, g = 0;
+    for (const Step& step : *prog) {
+        ++k;
+        l += add_launches(step);
+        for (const Exch& e : step.ex) g += (int)(e.send.size() + e.recv.size());
+    }
+    if (steps) *steps = k;
+    if (launches) *launches = l;
+    if (segments) *segments = g;
+    return ALLRED_OK;
 }
 
 int allred_dist_allreduce_host(const allred_dist_desc* d, int rank, uint16_t* buf, uint16_t* scratch,
@@ -414,9 +456,9 @@ int allred_dist_allreduce_host(const allred_dist_desc* d, int rank, uint16_t* bu
         host_tree_reduce(buf, n, n, ls, bucket);
     }
     const int C = channels_for(s, d->channels, n);
-    const std::vector<Step> prog = program(s, rank, d->variant, n, C);
+    const auto prog = cached_program(d, s, rank, C);
     std::vector<allred_seg> snd, rcv;
-    for (const Step& step : prog) {
+    for (const Step& step : *prog) {
         for (const Exch& e : step.ex) {  // channels in order: every channel is a perfect matching
             snd.clear();
             rcv.clear();
@@ -426,9 +468,8 @@ int allred_dist_allreduce_host(const allred_dist_desc* d, int rank, uint16_t* bu
             if (exchange(ctx, e.peer, (int)snd.size(), snd.data(), (int)rcv.size(), rcv.data()) != 0)
                 return ALLRED_ERR_TRANSPORT;
         }
-        for (const Exch& e : step.ex)
-            if (e.add)
-                for (const Seg& g : e.recv) host_add(bucket + g.off, scratch + g.off, g.len);
+        for (size_t i = 0; i < step.add_off.size(); ++i)   // the device path's one add launch per step
+            host_add(bucket + step.add_off[i], scratch + step.add_off[i], step.add_len[i]);
     }
     if (d->local_ranks > 1)
         for (int r = 0; r < d->local_ranks; ++r) std::memcpy(buf + (size_t)r * n, bucket, n * 2);

@@ -8,11 +8,12 @@
 //         allred_LOO_2D/kernels/dataflow_kernel.cpp for NUM_TILES < 64)
 //   MEM = reduce own block from the shared buffer, then read everything back
 //         (allred_mem_2D/kernels/*)
-// ALLRED_EXEC_STEPS keeps the reference's step structure (one launch per
-// schedule step, all ranks at once); ALLRED_EXEC_FUSED does the identical
-// arithmetic in one HBM pass (BO: k_tree*, LO: the butterfly k_butterfly*, or
-// the BO tree pass when every rank's tree is the same (lo_rank_uniform),
-// MEM: k_mem*).
+// ALLRED_EXEC_STEPS keeps the reference's step structure (every step's result
+// stored to the ranks' buckets; BO / LO as one persistent launch of
+// independent (block, column slice) units, k_bo_steps / k_lo_steps; MEM as
+// reduce + broadcast); ALLRED_EXEC_FUSED does the identical arithmetic in one
+// HBM pass (BO: k_tree*, LO: the butterfly k_butterfly*, or the BO tree pass
+// when every rank's tree is the same (lo_rank_uniform), MEM: k_mem*).
 #include <hip/hip_runtime.h>
 
 #include <cerrno>
@@ -20,8 +21,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <random>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -44,6 +47,10 @@ struct allred_plan {
     std::vector<int> blk_per_rank;          // m_k
     uint8_t* d_order = nullptr;
     uint8_t* d_dag = nullptr;               // LO: interned DAG (lo_dag_lanes form), 64 ranks only
+    uint8_t* d_steps_tab = nullptr;         // schedule form, one launch: BO per-block phase ranks / LO step pairs
+    uint8_t* d_partner8 = nullptr;          // [steps][total] uint8 (BO schedule form)
+    bool steps_persistent = false;          // schedule form as one launch (k_bo_steps / k_lo_steps)
+    std::vector<int8_t> last_phase;         // BO schedule form: [block][rank] phase of the rank's last write
     size_t ws_bytes = 0;
     int launches = 0;
     const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
@@ -55,6 +62,21 @@ namespace {
 
 int popcount64(uint64_t x) { return __builtin_popcountll(x); }
 
+// switches the calling thread to `device` (>= 0) for the scope, then back
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = true;
+    explicit DeviceGuard(int device) {
+        if (device < 0) return;
+        if (hipGetDevice(&prev) != hipSuccess) { ok = false; prev = -1; return; }
+        if (prev == device) { prev = -1; return; }
+        if (hipSetDevice(device) != hipSuccess) { ok = false; prev = -1; }
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 void free_plan(allred_plan* p) {
     if (!p) return;
     if (p->d_partner) (void)hipFree(p->d_partner);
@@ -62,6 +84,8 @@ void free_plan(allred_plan* p) {
     if (p->d_ag_blocks) (void)hipFree(p->d_ag_blocks);
     if (p->d_order) (void)hipFree(p->d_order);
     if (p->d_dag) (void)hipFree(p->d_dag);
+    if (p->d_steps_tab) (void)hipFree(p->d_steps_tab);
+    if (p->d_partner8) (void)hipFree(p->d_partner8);
     delete p;
 }
 
@@ -103,6 +127,52 @@ bool lo_rank_uniform(const allred_schedule& s, int total) {
 bool env_is(const char* name, const char* value) {
     const char* v = std::getenv(name);
     return v && std::string(v) == value;
+}
+
+// BO schedule form (k_bo_steps): per block b, the ranks WRITTEN at each of the
+// 2S phases — RS step k: the holders r with b in recv_k(r) (N >> (k+1) of
+// them); AG step k (phases S .. 2S-1 = steps S-1 .. 0): the receivers r with b
+// in send_k(r) — phase-major, 2(N-1) bytes per block.  last[b][r] = the phase
+// of rank r's last write of block b (the owner's last RS step, everyone else's
+// AG step), for the per-rank zones of the stamps.
+std::vector<uint8_t> bo_steps_table(const allred_schedule& s, int N, std::vector<int8_t>* last) {
+    const int S = s.steps;
+    std::vector<uint8_t> tab;
+    last->assign((size_t)N * N, -1);
+    for (int b = 0; b < N; ++b) {
+        for (int q = 0; q < 2 * S; ++q) {
+            const int k = q < S ? q : 2 * S - 1 - q;
+            int cnt = 0;
+            for (int r = 0; r < N; ++r) {
+                const uint64_t m = q < S ? s.recv[r][k] : s.send[r][k];
+                if ((m >> b) & 1ull) {
+                    tab.push_back((uint8_t)r);
+                    (*last)[(size_t)b * N + r] = (int8_t)q;
+                    ++cnt;
+                }
+            }
+            if (cnt != (N >> (k + 1))) return {};   // not a BO mask set (validated schedules never get here)
+        }
+    }
+    return tab;
+}
+
+// LO schedule form (k_lo_steps): per step, the N/2 exchanging pairs (r, p), r < p.
+std::vector<uint8_t> lo_steps_pairs(const allred_schedule& s, int N) {
+    std::vector<uint8_t> pairs;
+    for (int k = 0; k < s.steps; ++k) {
+        int cnt = 0;
+        for (int r = 0; r < N; ++r) {
+            const int p = s.partner[r][k];
+            if (r < p) {
+                pairs.push_back((uint8_t)r);
+                pairs.push_back((uint8_t)p);
+                ++cnt;
+            }
+        }
+        if (cnt != N / 2) return {};
+    }
+    return pairs;
 }
 
 // The LO butterfly as a DAG of its distinct sums, for the LDS pass of 64 ranks
@@ -240,7 +310,7 @@ std::vector<uint8_t> lo_dag_lanes(const std::vector<uint8_t>& dag, int steps) {
     return out;
 }
 
-std::vector<uint8_t> lo_dag(const allred_schedule& s, int total) {
+std::vector<uint8_t> lo_dag_build(const allred_schedule& s, int total) {
     if (total != 64) return {};
     std::vector<std::vector<std::pair<int, int>>> ops(s.steps);
     std::vector<int> cur(total), nxt(total);
@@ -263,7 +333,7 @@ std::vector<uint8_t> lo_dag(const allred_schedule& s, int total) {
     std::vector<std::vector<int>> slot(s.steps), row(s.steps);
     for (int k = 0; k < s.steps; ++k)
         for (int q = 0; q < (int)ops[k].size(); ++q) slot[k].push_back(q), row[k].push_back(q);
-    if (!env_is("ALLRED_DAG_PLACE", "0")) lo_dag_place(ops, slot, row, total);
+    if (tune(Tune::lo_dag_place)) lo_dag_place(ops, slot, row, total);
     std::vector<uint8_t> dag(kDagBytes, 0);
     for (int k = 0; k < s.steps; ++k) {
         for (int sl = 0; sl < 32; ++sl) dag[(size_t)k * 64 + 2 * sl] = dag[(size_t)k * 64 + 2 * sl + 1] = 0xFF;
@@ -279,6 +349,22 @@ std::vector<uint8_t> lo_dag(const allred_schedule& s, int total) {
     return dag;
 }
 
+// The placed DAG of a schedule, cached per (algo, side, total, placement): the
+// local search runs up to 200,000 iterations, so plans of the same schedule
+// reuse its result.
+std::vector<uint8_t> lo_dag(const allred_schedule& s, int total) {
+    static std::mutex mu;
+    static std::map<std::tuple<int, int, int, int64_t>, std::vector<uint8_t>> cache;
+    const auto key = std::make_tuple(s.algo, s.side, total, tune(Tune::lo_dag_place));
+    {
+        std::lock_guard<std::mutex> g(mu);
+        const auto it = cache.find(key);
+        if (it != cache.end()) return it->second;
+    }
+    std::vector<uint8_t> dag = lo_dag_build(s, total);
+    std::lock_guard<std::mutex> g(mu);
+    return cache.emplace(key, std::move(dag)).first->second;
+}
 
 }  // namespace
 
@@ -322,11 +408,12 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
             }
         }
     }
-    p->lo_tree = desc->variant == ALLRED_LO && n % (8 * (size_t)total) == 0 && !env_is("ALLRED_LO_TREE", "0") &&
+    p->lo_tree = desc->variant == ALLRED_LO && n % (8 * (size_t)total) == 0 && tune(Tune::lo_tree) &&
                  lo_rank_uniform(p->sched, total);
     std::vector<uint8_t> order(&p->sched.tree_order[0][0],
                                &p->sched.tree_order[0][0] + ALLRED_MAX_NODES * ALLRED_MAX_NODES);
-    if (desc->variant == ALLRED_LO && desc->exec == ALLRED_EXEC_FUSED) {
+    // the DAG of distinct sums only where the fused LO runs the butterfly (not the tree route)
+    if (desc->variant == ALLRED_LO && desc->exec == ALLRED_EXEC_FUSED && !p->lo_tree && tune(Tune::lo_dag)) {
         const std::vector<uint8_t> dag = lo_dag(p->sched, total);
         if ((st = upload(&p->d_dag, lo_dag_lanes(dag, p->sched.steps)))) {
             free_plan(p);
@@ -338,9 +425,34 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
         free_plan(p);
         return st;
     }
+    // schedule form: one persistent launch (default) or one launch per step (steps_form 1, A/B)
+    p->steps_persistent = desc->exec == ALLRED_EXEC_STEPS && desc->variant != ALLRED_MEM && tune(Tune::steps_form) == 0;
+    if (p->steps_persistent) {
+        std::vector<uint8_t> tab;
+        if (desc->variant == ALLRED_BO) {
+            tab = bo_steps_table(p->sched, total, &p->last_phase);
+            std::vector<uint8_t> p8(partner.begin(), partner.end());
+            if (steps && (tab.empty() || (st = upload(&p->d_partner8, p8)))) {
+                free_plan(p);
+                return st ? st : ALLRED_ERR_SCHEDULE;
+            }
+        } else {
+            tab = lo_steps_pairs(p->sched, total);
+            if (steps && tab.empty()) {
+                free_plan(p);
+                return ALLRED_ERR_SCHEDULE;
+            }
+        }
+        if ((st = upload(&p->d_steps_tab, tab))) {
+            free_plan(p);
+            return st;
+        }
+    }
     // workspace and launch count per execute
     if (desc->exec == ALLRED_EXEC_FUSED) {
         p->launches = 1;
+    } else if (p->steps_persistent) {
+        p->launches = steps ? 1 : 0;
     } else if (desc->variant == ALLRED_BO) {
         p->launches = 2 * steps;
     } else if (desc->variant == ALLRED_LO) {
@@ -379,13 +491,56 @@ int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size
     return (int)dag.size();
 }
 
-int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* workspace, void* stream) {
+uint64_t allred_plan_stamp_words(const allred_plan* p) {
+    if (!p || !p->steps_persistent || p->sched.steps == 0) return 0;
+    const int S = p->sched.steps;
+    if (p->desc.variant == ALLRED_BO) return bo_steps_units(p->block_elems, p->total) * (uint64_t)(2 * S + 1);
+    return lo_steps_units(p->n) * (uint64_t)(S + 1);
+}
+
+int allred_plan_rank_zones(const allred_plan* p, const uint64_t* stamps, uint64_t* zone_start, uint64_t* zone_end) {
+    if (!p || !stamps || !zone_start || !zone_end || allred_plan_stamp_words(p) == 0) return ALLRED_ERR_ARG;
+    const int N = p->total, S = p->sched.steps;
+    for (int r = 0; r < N; ++r) zone_start[r] = ~0ull, zone_end[r] = 0;
+    if (p->desc.variant == ALLRED_BO) {
+        // every rank takes part in RS step 0 of every block (the holders read their
+        // partners' copies): its zone opens at the earliest unit start; it closes
+        // at the latest end of the phase in which the rank last writes a block
+        const uint64_t slices = bo_steps_units(p->block_elems, N) / (uint64_t)N;
+        for (uint64_t u = 0; u < slices * (uint64_t)N; ++u) {
+            const uint64_t* st = stamps + u * (uint64_t)(2 * S + 1);
+            const int b = (int)(u / slices);
+            for (int r = 0; r < N; ++r) {
+                if (st[0] < zone_start[r]) zone_start[r] = st[0];
+                const int q = p->last_phase[(size_t)b * N + r];
+                if (q >= 0 && st[1 + q] > zone_end[r]) zone_end[r] = st[1 + q];
+            }
+        }
+    } else {
+        const uint64_t units = lo_steps_units(p->n);
+        for (uint64_t u = 0; u < units; ++u) {
+            const uint64_t* st = stamps + u * (uint64_t)(S + 1);
+            for (int r = 0; r < N; ++r) {
+                if (st[0] < zone_start[r]) zone_start[r] = st[0];
+                if (st[S] > zone_end[r]) zone_end[r] = st[S];
+            }
+        }
+    }
+    return ALLRED_OK;
+}
+
+int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t stride, void* workspace,
+                                 uint64_t* stamps, void* stream) {
     if (!p || !ranks || stride < p->n) return ALLRED_ERR_ARG;
     if (p->ws_bytes && !workspace) return ALLRED_ERR_ARG;
+    if (stamps && allred_plan_stamp_words(p) == 0) return ALLRED_ERR_UNSUPPORTED;
+    DeviceGuard guard(p->desc.device);   // a plan made for device d launches on d, then restores the caller's
+    if (!guard.ok) return ALLRED_ERR_HIP;
     const int N = p->total, steps = p->sched.steps;
+    const bool acc16 = p->desc.mem_accum == ALLRED_ACC_BF16;
     int st = ALLRED_OK;
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
-        if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, stream);
+        if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, acc16, stream);
         if (p->desc.variant == ALLRED_LO && !p->lo_tree)
             return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->d_dag, stream);
         if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
@@ -395,6 +550,12 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
             p->last_ranks = ranks;
         }
         return launch_tree_fused(ranks, stride, p->n, N, p->d_order, stream, p->last_host);
+    }
+    if (p->steps_persistent) {
+        if (p->desc.variant == ALLRED_BO)
+            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_partner8, p->block_elems, stamps,
+                                   stream);
+        return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->n, stamps, stream);
     }
     if (p->desc.variant == ALLRED_BO) {
         for (int k = 0; k < steps && st == ALLRED_OK; ++k)
@@ -416,9 +577,13 @@ int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* 
         return st;
     }
     uint16_t* dst = static_cast<uint16_t*>(workspace);
-    st = launch_mem_reduce(ranks, stride, p->n, N, dst, stream);
+    st = launch_mem_reduce(ranks, stride, p->n, N, dst, acc16, stream);
     if (st == ALLRED_OK) st = launch_broadcast(ranks, stride, p->n, N, dst, stream);
     return st;
+}
+
+int allred_plan_execute(allred_plan* p, uint16_t* ranks, uint64_t stride, void* workspace, void* stream) {
+    return allred_plan_execute_profiled(p, ranks, stride, workspace, nullptr, stream);
 }
 
 int allred_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream) {
@@ -426,11 +591,17 @@ int allred_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream) 
 }
 
 int allred_bf16_add_masked(uint16_t* dst, const uint16_t* src, uint64_t mask, size_t block_elems, void* stream) {
-    uint8_t blocks[ALLRED_MAX_NODES];
-    int nb = 0;
-    for (int b = 0; b < 64; ++b)
-        if ((mask >> b) & 1ull) blocks[nb++] = (uint8_t)b;
-    return launch_bf16_add_blocks(dst, src, blocks, nb, block_elems, stream);
+    uint64_t off[ALLRED_MAX_NODES], len[ALLRED_MAX_NODES];
+    int ns = 0;
+    for (int b = 0; b < 64;) {   // one segment per run of set bits
+        if (!((mask >> b) & 1ull)) { ++b; continue; }
+        int e = b;
+        while (e < 64 && ((mask >> e) & 1ull)) ++e;
+        off[ns] = (uint64_t)b * block_elems;
+        len[ns++] = (uint64_t)(e - b) * block_elems;
+        b = e;
+    }
+    return launch_bf16_add_segs(dst, src, off, len, ns, stream);
 }
 
 // ---------------------------------------------------------------------------
@@ -471,8 +642,17 @@ int allred_args_parse(int argc, const char* const* argv, int variant, allred_arg
     if (argc >= 10) { if (stoi_like(argv[9], &total)) return ALLRED_ERR_ARG; }
     else if (env_nodes && stoi_like(env_nodes, &total)) return ALLRED_ERR_ARG;
     a->total_nodes = total > 0 ? total : a->side_length * a->side_length;
-    a->exec = env_is("ALLRED_EXEC", "fused") ? ALLRED_EXEC_FUSED : ALLRED_EXEC_STEPS;
+    // the one-pass form is the default (bit-identical); ALLRED_EXEC=steps keeps
+    // the reference's step structure (every step's result in the buckets)
+    a->exec = env_is("ALLRED_EXEC", "steps") ? ALLRED_EXEC_STEPS : ALLRED_EXEC_FUSED;
     a->round_mode = env_is("ALLRED_BF16_ROUND", "rne") ? 1 : 0;
+    // the reference's AllredConfig is bound to the IDevice its main created
+    // (allred_BO_2D.cpp:8); here ALLRED_DEVICE (or AllredConfig's device
+    // argument) names the HIP device ordinal, -1 = the current device
+    a->device = -1;
+    const char* env_dev = std::getenv("ALLRED_DEVICE");
+    if (env_dev && stoi_like(env_dev, &a->device)) return ALLRED_ERR_ARG;
+    a->mem_accum = env_is("ALLRED_MEM_ACC", "bf16") ? ALLRED_ACC_BF16 : ALLRED_ACC_FP32;
     const bool large = variant == ALLRED_MEM || (variant == ALLRED_BO && a->bandwidth_optimal);
     a->num_tiles = allred_normalize_tiles(a->tiles, a->total_nodes, large ? 1 : 0);
     return ALLRED_OK;
@@ -492,6 +672,34 @@ int allred_args_parse(int argc, const char* const* argv, int variant, allred_arg
         if (st != ALLRED_OK) goto done;            \
     } while (0)
 
+namespace {
+
+// tt-metal's profile_log_device.csv layout, as python/profiler_results_analyzer*.py
+// read it (metadata line, column header, one row per zone event): every rank's
+// ALL_RED_LOOP ZONE_START / ZONE_END (DeviceZoneScopedN, allred_BO_2D/kernels/
+// dataflow_kernel.cpp:147).  Ranks sit on the Wormhole worker cores the
+// reference's grid ran on (physical x / y of python/timing_taker.py:17-18);
+// times in s_memrealtime ticks (100 MHz "cycles").
+int write_profile_log(const char* path, int N, int side, const uint64_t* start, const uint64_t* end) {
+    static const int phys_x[8] = {1, 2, 3, 4, 6, 7, 8, 9}, phys_y[8] = {1, 2, 3, 4, 5, 7, 8, 9};
+    FILE* f = std::fopen(path, "w");
+    if (!f) return ALLRED_ERR_ARG;
+    std::fprintf(f, "ARCH: gfx950, CHIP_FREQ[MHz]: 100\n");
+    std::fprintf(f, "PCIe slot, core_x, core_y, RISC processor type, timer_id, time[cycles since reset], stat value, "
+                    "run ID, run host ID,  zone name, type, source line, source file\n");
+    for (int r = 0; r < N; ++r) {
+        const int x = r % side, y = r / side;
+        const int cx = x < 8 ? phys_x[x] : x + 2, cy = y < 8 ? phys_y[y] : y + 2;
+        for (int e = 0; e < 2; ++e)
+            std::fprintf(f, "0,%d,%d,BRISC,%d,%llu,0,0,0,ALL_RED_LOOP,%s,0,kernels.hip\n", cx, cy, e,
+                         (unsigned long long)(e ? end[r] : start[r]), e ? "ZONE_END" : "ZONE_START");
+    }
+    std::fclose(f);
+    return ALLRED_OK;
+}
+
+}  // namespace
+
 int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     if (!a) return ALLRED_ERR_ARG;
     allred_report local_rep{};
@@ -507,6 +715,8 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     if (print_core < 0 || print_core >= N) return ALLRED_ERR_ARG;
     R->bytes_per_rank = bytes;
     R->total_nodes = N;
+    DeviceGuard guard(a->device);
+    if (!guard.ok) return ALLRED_ERR_HIP;
 
     allred_plan_desc d{};
     d.algo = a->swing ? ALLRED_SWING : ALLRED_RECDUB;
@@ -514,8 +724,9 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     d.exec = a->exec;
     d.side_length = a->side_length;
     d.total_nodes = N;
-    d.device = -1;
+    d.device = a->device;
     d.elems_per_rank = n;
+    d.mem_accum = a->mem_accum;
     allred_plan* plan = nullptr;
     int st = allred_plan_create(&d, &plan);
     if (st != ALLRED_OK) return st;
@@ -523,6 +734,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
 
     std::vector<uint32_t> src0(bytes / 4), src1(bytes / 4);
     uint16_t *h_in = nullptr, *h_out = nullptr, *d_ranks = nullptr, *d_scratch = nullptr, *d_stage = nullptr;
+    uint64_t* d_stamps = nullptr;
     void* d_ws = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr, e3 = nullptr;
     hipStream_t s = nullptr;
@@ -530,6 +742,10 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     const size_t stride = (size_t)allred_preferred_rank_stride(n);
     const size_t dev_bytes = (size_t)N * stride * 2;
     float ms = 0;
+    // ALLRED_PROFILE_LOG=<path> (the reference's TT_METAL_DEVICE_PROFILER=1 +
+    // profile_log_device.csv): per-rank ALL_RED_LOOP zones of the timed run
+    const char* profile_log = std::getenv("ALLRED_PROFILE_LOG");
+    const uint64_t stamp_words = profile_log ? allred_plan_stamp_words(plan) : 0;
     // end-to-end mode: "zerocopy" = the kernel reads / writes the pinned host
     // buckets in place (both PCIe directions at once; the default for the
     // fused BO pass, whose pipelined form is built for it), "dma" = one H2D
@@ -554,6 +770,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     HIPCK(hipMalloc((void**)&d_scratch, dev_bytes));
     HIPCK(hipMalloc((void**)&d_stage, all_bytes));
     if (plan->ws_bytes) HIPCK(hipMalloc(&d_ws, plan->ws_bytes));
+    if (stamp_words) HIPCK(hipMalloc((void**)&d_stamps, stamp_words * 8));
     HIPCK(hipEventCreate(&e0));
     HIPCK(hipEventCreate(&e1));
     HIPCK(hipEventCreate(&e2));
@@ -570,30 +787,39 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         HIPCK(hipHostGetDevicePointer((void**)&h_dev, h_in, 0));
         HIPCK(hipEventRecord(e0, s));
         HIPCK(hipEventRecord(e1, s));
-        if (a->run_kernel) ST(allred_plan_execute(plan, h_dev, n, d_ws, s));
+        if (a->run_kernel) ST(allred_plan_execute_profiled(plan, h_dev, n, d_ws, d_stamps, s));
         HIPCK(hipEventRecord(e2, s));
         HIPCK(hipEventRecord(e3, s));
         HIPCK(hipStreamSynchronize(s));
         std::memcpy(h_out, h_in, all_bytes);  // (untimed) the result, for validation below
     } else {
-    // timed: H2D | allreduce | D2H
-    HIPCK(hipEventRecord(e0, s));
-    // the 64 host buckets are contiguous: one DMA each way (per-bucket copies pay ~70 us each),
-    // then one HBM pass into / out of the skewed device layout
-    HIPCK(hipMemcpyAsync(d_stage, h_in, all_bytes, hipMemcpyHostToDevice, s));
-    ST(launch_copy_ranks(d_stage, n, d_ranks, stride, N, n, s));
-    HIPCK(hipEventRecord(e1, s));
-    if (a->run_kernel) ST(allred_plan_execute(plan, d_ranks, stride, d_ws, s));
-    HIPCK(hipEventRecord(e2, s));
-    ST(launch_copy_ranks(d_ranks, stride, d_stage, n, N, n, s));
-    HIPCK(hipMemcpyAsync(h_out, d_stage, all_bytes, hipMemcpyDeviceToHost, s));
-    HIPCK(hipEventRecord(e3, s));
-    HIPCK(hipStreamSynchronize(s));
+        // timed: H2D | allreduce | D2H.  The 64 host buckets are contiguous: one
+        // DMA each way (per-bucket copies pay ~70 us each), then one HBM pass
+        // into / out of the skewed device layout
+        HIPCK(hipEventRecord(e0, s));
+        HIPCK(hipMemcpyAsync(d_stage, h_in, all_bytes, hipMemcpyHostToDevice, s));
+        ST(launch_copy_ranks(d_stage, n, d_ranks, stride, N, n, s));
+        HIPCK(hipEventRecord(e1, s));
+        if (a->run_kernel) ST(allred_plan_execute_profiled(plan, d_ranks, stride, d_ws, d_stamps, s));
+        HIPCK(hipEventRecord(e2, s));
+        ST(launch_copy_ranks(d_ranks, stride, d_stage, n, N, n, s));
+        HIPCK(hipMemcpyAsync(h_out, d_stage, all_bytes, hipMemcpyDeviceToHost, s));
+        HIPCK(hipEventRecord(e3, s));
+        HIPCK(hipStreamSynchronize(s));
     }
     HIPCK(hipEventElapsedTime(&ms, e1, e2));
     R->device_seconds = ms * 1e-3;
     HIPCK(hipEventElapsedTime(&ms, e0, e3));
     R->e2e_seconds = ms * 1e-3;
+    if (profile_log) {
+        std::vector<uint64_t> zs(N, 0), ze(N, (uint64_t)(R->device_seconds * 1e8));
+        if (stamp_words && a->run_kernel) {   // the schedule form's per-unit stamps -> per-rank zones
+            std::vector<uint64_t> host(stamp_words);
+            HIPCK(hipMemcpy(host.data(), d_stamps, stamp_words * 8, hipMemcpyDeviceToHost));
+            ST(allred_plan_rank_zones(plan, host.data(), zs.data(), ze.data()));
+        }   // else: one device interval (hipEvents) for every rank, ticks from 0
+        ST(write_profile_log(profile_log, N, a->side_length, zs.data(), ze.data()));
+    }
     {
         float maxe = 0;
         const uint32_t* res = reinterpret_cast<const uint32_t*>(h_out + (size_t)print_core * n);
@@ -615,6 +841,7 @@ done:
     if (e2) (void)hipEventDestroy(e2);
     if (e3) (void)hipEventDestroy(e3);
     if (d_ws) (void)hipFree(d_ws);
+    if (d_stamps) (void)hipFree(d_stamps);
     if (d_ranks) (void)hipFree(d_ranks);
     if (d_scratch) (void)hipFree(d_scratch);
     if (d_stage) (void)hipFree(d_stage);

@@ -35,12 +35,18 @@ int steps_for(int total_nodes);
 // Build + validate (see allred_schedule_build in allred.h).
 int build_schedule(int algo, int side, int total, allred_schedule* out, std::string* why);
 
+// ---------------- tuning (tune.cpp; allred_tune_set / allred_tune_get) ----------------
+// Kernel-form switches between bit-identical forms; defaults = the product forms.
+enum class Tune { fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, count };
+int64_t tune(Tune key);
+
 // ---------------- device launchers (kernels.hip) ----------------
 // All take hipStream_t as void* and return ALLRED_OK / ALLRED_ERR_*.
-struct RankTable;  // opaque device tables of a plan
 int launch_bf16_add(uint16_t* dst, const uint16_t* src, size_t n, void* stream);
-int launch_bf16_add_blocks(uint16_t* dst, const uint16_t* src, const uint8_t* blocks, int nblocks,
-                           size_t block_elems, void* stream);
+// dst[seg] += src[seg] for up to kMaxAddSegs segments (elements, multiples of 8), ONE launch
+constexpr int kMaxAddSegs = 64;
+int launch_bf16_add_segs(uint16_t* dst, const uint16_t* src, const uint64_t* off, const uint64_t* len, int nsegs,
+                         void* stream);
 // host_memory: the ranks live in pinned host memory (zero-copy) -> pipelined form
 int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
                       bool host_memory = false);
@@ -59,9 +65,19 @@ int launch_lo_step(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint
                    int total, const int16_t* d_partner, size_t n, void* stream);
 int launch_copy_ranks(const uint16_t* src, uint64_t src_stride, uint16_t* dst, uint64_t dst_stride,
                       int total, size_t n, void* stream);
-int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, uint16_t* dst,
+// mem_2D; acc16: the reference's bf16 accumulation (every add rounded), else fp32 rounded once
+int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, uint16_t* dst, bool acc16,
                       void* stream);
-int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, void* stream);
+int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, bool acc16, void* stream);
+// the schedule form as one persistent launch (k_bo_steps / k_lo_steps).  BO: d_tab = per block
+// the ranks written at each of the 2S phases, d_partner8 = [S][N]; LO: d_pairs = per step N/2
+// (r, p) pairs.  stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)
+int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
+                    const uint8_t* d_partner8, size_t block_elems, uint64_t* stamps, void* stream);
+uint64_t bo_steps_units(size_t block_elems, int total);
+int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs, size_t n,
+                    uint64_t* stamps, void* stream);
+uint64_t lo_steps_units(size_t n);
 
 // peer flag area (uint32 words): [0, 64) the multi-kernel barrier, then the
 // one-kernel form's [2 phases][kPeerFusedMaxGroups][64 ranks] slots, then the
@@ -102,10 +118,6 @@ int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, 
 // the same step with LL (push) hand-offs: ll[q] = GPU q's LL area for this parity,
 // [inbox box_words words][result box box_words words]; nranks <= 8; epoch grows by 1 per call
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   void* stream);
-// the same step and LL layout, pipelined per tile on specialised waves (k_hier_ws)
-int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream);
 // allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * n / 8

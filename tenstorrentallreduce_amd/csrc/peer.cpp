@@ -55,7 +55,7 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
-    int hier_ll = 0;                // 0 off, 1 k_hier_ll (phased), 2 k_hier_ws (pipelined)
+    int hier_ll = 0;                // 0 off, 1 k_hier_ll (LL push hand-offs)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
@@ -66,13 +66,17 @@ extern "C" {
 int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, allred_peer** out) {
     if (!out || nranks < 1 || nranks > ALLRED_MAX_NODES || rank < 0 || rank >= nranks || max_elems == 0)
         return ALLRED_ERR_ARG;
+    // every IPC-exported window <= 1 GiB: a peer's hipIpcOpenMemHandle of a ~2 GiB
+    // allocation never returned (profiles/r01_peer_open_probe_2gib_hang.txt); checked
+    // before any HIP call, so the limit holds (and is testable) without a GPU
+    if (max_elems > ALLRED_PEER_MAX_WINDOW_BYTES / 2) return ALLRED_ERR_ARG;
     *out = nullptr;
     if (device >= 0 && hipSetDevice(device) != hipSuccess) return ALLRED_ERR_HIP;
     auto* p = new allred_peer();
     p->nranks = nranks;
     p->rank = rank;
     (void)hipGetDevice(&p->device);
-    p->max_elems = (max_elems + 127) / 128 * 128;  // LO halves stay 64-element aligned
+    p->max_elems = (max_elems + 127) / 128 * 128;  // LO halves stay 64-element aligned (still <= 2^29)
     // windows are uncached too: peers read them over xGMI straight from HBM, so
     // no write may linger in one of this GPU's eight per-XCD L2s.  The flag
     // allocation holds, behind the flags of internal.hpp: the hierarchical
@@ -193,9 +197,8 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
-        st = (p->hier_ll == 2 ? launch_hier_ws : launch_hier_ll)(buf, n, order, ll, p->nranks, p->rank, n,
-                                                                 p->ll_box_words, p->calls + 1u, p->status,
-                                                                 p->max_groups, stream);
+        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
+                            p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -308,7 +311,7 @@ int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
 
 int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
-    if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
+    if (enable < 0 || enable > 1) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
     return ALLRED_OK;
 }
@@ -337,6 +340,14 @@ int allred_peer_status(allred_peer* p, uint32_t* out) {
     if (!p->win_uncached) *out |= ALLRED_PEER_WIN_CACHED;
     if (!p->flags_uncached) *out |= ALLRED_PEER_FLAGS_CACHED;
     return ALLRED_OK;
+}
+
+int allred_peer_check(allred_peer* p, void* stream) {
+    if (!p) return ALLRED_ERR_ARG;
+    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ALLRED_ERR_HIP;
+    uint32_t st = 0;
+    if (hipMemcpy(&st, p->status, 4, hipMemcpyDeviceToHost) != hipSuccess) return ALLRED_ERR_HIP;
+    return (st & ALLRED_PEER_TIMEOUT) ? ALLRED_ERR_TRANSPORT : ALLRED_OK;
 }
 
 int allred_peer_destroy(allred_peer* p) {

@@ -1,0 +1,850 @@
+// peer_kernels.hip — CDNA4 (gfx950) kernels of the multi-GPU transports over
+// IPC-mapped peer windows (peer.cpp): the allred_mem_2D program across GPUs
+// (one-shot reduce-scatter / all-gather, allred_mem_2D/kernels/*), the Swing /
+// RecDub BO and LO program of dist.cpp with RCCL replaced by direct xGMI reads
+// of the partners' windows, the hierarchical step (64 local ranks per GPU) and
+// the LL (data + epoch word) push forms for small buckets.
+// Every cross-GPU wait is bounded (device.hpp peer_give_up): a dead or slow
+// peer sets ALLRED_PEER_TIMEOUT in the status word instead of hanging.
+#include "device.hpp"
+
+namespace tsa {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Peer-mapped one-shot allreduce (allred_mem_2D over xGMI): every GPU's window
+// is IPC-mapped into every other GPU; flags live in fine-grained (uncached)
+// memory and are written / polled with system-scope atomics.  Kernel
+// boundaries on the stream carry the system-scope release / acquire of the
+// window bytes (HIP dispatch packets fence at system scope).
+// ---------------------------------------------------------------------------
+
+struct PeerPtrs {
+    uint16_t* win[ALLRED_MAX_NODES];     // window of rank q (this parity), as mapped here
+    uint32_t* flags[ALLRED_MAX_NODES];   // flag array of rank q, as mapped here
+};
+
+// one workgroup: tell every peer "rank `me` reached `epoch`", then wait for all.
+// Bounded: on timeout bit 0 of *status is set and the kernel returns.
+__global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, uint32_t* status) {
+    const int t = threadIdx.x;
+    if (t < nranks)
+        __hip_atomic_store(pp.flags[t] + me, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < nranks) {
+        uint32_t* mine = pp.flags[me] + t;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
+            if (peer_give_up(spin, status)) break;   // ~ seconds: a peer never arrived
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
+// reduce-scatter: block `me` of every window, owner first then ranks in order
+// (fp32, one rounding), written to my window (peers gather it) and to my bucket
+__global__ __launch_bounds__(kBlock) void k_peer_rs(PeerPtrs pp, int nranks, int me, uint16_t* __restrict__ bucket,
+                                                    uint64_t blk_vec) {
+    const uint64_t off = (uint64_t)me * blk_vec;
+    for (uint64_t v = gtid(); v < blk_vec; v += gthreads()) {
+        const uint4 s = ld_nt(reinterpret_cast<const uint4*>(pp.win[me]) + off + v);
+        float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
+        uint4 y[ALLRED_MAX_NODES > 8 ? 8 : ALLRED_MAX_NODES];
+        for (int q0 = 0; q0 < nranks; q0 += 8) {
+            const int q1 = q0 + 8 < nranks ? q0 + 8 : nranks;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (q0 + i < q1 && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(pp.win[q0 + i]) + off + v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (q0 + i >= q1 || q0 + i == me) continue;
+                a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+            }
+        }
+        uint4 o;
+        o.x = pack_rne(a[0], a[1]);
+        o.y = pack_rne(a[2], a[3]);
+        o.z = pack_rne(a[4], a[5]);
+        o.w = pack_rne(a[6], a[7]);
+        st_nt(reinterpret_cast<uint4*>(pp.win[me]) + off + v, o);
+        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, o);
+    }
+}
+
+// all-gather: bucket[block q] = window_q[block q] for every q != me (grid.y = q)
+__global__ __launch_bounds__(kBlock) void k_peer_ag(PeerPtrs pp, int me, uint16_t* __restrict__ bucket,
+                                                    uint64_t blk_vec) {
+    const int q = blockIdx.y;
+    if (q == me) return;
+    const uint64_t off = (uint64_t)q * blk_vec;
+    for (uint64_t v = gtid(); v < blk_vec; v += gthreads())
+        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + off + v));
+}
+
+// ---- one-kernel form (latency regime) --------------------------------------
+// Workgroup g owns sub-slice g of every block and only ever synchronises with
+// workgroup g of the other GPUs, so there is no grid-wide barrier:
+//   1. copy sub-slice g of every block but mine to my window, signal phase 0
+//   2. wait phase 0 from all ranks; reduce sub-slice g of my block (own copy
+//      from the bucket, then ranks in order), write it to window + bucket,
+//      signal phase 1
+//   3. wait phase 1; gather sub-slice g of every other block from its owner.
+// Flag slot [phase][g][q] of rank r's fused flag area is written only by
+// workgroup g of rank q.  Windows and flags are uncached (MTYPE UC) device
+// memory, so a store is in HBM once it is acknowledged: every wave waits for
+// its stores (s_waitcnt vmcnt(0)) before the workgroup barrier, then the flag
+// goes out as a system-scope store, and the poll reads memory directly (no
+// L2 writeback / invalidate, which cost ~20 us at 128 KiB).  allred_peer
+// only selects this form when both allocations really are uncached.
+__device__ inline void peer_signal_wait(const PeerPtrs& pp, int nranks, int me, uint32_t slot_base, uint32_t epoch,
+                                        uint32_t* status) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < nranks)
+        __hip_atomic_store(pp.flags[t] + slot_base + me, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (t < nranks) {
+        uint32_t* mine = pp.flags[me] + slot_base + t;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
+            if (peer_give_up(spin, status)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks, int me, uint16_t* __restrict__ bucket,
+                                                         uint64_t blk_vec, uint64_t chunk, uint32_t epoch,
+                                                         uint32_t* status) {
+    const int g = blockIdx.x;
+    const uint64_t lo = (uint64_t)g * chunk;
+    const uint64_t hi = lo + chunk < blk_vec ? lo + chunk : blk_vec;
+    const uint64_t len = hi > lo ? hi - lo : 0;
+    const uint4* src = reinterpret_cast<const uint4*>(bucket);
+    uint4* mywin = reinterpret_cast<uint4*>(pp.win[me]);
+    // 1. my copy of every block but mine -> my window
+    for (uint64_t i = threadIdx.x; i < (uint64_t)nranks * len; i += blockDim.x) {
+        const uint64_t q = i / len, v = q * blk_vec + lo + i % len;
+        if ((int)q != me) st_nt(mywin + v, ld_nt(src + v));
+    }
+    const uint32_t base0 = kPeerFusedFlagOff + (uint32_t)g * 64u;
+    const uint32_t base1 = kPeerFusedFlagOff + (uint32_t)(kPeerFusedMaxGroups + g) * 64u;
+    peer_signal_wait(pp, nranks, me, base0, epoch, status);
+    // 2. reduce my block's sub-slice g
+    const uint64_t off = (uint64_t)me * blk_vec;
+    for (uint64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
+        const uint4 s = ld_nt(src + off + v);
+        float a[8] = {lo_f(s.x), hi_f(s.x), lo_f(s.y), hi_f(s.y), lo_f(s.z), hi_f(s.z), lo_f(s.w), hi_f(s.w)};
+        uint4 y[8];
+        for (int q0 = 0; q0 < nranks; q0 += 8) {
+            const int q1 = q0 + 8 < nranks ? q0 + 8 : nranks;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                if (q0 + i < q1 && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(pp.win[q0 + i]) + off + v);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (q0 + i >= q1 || q0 + i == me) continue;
+                a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+            }
+        }
+        uint4 o;
+        o.x = pack_rne(a[0], a[1]);
+        o.y = pack_rne(a[2], a[3]);
+        o.z = pack_rne(a[4], a[5]);
+        o.w = pack_rne(a[6], a[7]);
+        st_nt(mywin + off + v, o);
+        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, o);
+    }
+    peer_signal_wait(pp, nranks, me, base1, epoch, status);
+    // 3. gather every other block's sub-slice g from its owner
+    for (uint64_t i = threadIdx.x; i < (uint64_t)nranks * len; i += blockDim.x) {
+        const uint64_t q = i / len, v = q * blk_vec + lo + i % len;
+        if ((int)q != me)
+            st_nt(reinterpret_cast<uint4*>(bucket) + v, ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + v));
+    }
+}
+
+// ---- scheduled form: the Swing / RecDub BO or LO program over peer windows --
+// The RCCL program of dist.cpp with every exchange turned into a direct read
+// of the partner's IPC-mapped window: step k of rank r waits until its
+// partner p has finished step k-1 (p's progress slot in r's flag area), then
+// reads p's blocks straight over xGMI and adds them into its own window.
+// Workgroup g = channel g % C, sub-slice g / C of every block of the channel;
+// it only ever waits for workgroup g of its partners.  Progress values for a
+// call are base+1 (window filled) .. base+2S (all-gather step S-2 done).
+// Hazards (why no ack is needed in BO): at RS step k rank r writes only
+// recv_r[k], which no partner reads at step k or later; at AG step i it writes
+// send_r[i], whose only earlier reader is the same partner p_i, which has
+// finished its whole reduce-scatter before it can serve AG step i.
+// LO ping-pongs two halves of the window: step k reads half k&1 and writes
+// half (k+1)&1, after p_{k-1} (the previous reader of that half) finished k-1.
+__device__ inline void sched_signal(const PeerPtrs& pp, const PeerProg& pr, int c, int me, uint32_t slot,
+                                    uint32_t value) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int t = threadIdx.x;
+    if (t < pr.S)
+        __hip_atomic_store(pp.flags[pr.peer[c][t]] + slot + me, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ inline void sched_wait(const PeerPtrs& pp, int me, uint32_t slot, int q0, int q1, uint32_t value,
+                                  uint32_t* status) {
+    const int t = threadIdx.x;
+    const int q = t == 0 ? q0 : (t == 1 ? q1 : -1);
+    if (q >= 0) {
+        uint32_t* f = pp.flags[me] + slot + q;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= value) break;
+            if (peer_give_up(spin, status)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
+                                                       uint64_t half_vec, uint32_t base, uint32_t* status) {
+    const int C = pr.C, S = pr.S, N = pr.N;
+    const int g = blockIdx.x, c = g % C, Gc = gridDim.x / C, j = g / C;
+    const uint32_t slot = kPeerSchedFlagOff + (uint32_t)g * 64u;
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint4* mine = reinterpret_cast<uint4*>(pp.win[me]);
+    const uint64_t cb = pr.base[c];
+    const int tid = threadIdx.x;
+    if (!pr.lo) {
+        const uint64_t blk = pr.len[c] / N;
+        const uint64_t chunk = (blk + Gc - 1) / Gc;
+        const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk < blk ? lo + chunk : blk;
+        for (int b = 0; b < N; ++b)
+            for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) st_nt(mine + v, ld_nt(bk + v));
+        sched_signal(pp, pr, c, me, slot, base + 1);
+        for (int k = 0; k < S; ++k) {  // reduce-scatter
+            const int p = pr.peer[c][k];
+            sched_wait(pp, me, slot, p, -1, base + 1 + k, status);
+            const uint4* theirs = reinterpret_cast<const uint4*>(pp.win[p]);
+            const bool last = k == S - 1;
+            for (uint64_t m = pr.recv[c][k]; m; m &= m - 1) {
+                const int b = __builtin_ctzll(m);
+                for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) {
+                    const uint4 o = add8(ld_nt(mine + v), ld_nt(theirs + v));
+                    st_nt(mine + v, o);
+                    if (last) st_nt(bk + v, o);
+                }
+            }
+            sched_signal(pp, pr, c, me, slot, base + 2 + k);
+        }
+        for (int t = 0; t < S; ++t) {  // all-gather, steps in reverse
+            const int i = S - 1 - t, pos = S + t;
+            const int p = pr.peer[c][i];
+            sched_wait(pp, me, slot, p, -1, base + 1 + pos, status);
+            const uint4* theirs = reinterpret_cast<const uint4*>(pp.win[p]);
+            const bool keep = t < S - 1;  // later partners read these blocks from my window
+            for (uint64_t m = pr.send[c][i]; m; m &= m - 1) {
+                const int b = __builtin_ctzll(m);
+                for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) {
+                    const uint4 y = ld_nt(theirs + v);
+                    if (keep) st_nt(mine + v, y);
+                    st_nt(bk + v, y);
+                }
+            }
+            if (keep) sched_signal(pp, pr, c, me, slot, base + 2 + pos);
+        }
+        return;
+    }
+    // LO: full exchange + add every step, two window halves
+    const uint64_t L = pr.len[c];
+    const uint64_t chunk = (L + Gc - 1) / Gc;
+    const uint64_t lo = cb + (uint64_t)j * chunk, hi = (uint64_t)j * chunk + chunk < L ? lo + chunk : cb + L;
+    for (uint64_t v = lo + tid; v < hi; v += kBlock) st_nt(mine + v, ld_nt(bk + v));
+    sched_signal(pp, pr, c, me, slot, base + 1);
+    for (int k = 0; k < S; ++k) {
+        const int p = pr.peer[c][k];
+        const bool last = k == S - 1;
+        sched_wait(pp, me, slot, p, (k >= 1 && !last) ? pr.peer[c][k - 1] : -1, base + 1 + k, status);
+        const uint4* a = mine + (k & 1) * half_vec;
+        const uint4* b = reinterpret_cast<const uint4*>(pp.win[p]) + (k & 1) * half_vec;
+        uint4* dst = last ? bk : mine + ((k + 1) & 1) * half_vec;
+        for (uint64_t v = lo + tid; v < hi; v += kBlock) st_nt(dst + v, add8(ld_nt(a + v), ld_nt(b + v)));
+        if (!last) sched_signal(pp, pr, c, me, slot, base + 2 + k);
+    }
+}
+
+// ---- hierarchical one-kernel form: 64 local ranks per GPU -------------------
+// The whole hierarchical step (local tree of the 64 virtual ranks -> mem_2D
+// across the W GPUs -> broadcast back to the 64 ranks) as ONE persistent
+// launch with per-tile flags, so the xGMI latency of one tile hides behind
+// the HBM streaming of the others.  Tile = 256 elements (512 B per rank row);
+// owner(t) = t / (tiles / W), i.e. the block ownership of allred_mem_2D, so
+// the bits equal tree_reduce + allred_peer_allreduce + broadcast.
+//   A (all my tiles, double-buffered LDS as k_tree_lds_pipe): partial of tile
+//     t -> my window's partial region (local, uncached); flagA[t][me] -> owner.
+//   R (my tiles that I own): wait flagA[t][*]; read the W partials (remote
+//     loads), fp32 sum owner first then ascending, one rounding -> my result
+//     region; flagB[t] -> every GPU.
+//   B (all my tiles): wait flagB[t]; read the result from the owner's window;
+//     store it to the 64 rank rows.
+// A never waits, R waits only for A, B only for R: with the grid resident
+// (2 workgroups per CU) every wait is reached and satisfied.
+struct HierPtrs {
+    uint16_t* win[ALLRED_MAX_NODES];   // GPU q's window, this parity: [partial n][result n]
+    uint32_t* hfl[ALLRED_MAX_NODES];   // GPU q's per-tile flags: [tile][W + 1]
+};
+
+__device__ inline void hier_wait(const uint32_t* f, uint32_t epoch, uint32_t* status) {
+    for (uint64_t spin = 0;; ++spin) {
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) return;
+        if (peer_give_up(spin, status)) return;
+        __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_hier_oneshot(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                         const uint8_t* __restrict__ order, HierPtrs hp, int W, int me,
+                                                         uint64_t n, uint64_t ntiles, uint64_t tiles_per_owner,
+                                                         uint32_t epoch, uint32_t* status) {
+    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    __syncthreads();
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+        }
+    };
+    const uint64_t G = gridDim.x, nvec = n / 8;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    const uint32_t F = (uint32_t)W + 1;
+    uint4* my_partial = reinterpret_cast<uint4*>(hp.win[me]);
+    uint4* my_result = my_partial + nvec;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    // ---- A: local trees, partials published.  Each iteration starts with
+    // vmcnt(0): tile j's LDS-DMA and tile j-1's partial store are then done, so
+    // tile j-1's flag goes out there, one iteration late, without draining the
+    // prefetch of tile j+1 (issued after that wait).  (Interleaving R and B
+    // into this loop measured slower: 22.6 vs 19.6 us at W = 1 — each
+    // uncached round trip is then paid once per tile instead of once per batch.)
+    auto publish = [&](uint64_t t) {
+        if (threadIdx.x == 0)
+            __hip_atomic_store(hp.hfl[owner_of(t)] + t * F + me, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    if (mine > 0) issue(tile_of(0), 0);
+    for (int j = 0; j < mine; ++j) {
+        wait_vm<0>();
+        lds_barrier();
+        if (j > 0) publish(tile_of(j - 1));
+        if (j + 1 < mine) issue(tile_of(j + 1), (j + 1) & 1);
+        const uint4* tile = buf[j & 1];
+        const uint64_t v0 = tile_of(j) * TV;
+        const uint8_t* ord = ord_lds + RPW * w + LPL * h;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+        if (h == 0) part[w * TV + c] = pw;
+        lds_barrier();
+        if (w == 0 && h == 0)
+            st_nt(my_partial + v0 + c,
+                  add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c])));
+    }
+    wait_vm<0>();
+    if (mine > 0) publish(tile_of(mine - 1));
+    // ---- R: the tiles I own, 8 at a time: every flag, then every remote load in flight at once
+    {
+        int owned[8];
+        int no = 0;
+        auto flush = [&]() {
+            for (int i = threadIdx.x; i < no * W; i += kBlock)
+                hier_wait(hp.hfl[me] + tile_of(owned[i / W]) * F + i % W, epoch, status);
+            lds_barrier();
+            const int b = threadIdx.x / TV;
+            if (b < no) {
+                const uint64_t v0 = tile_of(owned[b]) * TV;
+                const uint4 s0 = ld_nt(my_partial + v0 + c);
+                float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y),
+                              lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+                for (int q0 = 0; q0 < W; q0 += 8) {   // 8 remote partials in flight at once
+                    uint4 y[8];
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+                        if (q0 + i < W && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(hp.win[q0 + i]) + v0 + c);
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        if (q0 + i >= W || q0 + i == me) continue;
+                        a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
+                        a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
+                        a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
+                        a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
+                    }
+                }
+                uint4 o;
+                o.x = pack_rne(a[0], a[1]);
+                o.y = pack_rne(a[2], a[3]);
+                o.z = pack_rne(a[4], a[5]);
+                o.w = pack_rne(a[6], a[7]);
+                st_nt(my_result + v0 + c, o);
+            }
+            wait_vm<0>();     // results are in HBM (uncached) before their flags
+            lds_barrier();
+            for (int i = threadIdx.x; i < no * W; i += kBlock)
+                __hip_atomic_store(hp.hfl[i % W] + tile_of(owned[i / W]) * F + W, epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            no = 0;
+        };
+        for (int j = 0; j < mine; ++j) {
+            if (owner_of(tile_of(j)) != me) continue;
+            owned[no++] = j;
+            if (no == 8) flush();
+        }
+        if (no) flush();
+    }
+    // ---- B: results back to the 64 rank rows, 4 tiles' remote loads in flight at once
+    constexpr int BB = 4;
+    for (int j0 = 0; j0 < mine; j0 += BB) {
+        const int nb = mine - j0 < BB ? mine - j0 : BB;
+        if (threadIdx.x < (unsigned)nb) hier_wait(hp.hfl[me] + tile_of(j0 + (int)threadIdx.x) * F + W, epoch, status);
+        lds_barrier();
+        uint4 res[BB];
+#pragma unroll
+        for (int b = 0; b < BB; ++b) {
+            if (b >= nb) break;
+            const uint64_t t = tile_of(j0 + b);
+            res[b] = ld_nt(reinterpret_cast<const uint4*>(hp.win[owner_of(t)]) + nvec + t * TV + c);
+        }
+#pragma unroll
+        for (int b = 0; b < BB; ++b) {
+            if (b >= nb) break;
+            const uint64_t v0 = tile_of(j0 + b) * TV;
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res[b]);
+            }
+        }
+    }
+}
+
+// ---- hierarchical one-kernel form, LL (push) variant ------------------------
+// Same bits as k_hier_oneshot (local tree per tile -> mem_2D across the W GPUs,
+// fp32 owner first then ascending, one rounding -> every GPU's 64 rank rows),
+// but every cross-GPU transfer is a PUSH of self-validating 8-byte words
+// (4 bytes of data + the call's epoch, RCCL's "LL" idea): the producer's
+// relaxed system-scope stores go straight into the consumer's uncached LL
+// area and the consumer polls its OWN memory until every word carries the
+// epoch.  No flag follows the data and no remote load is ever waited for, so
+// each hand-off costs one one-way xGMI trip instead of a flag trip plus a
+// remote read round trip (k_hier_oneshot: A publish -> R remote loads -> B
+// remote loads).
+//   A (all my tiles, double-buffered LDS): tile t's partial -> owner o's inbox
+//     slot [t - o*tpo][me] (1 KiB of LL words per tile).
+//   R (my tiles that I own): poll the W slots, fp32 sum owner first then
+//     ascending, one rounding -> every GPU's result box [t].
+//   B (all my tiles): poll my result box [t], store to the 64 rank rows.
+// A never waits, R waits only for A, B only for R; the grid is resident (2
+// workgroups per CU), so every wait is reached and satisfied.  Epochs grow by
+// one per call and the LL areas alternate by call parity, so a word of an
+// earlier call never carries the awaited epoch.
+constexpr int kLLMaxGpus = 8;
+struct LLPtrs {
+    uint64_t* ll[kLLMaxGpus];   // GPU q's LL area, this parity: [inbox: tiles x 128 words][result box: same]
+};
+
+__device__ __forceinline__ void ll_put(uint64_t* dst, uint4 v, uint32_t e) {
+    const uint64_t hi = (uint64_t)e << 32;
+    __hip_atomic_store(dst + 0, hi | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1, hi | v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 2, hi | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 3, hi | v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// poll 4 LL words until all carry epoch e (bounded: status bit 0 on timeout)
+__device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_t* status) {
+    uint64_t w0, w1, w2, w3;
+    for (uint64_t spin = 0;; ++spin) {
+        w0 = __hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w2 = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w3 = __hip_atomic_load(src + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(w0 >> 32) == e && (uint32_t)(w1 >> 32) == e && (uint32_t)(w2 >> 32) == e &&
+            (uint32_t)(w3 >> 32) == e)
+            break;
+        if (peer_give_up(spin, status)) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return make_uint4((uint32_t)w0, (uint32_t)w1, (uint32_t)w2, (uint32_t)w3);
+}
+
+__global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
+                                                    uint32_t epoch, uint32_t* status) {
+    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    __syncthreads();
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            const int r = RPW * w + 2 * k + h;
+            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
+            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+        }
+    };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    uint64_t* const my_ll = lp.ll[me];
+    // ---- A: local trees, partials pushed to their owners
+    if (mine > 0) issue(tile_of(0), 0);
+    for (int j = 0; j < mine; ++j) {
+        // in flight after tile j's loads: wave 0's four LL stores of tile j-1
+        // (wave-uniform branch: vmcnt is per wave)
+        if (j > 0 && w == 0) wait_vm<4>(); else wait_vm<0>();
+        lds_barrier();
+        if (j + 1 < mine) issue(tile_of(j + 1), (j + 1) & 1);
+        const uint4* tile = buf[j & 1];
+        const uint64_t t = tile_of(j);
+        const uint8_t* ord = ord_lds + RPW * w + LPL * h;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+        if (h == 0) part[w * TV + c] = pw;
+        lds_barrier();
+        if (w == 0 && h == 0) {
+            const int o = owner_of(t);
+            const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
+            ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, res, epoch);
+        }
+    }
+    __syncthreads();   // every wave is past A: buf may be reused below
+    uint4* xs = buf[0];   // [8 GPUs][32 columns] partials, then [32] results / [4][32] B rows
+    // ---- R: the tiles I own: W partials from my inbox -> every GPU's result box
+    for (int j = 0; j < mine; ++j) {
+        const uint64_t t = tile_of(j);
+        if (owner_of(t) != me) continue;
+        const uint64_t li = t - (uint64_t)me * tiles_per_owner;
+        const int q = threadIdx.x >> 5;   // source GPU of this lane's slot
+        if (q < W) xs[q * 32 + c] = ll_get(my_ll + (li * W + q) * 128 + c * 4, epoch, status);
+        __syncthreads();
+        if (threadIdx.x < 32) {
+            const uint4 s0 = xs[me * 32 + c];
+            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+            for (int qq = 0; qq < W; ++qq) {
+                if (qq == me) continue;
+                const uint4 y = xs[qq * 32 + c];
+                a[0] += lo_f(y.x); a[1] += hi_f(y.x);
+                a[2] += lo_f(y.y); a[3] += hi_f(y.y);
+                a[4] += lo_f(y.z); a[5] += hi_f(y.z);
+                a[6] += lo_f(y.w); a[7] += hi_f(y.w);
+            }
+            uint4 o;
+            o.x = pack_rne(a[0], a[1]);
+            o.y = pack_rne(a[2], a[3]);
+            o.z = pack_rne(a[4], a[5]);
+            o.w = pack_rne(a[6], a[7]);
+            xs[8 * 32 + c] = o;
+        }
+        __syncthreads();
+        if (q < W) ll_put(lp.ll[q] + box_words + t * 128 + c * 4, xs[8 * 32 + c], epoch);
+        __syncthreads();   // xs is reused by the next owned tile
+    }
+    // ---- B: my result box -> the 64 rank rows, 4 tiles at a time
+    constexpr int BB = 4;
+    for (int j0 = 0; j0 < mine; j0 += BB) {
+        const int nb = mine - j0 < BB ? mine - j0 : BB;
+        const int b = threadIdx.x >> 5;
+        if (b < nb) xs[16 * 32 + b * 32 + c] = ll_get(my_ll + box_words + tile_of(j0 + b) * 128 + c * 4, epoch, status);
+        __syncthreads();
+        uint4 res[BB];
+#pragma unroll
+        for (int bb = 0; bb < BB; ++bb)
+            if (bb < nb) res[bb] = xs[16 * 32 + bb * 32 + c];
+        __syncthreads();   // xs is reused by the next batch
+#pragma unroll
+        for (int bb = 0; bb < BB; ++bb) {
+            if (bb >= nb) break;
+            const uint64_t v0 = tile_of(j0 + bb) * TV;
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                const int r = RPW * w + 2 * k + h;
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res[bb]);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_peer_mem_ll: allred_mem_2D across GPUs for small buckets with LL hand-offs
+// (the flat counterpart of k_hier_ll).  A: every vector is pushed as four
+// data+epoch words to its block owner's inbox; R: the owner polls the W
+// copies of each of its vectors (all loads in flight at once), sums them in
+// fp32 owner first then ascending, one rounding (allred_mem_2D semantics, the
+// bits of k_peer_oneshot), and pushes the result into every GPU's box; B:
+// every GPU polls its box and writes its bucket.  Two one-way trips, no flag,
+// no remote read.  A never waits and the grid is resident (<= 128 groups), so
+// every wait of R and B is reached.  LL layout of the call's parity:
+// [inbox: owned vectors][W][4 words], then [box: vectors][4 words].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me, uint16_t* __restrict__ bucket,
+                                                        uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status) {
+    const uint64_t gt = gtid(), GT = gthreads();
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint64_t* const my_ll = lp.ll[me];
+    const uint64_t box = nv * 4;
+    for (uint64_t v = gt; v < nv; v += GT) {   // A
+        const int o = (int)(v / bv);
+        // the owner's area by an unrolled select over the (scalar) kernarg pointers: a
+        // per-lane index into lp.ll would be a vector load waiting behind every store
+        uint64_t* dst = lp.ll[0];
+#pragma unroll
+        for (int q = 1; q < kLLMaxGpus; ++q)
+            if (o == q) dst = lp.ll[q];
+        ll_put(dst + ((v - (uint64_t)o * bv) * W + me) * 4, ld_nt(bk + v), epoch);
+    }
+    for (uint64_t u = gt; u < bv; u += GT) {   // R: my block
+        const uint64_t* slots = my_ll + u * W * 4;
+        uint4 y[kLLMaxGpus];
+        for (uint64_t spin = 0;; ++spin) {
+            uint64_t wv[kLLMaxGpus][4];
+#pragma unroll
+            for (int q = 0; q < kLLMaxGpus; ++q)
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    wv[q][e] = q < W ? __hip_atomic_load(slots + q * 4 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                                     : (uint64_t)epoch << 32;
+            uint32_t bad = 0;
+#pragma unroll
+            for (int q = 0; q < kLLMaxGpus; ++q) {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bad |= (uint32_t)(wv[q][e] >> 32) ^ epoch;
+                y[q] = make_uint4((uint32_t)wv[q][0], (uint32_t)wv[q][1], (uint32_t)wv[q][2], (uint32_t)wv[q][3]);
+            }
+            if (bad == 0) break;
+            if (peer_give_up(spin, status)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        float a[8];
+#pragma unroll
+        for (int q = 0; q < kLLMaxGpus; ++q) {
+            if (q != me) continue;
+            a[0] = lo_f(y[q].x); a[1] = hi_f(y[q].x); a[2] = lo_f(y[q].y); a[3] = hi_f(y[q].y);
+            a[4] = lo_f(y[q].z); a[5] = hi_f(y[q].z); a[6] = lo_f(y[q].w); a[7] = hi_f(y[q].w);
+        }
+#pragma unroll
+        for (int q = 0; q < kLLMaxGpus; ++q) {
+            if (q >= W || q == me) continue;
+            a[0] += lo_f(y[q].x); a[1] += hi_f(y[q].x);
+            a[2] += lo_f(y[q].y); a[3] += hi_f(y[q].y);
+            a[4] += lo_f(y[q].z); a[5] += hi_f(y[q].z);
+            a[6] += lo_f(y[q].w); a[7] += hi_f(y[q].w);
+        }
+        const uint4 r = make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
+        const uint64_t v = (uint64_t)me * bv + u;
+        for (int q = 0; q < W; ++q) ll_put(lp.ll[q] + box + v * 4, r, epoch);
+    }
+    for (uint64_t v = gt; v < nv; v += GT) st_nt(bk + v, ll_get(my_ll + box + v * 4, epoch, status));   // B
+}
+
+// ---------------------------------------------------------------------------
+// k_peer_lo_ll: the LO program of allred_peer_dist_allreduce (one channel)
+// for small buckets with LL hand-offs: step k, every lane pushes its 16 bytes
+// as four self-validating 8-byte words (4 data bytes + the call's epoch) into
+// partner p_k's step-k slot, then polls its OWN step-k slot until the four
+// words of p_k carry the epoch, and adds (one bf16 rounding, the same add as
+// every LO form).  Per step one one-way xGMI trip instead of k_peer_sched's
+// progress flag + remote read round trip; no window, no flag area.  Slots
+// [step][vector][4 words] in the LL area of the call's parity; call k+2 may
+// reuse a parity because finishing call k+1 needs every rank to have started
+// it (the partners of all steps reach every rank of the schedule).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
+                                                       uint64_t nv, uint32_t epoch, uint32_t* status) {
+    const uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (v >= nv) return;
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint4 cur = ld_nt(bk + v);
+    const uint64_t* mine = lp.ll[me];
+    for (int k = 0; k < pr.S; ++k) {
+        const int p = pr.peer[0][k];
+        ll_put(lp.ll[p] + ((uint64_t)k * nv + v) * 4, cur, epoch);
+        cur = add8(cur, ll_get(mine + ((uint64_t)k * nv + v) * 4, epoch, status));
+    }
+    st_nt(bk + v, cur);
+}
+
+int peer_last_error() { return hip_status((int)hipGetLastError()); }
+
+}  // namespace
+
+int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
+                          size_t n, uint32_t epoch, uint32_t* status, void* stream) {
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    hipStream_t st = (hipStream_t)stream;
+    PeerPtrs pp{};
+    for (int q = 0; q < nranks; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+    }
+    const uint64_t nv = n / 8, bv = nv / nranks;
+    // 1. my bucket -> my window (the bytes peers will read)
+    int rc = launch_copy_ranks(bucket, 0, wins[me], 0, 1, n, stream);
+    if (rc != ALLRED_OK) return rc;
+    // 2. everyone's window is written
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, st, pp, nranks, me, epoch, status);
+    // 3. reduce my block from every window
+    hipLaunchKernelGGL(k_peer_rs, dim3(grid_all(bv)), dim3(kBlock), 0, st, pp, nranks, me, bucket, bv);
+    // 4. every block is reduced
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, st, pp, nranks, me, epoch + 1, status);
+    // 5. gather the other blocks
+    hipLaunchKernelGGL(k_peer_ag, dim3(grid_all(bv), nranks), dim3(kBlock), 0, st, pp, me, bucket, bv);
+    return peer_last_error();
+}
+
+int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epoch, uint32_t* status, void* stream) {
+    if (nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    for (int q = 0; q < nranks; ++q) pp.flags[q] = flags[q];
+    hipLaunchKernelGGL(k_peer_barrier, dim3(1), dim3(64), 0, (hipStream_t)stream, pp, nranks, me, epoch, status);
+    return peer_last_error();
+}
+
+int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
+                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, void* stream) {
+    if (!aligned16(bucket) || prog.N > ALLRED_MAX_NODES || prog.C < 1 || prog.C > kPeerMaxChannels ||
+        prog.S > kPeerMaxSteps)
+        return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    for (int q = 0; q < prog.N; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+    }
+    uint64_t per = 0;  // vectors per workgroup sub-slice unit (largest channel)
+    for (int c = 0; c < prog.C; ++c) {
+        const uint64_t u = prog.lo ? prog.len[c] : prog.len[c] / prog.N;
+        if (u > per) per = u;
+    }
+    uint64_t gc = (per + kBlock - 1) / kBlock;
+    const uint64_t gmax = kPeerSchedMaxGroups / prog.C;
+    if (gc > gmax) gc = gmax;
+    if (gc < 1) gc = 1;
+    hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
+                       bucket, half_vec, base_epoch, status);
+    return peer_last_error();
+}
+
+int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
+                       uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream) {
+    const uint64_t nv = n / 8;
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > kLLMaxGpus || 8 * nv > area_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    uint64_t groups = (nv + kBlock - 1) / kBlock;
+    const uint64_t cap = max_groups && max_groups < kPeerFusedMaxGroups ? max_groups : kPeerFusedMaxGroups;
+    if (groups > cap) groups = cap;   // resident: every wait is reached
+    hipLaunchKernelGGL(k_peer_mem_ll, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, lp, nranks, me,
+                       bucket, nv, nv / nranks, epoch, status);
+    return peer_last_error();
+}
+
+int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, const PeerProg& prog, size_t n,
+                      uint64_t area_words, uint32_t epoch, uint32_t* status, void* stream) {
+    const uint64_t nv = n / 8;
+    if (n % 8 || !aligned16(bucket) || nranks > kLLMaxGpus || !prog.lo || prog.C != 1 ||
+        nv * 4 * (uint64_t)prog.S > area_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    hipLaunchKernelGGL(k_peer_lo_ll, dim3((unsigned)((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       (hipStream_t)stream, lp, prog, me, bucket, nv, epoch, status);
+    return peer_last_error();
+}
+
+int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
+                        uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
+                        unsigned max_grid, void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > ALLRED_MAX_NODES || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks))
+        return ALLRED_ERR_ARG;
+    HierPtrs hp{};
+    for (int q = 0; q < nranks; ++q) {
+        hp.win[q] = wins[q];
+        hp.hfl[q] = hflags[q];
+    }
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
+    hipLaunchKernelGGL(k_hier_oneshot, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, hp,
+                       nranks, me, (uint64_t)n, ntiles, ntiles / nranks, epoch, status);
+    return peer_last_error();
+}
+
+int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                   void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
+        ntiles * 128 > box_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
+    hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
+                       me, ntiles, ntiles / nranks, box_words, epoch, status);
+    return peer_last_error();
+}
+
+int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nranks, int me, uint16_t* bucket,
+                        size_t n, uint32_t epoch, uint32_t* status, void* stream) {
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    for (int q = 0; q < nranks; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+    }
+    const uint64_t bv = n / 8 / nranks;
+    uint64_t groups = (bv + 63) / 64;
+    if (groups > kPeerFusedMaxGroups) groups = kPeerFusedMaxGroups;
+    if (groups < 1) groups = 1;
+    const uint64_t chunk = (bv + groups - 1) / groups;
+    hipLaunchKernelGGL(k_peer_oneshot, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, pp, nranks, me,
+                       bucket, bv, chunk, epoch, status);
+    return peer_last_error();
+}
+
+}  // namespace tsa

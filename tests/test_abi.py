@@ -40,15 +40,18 @@ def test_header_constants_match_python_bindings():
     defines = dict(re.findall(r"#define\s+(ALLRED_\w+)\s+(0x[0-9a-fA-F]+|\d+)u?\b", src))
     assert int(defines["ALLRED_PEER_HANDLE_BYTES"], 0) == _lib.PEER_HANDLE_BYTES
     assert int(defines["ALLRED_PEER_TIMEOUT"], 0) == t.PEER_TIMEOUT
+    assert int(defines["ALLRED_ABI_VERSION"], 0) == _lib.ABI_VERSION
+    assert (int(defines["ALLRED_ACC_FP32"]), int(defines["ALLRED_ACC_BF16"])) == (t.ACC_FP32, t.ACC_BF16)
 
 
 def test_status_strings():
-    assert _lib.lib.allred_abi_version() == 1
+    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 2
     for st in range(0, -8, -1):
         assert _lib.lib.allred_status_string(st)
 
 
-REF_DEFAULTS = dict(swing=0, run_kernel=0, side_length=1, seed=0, tiles=1, error=1, print_core=0, bandwidth_optimal=0)
+REF_DEFAULTS = dict(swing=0, run_kernel=0, side_length=1, seed=0, tiles=1, error=1, print_core=0, bandwidth_optimal=0,
+                    exec=t.EXEC_FUSED, device=-1, mem_accum=t.ACC_FP32)
 
 
 @pytest.mark.parametrize("argv,want", [
@@ -83,6 +86,72 @@ def test_args_parse_variants():
     assert a.num_tiles == 320 and a.print_core == 0
     a = t.parse_args(["allred_LO_2D", "1", "1", "8", "13", "5", "32"], t.LO)
     assert a.num_tiles == 8
+
+
+def test_args_parse_extension_envs(monkeypatch):
+    """Extensions never change a reference invocation: the one-pass form is the
+    default (ALLRED_EXEC=steps opts into the step structure), ALLRED_DEVICE
+    names the HIP device (the reference's CreateDevice(0), allred_BO_2D.cpp:8),
+    ALLRED_MEM_ACC=bf16 the reference's bf16 dest accumulation."""
+    argv = ["allred_mem_2D", "1", "1", "8", "13", "5", "32"]
+    monkeypatch.setenv("ALLRED_EXEC", "steps")
+    monkeypatch.setenv("ALLRED_DEVICE", "3")
+    monkeypatch.setenv("ALLRED_MEM_ACC", "bf16")
+    a = t.parse_args(argv, t.MEM)
+    assert (a.exec, a.device, a.mem_accum) == (t.EXEC_STEPS, 3, t.ACC_BF16)
+    monkeypatch.setenv("ALLRED_DEVICE", "x")
+    with pytest.raises(t.AllredError):
+        t.parse_args(argv, t.MEM)
+
+
+def test_tune_entry_point():
+    """allred_tune_set / allred_tune_get: the one switch for bit-identical kernel forms."""
+    assert t.tune("steps_form") == 0 and t.tune("lo_tree") == 1 and t.tune("fused_form") == 0
+    with t.tuned(steps_form=1, lo_dag_min_tiles=1024):
+        assert t.tune("steps_form") == 1 and t.tune("lo_dag_min_tiles") == 1024
+    assert t.tune("steps_form") == 0 and t.tune("lo_dag_min_tiles") == 256
+    with pytest.raises(t.AllredError):
+        t.tune("no_such_key")
+    with pytest.raises(t.AllredError):
+        t.tune("fused_form", 9)          # out of range
+    assert t.tune("fused_form") == 0
+
+
+def test_tune_env_is_read_at_load():
+    code = ("import sys; sys.path.insert(0, %r); import tenstorrentallreduce_amd as t;"
+            "print(t.tune('steps_form'), t.tune('lo_dag_place'), t.tune('pipe_grid'))" % ROOT)
+    env = dict(os.environ, ALLRED_TUNE="steps_form=1,lo_dag_place=0,bogus=3,pipe_grid=99999999")
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env).stdout.split()
+    assert out == ["1", "0", "0"]   # out-of-range and unknown keys are ignored
+
+
+def test_peer_window_limit_without_gpu():
+    """allred_peer_create rejects any window over 1 GiB (a ~2 GiB IPC export hung
+    the peer's hipIpcOpenMemHandle, profiles/r01_peer_open_probe_2gib_hang.txt)
+    before any HIP call, so the limit holds on a machine without a GPU."""
+    import ctypes as C
+    h = C.c_void_p()
+    for elems in ((1 << 29) + 1, 1 << 30, 3 << 29):
+        assert _lib.lib.allred_peer_create(2, 0, -1, elems, C.byref(h)) == _lib.ERR_ARG
+        assert not h.value
+    assert _lib.PEER_MAX_WINDOW_BYTES == 1 << 30
+
+
+@pytest.mark.parametrize("algo,variant,chans", [(t.SWING, t.BO, 7), (t.RECDUB, t.BO, 7), (t.RECDUB, t.BO, 1),
+                                                (t.SWING, t.LO, 1), (t.SWING, t.BO, 3)])
+def test_dist_program_one_add_launch_per_step(algo, variant, chans):
+    """The RCCL program (dist.cpp) adds every received run of every link-spreading
+    channel of a step in ONE launch: 8 ranks (4x2), BO = 3 reduce-scatter steps
+    with adds + 3 all-gather steps without; LO = 3 add steps."""
+    n = 8 * 8 * 7 * 640 * 4
+    desc = t.dist_desc(algo, variant, 4, 8, n, channels=chans)
+    for rank in range(8):
+        st = t.dist_program_stats(desc, rank)
+        if variant == t.BO:
+            assert st["steps"] == 6 and st["add_launches"] == 3, st
+        else:
+            assert st["steps"] == 3 and st["add_launches"] == 3, st
+        assert st["segments"] >= st["steps"] * 2 * (chans if variant == t.BO else 1)
 
 
 @pytest.mark.parametrize("bad", [["x"], ["1", "1", "abc"], ["1", "1", "8", "13", "99999999999"]])

@@ -2,6 +2,7 @@
 (README.md:23-45, python/timing_taker.py:60-65).  Pass signal = the
 reference's own stdout line "All values match!" (allred_helper.cpp:75)."""
 import json
+import os
 
 import pytest
 
@@ -90,3 +91,55 @@ def test_config2_fused_both_end_to_end_modes(e2e):
     out, rep = run("allred_BO_2D", ["1", "1", "8", "13", "5", "32", "0", "1"], ALLRED_EXEC="fused", ALLRED_E2E=e2e)
     assert "All values match!" in out
     assert rep["mismatches"] == 0
+
+
+@pytest.mark.parametrize("exec_mode", ["steps", "fused"])
+def test_allredconfig_runprogram_cpp_program(exec_mode):
+    """A reference-style C++ program against include/allred_helper.hpp alone
+    (bin/allred_config_main: AllredConfig(argc, argv, ALLRED_BO, device 0)
+    .RunProgram(), the shape of allred_BO_2D.cpp:7-215) on BASELINE config 2;
+    its pass signal is the reference's own stdout line."""
+    import os
+    import subprocess
+    exe = os.path.join(t._lib.BIN_DIR, "allred_config_main")
+    env = dict(os.environ, ALLRED_EXEC=exec_mode, ALLRED_CHECK_ALL="1")
+    p = subprocess.run([exe, "0", "1", "1", "8", "13", "5", "32", "0", "1"], capture_output=True, text=True,
+                       env=env, timeout=120)
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.startswith("All values match!\n"), p.stdout
+    assert "ranks 64 tiles 320 device 0" in p.stdout
+
+
+def test_cli_default_is_the_fused_form():
+    """The one-pass form is the reference CLI's default (bit-identical to the
+    step structure, which ALLRED_EXEC=steps keeps): one launch per allreduce."""
+    _, rep = run("allred_BO_2D", ["1", "1", "8", "13", "5", "32", "0", "1"])
+    assert rep["launches"] == 1 and rep["mismatches"] == 0
+    _, rep = run("allred_BO_2D", ["1", "1", "8", "13", "5", "32", "0", "1"], ALLRED_EXEC="steps")
+    assert rep["launches"] == 1 and rep["mismatches"] == 0   # the schedule form is one persistent launch too
+
+
+@pytest.mark.parametrize("argv,bo", [(["1", "1", "8", "13", "5", "32", "0", "1"], True),
+                                     (["0", "1", "8", "13", "5", "32", "0", "1"], True),
+                                     (["1", "1", "8", "13", "16", "32", "0", "0"], False)])
+def test_profile_log_per_rank_zones(argv, bo, tmp_path):
+    """ALLRED_PROFILE_LOG (the reference's TT_METAL_DEVICE_PROFILER=1 +
+    profile_log_device.csv): the schedule form stamps every unit on the device
+    (s_memrealtime), the library turns them into each rank's ALL_RED_LOOP zone,
+    and the reference's analysis (tools/profile_analyzer.py) reads the CSV:
+    64 cores, each zone non-empty, every start before every rank's end."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from profile_analyzer import analyze, normalized
+    log = tmp_path / "profile_log_device.csv"
+    out, rep = run("allred_BO_2D", argv, ALLRED_EXEC="steps", ALLRED_E2E="dma", ALLRED_PROFILE_LOG=str(log))
+    assert "All values match!" in out
+    stats = analyze(str(log))
+    assert stats["cores"] == 64 and stats["min"] > 0
+    norm = normalized(str(log))
+    assert len(norm) == 64
+    starts = [s for s, _ in norm.values()]
+    ends = [e for _, e in norm.values()]
+    assert min(starts) == 0 and max(starts) < min(ends)
+    # zones lie inside the event-timed device interval (100 MHz ticks), with slack for clock skew
+    assert max(ends) <= rep["device_s"] * 1e8 * 1.2 + 200

@@ -206,36 +206,37 @@ def test_lo_sizes_reference_inputs(tiles, exec_mode):
     assert (got == np.stack(want)).all()
 
 
-@pytest.mark.parametrize("place", ["1", "0"])
+@pytest.mark.parametrize("place,dag", [(1, 1), (0, 1), (1, 0)])
 @pytest.mark.parametrize("n", [1024 * 64, 327680])
-def test_fused_lo_dag_placement(n, place, monkeypatch):
+def test_fused_lo_dag_placement(n, place, dag):
     """The fused Swing 8x8 LO DAG pass (k_butterfly_lds64_pipe<4>) with its
-    bank-conflict-free node placement (engine.cpp lo_dag_place) and with
-    first-appearance rows and slots (ALLRED_DAG_PLACE=0): both bit-exact vs the
+    bank-conflict-free node placement (engine.cpp lo_dag_place), with
+    first-appearance rows and slots (tune lo_dag_place=0), and the per-rank
+    butterfly (lo_dag=0, k_butterfly_lds64_pipe<0>): all bit-exact vs the
     oracle's per-rank butterfly (allred_BO_2D/kernels/dataflow_kernel.cpp:19-29)."""
-    monkeypatch.setenv("ALLRED_DAG_PLACE", place)
     side, total = 8, 64
     ranks = rand_ranks(total, n, seed=71 + n % 97)
-    got = run_plan(t.SWING, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
+    with t.tuned(lo_dag_place=place, lo_dag=dag):
+        got = run_plan(t.SWING, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
     want = [r.copy() for r in ranks]
     oracle.allreduce("lo", t.SWING, side, want, total)
     assert (got == np.stack(want)).all()
 
 
-@pytest.mark.parametrize("lo_tree", ["1", "0"])
+@pytest.mark.parametrize("lo_tree", [1, 0])
 @pytest.mark.parametrize("algo,grid,n", [
     (t.RECDUB, (8, 64), 327680), (t.RECDUB, (8, 64), 1024 * 16), (t.RECDUB, (4, 16), 1024 * 64),
     (t.RECDUB, (2, 4), 1024), (t.SWING, (4, 16), 1024 * 64), (t.SWING, (2, 4), 1024),
     (t.RECDUB_1D, (8, 64), 1024 * 64), (t.SWING_1D, (2, 4), 1024 * 8)])
-def test_fused_lo_rank_uniform_tree_route(algo, grid, n, lo_tree, monkeypatch):
+def test_fused_lo_rank_uniform_tree_route(algo, grid, n, lo_tree):
     """Schedules whose LO trees are all the same up to child swaps (every RecDub,
     Swing up to 16 ranks) run the fused LO as the BO tree pass (engine.cpp
-    lo_rank_uniform); ALLRED_LO_TREE=0 keeps the butterfly.  Both against the
+    lo_rank_uniform); tune lo_tree=0 keeps the butterfly.  Both against the
     oracle's butterfly, bit-exact."""
-    monkeypatch.setenv("ALLRED_LO_TREE", lo_tree)
     side, total = grid
     ranks = rand_ranks(total, n, seed=29 + total + algo)
-    got = run_plan(algo, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
+    with t.tuned(lo_tree=lo_tree):
+        got = run_plan(algo, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
     want = [r.copy() for r in ranks]
     oracle.allreduce("lo", algo, side, want, total)
     assert (got == np.stack(want)).all()

@@ -104,12 +104,10 @@ def worker(rank, world, port, q):
         # launch form, two calls back to back each (then LL once more after the
         # launch form: its LL boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
-        # k_hier_ws (pipelined, specialised waves) in full and capped grids (a
-        # capped grid gives every workgroup many tiles: the whole pipeline)
+        # in full and capped grids (a capped grid gives every workgroup many tiles)
         for mi, (mode, limit, ll, cap) in enumerate((("hier_one_kernel", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
-                                                     ("hier_ws", 0, 2, 0), ("hier_ws_capped", 0, 2, 2),
-                                                     ("hier_ws_one_group", 0, 2, 1))):
+                                                     ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1))):
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
             peer.set_max_groups(cap)
@@ -311,8 +309,8 @@ def t_timeout_bit():
 
 @pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
 def test_hier_forms_single_gpu_bit_exact(n, cap):
-    """One GPU (W = 1), 64 local ranks: the pipelined k_hier_ws, the phased
-    k_hier_ll, the flag form k_hier_oneshot and the launch form give the same
+    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll, the flag form
+    k_hier_oneshot and the launch form give the same
     bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
     mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
     (both LL parities).  Config-2 size full grid and with capped grids (many
@@ -333,7 +331,7 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit in ((2, 0), (1, 0), (0, 1 << 40), (0, 0), (2, 0)):
+        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (1, 0)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
@@ -360,7 +358,7 @@ def test_peer_knob_argument_errors():
     peer.connect([peer.handle()])
     try:
         with pytest.raises(_lib.AllredError):
-            peer.set_hier_ll(3)            # 0, 1 or 2 only
+            peer.set_hier_ll(2)            # 0 or 1 only (the pipelined form is a tools/ubench study)
         with pytest.raises(_lib.AllredError):
             peer.set_hier_ll(-1)
         peer.set_lo_ll_max(0)
@@ -373,3 +371,71 @@ def test_peer_knob_argument_errors():
             peer.allreduce(buf.data_ptr(), 12, torch.cuda.current_stream())
     finally:
         peer.close()
+
+
+def config35_worker(rank, world, port, q):
+    """BASELINE config 3 (8-rank RecDub BO, 655,360 B per rank; one channel and
+    all 7 link-spreading channels) and config 5 (8-rank Swing LO at 2 / 8 / 32 /
+    128 kB; LL pushes and the scheduled flag form) through
+    allred_peer_dist_allreduce with 8 processes, bit-exact vs the oracle, then
+    allred_peer_check (no peer wait timed out)."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import tenstorrentallreduce_amd as t
+        import test_dist_host as tdh
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        side, total = tdh.GRIDS[world]
+        peer = t.Peer(world, rank, 0, 327680)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        fails = []
+        cases = [("bo", t.RECDUB, 327680, 1, 256 << 10), ("bo", t.RECDUB, 327680, 7, 256 << 10)]
+        for n in (1024, 4096, 16384, 65536):
+            cases += [("lo", t.SWING, n, 1, 256 << 10), ("lo", t.SWING, n, 1, 0)]
+        for ci, (variant, algo, n, chans, ll_max) in enumerate(cases):
+            peer.set_lo_ll_max(ll_max)
+            desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, side, total, n, channels=chans)
+            for rep in range(2):   # both window parities
+                data = tdh.inputs(world, 1, n, seed=7000 + 10 * ci + rep)
+                buf = torch.from_numpy(data[rank][0].view(np.int16)).to("cuda:0")
+                peer.dist_allreduce(desc, buf.data_ptr(), None, torch.cuda.current_stream(), check_status=True)
+                want = tdh.expected(variant, algo, world, 1, data, chans)[rank][0]
+                got = buf.cpu().numpy().view(np.uint16)
+                if not np.array_equal(got, want):
+                    fails.append((variant, algo, n, chans, ll_max, rep, int((got != want).sum())))
+            dist.barrier()
+        status = peer.status()
+        dist.barrier()
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+def test_config3_config5_eight_processes():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    world = 8
+    procs = [ctx.Process(target=config35_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in procs:
+            results.append(q.get(timeout=240))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails, status in results:
+        assert fails == [], (rank, fails)
+        assert status == 0, (rank, status)

@@ -73,11 +73,8 @@ def test_swing_dag_shape_and_placement():
     dag, conflicts = lo_dag(t.SWING)
     assert list(dag[448:454]) == [32, 16, 16, 16, 8, 4]   # 92 distinct sums per column
     assert conflicts == 0
-    os.environ["ALLRED_DAG_PLACE"] = "0"
-    try:
+    with t.tuned(lo_dag_place=0):
         unplaced, c0 = lo_dag(t.SWING)
-    finally:
-        del os.environ["ALLRED_DAG_PLACE"]
     assert c0 == 92   # first-appearance rows and slots: one extra cycle per read group and item on average
     np.testing.assert_array_equal(evaluate(unplaced, np.arange(64 * 8, dtype=np.uint16).reshape(64, 8) + 0x3F80),
                                   evaluate(dag, np.arange(64 * 8, dtype=np.uint16).reshape(64, 8) + 0x3F80))

@@ -3,6 +3,11 @@
   python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> \
       <kernel-substring> <key> <algorithmic_bytes_per_launch> [out.json]
 
+<key> is the kernel template the bench launches (bench.py FUSED_KERNEL, e.g.
+k_tree_lds_lag<64>); it is stored as "template" with the full Kernel_Name the
+counters were taken on and the git sha of the build (env PMC_GIT_SHA: the GPU
+box has no .git), so bench.py only reports traffic measured on its kernel.
+
 Counters are collected in SEPARATE passes (FETCH_SIZE uses 3 TCC slots,
 WRITE_SIZE 2).  Both are in KiB.  gfx950 correction: FETCH_SIZE reports half
 the bytes of a wide coalesced streaming read (16 B/lane) — doubled here;
@@ -15,13 +20,15 @@ import sys
 from collections import defaultdict
 
 
-def per_dispatch(path, counter, kernel_sub):
+def per_dispatch(path, counter, kernel_sub, names=None):
     vals = defaultdict(float)
     for r in csv.DictReader(open(path)):
         if kernel_sub not in r.get("Kernel_Name", ""):
             continue
         if r.get("Counter_Name") != counter:
             continue
+        if names is not None:
+            names.add(r["Kernel_Name"])
         vals[r.get("Dispatch_Id") or r.get("Correlation_Id")] += float(r["Counter_Value"])
     return list(vals.values())
 
@@ -30,11 +37,14 @@ def main():
     fetch_csv, write_csv, kernel_sub, key, alg = sys.argv[1:6]
     out_path = sys.argv[6] if len(sys.argv) > 6 else None
     alg = int(alg)
-    f = per_dispatch(fetch_csv, "FETCH_SIZE", kernel_sub)
-    w = per_dispatch(write_csv, "WRITE_SIZE", kernel_sub)
+    names = set()
+    f = per_dispatch(fetch_csv, "FETCH_SIZE", kernel_sub, names)
+    w = per_dispatch(write_csv, "WRITE_SIZE", kernel_sub, names)
     fetch_b = 2 * 1024 * statistics.median(f)  # gfx950: FETCH_SIZE reads half of wide streaming loads
     write_b = 1024 * statistics.median(w)
-    res = {"kernel": kernel_sub, "dispatches": [len(f), len(w)], "fetch_size_kib_median": statistics.median(f),
+    import os
+    res = {"kernel": kernel_sub, "template": key, "kernel_names": sorted(names),
+           "git_sha": os.environ.get("PMC_GIT_SHA", "unknown"), "dispatches": [len(f), len(w)], "fetch_size_kib_median": statistics.median(f),
            "write_size_kib_median": statistics.median(w), "read_bytes_corrected": fetch_b, "write_bytes": write_b,
            "hbm_bytes_per_launch": int(fetch_b + write_b), "algorithmic_bytes_per_launch": alg,
            "ratio_to_algorithmic": round((fetch_b + write_b) / alg, 4)}

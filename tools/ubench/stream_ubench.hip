@@ -3,7 +3,7 @@
 // Includes the product kernels translation unit so the baseline arms are the
 // shipped kernels; candidate arms are defined here.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include -I../../tenstorrentallreduce_amd/csrc \
-//         stream_ubench.hip -o stream_ubench
+//         stream_ubench.hip -o stream_ubench -L../../tenstorrentallreduce_amd/lib -lallred
 #include "../../tenstorrentallreduce_amd/csrc/kernels.hip"
 
 #include <algorithm>
