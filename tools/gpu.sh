@@ -1,0 +1,53 @@
+#!/bin/bash
+# tools/gpu.sh <what> [args] — the GPU-box command lines of this repo, run as
+#   /usr/local/graft/bin/gpurun --timeout <s> -- 'bash tools/gpu.sh <what>'
+# Every GPU step has its own time limit and the steps are chained with &&:
+# after a fault or a timeout nothing more runs on the GPU in that call.
+#   test [pytest args]   pytest -m gpu (per-test thread timeouts), then smoke()
+#   smoke                __graft_entry__.smoke()
+#   bench [bench args]   bench.py (default: the driver's N = 1 line)
+#   prof <tag>           rocprofv3 --kernel-trace --stats of bench.py --main-only,
+#                        then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+what=$1
+shift
+case "$what" in
+test)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -q -rf --maxfail=20 --timeout 240 \
+        --timeout-method thread "$@" > gpurun_out/gpu_tests.log 2>&1
+    rc=$?
+    tail -25 gpurun_out/gpu_tests.log
+    [ $rc -eq 0 ] && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
+    ;;
+smoke)
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
+    ;;
+bench)
+    timeout -k 10 600 python bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err
+    rc=$?
+    tail -3 gpurun_out/bench.err
+    cat gpurun_out/bench.json
+    exit $rc
+    ;;
+prof)
+    tag=${1:-prof}
+    out=gpurun_out/$tag
+    mkdir -p "$out"
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run -- \
+        python3 bench.py --main-only --steps 200 --warmup 20 > "$out/bench.json" 2> "$out/bench.err" &&
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -- \
+        python3 bench.py --main-only --steps 100 --warmup 10 --eager > /dev/null 2> "$out/fetch.err" &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -- \
+        python3 bench.py --main-only --steps 100 --warmup 10 --eager > /dev/null 2> "$out/write.err"
+    rc=$?
+    find "$out" -name "*.csv" | head -20
+    exit $rc
+    ;;
+*)
+    echo "usage: $0 test|smoke|bench|prof" >&2
+    exit 2
+    ;;
+esac
