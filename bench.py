@@ -133,12 +133,17 @@ def bench_single(args) -> dict:
     def step(i, p=plan):
         p.execute(sets[i % nsets].data_ptr(), stride, None, stream)
 
-    # the K timed steps as one HIP graph, captured BEFORE the prewarm so that no
-    # host-only phase (capture) sits between the steady-clock prewarm and the
-    # timed replays (a capture gap after the prewarm measured 14.8 us per step at
-    # K = 20 vs 14.2-14.3 at K = 200: the clocks had dropped)
+    # How the K timed steps are issued (tools/timing_probe.py, profiles/r02_timing_methods.jsonl):
+    #   K >= 100: R back-to-back replays of a K-step HIP graph; each replay of a
+    #     ROCm graph starts with a fixed ~7 us of GPU-side launch latency, which
+    #     costs < 0.1 us per step here (K = 200: 14.02 us graph vs 14.14 eager);
+    #   K < 100: K eager launches behind a spin kernel that covers the host's
+    #     submission (K = 20: 14.2-14.4 us vs 14.4-14.6 for graph replays).
+    # The graph is captured BEFORE the prewarm, so no host-only phase sits
+    # between the steady-clock prewarm and the timed steps.
+    use_graph = not args.eager and args.steps >= 100
     graph = None
-    if not args.eager:
+    if use_graph:
         try:
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=stream):
@@ -164,18 +169,17 @@ def bench_single(args) -> dict:
             step(i)
     torch.cuda.synchronize()
 
-    # R back-to-back replays of the K steps, an event between consecutive ones;
-    # ms_per_step = the median replay / K (each interval is exactly K steps; the
-    # GPU never idles between them).  The whole R x K region is bracketed by
-    # synchronize on both sides.
+    # R repetitions of the K timed steps, an event between consecutive ones;
+    # ms_per_step = the median repetition / K (each interval is exactly K
+    # steps).  The whole R x K region is bracketed by synchronize on both sides.
     reps = max(1, args.reps)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     with torch.cuda.stream(stream):
-        # a ~0.1 ms spin kernel ahead of the first event keeps the GPU busy while
-        # the host submits the replays (host_wall_s below includes everything)
-        torch.cuda._sleep(200000)
+        # a spin kernel ahead of the first event keeps the GPU busy while the host
+        # submits (eager: ~4 us of host time per launch; host_wall_s below includes everything)
+        torch.cuda._sleep(max(200000, 15000 * args.steps * (1 if graph is not None else reps)))
     ev[0].record(stream)
     for r in range(reps):
         k_steps()
@@ -242,7 +246,7 @@ def bench_single(args) -> dict:
     torch.cuda.synchronize()
     c1_ok = bool((c1 == 0x4080).all())   # every element = 4.0 (the known answer)
     c1_graph = None
-    if graph is not None:   # the same launches replayed from a HIP graph, as the main workload
+    if not args.eager:   # the same launches replayed from a HIP graph (launch-bound: the graph is the faster)
         try:
             c1_graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(c1_graph, stream=stream):
@@ -294,8 +298,9 @@ def bench_single(args) -> dict:
         "dtype": "bf16",
         "data": "synthetic (uniform [0,100) bf16, reference rank convention); 32 rotating bucket sets in HBM (1.3 GB), "
                 "rank rows 655,360 B + 128 B skew",
-        "timing": {"replays": reps, "ms_per_replay": [round(x, 5) for x in rep_ms],
-                   "ms_per_step": "median replay / steps (each replay = the K steps, back to back)"},
+        "timing": {"method": "hip_graph_replays" if graph is not None else "eager_behind_spin_kernel",
+                   "repetitions": reps, "ms_per_repetition": [round(x, 5) for x in rep_ms],
+                   "ms_per_step": "median repetition / steps (each repetition = the K steps, back to back)"},
         "config": {"workload": "BASELINE config 2: 8x8 Swing BO allreduce, 64 virtual ranks x 655,360 B bf16 "
                                "(5 tiles/block) on one MI355X, fused one-pass HIP kernel, no RCCL",
                    "ranks": RANKS, "bytes_per_rank": ELEMS * 2, "algo": "swing", "variant": "BO",

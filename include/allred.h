@@ -46,7 +46,7 @@ extern "C" {
 #define ALLRED_LO 1
 #define ALLRED_MEM 2
 /* execution form of a virtual-rank plan */
-#define ALLRED_EXEC_STEPS 0  /* the reference's step structure: every step's result stored to the buckets */
+#define ALLRED_EXEC_STEPS 0  /* the reference's step program, step by step (partner exchange + add per step) */
 #define ALLRED_EXEC_FUSED 1  /* one HBM pass for the whole allreduce, same arithmetic, same bits */
 /* mem_2D accumulation (allred_mem_2D/kernels/compute_kernel.cpp:44-67) */
 #define ALLRED_ACC_FP32 0    /* fp32 sum, rounded to bf16 once (default) */
@@ -115,7 +115,7 @@ int allred_schedule_build(int algo, int side_length, int total_nodes, allred_sch
  * the bytes written, 0 when the schedule has no DAG form (not 64 ranks, a
  * step with more than 32 distinct sums), or a negative status.
  * *read_conflicts = extra LDS bank cycles of its reads per column group and
- * tile (0 once placed; ALLRED_DAG_PLACE=0 keeps first-appearance order). */
+ * tile (0 once placed; allred_tune_set("lo_dag_place", 0) keeps first-appearance order). */
 int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size_t cap, int* read_conflicts);
 
 /* ======================================================================
@@ -208,7 +208,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   lo_dag_place      1: bank-conflict-free DAG placement (0 = first-appearance order)
  *   lo_dag_min_tiles  256: smallest bucket (256-element tiles) for the DAG pass
  *   mem_reduce_lds    1: mem_2D schedule-form reduce staged through LDS
- *   steps_form        0: schedule form as one persistent launch | 1: one launch per step
+ *   steps_form        schedule form: 0 one persistent launch (rank copies in LDS between steps)
+ *                     | 1 one launch per step (rank copies in the buckets)
  *   pipe_grid         0: auto grid of the persistent passes
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference

@@ -48,9 +48,7 @@ struct allred_plan {
     uint8_t* d_order = nullptr;
     uint8_t* d_dag = nullptr;               // LO: interned DAG (lo_dag_lanes form), 64 ranks only
     uint8_t* d_steps_tab = nullptr;         // schedule form, one launch: BO per-block phase ranks / LO step pairs
-    uint8_t* d_partner8 = nullptr;          // [steps][total] uint8 (BO schedule form)
     bool steps_persistent = false;          // schedule form as one launch (k_bo_steps / k_lo_steps)
-    std::vector<int8_t> last_phase;         // BO schedule form: [block][rank] phase of the rank's last write
     size_t ws_bytes = 0;
     int launches = 0;
     const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
@@ -85,7 +83,6 @@ void free_plan(allred_plan* p) {
     if (p->d_order) (void)hipFree(p->d_order);
     if (p->d_dag) (void)hipFree(p->d_dag);
     if (p->d_steps_tab) (void)hipFree(p->d_steps_tab);
-    if (p->d_partner8) (void)hipFree(p->d_partner8);
     delete p;
 }
 
@@ -129,49 +126,78 @@ bool env_is(const char* name, const char* value) {
     return v && std::string(v) == value;
 }
 
-// BO schedule form (k_bo_steps): per block b, the ranks WRITTEN at each of the
-// 2S phases — RS step k: the holders r with b in recv_k(r) (N >> (k+1) of
-// them); AG step k (phases S .. 2S-1 = steps S-1 .. 0): the receivers r with b
-// in send_k(r) — phase-major, 2(N-1) bytes per block.  last[b][r] = the phase
-// of rank r's last write of block b (the owner's last RS step, everyone else's
-// AG step), for the per-rank zones of the stamps.
-std::vector<uint8_t> bo_steps_table(const allred_schedule& s, int N, std::vector<int8_t>* last) {
-    const int S = s.steps;
+// BO schedule form (k_bo_steps, kernels.hip): per block b, in phase order,
+//   RS step 0          (r, p) for the N/2 holders r of b (recv_0(r) has b), row i = i-th holder
+//   RS 1..S-1, AG S-1..1  (row of r, row of p) for the step's N >> (k+1) writers r (RS:
+//                      holders of b, AG: receivers, b in send_k(r)), p = partner_k(r)
+//   AG step 0          (r, row of p) for the N/2 receivers r (the step-0 non-holders)
+//   then the N/2 holders' ranks in row order.
+// Every operand of steps >= 1 is a step-0 holder's row (a partner that sends b
+// at RS step k held b at step k-1; AG steps >= 1 stay among the holders), which
+// the builder checks: 4(N-1) + N/2 bytes per block, empty if the check fails.
+std::vector<uint8_t> bo_steps_table(const allred_schedule& s, int N) {
+    const int S = s.steps, H = N / 2;
     std::vector<uint8_t> tab;
-    last->assign((size_t)N * N, -1);
     for (int b = 0; b < N; ++b) {
-        for (int q = 0; q < 2 * S; ++q) {
-            const int k = q < S ? q : 2 * S - 1 - q;
+        std::vector<int> row(N, -1), holders;
+        for (int r = 0; r < N; ++r)
+            if ((s.recv[r][0] >> b) & 1ull) row[r] = (int)holders.size(), holders.push_back(r);
+        if ((int)holders.size() != H) return {};
+        for (int r : holders) {
+            tab.push_back((uint8_t)r);
+            tab.push_back((uint8_t)s.partner[r][0]);
+        }
+        for (int q = 1; q < 2 * S; ++q) {
+            const bool rs = q < S;
+            const int k = rs ? q : 2 * S - 1 - q;
             int cnt = 0;
             for (int r = 0; r < N; ++r) {
-                const uint64_t m = q < S ? s.recv[r][k] : s.send[r][k];
-                if ((m >> b) & 1ull) {
+                const uint64_t m = rs ? s.recv[r][k] : s.send[r][k];
+                if (!((m >> b) & 1ull)) continue;
+                const int p = s.partner[r][k];
+                if (row[p] < 0) return {};
+                if (q < 2 * S - 1) {
+                    if (row[r] < 0) return {};
+                    tab.push_back((uint8_t)row[r]);
+                } else {
                     tab.push_back((uint8_t)r);
-                    (*last)[(size_t)b * N + r] = (int8_t)q;
-                    ++cnt;
                 }
+                tab.push_back((uint8_t)row[p]);
+                ++cnt;
             }
-            if (cnt != (N >> (k + 1))) return {};   // not a BO mask set (validated schedules never get here)
+            if (cnt != (N >> (k + 1))) return {};
         }
+        if (S == 0) return {};
+        for (int r : holders) tab.push_back((uint8_t)r);
     }
     return tab;
 }
 
-// LO schedule form (k_lo_steps): per step, the N/2 exchanging pairs (r, p), r < p.
+// LO schedule form (k_lo_steps, kernels.hip): per step, the N/2 exchanging
+// pairs (r, p), r < p, numbered in order (after step k, pair i's two ranks
+// hold the same value: LDS row i); then per step k >= 1, for each of its pairs
+// the rows of its two ranks after step k-1.
 std::vector<uint8_t> lo_steps_pairs(const allred_schedule& s, int N) {
-    std::vector<uint8_t> pairs;
-    for (int k = 0; k < s.steps; ++k) {
+    const int S = s.steps;
+    std::vector<uint8_t> pairs, rows;
+    std::vector<int> prev(N, -1), cur(N, -1);
+    for (int k = 0; k < S; ++k) {
         int cnt = 0;
         for (int r = 0; r < N; ++r) {
             const int p = s.partner[r][k];
-            if (r < p) {
-                pairs.push_back((uint8_t)r);
-                pairs.push_back((uint8_t)p);
-                ++cnt;
+            if (r >= p) continue;
+            pairs.push_back((uint8_t)r);
+            pairs.push_back((uint8_t)p);
+            if (k > 0) {
+                rows.push_back((uint8_t)prev[r]);
+                rows.push_back((uint8_t)prev[p]);
             }
+            cur[r] = cur[p] = cnt++;
         }
         if (cnt != N / 2) return {};
+        prev = cur;
     }
+    pairs.insert(pairs.end(), rows.begin(), rows.end());
     return pairs;
 }
 
@@ -430,11 +456,10 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
     if (p->steps_persistent) {
         std::vector<uint8_t> tab;
         if (desc->variant == ALLRED_BO) {
-            tab = bo_steps_table(p->sched, total, &p->last_phase);
-            std::vector<uint8_t> p8(partner.begin(), partner.end());
-            if (steps && (tab.empty() || (st = upload(&p->d_partner8, p8)))) {
+            tab = bo_steps_table(p->sched, total);
+            if (steps && tab.empty()) {
                 free_plan(p);
-                return st ? st : ALLRED_ERR_SCHEDULE;
+                return ALLRED_ERR_SCHEDULE;
             }
         } else {
             tab = lo_steps_pairs(p->sched, total);
@@ -503,17 +528,16 @@ int allred_plan_rank_zones(const allred_plan* p, const uint64_t* stamps, uint64_
     const int N = p->total, S = p->sched.steps;
     for (int r = 0; r < N; ++r) zone_start[r] = ~0ull, zone_end[r] = 0;
     if (p->desc.variant == ALLRED_BO) {
-        // every rank takes part in RS step 0 of every block (the holders read their
-        // partners' copies): its zone opens at the earliest unit start; it closes
-        // at the latest end of the phase in which the rank last writes a block
-        const uint64_t slices = bo_steps_units(p->block_elems, N) / (uint64_t)N;
-        for (uint64_t u = 0; u < slices * (uint64_t)N; ++u) {
+        // every rank's copy of every block is read at RS step 0 (holders add their
+        // partners' copies) and written in the last phase (AG step 0 for the
+        // receivers, the holders' results beside it): the zone opens at the
+        // earliest unit start and closes at the latest unit end
+        const uint64_t units = bo_steps_units(p->block_elems, N);
+        for (uint64_t u = 0; u < units; ++u) {
             const uint64_t* st = stamps + u * (uint64_t)(2 * S + 1);
-            const int b = (int)(u / slices);
             for (int r = 0; r < N; ++r) {
                 if (st[0] < zone_start[r]) zone_start[r] = st[0];
-                const int q = p->last_phase[(size_t)b * N + r];
-                if (q >= 0 && st[1 + q] > zone_end[r]) zone_end[r] = st[1 + q];
+                if (st[2 * S] > zone_end[r]) zone_end[r] = st[2 * S];
             }
         }
     } else {
@@ -553,8 +577,7 @@ int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t strid
     }
     if (p->steps_persistent) {
         if (p->desc.variant == ALLRED_BO)
-            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_partner8, p->block_elems, stamps,
-                                   stream);
+            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->block_elems, stamps, stream);
         return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->n, stamps, stream);
     }
     if (p->desc.variant == ALLRED_BO) {

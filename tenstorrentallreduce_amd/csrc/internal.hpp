@@ -37,7 +37,10 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 
 // ---------------- tuning (tune.cpp; allred_tune_set / allred_tune_get) ----------------
 // Kernel-form switches between bit-identical forms; defaults = the product forms.
-enum class Tune { fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, count };
+enum class Tune {
+    fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid,
+    count
+};
 int64_t tune(Tune key);
 
 // ---------------- device launchers (kernels.hip) ----------------
@@ -70,10 +73,10 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
                       void* stream);
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, bool acc16, void* stream);
 // the schedule form as one persistent launch (k_bo_steps / k_lo_steps).  BO: d_tab = per block
-// the ranks written at each of the 2S phases, d_partner8 = [S][N]; LO: d_pairs = per step N/2
-// (r, p) pairs.  stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)
-int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    const uint8_t* d_partner8, size_t block_elems, uint64_t* stamps, void* stream);
+// the phase table of engine.cpp bo_steps_table; LO: d_pairs = per step N/2 (r, p) pairs.
+// stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)
+int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab, size_t block_elems,
+                    uint64_t* stamps, void* stream);
 uint64_t bo_steps_units(size_t block_elems, int total);
 int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs, size_t n,
                     uint64_t* stamps, void* stream);

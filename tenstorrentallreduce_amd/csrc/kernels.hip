@@ -744,9 +744,8 @@ __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, ui
 }
 
 // ---------------------------------------------------------------------------
-// Schedule form (ALLRED_EXEC_STEPS): the reference's step program with every
-// step's result stored to the ranks' buckets — the intermediate states of the
-// reference's per-core L1 buffers, step by step:
+// Schedule form (ALLRED_EXEC_STEPS): the reference's per-core step program,
+// executed step by step:
 //   BO  S reduce-scatter steps, then the S all-gather steps in reverse
 //       (allred_BO_2D/kernels/dataflow_kernel.cpp:152-267, compute_kernel.cpp:35-67):
 //       RS step k: rank r adds partner p_k(r)'s copy of every block b in
@@ -755,107 +754,187 @@ __global__ __launch_bounds__(kBlock) void k_mem(uint16_t* __restrict__ ranks, ui
 //       bandwidth_optimal = 0, dataflow_kernel.cpp:19-29): r and p_k(r) both
 //       become old_r + old_p (one fp32 add, commutative, one rounding).
 // Step k of block b only touches block b's bytes (LO: column v only column
-// v), so the program splits into independent units — (block, 512-byte
-// column slice) for BO, a column slice of the whole vector for LO — that run
-// every step with one workgroup barrier per step: ONE persistent launch, no
-// grid-wide synchronisation, no partner handshake across workgroups, and a
-// step's result is re-read by the next step from the XCD's L2 (nt stores keep
-// the line there; nt loads skip the CU's L1).  The round-1 form (one launch
-// per step, allred_tune_set("steps_form", 1)) paid a kernel boundary and a
-// latency-bound tail per step: 67.8 us at config 2.
-//   tab (BO): per block b, the ranks written at each of the 2S phases
-//     (RS step k: the N >> (k+1) holders of b; AG step k: its N >> (k+1)
-//     receivers), phase-major, uint8; partner: [S][N] uint8.
+// v), so the program splits into independent units — (block, column slice)
+// for BO, a column slice of the whole vector for LO — that run every step
+// with one workgroup barrier per step: ONE persistent launch, no grid-wide
+// synchronisation, no partner handshake across workgroups.  Between steps a
+// unit's rank copies live in LDS, the Tensix L1 of the reference: loaded from
+// the buckets once (DRAM -> L1, dataflow_kernel.cpp:126-130), every step
+// reads the partner's copy and writes its own (the NoC write + add_tiles into
+// the local CB), and each rank's result is written back once (L1 -> DRAM,
+// :271-280).  BO keeps only the live copies: RS step 0 reads both operands
+// from the buckets into the N/2 rows of its holders (their partners' copies
+// are never read again), steps 1 .. 2S-2 run among those rows, and AG step 0
+// writes its receivers' copies straight to their buckets, beside the
+// holders' own results: 16 KiB of LDS per 512-byte unit, the whole of
+// config 2 resident at once (64 rows: 32 KiB, one unit per CU could not
+// start until another had finished: 30.4 us).  Measured forms that read the
+// partner's copy back from the buckets instead (one launch 40.4 us, one
+// launch per step 67.8 us; steps_form 1 keeps the latter): DESIGN.md §4.
+//   tab (BO, per block, bytes): phase 0: (r, p) x N/2 ranks — holder r adds
+//     partner p into LDS row i; phases 1 .. 2S-2: (row of r, row of p) x the
+//     step's count; phase 2S-1: (r, row of p) x N/2 — receiver r's bucket
+//     gets row p — then the N/2 holders' ranks (their rows' results).
 //   pairs (LO): per step, N/2 (r, p) pairs with r < p, uint8.
 //   stamps (optional, profiling): per unit, s_memrealtime (100 MHz) at its
 //     start and at the end of every phase; the host derives each rank's
 //     ALL_RED_LOOP zone (DeviceZoneScopedN, dataflow_kernel.cpp:147) from
 //     them (allred_plan_rank_zones).
 // ---------------------------------------------------------------------------
-constexpr int kStepSV = 32;   // 16-byte vectors per unit row: 512 B, the fused passes' tile width
-constexpr int kStepIPT = 4;   // items per thread per round (8 loads in flight for an RS round)
-
 __device__ __forceinline__ void stamp(uint64_t* stamps, uint64_t at) {
     if (stamps && threadIdx.x == 0) stamps[at] = __builtin_amdgcn_s_memrealtime();
 }
 
-__global__ __launch_bounds__(kBlock) void k_bo_steps(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                     const uint8_t* __restrict__ tab,
-                                                     const uint8_t* __restrict__ partner, int N, int S, uint64_t bv,
-                                                     uint64_t slices, uint64_t units, uint64_t* __restrict__ stamps) {
-    const int L = 2 * (N - 1);   // tab entries per block
-    const int P = 2 * S + 1;     // stamps per unit
-    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint64_t b = u / slices, j = u % slices;
-        const uint64_t v0 = b * bv + j * kStepSV;
-        const int width = (int)(bv - j * kStepSV < (uint64_t)kStepSV ? bv - j * kStepSV : (uint64_t)kStepSV);
-        stamp(stamps, u * P);
-        const uint8_t* lst = tab + b * (uint64_t)L;
-        for (int q = 0; q < 2 * S; ++q) {
-            const bool rs = q < S;
-            const int k = rs ? q : 2 * S - 1 - q;
-            const int cnt = N >> (k + 1);
-            const uint8_t* pk = partner + k * N;
-            const int items = cnt * width;
-            for (int i0 = threadIdx.x; i0 < items; i0 += kStepIPT * kBlock) {
-                uint4 mine[kStepIPT], theirs[kStepIPT];
-                uint4* dst[kStepIPT];
+// the unit's N rows (rank r's columns [v0, v0 + width)) bucket <-> LDS rows of SV vectors
+template <bool LOAD, int SV, int T>
+__device__ __forceinline__ void unit_rows(uint16_t* __restrict__ ranks, uint64_t stride, int N, uint64_t v0, int width,
+                                          uint4* tile) {
+    const int items = N * width;
+    for (int i0 = threadIdx.x; i0 < items; i0 += 8 * T) {
+        uint4 x[8];
 #pragma unroll
-                for (int t = 0; t < kStepIPT; ++t) {
-                    const int i = i0 + t * kBlock;
-                    if (i < items) {
-                        const int r = lst[i / width], v = i % width;
-                        dst[t] = reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + v;
-                        theirs[t] = ld_nt(reinterpret_cast<const uint4*>(ranks + (uint64_t)pk[r] * stride) + v0 + v);
-                        if (rs) mine[t] = ld_nt(dst[t]);
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < kStepIPT; ++t)
-                    if (i0 + t * kBlock < items) st_nt(dst[t], rs ? add8(mine[t], theirs[t]) : theirs[t]);
+        for (int t = 0; t < 8; ++t) {
+            const int i = i0 + t * T;
+            if (i < items) {
+                const int r = i / width, v = i - r * width;
+                uint4* g = reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + v;
+                if (LOAD) x[t] = ld_nt(g);
+                else st_nt(g, tile[r * SV + v]);
             }
-            lst += cnt;
-            __syncthreads();   // this step's stores are done (release) before the next step reads them
-            stamp(stamps, u * P + 1 + q);
+        }
+        if (LOAD) {
+#pragma unroll
+            for (int t = 0; t < 8; ++t) {
+                const int i = i0 + t * T;
+                if (i < items) {
+                    const int r = i / width, v = i - r * width;
+                    tile[r * SV + v] = x[t];
+                }
+            }
         }
     }
 }
 
+constexpr int kStepSV = 32;   // BO unit row: 32 x 16 B = 512 B, the fused passes' tile width
+
+__global__ __launch_bounds__(kBlock) void k_bo_steps(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                     const uint8_t* __restrict__ tab, int N, int S, uint64_t bv,
+                                                     uint64_t slices, uint64_t units, uint64_t* __restrict__ stamps) {
+    constexpr int SV = kStepSV, T = kBlock;
+    __shared__ __attribute__((aligned(16))) uint4 tile[ALLRED_MAX_NODES / 2 * SV];
+    const int H = N / 2;
+    const int L = 2 * 2 * (N - 1) + H;   // tab bytes per block
+    const int P = 2 * S + 1;             // stamps per unit
+    auto grow = [&](int r) { return reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride); };
+    for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+        const uint64_t b = u / slices, j = u % slices;
+        const uint64_t v0 = b * bv + j * SV;
+        const int width = (int)(bv - j * SV < (uint64_t)SV ? bv - j * SV : (uint64_t)SV);
+        const uint8_t* tb = tab + b * (uint64_t)L;
+        stamp(stamps, u * P);
+        // RS step 0: holder r (row i) = r's copy + partner's copy, both from the buckets
+        for (int i0 = threadIdx.x; i0 < H * width; i0 += 4 * T) {
+            uint4 x[4], y[4];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = i0 + t * T;
+                if (i < H * width) {
+                    const int row = i / width, v = i - row * width;
+                    x[t] = ld_nt(grow(tb[2 * row]) + v0 + v);
+                    y[t] = ld_nt(grow(tb[2 * row + 1]) + v0 + v);
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = i0 + t * T;
+                if (i < H * width) {
+                    const int row = i / width, v = i - row * width;
+                    tile[row * SV + v] = add8(x[t], y[t]);
+                }
+            }
+        }
+        __syncthreads();
+        stamp(stamps, u * P + 1);
+        // RS steps 1 .. S-1 and AG steps S-1 .. 1 among the holder rows.  A step's
+        // writers never read each other's rows (its pairs are disjoint), so
+        // reading and writing row by row within the step is safe.
+        const uint8_t* e = tb + 2 * H;
+        for (int q = 1; q < 2 * S - 1; ++q) {
+            const bool rs = q < S;
+            const int k = rs ? q : 2 * S - 1 - q;
+            const int cnt = N >> (k + 1);
+            for (int i = threadIdx.x; i < cnt * width; i += T) {
+                const int x = i / width, v = i - x * width;
+                const int a = e[2 * x] * SV + v, c = e[2 * x + 1] * SV + v;
+                tile[a] = rs ? add8(tile[a], tile[c]) : tile[c];
+            }
+            e += 2 * cnt;
+            lds_barrier();
+            stamp(stamps, u * P + 1 + q);
+        }
+        // AG step 0: receivers' buckets get their partners' rows; the holders' results leave too
+        const uint8_t* fin = e + 2 * H;   // the holders' ranks, row order
+        for (int i = threadIdx.x; i < 2 * H * width; i += T) {
+            const int x = i / width, v = i - x * width;
+            if (x < H) st_nt(grow(e[2 * x]) + v0 + v, tile[e[2 * x + 1] * SV + v]);
+            else st_nt(grow(fin[x - H]) + v0 + v, tile[(x - H) * SV + v]);
+        }
+        __syncthreads();   // the rows are read out before the next unit overwrites them
+        stamp(stamps, u * P + 2 * S);
+    }
+}
+
+// LO: after step k the two ranks of every step-k pair hold the same value
+// (old_r + old_p: one add, commutative), so a unit keeps one LDS row per pair
+// — N/2 rows, 16 KiB at 512-byte rows: every unit of a 640 kB bucket resident
+// at once (one row per rank, 32 KiB, left one unit per CU waiting: 28.6 us).
+// Step 0 adds the pair's two bucket rows into row i; step k (1 .. S-2) reads
+// the rows of its pairs' step-(k-1) pairs into registers, barrier, writes its
+// own rows; the last step stores each pair's sum straight to both buckets.
+//   pairs: per step, N/2 (r, p) ranks, r < p; then per step >= 1 the N/2
+//   (row of r, row of p) in the previous step's rows.
 __global__ __launch_bounds__(kBlock) void k_lo_steps(uint16_t* __restrict__ ranks, uint64_t stride,
                                                      const uint8_t* __restrict__ pairs, int N, int S, uint64_t n_vec,
                                                      uint64_t units, uint64_t* __restrict__ stamps) {
+    constexpr int SV = kStepSV, T = kBlock, IPT = ALLRED_MAX_NODES / 2 * SV / T;
+    __shared__ __attribute__((aligned(16))) uint4 tile[ALLRED_MAX_NODES / 2 * SV];
     const int H = N / 2;
+    const uint8_t* rows = pairs + 2 * H * S;   // [step >= 1][H] (row of r, row of p)
+    auto grow = [&](int r) { return reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride); };
     for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
-        const uint64_t v0 = u * kStepSV;
-        const int width = (int)(n_vec - v0 < (uint64_t)kStepSV ? n_vec - v0 : (uint64_t)kStepSV);
+        const uint64_t v0 = u * SV;
+        const int width = (int)(n_vec - v0 < (uint64_t)SV ? n_vec - v0 : (uint64_t)SV);
+        const int items = H * width;
         stamp(stamps, u * (S + 1));
         for (int k = 0; k < S; ++k) {
-            const uint8_t* pk = pairs + k * N;
-            const int items = H * width;
-            for (int i0 = threadIdx.x; i0 < items; i0 += kStepIPT * kBlock) {
-                uint4 a[kStepIPT], c[kStepIPT];
-                uint4 *pa[kStepIPT], *pc[kStepIPT];
+            const uint8_t* pk = pairs + 2 * H * k;
+            const uint8_t* rk = rows + 2 * H * (k - 1);
+            uint4 val[IPT];
 #pragma unroll
-                for (int t = 0; t < kStepIPT; ++t) {
-                    const int i = i0 + t * kBlock;
-                    if (i < items) {
-                        const int pr = i / width, v = i % width;
-                        pa[t] = reinterpret_cast<uint4*>(ranks + (uint64_t)pk[2 * pr] * stride) + v0 + v;
-                        pc[t] = reinterpret_cast<uint4*>(ranks + (uint64_t)pk[2 * pr + 1] * stride) + v0 + v;
-                        a[t] = ld_nt(pa[t]);
-                        c[t] = ld_nt(pc[t]);
-                    }
+            for (int t = 0; t < IPT; ++t) {
+                const int i = threadIdx.x + t * T;
+                if (i < items) {
+                    const int x = i / width, v = i - x * width;
+                    if (k == 0) val[t] = add8(ld_nt(grow(pk[2 * x]) + v0 + v), ld_nt(grow(pk[2 * x + 1]) + v0 + v));
+                    else val[t] = add8(tile[rk[2 * x] * SV + v], tile[rk[2 * x + 1] * SV + v]);
                 }
+            }
+            if (k > 0) lds_barrier();   // every read of the step-(k-1) rows is done
 #pragma unroll
-                for (int t = 0; t < kStepIPT; ++t) {
-                    if (i0 + t * kBlock < items) {
-                        const uint4 s = add8(a[t], c[t]);
-                        st_nt(pa[t], s);
-                        st_nt(pc[t], s);
+            for (int t = 0; t < IPT; ++t) {
+                const int i = threadIdx.x + t * T;
+                if (i < items) {
+                    const int x = i / width, v = i - x * width;
+                    if (k == S - 1) {   // the last step's sums leave for both ranks' buckets
+                        st_nt(grow(pk[2 * x]) + v0 + v, val[t]);
+                        st_nt(grow(pk[2 * x + 1]) + v0 + v, val[t]);
+                    } else {
+                        tile[x * SV + v] = val[t];
                     }
                 }
             }
-            __syncthreads();
+            if (k == S - 1) __syncthreads();   // (the rows are free for the next unit)
+            else lds_barrier();
             stamp(stamps, u * (S + 1) + 1 + k);
         }
     }
@@ -1115,13 +1194,13 @@ int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
 }
 
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    const uint8_t* d_partner8, size_t block_elems, uint64_t* stamps, void* stream) {
-    if (block_elems % 8 || stride % 8 || !aligned16(ranks) || total < 1 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
-    if (steps == 0) return ALLRED_OK;
+                    size_t block_elems, uint64_t* stamps, void* stream) {
+    if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
+    if (block_elems % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
-    hipLaunchKernelGGL(k_bo_steps, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_tab, d_partner8,
-                       total, steps, bv, slices, units, stamps);
+    hipLaunchKernelGGL(k_bo_steps, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_tab, total, steps,
+                       bv, slices, units, stamps);
     return last_error();
 }
 
@@ -1131,8 +1210,8 @@ uint64_t bo_steps_units(size_t block_elems, int total) {
 
 int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs, size_t n,
                     uint64_t* stamps, void* stream) {
-    if (n % 8 || stride % 8 || !aligned16(ranks) || total < 1 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
-    if (steps == 0) return ALLRED_OK;
+    if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
+    if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
     hipLaunchKernelGGL(k_lo_steps, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_pairs, total,

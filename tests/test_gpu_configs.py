@@ -99,9 +99,10 @@ def test_config5_reference_inputs(n):
                                          (t.SWING, (1, 1), 64)])
 def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form):
     """The schedule form as one persistent launch of (block, column slice)
-    units (k_bo_steps / k_lo_steps, steps_form 0) and as one launch per step
-    (steps_form 1, the round-1 kernels), on slices narrower than a unit (3 and
-    5 vectors per block) and at config-2 size, against the oracle."""
+    units with the rank copies in LDS between steps (k_bo_steps / k_lo_steps,
+    steps_form 0) and as one launch per step (steps_form 1, the round-1
+    kernels), on slices narrower than a unit (3 and 5 vectors per block) and at
+    config-2 size, against the oracle."""
     side, total = grid
     ranks = rand_ranks(total, n, seed=7 * total + n % 97 + algo)
     with t.tuned(steps_form=steps_form):

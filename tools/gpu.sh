@@ -36,11 +36,11 @@ prof)
     tag=${1:-prof}
     out=gpurun_out/$tag
     mkdir -p "$out"
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run -- \
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$out/trace" -o run -- \
         python3 bench.py --main-only --steps 200 --warmup 20 > "$out/bench.json" 2> "$out/bench.err" &&
-    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run -- \
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d "$out/fetch" -o run -- \
         python3 bench.py --main-only --steps 100 --warmup 10 --eager > /dev/null 2> "$out/fetch.err" &&
-    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run -- \
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d "$out/write" -o run -- \
         python3 bench.py --main-only --steps 100 --warmup 10 --eager > /dev/null 2> "$out/write.err"
     rc=$?
     find "$out" -name "*.csv" | head -20
