@@ -71,12 +71,18 @@ int main(int argc, char** argv) {
             fprintf(f, "ARCH: cpu_loopback, CHIP_FREQ[MHz]: 1000\n");
             fprintf(f, "PCIe slot, core_x, core_y, RISC processor type, timer_id, time[cycles since reset], stat value, "
                        "run ID, run host ID,  zone name, type, source line, source file\n");
+            /* ranks on the Wormhole worker cores of the reference's grid (physical
+             * x / y of python/timing_taker.py:17-18), as the MI355X engine's log */
+            static const int phys_x[8] = {1, 2, 3, 4, 6, 7, 8, 9}, phys_y[8] = {1, 2, 3, 4, 5, 7, 8, 9};
             for (int rep = 0; rep < a.reps; ++rep)
                 for (int r = 0; r < total; ++r)
-                    for (int e = 0; e < 2; ++e)
-                        fprintf(f, "0,%d,%d,BRISC,%d,%llu,0,%d,%d,ALL_RED_LOOP,%s,0,allred_oracle.c\n", r % side,
-                                r / side, e, (unsigned long long)(stamps[((size_t)rep * total + r) * 2 + e] * 1e9),
-                                rep, rep, e ? "ZONE_END" : "ZONE_START");
+                    for (int e = 0; e < 2; ++e) {
+                        const int x = r % side, y = r / side;
+                        fprintf(f, "0,%d,%d,BRISC,%d,%llu,0,%d,%d,ALL_RED_LOOP,%s,0,allred_oracle.c\n",
+                                x < 8 ? phys_x[x] : x + 2, y < 8 ? phys_y[y] : y + 2, e,
+                                (unsigned long long)(stamps[((size_t)rep * total + r) * 2 + e] * 1e9), rep, rep,
+                                e ? "ZONE_END" : "ZONE_START");
+                    }
             fclose(f);
         }
     }

@@ -46,6 +46,23 @@ def plan():
             yield mode, "allred_mem_2D", SWING_MEM, SIZES_BO_MEM, None
 
 
+def header():
+    return (["mode", "swing_algo", "data_size", "run_num"] + [f"{x}{y}_start" for y in RANGE_Y for x in RANGE_X] +
+            [f"{x}{y}_end" for y in RANGE_Y for x in RANGE_X] + ["device_ns", "e2e_ns", "mismatches"])
+
+
+def row_from_log(mode, swing, size, run, log, rep) -> list:
+    """The reference's CSV row (python/timing_taker.py:83-101): the 64 cores'
+    normalized starts, then their ends ("N/A" for a core without a zone)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from profile_analyzer import normalized
+    core = normalized(log)
+    starts = [core.get((x, y), ("N/A", "N/A"))[0] for y in RANGE_Y for x in RANGE_X]
+    ends = [core.get((x, y), ("N/A", "N/A"))[1] for y in RANGE_Y for x in RANGE_X]
+    return [mode, swing, size, run, *starts, *ends, round(rep["device_s"] * 1e9), round(rep["e2e_s"] * 1e9),
+            rep["mismatches"]]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=20)
@@ -55,8 +72,6 @@ def main():
     ap.add_argument("--summary", action="store_true")
     args = ap.parse_args()
     import tenstorrentallreduce_amd as t
-    sys.path.insert(0, os.path.join(ROOT, "tools"))
-    from profile_analyzer import normalized
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     log = os.path.join(os.path.dirname(args.out), "profile_log_device.csv")
     rows = []
@@ -71,16 +86,10 @@ def main():
                     p = t.run_cli(binary, argv, env={"ALLRED_REPORT": "1", "ALLRED_EXEC": args.exec,
                                                      "ALLRED_E2E": "dma", "ALLRED_PROFILE_LOG": log})
                     rep = json.loads(p.stderr.strip().splitlines()[-1])
-                    core = normalized(log)
-                    starts = [core.get((x, y), ("N/A", "N/A"))[0] for y in RANGE_Y for x in RANGE_X]
-                    ends = [core.get((x, y), ("N/A", "N/A"))[1] for y in RANGE_Y for x in RANGE_X]
-                    rows.append([mode, swing, size, run, *starts, *ends, round(rep["device_s"] * 1e9),
-                                 round(rep["e2e_s"] * 1e9), rep["mismatches"]])
-    header = (["mode", "swing_algo", "data_size", "run_num"] + [f"{x}{y}_start" for y in RANGE_Y for x in RANGE_X] +
-              [f"{x}{y}_end" for y in RANGE_Y for x in RANGE_X] + ["device_ns", "e2e_ns", "mismatches"])
+                    rows.append(row_from_log(mode, swing, size, run, log, rep))
     with open(args.out, "w", newline="") as f:
         w = csv.writer(f)
-        w.writerow(header)
+        w.writerow(header())
         w.writerows(rows)
     if args.summary:
         groups = {}
