@@ -80,7 +80,9 @@ def cpu_baseline() -> dict:
     out = oracle.loopback("bo", argv, reps=reps, timeout=300, profile_log=log)
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from profile_analyzer import analyze  # profiler_results_analyzer.py statistics over the 64 ranks
-    per_rank = analyze(log)
+    secs = out["seconds"]
+    median_rep = sorted(range(len(secs)), key=lambda i: secs[i])[len(secs) // 2]
+    per_rank = analyze(log, run_id=median_rep)   # the rep of median time (one slow rep says nothing)
     bytes_all = RANKS * ELEMS * 2
     # BASELINE config 1 on the CPU: the reference's own CPU-runnable case
     # (allred_BO_2D 0 1 2 -1 1 32 0 0: 2x2 RecDub LO, 1 tile, all ones), 4 rank processes
@@ -94,7 +96,7 @@ def cpu_baseline() -> dict:
                    f"of the full config-2 allreduce, {reps} reps, median {out['median_s'] * 1e3:.3f} ms "
                    f"(min {out['min_s'] * 1e3:.3f}, max {out['max_s'] * 1e3:.3f}); mismatches {out['mismatches']}"),
         "online_cpus": os.sysconf("SC_NPROCESSORS_ONLN"),
-        "per_rank_last_rep_ns": per_rank,
+        "per_rank_median_rep_ns": per_rank,
         "config1": {"us_per_allreduce_median": round(c1["median_s"] * 1e6, 3), "cores": min(4, cpu_cores()),
                     "sample": f"oracle loopback, 4 rank processes, 200 reps; mismatches {c1['mismatches']}"},
     }

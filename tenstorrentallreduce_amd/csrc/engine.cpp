@@ -51,8 +51,13 @@ struct allred_plan {
     bool steps_persistent = false;          // schedule form as one launch (k_bo_steps / k_lo_steps)
     size_t ws_bytes = 0;
     int launches = 0;
-    const void* last_ranks = nullptr;  // memory-type cache of the last bucket pointer
-    bool last_host = false;
+    // memory type of recent bucket pointers (pinned host buckets take the
+    // zero-copy form): a rotation of up to kPtrCache bucket sets costs one
+    // hipPointerGetAttributes each, once
+    static constexpr int kPtrCache = 64;
+    const void* ptr_seen[kPtrCache] = {};
+    bool ptr_host[kPtrCache] = {};
+    int ptr_next = 0;
     bool lo_tree = false;  // fused LO runs as the BO tree pass (lo_rank_uniform)
 };
 
@@ -567,13 +572,18 @@ int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t strid
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, acc16, stream);
         if (p->desc.variant == ALLRED_LO && !p->lo_tree)
             return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->d_dag, stream);
-        if (ranks != p->last_ranks) {  // pinned host buckets (zero-copy) take the pipelined form
+        int slot = -1;
+        for (int i = 0; i < allred_plan::kPtrCache && slot < 0; ++i)
+            if (p->ptr_seen[i] == ranks) slot = i;
+        if (slot < 0) {   // pinned host buckets (zero-copy) take the pipelined form
             hipPointerAttribute_t at{};
-            p->last_host = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;
+            slot = p->ptr_next;
+            p->ptr_next = (p->ptr_next + 1) % allred_plan::kPtrCache;
+            p->ptr_host[slot] = hipPointerGetAttributes(&at, ranks) == hipSuccess && at.type == hipMemoryTypeHost;
             (void)hipGetLastError();
-            p->last_ranks = ranks;
+            p->ptr_seen[slot] = ranks;
         }
-        return launch_tree_fused(ranks, stride, p->n, N, p->d_order, stream, p->last_host);
+        return launch_tree_fused(ranks, stride, p->n, N, p->d_order, stream, p->ptr_host[slot]);
     }
     if (p->steps_persistent) {
         if (p->desc.variant == ALLRED_BO)

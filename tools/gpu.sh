@@ -8,6 +8,8 @@
 #   bench [bench args]   bench.py (default: the driver's N = 1 line)
 #   prof <tag>           rocprofv3 --kernel-trace --stats of bench.py --main-only,
 #                        then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
+#   share <n>            the N > 1 bench path rehearsed with n ranks on the one GPU
+#                        (bench.py --share-gpu: peer transports, no RCCL; numbers mean nothing)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -46,8 +48,18 @@ prof)
     find "$out" -name "*.csv" | head -20
     exit $rc
     ;;
+share)
+    n=${1:-2}
+    timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+        --master-port 29533 bench.py --gpus "$n" --share-gpu --steps 20 --warmup 5 \
+        > gpurun_out/share_n$n.json 2> gpurun_out/share_n$n.err
+    rc=$?
+    tail -5 gpurun_out/share_n$n.err
+    cat gpurun_out/share_n$n.json
+    exit $rc
+    ;;
 *)
-    echo "usage: $0 test|smoke|bench|prof" >&2
+    echo "usage: $0 test|smoke|bench|prof|share" >&2
     exit 2
     ;;
 esac

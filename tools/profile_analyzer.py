@@ -21,9 +21,12 @@ import numpy as np
 import pandas as pd
 
 
-def analyze(csv_file: str) -> dict:
+def analyze(csv_file: str, run_id: int | None = None) -> dict:
+    """run_id: only that run's zones (the loopback log holds every rep)."""
     df = pd.read_csv(csv_file, skiprows=1)
     loop = df[df["  zone name"] == "ALL_RED_LOOP"]
+    if run_id is not None:
+        loop = loop[loop[" run ID"] == run_id]
     latest: dict = {}
     for (x, y, proc, phase), g in loop.groupby([" core_x", " core_y", " RISC processor type", " type"]):
         t = g[" time[cycles since reset]"].max()
