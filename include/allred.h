@@ -211,6 +211,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   steps_form        schedule form: 0 one persistent launch (rank copies in LDS between steps)
  *                     | 1 one launch per step (rank copies in the buckets)
  *   pipe_grid         0: auto grid of the persistent passes
+ *   lo_dag_reg        1: fused LO of the non-rank-uniform Swing schedules (32 / 64 ranks) as the
+ *                     build-time DAG of distinct sums in registers (0 = the LDS DAG pass above)
+ *   lo_dag_reg_min_tiles  64: smallest bucket (256-element tiles per rank, 32 kB) for lo_dag_reg
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

@@ -570,8 +570,14 @@ int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t strid
     int st = ALLRED_OK;
     if (p->desc.exec == ALLRED_EXEC_FUSED) {
         if (p->desc.variant == ALLRED_MEM) return launch_mem_fused(ranks, stride, p->n, N, acc16, stream);
-        if (p->desc.variant == ALLRED_LO && !p->lo_tree)
+        if (p->desc.variant == ALLRED_LO && !p->lo_tree) {
+            // the build-time DAG in registers where one was generated for this schedule
+            if (tune(Tune::lo_dag_reg) && p->n / 256 >= (uint64_t)tune(Tune::lo_dag_reg_min_tiles)) {
+                st = launch_lo_dag_reg(ranks, stride, p->n, p->desc.algo, p->desc.side_length, N, stream);
+                if (st != ALLRED_ERR_UNSUPPORTED) return st;
+            }
             return launch_butterfly(ranks, stride, p->n, N, p->d_partner, steps, p->d_dag, stream);
+        }
         int slot = -1;
         for (int i = 0; i < allred_plan::kPtrCache && slot < 0; ++i)
             if (p->ptr_seen[i] == ranks) slot = i;

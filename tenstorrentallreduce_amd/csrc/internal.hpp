@@ -38,7 +38,8 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 // ---------------- tuning (tune.cpp; allred_tune_set / allred_tune_get) ----------------
 // Kernel-form switches between bit-identical forms; defaults = the product forms.
 enum class Tune {
-    fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid,
+    fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
+    lo_dag_reg_min_tiles,
     count
 };
 int64_t tune(Tune key);
@@ -56,6 +57,10 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
 // dag: the interned LO DAG of a 64-rank schedule (engine.cpp lo_dag), or null
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,
                      const uint8_t* dag, void* stream);
+// fused LO of a non-rank-uniform Swing schedule as its build-time DAG in registers
+// (k_lo_dag_reg); ALLRED_ERR_UNSUPPORTED when no DAG was generated for (algo, side,
+// total) or n is not a multiple of 256
+int launch_lo_dag_reg(uint16_t* ranks, uint64_t stride, size_t n, int algo, int side, int total, void* stream);
 int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total,
                        const uint8_t* order, uint16_t* out, void* stream);
 int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src,

@@ -14,10 +14,16 @@
 // one GPU's HBM, where a "send" is a load of the partner's bytes.
 // Kernel selection is fixed (the measured product forms);
 // allred_tune_set (tune.cpp) switches between bit-identical forms for A/B.
+#include <utility>
+
 #include "device.hpp"
 
 namespace tsa {
 namespace {
+
+// LO DAGs of the non-rank-uniform Swing schedules (generated at build time
+// from the schedule by csrc/gen_lo_dag.cpp): struct LoDag<i> + TSA_LO_DAGS(X)
+#include "lo_dag_gen.inc"
 
 // ---------------------------------------------------------------------------
 // dst += src over n_vec 16-byte vectors: one vector per lane (grid covers the
@@ -551,6 +557,104 @@ __global__ __launch_bounds__(kBlock) void k_butterfly_lds64_pipe(uint16_t* __res
             const int fr = EX == 4 ? fin[k] : r;  // LDS row holding rank r's result
             st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + (l32 ^ (fr & 31)), tile[fr * TV + l32]);
         }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_lo_dag_reg<D>: fused LO of a Swing schedule whose ranks do not share one
+// tree (Swing 8x8: the per-rank results take 4 distinct values per element),
+// as the DAG of its distinct sums evaluated in REGISTERS.  D is the schedule's
+// DAG generated at build time (csrc/gen_lo_dag.cpp -> build/lo_dag_gen.inc,
+// engine.cpp lo_dag_build's interning): node P + i = RNE(v[a[i]] + v[b[i]]),
+// the leaves are the P rank rows.  Thread t of the workgroup owns element t of
+// the 256-element tile: it reads its P leaves out of the LDS tile (each wave
+// reads 128 contiguous bytes per rank row), evaluates the N nodes with two
+// VALU ops each (v_add_f32, v_cvt_pk_bf16_f32 with a zero low half: the
+// rounded value stays an fp32 with zero low bits, ready for the next add),
+// and writes the F distinct finals into F LDS rows.  Rank r's row then leaves
+// from final row fin[r].  No LDS round trip or wave barrier between DAG steps
+// (k_butterfly_lds64_pipe<4> writes and re-reads every node through LDS).
+// The pipeline is k_tree_lds_lag's: two workgroups per CU, two tiles of LDS,
+// tile j+2's LDS-DMA loads interleaved with tile j-1's stores.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float rne_bf16(float s) { return __uint_as_float(pack_rne(0.0f, s)); }
+
+template <class D, int... I>
+__device__ __forceinline__ void lo_dag_eval(float* v, std::integer_sequence<int, I...>) {
+    ((v[D::P + I] = rne_bf16(v[D::a[I]] + v[D::b[I]])), ...);
+}
+
+template <class D>
+__global__ __launch_bounds__(kBlock) void k_lo_dag_reg(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                       uint64_t ntiles) {
+    constexpr int P = D::P, F = D::F, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI;
+    static_assert(OPS >= 1 && 3 * OPS <= 63, "vmcnt is 6 bits");
+    static_assert(NW * 64 == 256 && TV * 8 == 256, "one element of the 256-element tile per thread");
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 fin[2][F * TV];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    auto row = [&](int k) { return ranks + (uint64_t)(RPW * w + RPI * k + q) * stride; };
+    // final row of each rank row this lane stores (rank RPW*w + RPI*k + q)
+    int fsel[OPS];
+#pragma unroll
+    for (int k = 0; k < OPS; ++k) {
+        int f = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww)
+#pragma unroll
+            for (int qq = 0; qq < RPI; ++qq)
+                if (w == ww && q == qq) f = D::fin[RPW * ww + RPI * k + qq];
+        fsel[k] = f;
+    }
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + t * TV + c,
+                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
+    };
+    if (mine > 0) issue(tile_of(0), 0);
+    if (mine > 1) issue(tile_of(1), 1);
+    for (int j = 0; j < mine; ++j) {
+        // after L(j): the last op of S(j-3) (interleaved with L(j)), L(j+1), S(j-2)
+        wait_any((j >= 3 ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 2 ? OPS : 0));
+        lds_barrier();   // tile j is in LDS; fin[(j-1) & 1] is complete
+        {
+            const uint16_t* t16 = reinterpret_cast<const uint16_t*>(buf[j & 1]) + threadIdx.x;
+            float v[P + D::N];
+#pragma unroll
+            for (int r = 0; r < P; ++r) v[r] = __uint_as_float((uint32_t)t16[r * 256] << 16);
+            lo_dag_eval<D>(v, std::make_integer_sequence<int, D::N>{});
+            uint16_t* f16 = reinterpret_cast<uint16_t*>(fin[j & 1]) + threadIdx.x;
+#pragma unroll
+            for (int f = 0; f < F; ++f) f16[f * 256] = (uint16_t)(__float_as_uint(v[D::fnode[f]]) >> 16);
+        }
+        lds_barrier();   // every wave has read tile j out of buf[j & 1]; fin[j & 1] is complete
+        if (j >= 1 || j + 2 < mine) {   // tile j+2's loads and tile j-1's stores, interleaved op by op
+            const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 1);
+            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+            const uint4* fp = fin[(j + 1) & 1];
+            uint4 sv[OPS];
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) sv[k] = fp[fsel[k] * TV + c];
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                if (j + 2 < mine)
+                    lds_dma16(reinterpret_cast<const uint4*>(row(k)) + tl * TV + c, bl + (uint32_t)(RPI * k * TV * 16));
+                if (j >= 1) st_nt(reinterpret_cast<uint4*>(row(k)) + ts * TV + c, sv[k]);
+            }
+        }
+    }
+    if (mine > 0) {
+        const uint4* fp = fin[(mine - 1) & 1];
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            st_nt(reinterpret_cast<uint4*>(row(k)) + tile_of(mine - 1) * TV + c, fp[fsel[k] * TV + c]);
     }
 }
 
@@ -1122,6 +1226,21 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
         return last_error();
     }
     return tree_dispatch<true>(ranks, stride, nv, total, order, bv, nullptr, st);
+}
+
+int launch_lo_dag_reg(uint16_t* ranks, uint64_t stride, size_t n, int algo, int side, int total, void* stream) {
+    if (n % 256 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_UNSUPPORTED;
+    const uint64_t tiles = n / 256;
+    const dim3 grid(persistent_grid(tiles, 512));
+    hipStream_t st = (hipStream_t)stream;
+#define TSA_X(D, A, S, T)                                                                             \
+    if (algo == (A) && total == (T) && ((A) == ALLRED_SWING_1D || side == (S))) {                      \
+        hipLaunchKernelGGL(k_lo_dag_reg<D>, grid, dim3(kBlock), 0, st, ranks, stride, tiles);          \
+        return last_error();                                                                          \
+    }
+    TSA_LO_DAGS(TSA_X)
+#undef TSA_X
+    return ALLRED_ERR_UNSUPPORTED;
 }
 
 int launch_butterfly(uint16_t* ranks, uint64_t stride, size_t n, int total, const int16_t* d_partner, int steps,

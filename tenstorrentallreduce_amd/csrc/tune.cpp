@@ -30,6 +30,8 @@ const Key kKeys[] = {
     {"mem_reduce_lds", 1, 0, 1},      // mem_2D schedule-form reduce through LDS
     {"steps_form", 0, 0, 1},          // 0 one persistent launch | 1 one launch per step
     {"pipe_grid", 0, 0, 1 << 20},     // 0 auto
+    {"lo_dag_reg", 1, 0, 1},          // non-rank-uniform Swing fused LO: build-time DAG in registers
+    {"lo_dag_reg_min_tiles", 64, 1, 1ll << 40},   // 256-element tiles per rank (64: 32 kB)
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

@@ -209,17 +209,42 @@ def test_lo_sizes_reference_inputs(tiles, exec_mode):
 @pytest.mark.parametrize("place,dag", [(1, 1), (0, 1), (1, 0)])
 @pytest.mark.parametrize("n", [1024 * 64, 327680])
 def test_fused_lo_dag_placement(n, place, dag):
-    """The fused Swing 8x8 LO DAG pass (k_butterfly_lds64_pipe<4>) with its
+    """The fused Swing 8x8 LO DAG pass through LDS (k_butterfly_lds64_pipe<4>,
+    tune lo_dag_reg=0: the register DAG below is the default) with its
     bank-conflict-free node placement (engine.cpp lo_dag_place), with
     first-appearance rows and slots (tune lo_dag_place=0), and the per-rank
     butterfly (lo_dag=0, k_butterfly_lds64_pipe<0>): all bit-exact vs the
     oracle's per-rank butterfly (allred_BO_2D/kernels/dataflow_kernel.cpp:19-29)."""
     side, total = 8, 64
     ranks = rand_ranks(total, n, seed=71 + n % 97)
-    with t.tuned(lo_dag_place=place, lo_dag=dag):
+    with t.tuned(lo_dag_place=place, lo_dag=dag, lo_dag_reg=0):
         got = run_plan(t.SWING, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
     want = [r.copy() for r in ranks]
     oracle.allreduce("lo", t.SWING, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
+def signed_ranks(total, n, seed):
+    """finite bf16 of both signs from denormals to 2^96 (no overflow in a 64-leaf sum)"""
+    rng = np.random.default_rng(seed)
+    return [(rng.integers(0, 0x7000, n) | (rng.integers(0, 2, n) << 15)).astype(np.uint16) for _ in range(total)]
+
+
+@pytest.mark.parametrize("algo,grid", [(t.SWING, (8, 64)), (t.SWING, (8, 32)), (t.SWING_1D, (1, 32))])
+@pytest.mark.parametrize("n,pad", [(256, 0), (768, 64), (1024 * 64, 64), (327680, 64), (1 << 20, 0)])
+def test_fused_lo_register_dag(algo, grid, n, pad):
+    """The fused LO of the non-rank-uniform Swing schedules as the build-time
+    DAG of distinct sums evaluated in registers (k_lo_dag_reg, the default from
+    lo_dag_reg_min_tiles): one tile, an odd tile count (the persistent grid's
+    ragged tail), 128 kB, config-2 size and 2 MiB per rank, padded and unpadded
+    rank strides, both signs, denormals to 2^96 — bit-exact vs the oracle's
+    per-rank butterfly (allred_LOO_2D/kernels/dataflow_kernel.cpp:127-175)."""
+    side, total = grid
+    ranks = signed_ranks(total, n, seed=501 + n % 89 + total)
+    with t.tuned(lo_dag_reg=1, lo_dag_reg_min_tiles=1):
+        got = run_plan(algo, t.LO, side, total, ranks, t.EXEC_FUSED, stride=n + pad)
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("lo", algo, side, want, total)
     assert (got == np.stack(want)).all()
 
 

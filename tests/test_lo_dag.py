@@ -83,3 +83,53 @@ def test_swing_dag_shape_and_placement():
 def test_no_dag_off_64_ranks():
     assert lo_dag(t.SWING, 4, 16)[0].size == 0
     assert lo_dag(t.SWING, 2, 4)[0].size == 0
+
+
+# ------------------------------------------------------------------ register DAG (build-time)
+INC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tenstorrentallreduce_amd", "build",
+                   "lo_dag_gen.inc")
+
+
+def generated_dags():
+    """The DAGs csrc/gen_lo_dag.cpp wrote into build/lo_dag_gen.inc at build time
+    (k_lo_dag_reg's compile-time tables), parsed back: {(algo, side, total): dict}."""
+    import re
+    text = open(INC).read()
+    out = {}
+    for m in re.finditer(r"struct (LoDag\d+) \{[^\n]*\n(.*?)\n\};", text, re.S):
+        body = m.group(2)
+        arr = {k: [int(x) for x in v.replace("\n", " ").split(",")]
+               for k, v in re.findall(r"static constexpr int (\w+)\[\d+\] = \{(.*?)\};", body, re.S)}
+        hdr = dict(re.findall(r"(\w+) = (\d+)", body.split("\n")[0]))
+        arr.update({k: int(v) for k, v in hdr.items()})
+        out[m.group(1)] = arr
+    keys = {}
+    for name, algo, side, total in re.findall(r"X\((LoDag\d+), (\d+), (\d+), (\d+)\)", text):
+        keys[(int(algo), int(side), int(total))] = out[name]
+    return keys
+
+
+@pytest.mark.skipif(not os.path.exists(INC), reason="build() writes the generated DAG header")
+def test_register_dag_header_matches_oracle_lo():
+    """Every generated DAG, evaluated the way k_lo_dag_reg does (node P + i =
+    RNE(v[a[i]] + v[b[i]]), rank r gets node fnode[fin[r]]), reproduces the
+    oracle's per-rank LO butterfly bit for bit; and it covers exactly the Swing
+    schedules at 32 / 64 ranks whose ranks do not share one tree (8x8 and 8x4
+    2D, 1D at 32; 1D at 64 has 16 distinct finals and keeps the LDS DAG pass)."""
+    dags = generated_dags()
+    assert set(dags) == {(t.SWING, 8, 64), (t.SWING, 8, 32), (t.SWING_1D, 1, 32)}
+    assert dags[(t.SWING, 8, 64)]["N"] == 92 and dags[(t.SWING, 8, 64)]["F"] == 4
+    rng = np.random.default_rng(7)
+    for (algo, side, total), d in dags.items():
+        P, N, F = d["P"], d["N"], d["F"]
+        assert P == total and len(d["a"]) == len(d["b"]) == N and len(d["fnode"]) == F and len(d["fin"]) == P
+        n = 512
+        ranks = [(rng.integers(0, 0x7000, n) | (rng.integers(0, 2, n) << 15)).astype(np.uint16) for _ in range(P)]
+        v = list(ranks)
+        for i in range(N):
+            assert d["a"][i] < P + i and d["b"][i] < P + i, "operands precede the node"
+            v.append(bf16_add(v[d["a"][i]], v[d["b"][i]]))
+        got = np.stack([v[d["fnode"][d["fin"][r]]] for r in range(P)])
+        want = [r.copy() for r in ranks]
+        oracle.allreduce("lo", algo, side, want, total)
+        assert (got == np.stack(want)).all(), (algo, side, total)

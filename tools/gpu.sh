@@ -48,6 +48,29 @@ prof)
     find "$out" -name "*.csv" | head -20
     exit $rc
     ;;
+ab)
+    # ab <bo|lo|mem> "<tiles list>" "<ALLRED_TUNE a>" "<ALLRED_TUNE b>" ... : tools/ab_fused.py
+    # per size, the arms interleaved three times (32 rotating sets: cold HBM)
+    variant=$1 sizes=$2
+    shift 2
+    for tiles in $sizes; do
+        for rep in 1 2 3; do
+            for arm in "$@"; do
+                ALLRED_TUNE="$arm" AB_SETS=${AB_SETS:-32} timeout -k 10 120 python tools/ab_fused.py "$variant" "$tiles" \
+                    >> gpurun_out/ab.jsonl 2>> gpurun_out/ab.err || exit 1
+            done
+        done
+    done
+    python - <<'EOF'
+import json, collections
+rows = [json.loads(l) for l in open("gpurun_out/ab.jsonl")]
+by = collections.defaultdict(list)
+for r in rows:
+    by[(r["variant"], r["bytes_per_rank"], r["env"].get("ALLRED_TUNE", ""))].append(r["us"])
+for k, v in by.items():
+    print(k, sorted(v))
+EOF
+    ;;
 share)
     n=${1:-2}
     timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
