@@ -480,33 +480,48 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
     arms += [(f"config5_swing_lo_{kb}kB", t.SWING, t.LO, kb << 10, 100, 1, 1) for kb in (2, 8, 32, 128)]
     arms += [(f"mem_{kb}kB", t.SWING, t.MEM, kb << 10, 100, 1, 1) for kb in (2, 32)]
     arms += [("mem_640kB", t.SWING, t.MEM, ELEMS * 2, 100, 1, 1), ("mem_256MiB", t.SWING, t.MEM, 256 << 20, 5, 1, 1)]
-    for name, algo, variant, nbytes, reps, chans, local in arms:
-        n = nbytes // 2
-        d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
-                         channels=chans)
-        b2 = torch.empty((local, n), dtype=torch.int16, device=dev)   # real data: uniform [0,100) bf16
-        g = torch.Generator(device=dev).manual_seed(4000 + 17 * len(out) + torch.distributed.get_rank())
-        for r in range(local):
-            b2[r].copy_((torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16).view(torch.int16))
-        w2 = torch.empty(max(16, t.dist_workspace_bytes(d2)), dtype=torch.uint8, device=dev)
-        if variant != t.MEM and comm is not None:
-            ms = timed_max(lambda: t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-            out[name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
-        if peer is not None:
-            ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-            out["peer_" + name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
-            if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
-                peer.set_lo_ll_max(0)
-                ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-                peer.set_lo_ll_max(256 << 10)
-                out["peer_sched_" + name] = {**arm_stats(ms, nbytes, world, True), "channels": chans}
-            if variant == t.MEM and nbytes <= (256 << 10):   # mem_2D without LL hand-offs (k_peer_oneshot)
-                peer.set_mem_ll_max(0)
-                ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-                peer.set_mem_ll_max(256 << 10)
-                out["peer_oneshot_" + name] = {**arm_stats(ms, nbytes, world, False), "channels": chans}
-        del b2, w2
+    for arm in arms:
+        # every arm runs the same calls with the same arguments on every rank, so an
+        # error (an RCCL / HIP status turned exception) is raised on every rank alike:
+        # record it, agree, and go on with the next arm instead of losing the line
+        err = None
+        try:
+            xgmi_arm(out, comm, peer, world, dev, stream, side, total, *arm)
+        except Exception as e:  # reported, never silently dropped
+            err = repr(e)
+        if not agreed(err is None):
+            out[arm[0] + "_error"] = err or "failed on another rank"
+            torch.cuda.synchronize()
     return out
+
+
+def xgmi_arm(out, comm, peer, world, dev, stream, side, total, name, algo, variant, nbytes, reps, chans, local):
+    """One arm of xgmi_arms: its RCCL and peer-window timings into out."""
+    n = nbytes // 2
+    d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
+                     channels=chans)
+    b2 = torch.empty((local, n), dtype=torch.int16, device=dev)   # real data: uniform [0,100) bf16
+    g = torch.Generator(device=dev).manual_seed(4000 + 17 * len(out) + torch.distributed.get_rank())
+    for r in range(local):
+        b2[r].copy_((torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16).view(torch.int16))
+    w2 = torch.empty(max(16, t.dist_workspace_bytes(d2)), dtype=torch.uint8, device=dev)
+    if variant != t.MEM and comm is not None:
+        ms = timed_max(lambda: t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+        out[name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+    if peer is not None:
+        ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+        out["peer_" + name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+        if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
+            peer.set_lo_ll_max(0)
+            ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+            peer.set_lo_ll_max(256 << 10)
+            out["peer_sched_" + name] = {**arm_stats(ms, nbytes, world, True), "channels": chans}
+        if variant == t.MEM and nbytes <= (256 << 10):   # mem_2D without LL hand-offs (k_peer_oneshot)
+            peer.set_mem_ll_max(0)
+            ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
+            peer.set_mem_ll_max(256 << 10)
+            out["peer_oneshot_" + name] = {**arm_stats(ms, nbytes, world, False), "channels": chans}
+    del b2, w2
 
 
 def bench_multi(args, rank, world, local_rank) -> dict | None:
@@ -516,11 +531,19 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     dev = torch.device(f"cuda:{dev_index}")
     torch.cuda.set_device(dev)
     side, total = GRIDS[world]
-    comm = None
+    comm, comm_err = None, None
     if not args.share_gpu:
-        uid = [t.Comm.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        comm = t.Comm(uid[0], world, rank, local_rank)
+        try:   # RCCL communicator (allred_dist_comm_create); without it the peer transports still run
+            uid = [t.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = t.Comm(uid[0], world, rank, local_rank)
+        except Exception as e:  # reported in the line (xgmi.rccl_error), never silently dropped
+            comm_err = repr(e)
+            note(rank, f"RCCL communicator failed: {comm_err}")
+        if not agreed(comm is not None):
+            if comm is not None:
+                comm.close()
+            comm, comm_err = None, comm_err or "failed on another rank"
     note(rank, f"world {world}, device {dev_index}: opening peer windows")
     peer, peer_err = open_peer(rank, world, dev_index, (1 << 30) // 2)   # windows for 1 GiB buckets
     note(rank, f"peer windows: {'ok' if peer is not None else peer_err}")
@@ -570,7 +593,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     base = "rccl" if comm is not None else "peer_launches"
     candidates, verify = [base], {}
     if peer is None and comm is None:
-        raise RuntimeError("--share-gpu needs the peer windows")
+        raise RuntimeError("neither the RCCL communicator nor the peer windows could be opened"
+                           f" (rccl: {comm_err}, peer: {peer_err})")
     if peer is not None:
         small = torch.zeros_like(buf)
         small[:4] = torch.randint(0, 2, (4, ELEMS), device=dev).to(torch.bfloat16).view(torch.int16)
@@ -578,26 +602,31 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
         for kind in ("peer_swing", "peer_hier", "peer_hier_ll"):
-            x = small.clone()
             note(rank, f"verify: {kind}")
-            run(kind, x, fresh=True)
-            torch.cuda.synchronize()
-            ok = torch.equal(x, ref)
-            a, b2 = buf.clone(), buf.clone()
-            if kind == "peer_swing" and base == "rccl":
-                run("rccl", a, fresh=True)
-                run("peer_swing", b2)
-            elif kind == "peer_swing":   # --share-gpu: same semantics (Swing trees) only on small integers
-                a = b2 = None
-            else:   # the one-kernel forms against the launch form of the same semantics
-                run("peer_launches", a, fresh=True)
-                run(kind, b2)
-            torch.cuda.synchronize()
-            ok = ok and (a is None or torch.equal(a, b2)) and (peer.status() & t.PEER_TIMEOUT) == 0
+            try:   # the same calls on every rank: a raised status is raised everywhere
+                x = small.clone()
+                run(kind, x, fresh=True)
+                torch.cuda.synchronize()
+                ok = torch.equal(x, ref)
+                a, b2 = buf.clone(), buf.clone()
+                if kind == "peer_swing" and base == "rccl":
+                    run("rccl", a, fresh=True)
+                    run("peer_swing", b2)
+                elif kind == "peer_swing":   # --share-gpu: same semantics (Swing trees) only on small integers
+                    a = b2 = None
+                else:   # the one-kernel forms against the launch form of the same semantics
+                    run("peer_launches", a, fresh=True)
+                    run(kind, b2)
+                torch.cuda.synchronize()
+                ok = ok and (a is None or torch.equal(a, b2)) and (peer.status() & t.PEER_TIMEOUT) == 0
+                del x, a, b2
+            except Exception as e:  # reported, never silently dropped: the candidate is not used
+                note(rank, f"verify: {kind} raised {e!r}")
+                verify[kind + "_error"] = repr(e)
+                ok = False
             verify[kind] = agreed(ok)
             if verify[kind]:
                 candidates.append(kind)
-            del x, a, b2
         del small, ref
     quick = {}
     for kind in candidates:
@@ -680,6 +709,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
               "peer_timeout_in_timed_loop": peer_timeout}
     if peer_err:
         extras["peer_error"] = peer_err
+    if comm_err:
+        extras["rccl_error"] = comm_err
     if args.extras:
         extras.update(xgmi_arms(comm, peer if verify.get("peer_swing") else None, world, dev, stream, side, total))
         if world > 1 and comm is not None:

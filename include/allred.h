@@ -208,8 +208,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   lo_dag_place      1: bank-conflict-free DAG placement (0 = first-appearance order)
  *   lo_dag_min_tiles  256: smallest bucket (256-element tiles) for the DAG pass
  *   mem_reduce_lds    1: mem_2D schedule-form reduce staged through LDS
- *   steps_form        schedule form: 0 one persistent launch (rank copies in LDS between steps)
- *                     | 1 one launch per step (rank copies in the buckets)
+ *   steps_form        schedule form: 0 one pipelined launch (units staged into LDS two ahead, the step
+ *                     program among LDS rows, stores one unit late) | 1 one launch per step (rank
+ *                     copies in the buckets) | 2 one launch with every unit resident at once
  *   pipe_grid         0: auto grid of the persistent passes
  *   lo_dag_reg        1: fused LO of the non-rank-uniform Swing schedules (32 / 64 ranks) as the
  *                     build-time DAG of distinct sums in registers (0 = the LDS DAG pass above)

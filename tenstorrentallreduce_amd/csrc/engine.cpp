@@ -48,6 +48,7 @@ struct allred_plan {
     uint8_t* d_order = nullptr;
     uint8_t* d_dag = nullptr;               // LO: interned DAG (lo_dag_lanes form), 64 ranks only
     uint8_t* d_steps_tab = nullptr;         // schedule form, one launch: BO per-block phase ranks / LO step pairs
+    uint8_t* d_steps_pipe_tab = nullptr;    // the same programs in the pipelined form's layout (k_steps_pipe)
     bool steps_persistent = false;          // schedule form as one launch (k_bo_steps / k_lo_steps)
     size_t ws_bytes = 0;
     int launches = 0;
@@ -88,6 +89,7 @@ void free_plan(allred_plan* p) {
     if (p->d_order) (void)hipFree(p->d_order);
     if (p->d_dag) (void)hipFree(p->d_dag);
     if (p->d_steps_tab) (void)hipFree(p->d_steps_tab);
+    if (p->d_steps_pipe_tab) (void)hipFree(p->d_steps_pipe_tab);
     delete p;
 }
 
@@ -178,6 +180,29 @@ std::vector<uint8_t> bo_steps_table(const allred_schedule& s, int N) {
     return tab;
 }
 
+// The BO program in k_steps_pipe's layout, 256 bytes per block: phase 0 and
+// phases 1 .. 2S-2 as in bo_steps_table, then N bytes: the row holding rank
+// r's result after AG step 0 (holders: their own row; receivers: the row of
+// their step-0 partner, whose copy AG step 0 sends them).
+std::vector<uint8_t> bo_steps_pipe_table(const std::vector<uint8_t>& tab, int N, int S) {
+    if (S < 1 || N < 2 || tab.empty()) return {};
+    const int H = N / 2, L = 4 * (N - 1) + H, body = 2 * H + 2 * (H - 1) * 2;
+    if (tab.size() != (size_t)L * N || body + N > kBoPipeTabBytes) return {};
+    std::vector<uint8_t> out((size_t)kBoPipeTabBytes * N, 0);
+    for (int b = 0; b < N; ++b) {
+        const uint8_t* t = &tab[(size_t)b * L];
+        uint8_t* o = &out[(size_t)b * kBoPipeTabBytes];
+        std::memcpy(o, t, (size_t)body);
+        const uint8_t* ag0 = t + body;          // (receiver r, row of its partner) x H
+        const uint8_t* holders = ag0 + 2 * H;   // holder ranks, row order
+        for (int x = 0; x < H; ++x) {
+            o[body + ag0[2 * x]] = ag0[2 * x + 1];
+            o[body + holders[x]] = (uint8_t)x;
+        }
+    }
+    return out;
+}
+
 // LO schedule form (k_lo_steps, kernels.hip): per step, the N/2 exchanging
 // pairs (r, p), r < p, numbered in order (after step k, pair i's two ranks
 // hold the same value: LDS row i); then per step k >= 1, for each of its pairs
@@ -204,6 +229,22 @@ std::vector<uint8_t> lo_steps_pairs(const allred_schedule& s, int N) {
     }
     pairs.insert(pairs.end(), rows.begin(), rows.end());
     return pairs;
+}
+
+// The LO program in k_steps_pipe's layout: step 0's N/2 (r, p) rank pairs,
+// steps 1 .. S-1's (row of r, row of p), then N bytes: rank r's pair (row) at
+// the last step.
+std::vector<uint8_t> lo_steps_pipe_table(const allred_schedule& s, int N) {
+    const int S = s.steps, H = N / 2;
+    const std::vector<uint8_t> pr = lo_steps_pairs(s, N);
+    if (S == 0 || pr.size() != (size_t)(2 * H * S + 2 * H * (S - 1))) return {};
+    std::vector<uint8_t> out(pr.begin(), pr.begin() + 2 * H);       // step 0 rank pairs
+    out.insert(out.end(), pr.begin() + 2 * H * S, pr.end());         // steps >= 1 row pairs
+    std::vector<uint8_t> last(N, 0);
+    const uint8_t* lp = &pr[(size_t)2 * H * (S - 1)];
+    for (int i = 0; i < H; ++i) last[lp[2 * i]] = last[lp[2 * i + 1]] = (uint8_t)i;
+    out.insert(out.end(), last.begin(), last.end());
+    return out;
 }
 
 // The LO butterfly as a DAG of its distinct sums, for the LDS pass of 64 ranks
@@ -457,7 +498,7 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
         return st;
     }
     // schedule form: one persistent launch (default) or one launch per step (steps_form 1, A/B)
-    p->steps_persistent = desc->exec == ALLRED_EXEC_STEPS && desc->variant != ALLRED_MEM && tune(Tune::steps_form) == 0;
+    p->steps_persistent = desc->exec == ALLRED_EXEC_STEPS && desc->variant != ALLRED_MEM && tune(Tune::steps_form) != 1;
     if (p->steps_persistent) {
         std::vector<uint8_t> tab;
         if (desc->variant == ALLRED_BO) {
@@ -473,7 +514,9 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
                 return ALLRED_ERR_SCHEDULE;
             }
         }
-        if ((st = upload(&p->d_steps_tab, tab))) {
+        const std::vector<uint8_t> pipe = desc->variant == ALLRED_BO ? bo_steps_pipe_table(tab, total, steps)
+                                                                     : lo_steps_pipe_table(p->sched, total);
+        if ((st = upload(&p->d_steps_tab, tab)) || (st = upload(&p->d_steps_pipe_tab, pipe))) {
             free_plan(p);
             return st;
         }
@@ -593,8 +636,9 @@ int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t strid
     }
     if (p->steps_persistent) {
         if (p->desc.variant == ALLRED_BO)
-            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->block_elems, stamps, stream);
-        return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->n, stamps, stream);
+            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab, p->block_elems,
+                                   stamps, stream);
+        return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab, p->n, stamps, stream);
     }
     if (p->desc.variant == ALLRED_BO) {
         for (int k = 0; k < steps && st == ALLRED_OK; ++k)

@@ -80,11 +80,13 @@ int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, bool
 // the schedule form as one persistent launch (k_bo_steps / k_lo_steps).  BO: d_tab = per block
 // the phase table of engine.cpp bo_steps_table; LO: d_pairs = per step N/2 (r, p) pairs.
 // stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)
-int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab, size_t block_elems,
-                    uint64_t* stamps, void* stream);
+constexpr int kBoPipeTabBytes = 256;   // k_steps_pipe's BO table bytes per block (4N - 4 <= 252)
+// d_pipe_tab: the pipelined form's table (engine.cpp bo_steps_pipe_table / lo_steps_pipe_table), or null
+int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
+                    const uint8_t* d_pipe_tab, size_t block_elems, uint64_t* stamps, void* stream);
 uint64_t bo_steps_units(size_t block_elems, int total);
-int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs, size_t n,
-                    uint64_t* stamps, void* stream);
+int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs,
+                    const uint8_t* d_pipe_tab, size_t n, uint64_t* stamps, void* stream);
 uint64_t lo_steps_units(size_t n);
 
 // peer flag area (uint32 words): [0, 64) the multi-kernel barrier, then the

@@ -1049,6 +1049,185 @@ __global__ __launch_bounds__(kBlock) void k_lo_steps(uint16_t* __restrict__ rank
 //   RS: ranks[r][b] += ranks[p][b] for b in recv_mask_k(r)   (in place: the
 //       pair's recv masks are disjoint, so nobody reads what another writes)
 //   AG: ranks[r][b]  = ranks[p][b] for b in send_mask_k(r) (= recv_mask_k(p))
+// ---------------------------------------------------------------------------
+// k_steps_pipe<P, BO>: the schedule form (every RS / AG step of BO, every
+// exchange step of LO, in order, on the unit's rows) on k_tree_lds_lag's
+// pipeline: a persistent grid of two workgroups per CU, each unit (a 512-byte
+// column slice of all P rank rows, 32 KiB at P = 64) staged into LDS by
+// LDS-DMA two units ahead — the reference's DRAM -> L1 reads — then the step
+// program runs among LDS rows (the Tensix L1 of the reference), and the
+// unit's P result rows are read into registers and stored one iteration late,
+// interleaved with the loads of unit j+2.  Step 0 reads the staged rows of
+// both partners (its sums go to compact rows: the staged rows are the work
+// rows too).  Wave w owns columns 8w .. 8w+7 of every row, so the steps need
+// no workgroup barrier, and each lane fetches all its table entries of the
+// unit in one batch (a step then waits for its operand rows only).  S =
+// log2(P) (every 2D and 1D schedule of P ranks), so the step loop unrolls.
+//   BO tab (bo_steps_pipe_table, 256 bytes per block, staged by LDS-DMA with
+//     the unit): (r, p) x P/2 of RS step 0 -> row i; (row a, row c) pairs of
+//     RS 1..S-1 and AG S-1..1 (RS: a += c, AG: a = c); then P bytes: the row
+//     holding rank r's result after AG step 0 (holders: their own row,
+//     receivers: their step-0 partner's).
+//   LO tab (lo_steps_pipe_table, staged once): per step P/2 (r, p) ranks (step
+//     0) / (row of r, row of p) (steps >= 1) -> row i = pair i; then P bytes:
+//     rank r's pair at the last step.
+// Measured against k_bo_steps / k_lo_steps (all units resident at once, the
+// loads before and the stores after the whole step chain): DESIGN.md §4.
+// ---------------------------------------------------------------------------
+constexpr int kBoPipeTab = kBoPipeTabBytes;
+
+template <int P>
+constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
+
+template <int P, bool BO>
+__global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                       const uint8_t* __restrict__ tab, uint64_t bv, uint64_t slices,
+                                                       uint64_t units, uint64_t* __restrict__ stamps) {
+    constexpr int NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, H = P / 2, S = log2_of<P>();
+    constexpr int IPW = (H * 8 + 63) / 64;   // items (row pair, one of the wave's 8 columns) per lane, H pairs
+    constexpr int TOPS = BO ? 1 : 0;          // the BO unit's table comes with its rows
+    constexpr int NPH = BO ? 2 * S - 2 : S - 1;   // phases after step 0
+    constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
+    static_assert(OPS >= 1 && 2 * (OPS + TOPS) + OPS <= 63, "vmcnt is 6 bits");
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t tl[BO ? 2 : 1][BO ? kBoPipeTab : 16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    const uint32_t tbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&tl[0][0] + (uint32_t)(w * 64));
+    auto row = [&](int k) { return ranks + (uint64_t)(RPW * w + RPI * k + q) * stride; };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < units ? (int)((units - 1 - blockIdx.x) / G + 1) : 0;
+    auto unit_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto col0 = [&](uint64_t u) { return BO ? (u / slices) * bv + (u % slices) * TV : u * TV; };
+    auto issue_tab = [&](uint64_t u, int b) {   // BO: 64 bytes of the block's table per wave (lanes 0-3)
+        if constexpr (BO) {
+            if (lane < 4) lds_dma16(tab + (u / slices) * kBoPipeTab + w * 64 + lane * 16, tbase + (uint32_t)(b * kBoPipeTab));
+        }
+    };
+    auto issue = [&](uint64_t u, int b) {
+        issue_tab(u, b);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + col0(u) + c, wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
+    };
+    // phase ph (1 .. NPH): its pair count and table offset (bytes), compile-time after unrolling
+    auto cnt_of = [](int ph) {
+        if (!BO) return H;
+        const int k = ph < S ? ph : 2 * S - 1 - ph;
+        return P >> (k + 1);
+    };
+    auto off_of = [&](int ph) {
+        int o = 2 * H;
+        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
+        return o;
+    };
+    constexpr int MPH = BO ? (P / 4 * 8 + 63) / 64 : IPW;   // most items per lane in one phase
+    // This lane's table entries (pair = a | b << 8; final row) for the whole unit,
+    // fetched in one batch: a phase then waits for its operand rows only.
+    uint32_t p0[IPW], pp[NPH > 0 ? NPH : 1][MPH];
+    int fin[OPS];
+    auto fetch = [&](const uint8_t* tb) {   // tb: LDS (BO, per unit) or global (LO, once)
+        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
+#pragma unroll
+        for (int t = 0; t < IPW; ++t) {
+            const int i = lane + 64 * t;
+            p0[t] = i < H * 8 ? t16[i >> 3] : 0;
+        }
+#pragma unroll
+        for (int ph = 1; ph <= NPH; ++ph)
+#pragma unroll
+            for (int m = 0; m < MPH; ++m) {
+                const int i = lane + 64 * m;
+                pp[ph - 1][m] = i < cnt_of(ph) * 8 ? t16[off_of(ph) / 2 + (i >> 3)] : 0;
+            }
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) fin[k] = tb[off_of(NPH + 1) + RPW * w + RPI * k + q];
+    };
+    if constexpr (!BO) {   // the LO step program is the same for every unit
+        fetch(tab);
+        wait_vm<0>();
+    }
+    if (mine > 0) issue(unit_of(0), 0);
+    if (mine > 1) issue(unit_of(1), 1);
+    uint4 prev[OPS];
+    for (int j = 0; j < mine; ++j) {
+        const uint64_t u = unit_of(j);
+        // after L(j): the last op of S(j-3), L(j+1) (+ its table op), S(j-2)
+        wait_any((j >= 3 ? 1 : 0) + (j + 1 < mine ? OPS + TOPS : 0) + (j >= 2 ? OPS : 0));
+        lds_barrier();   // unit j's rows (and table) are in LDS
+        stamp(stamps, u * STAMPS);
+        uint4* tile = buf[j & 1];
+        if constexpr (BO) fetch(tl[j & 1]);
+        // The step program runs per column: wave w owns columns 8w .. 8w+7 of
+        // every row, so a step needs no workgroup barrier — LDS operations of
+        // one wave execute in order, and no other wave touches these columns.
+        const int cw = 8 * w + (lane & 7);
+        {   // step 0 from the staged rows: pair x = (r, p) -> row x (every read before any write)
+            uint4 val[IPW];
+#pragma unroll
+            for (int t = 0; t < IPW; ++t)
+                if (lane + 64 * t < H * 8)
+                    val[t] = add8(tile[(p0[t] & 255) * TV + cw], tile[(p0[t] >> 8) * TV + cw]);
+#pragma unroll
+            for (int t = 0; t < IPW; ++t)
+                if (lane + 64 * t < H * 8) tile[((lane + 64 * t) >> 3) * TV + cw] = val[t];
+            __builtin_amdgcn_wave_barrier();
+            stamp(stamps, u * STAMPS + 1);
+        }
+#pragma unroll
+        for (int ph = 1; ph <= NPH; ++ph) {
+            if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
+                const bool rs = ph < S;
+#pragma unroll
+                for (int m = 0; m < MPH; ++m)
+                    if (lane + 64 * m < cnt_of(ph) * 8) {
+                        const int a = (pp[ph - 1][m] & 255) * TV + cw, cc = (pp[ph - 1][m] >> 8) * TV + cw;
+                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
+                    }
+            } else {   // exchange step ph: pair x = rows of its ranks after step ph-1 -> row x
+                uint4 val[IPW];
+#pragma unroll
+                for (int m = 0; m < IPW; ++m)
+                    if (lane + 64 * m < H * 8)
+                        val[m] = add8(tile[(pp[ph - 1][m] & 255) * TV + cw], tile[(pp[ph - 1][m] >> 8) * TV + cw]);
+#pragma unroll
+                for (int m = 0; m < IPW; ++m)
+                    if (lane + 64 * m < H * 8) tile[((lane + 64 * m) >> 3) * TV + cw] = val[m];
+            }
+            __builtin_amdgcn_wave_barrier();
+            stamp(stamps, u * STAMPS + 1 + ph);
+        }
+        lds_barrier();   // every column's program is done
+        // the unit's result rows: rank r's value is row fin
+        uint4 cur[OPS];
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) cur[k] = tile[fin[k] * TV + c];
+        lds_barrier();   // every wave has read unit j out of buf[j & 1] (and its table)
+        {   // unit j+2's loads and unit j-1's stores, interleaved op by op
+            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+            const uint64_t cl = j + 2 < mine ? col0(unit_of(j + 2)) : 0, cs = j >= 1 ? col0(unit_of(j - 1)) : 0;
+            if (j + 2 < mine) issue_tab(unit_of(j + 2), j & 1);
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                if (j + 2 < mine)
+                    lds_dma16(reinterpret_cast<const uint4*>(row(k)) + cl + c, bl + (uint32_t)(RPI * k * TV * 16));
+                if (j >= 1) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + c, prev[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) prev[k] = cur[k];
+        if (BO) stamp(stamps, u * STAMPS + 2 * S);
+    }
+    if (mine > 0) {
+        const uint64_t cs = col0(unit_of(mine - 1));
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + c, prev[k]);
+    }
+}
+
 template <bool ADD, int U>
 __global__ __launch_bounds__(64) void k_step_w(uint16_t* __restrict__ ranks, uint64_t stride,
                                                const int16_t* __restrict__ partner,
@@ -1313,12 +1492,24 @@ int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
 }
 
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    size_t block_elems, uint64_t* stamps, void* stream) {
+                    const uint8_t* d_pipe_tab, size_t block_elems, uint64_t* stamps, void* stream) {
     if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
     if (block_elems % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
+    hipStream_t st = (hipStream_t)stream;
+    // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
+    if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
+        const dim3 grid(persistent_grid(units, 512));
+        switch (total) {
+            case 8: hipLaunchKernelGGL((k_steps_pipe<8, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
+            case 16: hipLaunchKernelGGL((k_steps_pipe<16, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
+            case 32: hipLaunchKernelGGL((k_steps_pipe<32, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
+            case 64: hipLaunchKernelGGL((k_steps_pipe<64, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
+            default: break;
+        }
+    }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
-    hipLaunchKernelGGL(k_bo_steps, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_tab, total, steps,
+    hipLaunchKernelGGL(k_bo_steps, dim3(grid), dim3(kBlock), 0, st, ranks, stride, d_tab, total, steps,
                        bv, slices, units, stamps);
     return last_error();
 }
@@ -1327,13 +1518,24 @@ uint64_t bo_steps_units(size_t block_elems, int total) {
     return (block_elems / 8 + kStepSV - 1) / kStepSV * (uint64_t)total;
 }
 
-int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs, size_t n,
-                    uint64_t* stamps, void* stream) {
+int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs,
+                    const uint8_t* d_pipe_tab, size_t n, uint64_t* stamps, void* stream) {
     if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
     if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
+    hipStream_t st = (hipStream_t)stream;
+    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
+        const dim3 grid(persistent_grid(units, 512));
+        switch (total) {
+            case 8: hipLaunchKernelGGL((k_steps_pipe<8, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
+            case 16: hipLaunchKernelGGL((k_steps_pipe<16, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
+            case 32: hipLaunchKernelGGL((k_steps_pipe<32, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
+            case 64: hipLaunchKernelGGL((k_steps_pipe<64, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
+            default: break;
+        }
+    }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
-    hipLaunchKernelGGL(k_lo_steps, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, d_pairs, total,
+    hipLaunchKernelGGL(k_lo_steps, dim3(grid), dim3(kBlock), 0, st, ranks, stride, d_pairs, total,
                        steps, nv, units, stamps);
     return last_error();
 }

@@ -28,7 +28,7 @@ const Key kKeys[] = {
     {"lo_dag_place", 1, 0, 1},        // bank-conflict-free DAG placement
     {"lo_dag_min_tiles", 256, 1, 1ll << 40},
     {"mem_reduce_lds", 1, 0, 1},      // mem_2D schedule-form reduce through LDS
-    {"steps_form", 0, 0, 1},          // 0 one persistent launch | 1 one launch per step
+    {"steps_form", 0, 0, 2},          // 0 pipelined launch | 1 one launch per step | 2 all units resident
     {"pipe_grid", 0, 0, 1 << 20},     // 0 auto
     {"lo_dag_reg", 1, 0, 1},          // non-rank-uniform Swing fused LO: build-time DAG in registers
     {"lo_dag_reg_min_tiles", 64, 1, 1ll << 40},   // 256-element tiles per rank (64: 32 kB)

@@ -91,17 +91,21 @@ def test_config5_reference_inputs(n):
 
 
 # ------------------------------------------------------------------ schedule form
-@pytest.mark.parametrize("steps_form", [0, 1])
+@pytest.mark.parametrize("steps_form", [0, 1, 2])
 @pytest.mark.parametrize("variant", ["bo", "lo"])
 @pytest.mark.parametrize("algo,grid,n", [(t.SWING, (8, 64), 327680), (t.RECDUB, (8, 64), 327680),
                                          (t.SWING, (8, 64), 64 * 8 * 3), (t.SWING, (4, 8), 8 * 8 * 5),
                                          (t.RECDUB, (2, 2), 1024), (t.SWING_1D, (1, 16), 16 * 8 * 33),
-                                         (t.SWING, (1, 1), 64)])
+                                         (t.SWING, (1, 1), 64), (t.SWING, (4, 8), 8 * 256 * 3),
+                                         (t.SWING, (8, 32), 32 * 256 * 3), (t.RECDUB, (4, 16), 16 * 256 * 5),
+                                         (t.SWING_1D, (1, 16), 16 * 256 * 2)])
 def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form):
-    """The schedule form as one persistent launch of (block, column slice)
-    units with the rank copies in LDS between steps (k_bo_steps / k_lo_steps,
-    steps_form 0) and as one launch per step (steps_form 1, the round-1
-    kernels), on slices narrower than a unit (3 and 5 vectors per block) and at
+    """The schedule form as one pipelined launch (k_steps_pipe, steps_form 0:
+    whole 512-byte units of 8..64 ranks staged into LDS two ahead, the step
+    program among LDS rows, stores one unit late; other shapes fall back to
+    k_bo_steps / k_lo_steps), with every unit resident at once (steps_form 2)
+    and as one launch per step (steps_form 1, the round-1 kernels), on slices
+    narrower than a unit (3 and 5 vectors per block), odd unit counts and at
     config-2 size, against the oracle."""
     side, total = grid
     ranks = rand_ranks(total, n, seed=7 * total + n % 97 + algo)
@@ -113,8 +117,9 @@ def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form):
     assert np.array_equal(got, np.stack(want))
 
 
+@pytest.mark.parametrize("steps_form", [0, 2])
 @pytest.mark.parametrize("variant", [t.BO, t.LO])
-def test_schedule_form_device_stamps(variant):
+def test_schedule_form_device_stamps(variant, steps_form):
     """execute(stamps_ptr=...): every unit's start and per-step stamps
     (s_memrealtime, 100 MHz) are written and monotonic within a unit; the
     per-rank zones (allred_plan_rank_zones) open before they close, and the
@@ -123,10 +128,12 @@ def test_schedule_form_device_stamps(variant):
     ranks = rand_ranks(total, n, seed=99)
     host = np.stack(ranks)
     buf = torch.from_numpy(host.view(np.int16)).to(DEV)
-    plan = t.Plan(t.SWING, variant, side, n, total, t.EXEC_STEPS)
+    with t.tuned(steps_form=steps_form):
+        plan = t.Plan(t.SWING, variant, side, n, total, t.EXEC_STEPS)
     assert plan.launches == 1 and plan.stamp_words > 0
     st = torch.zeros(plan.stamp_words, dtype=torch.int64, device=DEV)
-    plan.execute(buf.data_ptr(), n, None, torch.cuda.current_stream(), stamps_ptr=st.data_ptr())
+    with t.tuned(steps_form=steps_form):
+        plan.execute(buf.data_ptr(), n, None, torch.cuda.current_stream(), stamps_ptr=st.data_ptr())
     torch.cuda.synchronize()
     stamps = st.cpu().numpy().view(np.uint64)
     per = 2 * 6 + 1 if variant == t.BO else 6 + 1
