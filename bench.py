@@ -565,6 +565,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
     #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
+    #   peer_hier_pipe  the same LL hand-offs on the lagged-store pipeline (k_hier_pipe)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -585,7 +586,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         else:
             if mode[0] != kind:
                 peer.set_oneshot_max(0 if kind == "peer_launches" else (4 << 20))
-                peer.set_hier_ll(1 if kind == "peer_hier_ll" else 0)
+                peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_pipe": 2}.get(kind, 0))
                 mode[0] = kind
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
@@ -601,7 +602,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         ref = small.clone()
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
-        for kind in ("peer_swing", "peer_hier", "peer_hier_ll"):
+        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe"):
             note(rank, f"verify: {kind}")
             try:   # the same calls on every rank: a raised status is raised everywhere
                 x = small.clone()
@@ -734,7 +735,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         return None
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll"}
+    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe"}
     if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
         roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
@@ -747,6 +748,8 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
            "peer_swing": "on-GPU tree reduce, 2D Swing BO over peer-mapped xGMI windows (one kernel), broadcast",
            "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "
                         "windows, broadcast (per-tile flags)",
+           "peer_hier_pipe": "ONE kernel, pipelined per tile: on-GPU tree reduce, mem_2D one-shot across GPUs with LL "
+                             "pushes into peer-mapped xGMI windows, broadcast (tile j read, j-1 summed, j-2 written)",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     return {

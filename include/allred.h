@@ -359,7 +359,10 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * (allred_mem_2D semantics over the per-GPU trees).  Every rank must use the
  * same setting.  Replaces nothing in the reference (its mem_2D phases sync
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
-/* 0 = off.  (The pipelined specialised-wave form of round 1 lives in
+/* 0 = off, 1 = k_hier_ll (all tiles read, owned tiles summed, all tiles
+ * written: three phases), 2 = k_hier_pipe (the same hand-offs on the
+ * lagged-store pipeline: iteration j reads tile j, sums owned tile j-1 and
+ * writes tile j-2).  (The specialised-wave form of round 1 lives in
  * tools/ubench/ws_trace.hip: 27-38 us vs 18 at W = 1, never a candidate.) */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
 /* Caps the grid of the hierarchical one-kernel forms at `groups` workgroups

@@ -130,6 +130,11 @@ int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, 
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream);
+// the same step on the lagged-store pipeline (k_hier_pipe): tree / owner sum / row stores of
+// tiles j, j-1, j-2 in one iteration; same arguments and bits as launch_hier_ll
+int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                     size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                     void* stream);
 // allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * n / 8
 int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
                        uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream);

@@ -55,7 +55,7 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
-    int hier_ll = 0;                // 0 off, 1 k_hier_ll (LL push hand-offs)
+    int hier_ll = 0;                // 0 off, 1 k_hier_ll (LL push hand-offs), 2 k_hier_pipe (the same, pipelined)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
@@ -197,8 +197,9 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
-        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
-                            p->max_groups, stream);
+        st = (p->hier_ll == 2 ? launch_hier_pipe : launch_hier_ll)(buf, n, order, ll, p->nranks, p->rank, n,
+                                                                   p->ll_box_words, p->calls + 1u, p->status,
+                                                                   p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -311,7 +312,7 @@ int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
 
 int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
-    if (enable < 0 || enable > 1) return ALLRED_ERR_ARG;
+    if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
     return ALLRED_OK;
 }

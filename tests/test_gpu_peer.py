@@ -100,14 +100,15 @@ def worker(rank, world, port, q):
         if not all(np.array_equal(got[i], partials[rank]) for i in range(local)):
             fails.append(("hier", 0, 1))
         # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form
-        # (k_hier_oneshot, per-tile flags), the LL push form (k_hier_ll) and the
-        # launch form, two calls back to back each (then LL once more after the
+        # (k_hier_oneshot, per-tile flags), the LL push form (k_hier_ll), its
+        # pipelined form (k_hier_pipe) and the launch form, two calls back to back each (then LL once more after the
         # launch form: its LL boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
         # in full and capped grids (a capped grid gives every workgroup many tiles)
         for mi, (mode, limit, ll, cap) in enumerate((("hier_one_kernel", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
-                                                     ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1))):
+                                                     ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1),
+                                                     ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2))):
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
             peer.set_max_groups(cap)
@@ -309,8 +310,8 @@ def t_timeout_bit():
 
 @pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
 def test_hier_forms_single_gpu_bit_exact(n, cap):
-    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll, the flag form
-    k_hier_oneshot and the launch form give the same
+    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll, its pipelined
+    form k_hier_pipe, the flag form k_hier_oneshot and the launch form give the same
     bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
     mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
     (both LL parities).  Config-2 size full grid and with capped grids (many
@@ -331,7 +332,7 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (1, 0)):
+        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (2, 0), (1, 0), (2, 0)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
@@ -358,7 +359,7 @@ def test_peer_knob_argument_errors():
     peer.connect([peer.handle()])
     try:
         with pytest.raises(_lib.AllredError):
-            peer.set_hier_ll(2)            # 0 or 1 only (the pipelined form is a tools/ubench study)
+            peer.set_hier_ll(3)            # 0 off, 1 k_hier_ll, 2 k_hier_pipe
         with pytest.raises(_lib.AllredError):
             peer.set_hier_ll(-1)
         peer.set_lo_ll_max(0)

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
+x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_oneshot,
+k_hier_ll and k_hier_pipe — the N > 1 bench's candidates with the cross-GPU
+hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
+kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
+arms interleaved.   python tools/hier_step.py [steps] [rounds]"""
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import tenstorrentallreduce_amd as t  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+P, n = 64, 327680
+NS = int(os.environ.get("AB_SETS", "32"))
+sets = [torch.randint(0x3F80, 0x42C8, (P, n), dtype=torch.int16, device="cuda") for _ in range(NS)]
+ws = torch.empty(n, dtype=torch.int16, device="cuda")
+peer = t.Peer(1, 0, 0, 2 * n)
+peer.connect([peer.handle()])
+s = torch.cuda.Stream()
+arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
+res = {k: [] for k in arms}
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for _ in range(rounds):
+    for name, (limit, ll) in arms.items():
+        peer.set_oneshot_max(limit)
+        peer.set_hier_ll(ll)
+        for i in range(20):
+            peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(200000)
+        e0.record(s)
+        for i in range(steps):
+            peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
+        e1.record(s)
+        torch.cuda.synchronize()
+        res[name].append(round(e0.elapsed_time(e1) * 1e3 / steps, 3))
+status = peer.status()
+peer.close()
+print(json.dumps({"W": 1, "bytes_per_rank": n * 2, "ranks": P, "sets": NS, "steps": steps,
+                  "us_per_step": res, "median": {k: statistics.median(v) for k, v in res.items()},
+                  "peer_status": status}))
