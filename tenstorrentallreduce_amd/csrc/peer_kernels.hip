@@ -610,7 +610,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
 // k_hier_pipe: the same step and the same bits as k_hier_ll, on k_tree_lds_lag's
 // pipeline instead of three phases.  k_hier_ll first reads every tile (A), then
 // sums the owned ones (R), then writes every tile (B): the chip reads only,
-// then writes only (18.1 us at W = 1 vs 14.1 for the fused one-GPU pass, whose
+// then writes only (17.6 us at W = 1 vs 14.1 for the fused one-GPU pass, whose
 // reads and writes overlap).  Here iteration j of a workgroup (two per CU, two
 // 32 KiB tiles of LDS) does
 //   A(j)    tile j's local tree -> its partial pushed to the owner's inbox
@@ -618,47 +618,78 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
 //           summed (fp32, owner first, one rounding), pushed to every GPU's box
 //   B(j-2)  tile j-2's result polled from this GPU's box, its 64 rank rows
 //           stored interleaved with tile j+2's LDS-DMA loads
-// and two drain iterations finish R / B.  Every poll waits only for work of
-// strictly earlier iterations of the same workgroup index on every GPU (A(j-1)
-// before R(j-1), R(j-2) before B(j-2)), and the grid is resident, so every wait
-// is reached and satisfied; a GPU's hand-offs have one (R) and two (B)
-// iterations of local work to arrive in.  The top-of-iteration vmcnt wait
-// counts only the tile loads and row stores (puts and polls issued in between
-// only make it wait a little longer).
+// and two drain iterations finish R / B.  A poll is a VMEM load, and CDNA
+// retires a wave's VMEM operations in order, so a poll issued behind the next
+// tile's loads would wait for them.  Hence the tile parity split: waves 0-1
+// load, poll, push and store the even tiles, waves 2-3 the odd ones (16 row
+// loads / stores per wave and tile; all four waves reduce every tile).  At
+// iteration j the waves of tile j's parity have nothing else outstanding, so
+// their polls wait for the polled words only, while tile j+1's loads (the
+// other pair's) stay in flight.  Every poll waits for strictly earlier
+// iterations of the same workgroup index on every GPU (A(j-1) before R(j-1),
+// R(j-2) before B(j-2)), and the grid is resident, so every wait is reached
+// and satisfied; the hand-offs have one (R) and two (B) iterations of local
+// work to arrive in.
+__device__ __forceinline__ void ll_load(const uint64_t* src, uint64_t (&wd)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool ll_fresh(const uint64_t (&wd)[4], uint32_t e) {
+    return (uint32_t)(wd[0] >> 32) == e && (uint32_t)(wd[1] >> 32) == e && (uint32_t)(wd[2] >> 32) == e &&
+           (uint32_t)(wd[3] >> 32) == e;
+}
+__device__ __forceinline__ uint4 ll_data(const uint64_t (&wd)[4]) {
+    return make_uint4((uint32_t)wd[0], (uint32_t)wd[1], (uint32_t)wd[2], (uint32_t)wd[3]);
+}
+
 __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                       const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                       uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
                                                       uint32_t epoch, uint32_t* status) {
-    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    constexpr int P = 64, NW = 4, TV = 32, RPW = P / NW, LPL = 8, OPS = 16;   // OPS: row ops per wave and tile
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 xs[(kLLMaxGpus + 1) * TV];   // R: W partials + the sum
-    __shared__ __attribute__((aligned(16))) uint4 resb[TV];                     // B: one tile's result
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
+    const int par = __builtin_amdgcn_readfirstlane(w >> 1), li = (w & 1) * 64 + lane;   // tile parity; lane in the pair
+    // rows of a pair wave: 32 (w & 1) + 2k + q, k < 16
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
-    auto row = [&](int k) { return ranks + (uint64_t)(RPW * w + RPI * k + q) * stride; };
-    auto issue = [&](uint64_t t, int b) {
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + t * TV + c,
-                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
-    };
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(32 * (w & 1) * TV * 16));
+    auto row = [&](int k) { return ranks + (uint64_t)(32 * (w & 1) + 2 * k + q) * stride; };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
     auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
     uint64_t* const my_ll = lp.ll[me];
-    if (mine > 0) issue(tile_of(0), 0);
-    if (mine > 1) issue(tile_of(1), 1);
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + t * TV + c, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
+    };
     if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
-    wait_vm<0>();   // (the order bytes; tiles 0 and 1 are waited for below anyway)
+    wait_vm<0>();
+    if (mine > par) issue(tile_of(par), par);   // tile 0 by waves 0-1, tile 1 by waves 2-3
     for (int j = 0; j < mine + 2; ++j) {
-        if (j < mine) {   // ---- A(j)
-            // after L(j): S(j-4)'s last op, L(j+1), S(j-3) (+ puts and polls: waits a little longer)
-            wait_any((j >= 4 ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 3 ? OPS : 0));
+        const bool mp = par == (j & 1);   // this wave serves tile j's parity (wave-uniform)
+        const bool own_r = j >= 1 && j - 1 < mine && owner_of(tile_of(j - 1)) == me;   // workgroup-uniform
+        const bool do_b = j >= 2 && j - 2 < mine;
+        const bool rl = mp && own_r && li < TV;   // this lane sums column c of tile j-1
+        // polls of R(j-1) (the W partials of column c) and B(j-2) (tile j-2's result
+        // in column c, every lane of the pair), issued before the tree: their
+        // latency hides behind it.  The pair has no other VMEM operation in flight.
+        uint64_t wr[kLLMaxGpus][4], wb[4];
+        if (mp) {
+            if (j < mine) wait_vm<0>();   // this pair's loads of tile j (and its older stores) are done
+            if (rl) {
+                const uint64_t lr = tile_of(j - 1) - (uint64_t)me * tiles_per_owner;
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) ll_load(my_ll + (lr * W + src) * 128 + c * 4, wr[src]);
+            }
+            if (do_b) ll_load(my_ll + box_words + tile_of(j - 2) * 128 + c * 4, wb);
+        }
+        if (j < mine) {   // ---- A(j): every wave reduces
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -672,57 +703,56 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            if (w == 0 && q == 0) {
+            if (mp && li < TV) {   // the partial of tile j -> its owner's inbox
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
-                const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-                ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, res, epoch);
+                const uint4 pr = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
+                ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, pr, epoch);
             }
         }
-        if (j >= 1 && j - 1 < mine && owner_of(tile_of(j - 1)) == me) {   // ---- R(j-1) (workgroup-uniform)
-            const uint64_t t = tile_of(j - 1), li = t - (uint64_t)me * tiles_per_owner;
-            const int src = threadIdx.x >> 5;   // source GPU of this lane's slot
-            if (src < W) xs[src * TV + c] = ll_get(my_ll + (li * W + src) * 128 + c * 4, epoch, status);
-            lds_barrier();
-            if (threadIdx.x < TV) {
-                const uint4 s0 = xs[me * TV + c];
-                float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
-                for (int qq = 0; qq < W; ++qq) {
-                    if (qq == me) continue;
-                    const uint4 y = xs[qq * TV + c];
-                    a[0] += lo_f(y.x); a[1] += hi_f(y.x);
-                    a[2] += lo_f(y.y); a[3] += hi_f(y.y);
-                    a[4] += lo_f(y.z); a[5] += hi_f(y.z);
-                    a[6] += lo_f(y.w); a[7] += hi_f(y.w);
-                }
-                uint4 o;
-                o.x = pack_rne(a[0], a[1]);
-                o.y = pack_rne(a[2], a[3]);
-                o.z = pack_rne(a[4], a[5]);
-                o.w = pack_rne(a[6], a[7]);
-                xs[kLLMaxGpus * TV + c] = o;
-            }
-            lds_barrier();
-            if (src < W) ll_put(lp.ll[src] + box_words + t * 128 + c * 4, xs[kLLMaxGpus * TV + c], epoch);
-        }
-        uint4 rv = make_uint4(0, 0, 0, 0);
-        const bool store = j >= 2 && j - 2 < mine;
-        if (store) {   // ---- B(j-2): poll
-            if (threadIdx.x < TV) resb[c] = ll_get(my_ll + box_words + tile_of(j - 2) * 128 + c * 4, epoch, status);
-            lds_barrier();
-            rv = resb[c];
-        }
-        if (store || j + 2 < mine) {   // tile j+2's loads and tile j-2's stores, interleaved op by op
-            const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 2);
-            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+        if (!mp) continue;
+        if (rl) {   // ---- R(j-1): owner first, then ascending; fp32, one rounding -> every GPU's box
+            const uint64_t t = tile_of(j - 1), lr = t - (uint64_t)me * tiles_per_owner;
+            uint4 y[kLLMaxGpus];
 #pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                if (j + 2 < mine)
-                    lds_dma16(reinterpret_cast<const uint4*>(row(k)) + tl * TV + c, bl + (uint32_t)(RPI * k * TV * 16));
-                if (store) st_nt(reinterpret_cast<uint4*>(row(k)) + ts * TV + c, rv);
+            for (int src = 0; src < kLLMaxGpus; ++src) {
+                if (src >= W) continue;
+                const uint64_t* at = my_ll + (lr * W + src) * 128 + c * 4;
+                y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(at, epoch, status);
             }
+            uint4 s0 = y[0];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src == me) s0 = y[src];
+            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+#pragma unroll
+            for (int qq = 0; qq < kLLMaxGpus; ++qq) {
+                if (qq >= W || qq == me) continue;
+                a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
+                a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
+                a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
+                a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
+            }
+            uint4 o;
+            o.x = pack_rne(a[0], a[1]);
+            o.y = pack_rne(a[2], a[3]);
+            o.z = pack_rne(a[4], a[5]);
+            o.w = pack_rne(a[6], a[7]);
+#pragma unroll
+            for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c * 4, o, epoch);
         }
-        lds_barrier();   // resb / xs / part are free for the next iteration
+        uint4 res = make_uint4(0, 0, 0, 0);
+        if (do_b) res = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + tile_of(j - 2) * 128 + c * 4, epoch, status);
+        // tile j+2's loads and tile j-2's stores, interleaved op by op (both of this parity)
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 2);
+        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            if (j + 2 < mine)
+                lds_dma16(reinterpret_cast<const uint4*>(row(k)) + tl * TV + c, bl + (uint32_t)(2 * k * TV * 16));
+            if (do_b) st_nt(reinterpret_cast<uint4*>(row(k)) + ts * TV + c, res);
+        }
     }
 }
 
