@@ -215,6 +215,14 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   lo_dag_reg        1: fused LO of the non-rank-uniform Swing schedules (32 / 64 ranks) as the
  *                     build-time DAG of distinct sums in registers (0 = the LDS DAG pass above)
  *   lo_dag_reg_min_tiles  64: smallest bucket (256-element tiles per rank, 32 kB) for lo_dag_reg
+ *   check             0; 1: check mode of the N > 1 step programs (allred_dist_allreduce and its
+ *                     host twin): each rank's program is verified once against its partners'
+ *                     (what a partner sends at step k is exactly what this rank receives; the
+ *                     received runs of a step are disjoint, inside the bucket) — ALLRED_ERR_SCHEDULE
+ *                     if not — and every receive region is filled with 0xFFFF (a bf16 NaN) before
+ *                     its step, so an element the transport never delivered surfaces as NaN in the
+ *                     result instead of stale data.  Same result bits on a correct run.  (The
+ *                     reference has no invariant or race checking)
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

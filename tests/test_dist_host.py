@@ -167,3 +167,78 @@ def test_dist_desc_validation():
     bad = t.dist_desc(t.SWING, t.BO, 4, 8, 100)              # not a multiple of 8 * total
     with pytest.raises(t.AllredError):
         t.dist_allreduce_host(bad, 0, buf, scratch, gloo_exchange)
+
+
+# ------------------------------------------------------------------ check mode
+def check_worker(rank, world, port, q):
+    """tune check=1: the same programs verified against the partners' and run
+    with every receive region poisoned (0xFFFF) first — results stay bit-exact;
+    then fault injection: the exchange silently drops one received run at one
+    rank.  Without the check mode the result is stale data that passes as
+    numbers; with it the dropped elements come out as NaN (detected)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import tenstorrentallreduce_amd as t
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    side, total = GRIDS[world]
+    n = 8 * total * 16
+    out = {}
+    with t.tuned(check=1):
+        for ci, (variant, algo, local, chans) in enumerate(cases(world)):
+            data = inputs(world, local, n, seed=300 * world + ci)
+            buf = np.concatenate(data[rank]).astype(np.uint16)
+            scratch = np.zeros(2 * n, dtype=np.uint16)
+            desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
+                               local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
+            t.dist_allreduce_host(desc, rank, buf, scratch, gloo_exchange)
+            want = np.concatenate(expected(variant, algo, world, local, data, chans)[rank])
+            out.setdefault("exact", []).append(bool(np.array_equal(buf, want)))
+
+    calls = [0]
+
+    def dropping_exchange(peer, sends, recvs):   # rank 0 loses its first received run of the first step
+        tmps = [torch.from_numpy(v.copy()) for v in recvs]
+        reqs = [dist.isend(torch.from_numpy(v), peer, tag=i) for i, v in enumerate(sends)]
+        reqs += [dist.irecv(x, peer, tag=i) for i, x in enumerate(tmps)]
+        for r in reqs:
+            r.wait()
+        for i, (v, x) in enumerate(zip(recvs, tmps)):
+            if not (rank == 0 and calls[0] == 0 and i == 0):
+                v[:] = x.numpy()
+        calls[0] += 1
+
+    for check in (0, 1):
+        calls[0] = 0
+        data = inputs(world, 1, n, seed=77)
+        buf = data[rank][0].copy()
+        scratch = np.zeros(2 * n, dtype=np.uint16)
+        desc = t.dist_desc(t.SWING, t.BO, side, total, n)
+        with t.tuned(check=check):
+            t.dist_allreduce_host(desc, rank, buf, scratch, dropping_exchange)
+        f = (buf.astype(np.uint32) << 16).view(np.float32)
+        want = expected("bo", t.SWING, world, 1, data, 1)[rank][0]
+        out[f"check{check}"] = (int(np.isnan(f).sum()), int((buf != want).sum()))
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_check_mode_poison_and_fault_injection(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=check_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, out in results.items():
+        assert all(out["exact"]), (rank, out["exact"])
+    # the dropped run corrupts results (somewhere) either way; only the check mode makes it NaN
+    assert sum(out["check0"][1] for out in results.values()) > 0
+    assert all(out["check0"][0] == 0 for out in results.values())
+    assert sum(out["check1"][0] for out in results.values()) > 0
+    assert all(out["check1"][0] == out["check1"][1] for out in results.values())
