@@ -231,19 +231,71 @@ std::vector<uint8_t> lo_steps_pairs(const allred_schedule& s, int N) {
     return pairs;
 }
 
-// The LO program in k_steps_pipe's layout: step 0's N/2 (r, p) rank pairs,
-// steps 1 .. S-1's (row of r, row of p), then N bytes: rank r's pair (row) at
-// the last step.
+// The LO program in k_steps_pipe's layout: step 0's N/2 (r, p) rank pairs ->
+// row i; steps 1 .. S-1's (row of r, row of p) per pair; then N bytes: rank
+// r's pair (row) at the last step.  A pair (r, p) of step k holds one value
+// for both its ranks, so each row of step k-1 is an operand of exactly two
+// pairs of step k: the operand graph is 2-regular (a union of cycles), and
+// walking each cycle assigns every pair of step k one of its operand rows as
+// its own row, a different one for every pair.  The table lists that operand
+// first (a == x for pair x), so the lane that computed row x at step k-1 keeps
+// it in a register and reads only the other operand from LDS.
 std::vector<uint8_t> lo_steps_pipe_table(const allred_schedule& s, int N) {
     const int S = s.steps, H = N / 2;
-    const std::vector<uint8_t> pr = lo_steps_pairs(s, N);
-    if (S == 0 || pr.size() != (size_t)(2 * H * S + 2 * H * (S - 1))) return {};
-    std::vector<uint8_t> out(pr.begin(), pr.begin() + 2 * H);       // step 0 rank pairs
-    out.insert(out.end(), pr.begin() + 2 * H * S, pr.end());         // steps >= 1 row pairs
-    std::vector<uint8_t> last(N, 0);
-    const uint8_t* lp = &pr[(size_t)2 * H * (S - 1)];
-    for (int i = 0; i < H; ++i) last[lp[2 * i]] = last[lp[2 * i + 1]] = (uint8_t)i;
-    out.insert(out.end(), last.begin(), last.end());
+    if (S == 0 || N < 2) return {};
+    std::vector<uint8_t> out;
+    std::vector<int> row(N, -1), nrow(N, -1);
+    int cnt = 0;
+    for (int r = 0; r < N; ++r) {   // step 0: pairs in rank order
+        const int p = s.partner[r][0];
+        if (r >= p) continue;
+        out.push_back((uint8_t)r);
+        out.push_back((uint8_t)p);
+        row[r] = row[p] = cnt++;
+    }
+    if (cnt != H) return {};
+    for (int k = 1; k < S; ++k) {
+        // this step's pairs as edges between the previous step's rows
+        std::vector<std::pair<int, int>> edge;   // (rank r, rank p), r < p
+        std::vector<std::vector<int>> at(H);     // row -> incident edges
+        for (int r = 0; r < N; ++r) {
+            const int p = s.partner[r][k];
+            if (r >= p) continue;
+            at[row[r]].push_back((int)edge.size());
+            at[row[p]].push_back((int)edge.size());
+            edge.emplace_back(r, p);
+        }
+        if ((int)edge.size() != H) return {};
+        for (const auto& a : at)
+            if (a.size() != 2) return {};
+        // walk every cycle: edge e leaves row u and is assigned to u
+        std::vector<int> own(H, -1);   // edge -> its row
+        std::vector<bool> used(H, false);
+        for (int start = 0; start < H; ++start) {
+            if (used[start]) continue;
+            int u = start, e = at[u][0];
+            while (own[e] < 0) {
+                own[e] = u;
+                used[u] = true;
+                const int a = row[edge[e].first], b = row[edge[e].second];
+                const int v = a == u ? b : a;   // the edge's other end
+                e = at[v][0] == e ? at[v][1] : at[v][0];
+                u = v;
+            }
+        }
+        std::vector<uint8_t> step(2 * H, 0);
+        for (int e = 0; e < H; ++e) {
+            const int x = own[e];
+            if (x < 0) return {};
+            const int a = row[edge[e].first], b = row[edge[e].second];
+            step[2 * x] = (uint8_t)x;               // kept in a register
+            step[2 * x + 1] = (uint8_t)(a == x ? b : a);
+            nrow[edge[e].first] = nrow[edge[e].second] = x;
+        }
+        out.insert(out.end(), step.begin(), step.end());
+        row = nrow;
+    }
+    for (int r = 0; r < N; ++r) out.push_back((uint8_t)row[r]);
     return out;
 }
 

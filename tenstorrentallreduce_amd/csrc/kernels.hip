@@ -1165,8 +1165,8 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
         // every row, so a step needs no workgroup barrier — LDS operations of
         // one wave execute in order, and no other wave touches these columns.
         const int cw = 8 * w + (lane & 7);
+        uint4 val[IPW];   // LO: this lane's rows (x = (lane + 64t) >> 3) after the latest step
         {   // step 0 from the staged rows: pair x = (r, p) -> row x (every read before any write)
-            uint4 val[IPW];
 #pragma unroll
             for (int t = 0; t < IPW; ++t)
                 if (lane + 64 * t < H * 8)
@@ -1187,15 +1187,17 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
                         const int a = (pp[ph - 1][m] & 255) * TV + cw, cc = (pp[ph - 1][m] >> 8) * TV + cw;
                         tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
                     }
-            } else {   // exchange step ph: pair x = rows of its ranks after step ph-1 -> row x
-                uint4 val[IPW];
+            } else {   // exchange step ph: pair x = row x (kept in val) + the row of its other rank
+                uint4 oth[IPW];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * 8)
-                        val[m] = add8(tile[(pp[ph - 1][m] & 255) * TV + cw], tile[(pp[ph - 1][m] >> 8) * TV + cw]);
+                    if (lane + 64 * m < H * 8) oth[m] = tile[(pp[ph - 1][m] >> 8) * TV + cw];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * 8) tile[((lane + 64 * m) >> 3) * TV + cw] = val[m];
+                    if (lane + 64 * m < H * 8) {
+                        val[m] = add8(val[m], oth[m]);
+                        tile[((lane + 64 * m) >> 3) * TV + cw] = val[m];
+                    }
             }
             __builtin_amdgcn_wave_barrier();
             stamp(stamps, u * STAMPS + 1 + ph);
