@@ -117,6 +117,14 @@ int allred_schedule_build(int algo, int side_length, int total_nodes, allred_sch
  * *read_conflicts = extra LDS bank cycles of its reads per column group and
  * tile (0 once placed; allred_tune_set("lo_dag_place", 0) keeps first-appearance order). */
 int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size_t cap, int* read_conflicts);
+/* The schedule form's step program as k_steps_pipe reads it (kernels.hip):
+ * the per-core RS / AG loops of allred_BO_2D/kernels/dataflow_kernel.cpp:152-267
+ * (variant ALLRED_BO: total x 256 bytes, one block per 256) or the LO exchange
+ * steps of allred_LOO_2D/kernels/dataflow_kernel.cpp:127-175 (ALLRED_LO:
+ * 2 (total/2) S + total bytes), restated on the unit's LDS rows.  Returns the
+ * bytes written into out[cap], 0 when the schedule has no such program, or a
+ * negative status.  For inspection and CPU checks (tests/test_steps_program.py). */
+int allred_steps_program(int algo, int variant, int side_length, int total_nodes, uint8_t* out, size_t cap);
 
 /* ======================================================================
  * Host data — tt-metal bfloat16 helpers the reference calls

@@ -122,6 +122,7 @@ SIGNATURES = [
     ("allred_get_comm_partner_recdub_1d", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_uint32)]),
     ("allred_schedule_build", C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(Schedule)]),
     ("allred_lo_dag", C.c_int, [C.c_int, C.c_int, C.c_int, _P, C.c_size_t, C.POINTER(C.c_int)]),
+    ("allred_steps_program", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, _P, C.c_size_t]),
     ("allred_random_bf16_vector", None, [C.c_size_t, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_constant_bf16_vector", None, [C.c_size_t, C.c_float, _P]),
     ("allred_validate_result_vector", C.c_long,
