@@ -27,6 +27,7 @@ import os
 import statistics
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -524,7 +525,7 @@ def xgmi_arm(out, comm, peer, world, dev, stream, side, total, name, algo, varia
     del b2, w2
 
 
-def bench_multi(args, rank, world, local_rank) -> dict | None:
+def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     # --share-gpu (rehearsal only): every rank on cuda:0 and no RCCL (it refuses two
     # ranks on one device), so the whole N>1 path except RCCL runs on a 1-GPU box
     dev_index = 0 if args.share_gpu else local_rank
@@ -712,7 +713,29 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         extras["peer_error"] = peer_err
     if comm_err:
         extras["rccl_error"] = comm_err
+
+    def line(ex):
+        return multi_line(args, world, transport, ms_per_step, local_ms, wall, ex)
+
     if args.extras:
+        # The headline is measured; the extras must not be able to lose it.  If
+        # they have not finished after --extras-timeout s (a hung transport on an
+        # untried machine), rank 0 prints the line with what it has and every
+        # rank leaves; the driver still gets its one JSON line.
+        def give_up():
+            if rank == 0:
+                try:
+                    ex = {k: v for k, v in list(extras.items())}
+                except Exception:  # extras being written concurrently: headline only
+                    ex = {}
+                ex["extras_error"] = f"extras did not finish within {args.extras_timeout:g} s"
+                emit(line(ex))
+            os._exit(0)
+
+        HEADLINE_DONE.set()
+        guard = threading.Timer(args.extras_timeout + (0 if rank == 0 else 10), give_up)
+        guard.daemon = True
+        guard.start()
         extras.update(xgmi_arms(comm, peer if verify.get("peer_swing") else None, world, dev, stream, side, total))
         if world > 1 and comm is not None:
             try:
@@ -723,6 +746,7 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
                         v["xgmi_frac_measured_link"] = round(v["busbw_GBps"] / ((world - 1) * mb), 4)
             except Exception as e:  # reported, never silently dropped
                 extras["link_probe"] = {"error": repr(e)}
+        guard.cancel()
     if peer is not None:
         st = torch.tensor([peer.status()], dtype=torch.int64)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
@@ -733,6 +757,16 @@ def bench_multi(args, rank, world, local_rank) -> dict | None:
         comm.close()
     if rank != 0:
         return None
+    return line(extras)
+
+
+# set once the N > 1 headline is measured: a rank that then loses its peers
+# (rank 0 gave up on the extras and left) exits cleanly instead of failing the job
+HEADLINE_DONE = threading.Event()
+
+
+def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> dict:
+    """rank 0's JSON line of the N > 1 bench"""
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
     one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe"}
@@ -795,6 +829,8 @@ def main():
                     help="N = 1: back-to-back replays of the K timed steps; ms_per_step = median replay / K")
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     ap.add_argument("--no-extras", dest="extras", action="store_false")
+    ap.add_argument("--extras-timeout", type=float, default=240.0,
+                    help="N > 1: seconds the extras may take before the headline line is printed without them")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
     ap.add_argument("--force-dist", action="store_true", help="run the N>1 code path on one GPU (1-rank RCCL)")
     ap.add_argument("--share-gpu", action="store_true",
@@ -810,7 +846,18 @@ def main():
             dist.init_process_group("gloo", rank=0, world_size=1)
         else:
             dist.init_process_group("gloo")
-        out = bench_multi(args, rank, world, local_rank)
+        def emit(line):
+            sys.stdout.flush()
+            os.write(real_stdout, (json.dumps(line) + "\n").encode())
+
+        try:
+            out = bench_multi(args, rank, world, local_rank, emit)
+        except Exception as e:
+            if rank == 0 or not HEADLINE_DONE.is_set():
+                raise
+            note(rank, f"extras ended by a peer's exit ({e!r}); rank 0 reports the headline")
+            sys.stderr.flush()
+            os._exit(0)
         dist.destroy_process_group()
     else:
         out = bench_single(args)
