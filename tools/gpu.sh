@@ -8,6 +8,8 @@
 #   bench [bench args]   bench.py (default: the driver's N = 1 line)
 #   prof <tag>           rocprofv3 --kernel-trace --stats of bench.py --main-only,
 #                        then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
+#   ab <v> "<tiles>" <tune a> <tune b> ...   tools/ab_fused.py arms interleaved (ALLRED_TUNE per arm)
+#   skew ["<pads>"]      rank-row skew A/B of the config-2 fused pass
 #   share <n>            the N > 1 bench path rehearsed with n ranks on the one GPU
 #                        (bench.py --share-gpu: peer transports, no RCCL; numbers mean nothing)
 set -o pipefail
@@ -70,6 +72,23 @@ for r in rows:
 for k, v in by.items():
     print(k, sorted(v))
 EOF
+    ;;
+skew)
+    # skew "<pads in elements>": rank-row skew A/B of the config-2 fused pass (stride = n + pad)
+    rm -f gpurun_out/pad.jsonl
+    for rep in 1 2; do
+        for pad in ${1:-0 64 128 256 512 1024 2048 4096}; do
+            AB_PAD=$pad AB_SETS=32 timeout -k 10 120 python tools/ab_fused.py bo 5 200 >> gpurun_out/pad.jsonl \
+                2>> gpurun_out/pad.err || exit 1
+        done
+    done
+    python - <<'EOF2'
+import json, collections
+by = collections.defaultdict(list)
+for l in open("gpurun_out/pad.jsonl"):
+    r = json.loads(l); by[int(r["env"]["AB_PAD"])].append(r["us"])
+for k in sorted(by): print(k * 2, "B skew:", sorted(by[k]))
+EOF2
     ;;
 share)
     n=${1:-2}
