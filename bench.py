@@ -324,10 +324,13 @@ def bench_single(args) -> dict:
     return out
 
 
-def timed_max(fn, reps, stream) -> float:
-    """ms per call on `stream`, max over ranks."""
+def timed_max(fn, reps, stream, after=None) -> float:
+    """ms per call on `stream`, max over ranks.  after(): completes the calls
+    (the pipelined transport's last bucket), inside the timed region."""
     for _ in range(2):
         fn()
+    if after:
+        after()
     torch.cuda.synchronize()
     dist.barrier()
     e0 = torch.cuda.Event(enable_timing=True)
@@ -335,6 +338,8 @@ def timed_max(fn, reps, stream) -> float:
     e0.record(stream)
     for _ in range(reps):
         fn()
+    if after:
+        after()
     e1.record(stream)
     torch.cuda.synchronize()
     m = torch.tensor([e0.elapsed_time(e1) / reps], dtype=torch.float64)
@@ -567,6 +572,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
     #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
     #   peer_hier_pipe  the same LL hand-offs on the lagged-store pipeline (k_hier_pipe)
+    #   peer_hier_x   the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
+    #                 reads bucket i+1 while it writes bucket i; the last flush is timed)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -577,9 +584,21 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
 
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
 
+    pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
+
+    def flush():
+        if pend[0] is not None:
+            peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
+            pend[0] = None
+
     def run(kind, b, fresh=False):
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
+        if kind == "peer_hier_x":   # buckets pipelined: this call finishes the previous one
+            peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
+            pend[0] = b.data_ptr()
+            return
+        flush()
         if kind == "rccl":
             t.dist_allreduce(comm, desc, b.data_ptr(), ws.data_ptr(), stream)
         elif kind == "peer_swing":
@@ -603,11 +622,12 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         ref = small.clone()
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
-        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe"):
+        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe", "peer_hier_x"):
             note(rank, f"verify: {kind}")
             try:   # the same calls on every rank: a raised status is raised everywhere
                 x = small.clone()
                 run(kind, x, fresh=True)
+                flush()
                 torch.cuda.synchronize()
                 ok = torch.equal(x, ref)
                 a, b2 = buf.clone(), buf.clone()
@@ -619,6 +639,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 else:   # the one-kernel forms against the launch form of the same semantics
                     run("peer_launches", a, fresh=True)
                     run(kind, b2)
+                    flush()
                 torch.cuda.synchronize()
                 ok = ok and (a is None or torch.equal(a, b2)) and (peer.status() & t.PEER_TIMEOUT) == 0
                 del x, a, b2
@@ -634,7 +655,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     for kind in candidates:
         note(rank, f"quick timing: {kind}")
         it = iter(range(1 << 30))
-        quick[kind] = round(timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), 50, stream), 4)
+        quick[kind] = round(timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), 50, stream, after=flush), 4)
     transport = min(candidates, key=lambda k: quick[k])
 
     def step(i):
@@ -649,6 +670,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         step(i)
     for i in range(args.warmup):
         step(i)
+    flush()
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
@@ -660,6 +682,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     e0.record(stream)
     for i in range(args.steps):
         step(i)
+    flush()   # peer_hier_x: the last bucket's finishing launch is part of the K steps' time
     e1.record(stream)
     torch.cuda.synchronize()
     dist.barrier()
@@ -769,7 +792,8 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
     """rank 0's JSON line of the N > 1 bench"""
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe"}
+    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
+                  "peer_hier_x": "k_hier_x"}
     if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
         roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
@@ -784,6 +808,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                         "windows, broadcast (per-tile flags)",
            "peer_hier_pipe": "ONE kernel, pipelined per tile: on-GPU tree reduce, mem_2D one-shot across GPUs with LL "
                              "pushes into peer-mapped xGMI windows, broadcast (tile j read, j-1 summed, j-2 written)",
+           "peer_hier_x": "ONE kernel per bucket, consecutive buckets pipelined (K buckets in K + 1 launches, all "
+                          "inside the timed region): on-GPU tree reduce of bucket i+1 while bucket i's rows are written, "
+                          "mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     return {

@@ -362,6 +362,20 @@ int allred_peer_connect(allred_peer* peer, const uint8_t* all_handles /*[nranks 
  * (tree of local rank 0) into `workspace` (elems * 2 bytes), then broadcast. */
 int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream);
+/* The hierarchical step of allred_peer_allreduce (64 local ranks per GPU, the
+ * same result bits) PIPELINED across consecutive buckets: one launch
+ * (k_hier_x) finishes `prev` — the bucket the previous call started — and
+ * starts `cur`, streaming cur's rank rows in while prev's rank rows go out
+ * (a bucket's own rows can only be written after every GPU has reduced it).
+ * A sequence of K buckets is K + 1 calls: (b0, NULL), (b1, b0), ...,
+ * (NULL, b_{K-1}); on return (stream order) prev holds its allreduced rows.
+ * While a bucket is pending, the other peer allreduce calls return
+ * ALLRED_ERR_ARG; so does a prev that is not the pending bucket.
+ * ALLRED_ERR_UNSUPPORTED: local_ranks != 64, more than 8 GPUs, flags not
+ * uncached, or more than 8 tiles of 256 elements per workgroup (n > 2^20).
+ * No reference counterpart (the reference runs one vector per program). */
+int allred_peer_allreduce_pipelined(allred_peer* peer, uint16_t* cur, uint16_t* prev, uint64_t elems,
+                                    int local_ranks, int local_side, int local_algo, void* stream);
 /* Buckets of at most `bytes` (default 4 MiB) run as one kernel (per-workgroup
  * flags, no kernel boundaries); larger ones as copy / barrier / reduce-scatter /
  * barrier / all-gather launches.  Same result bits either way.  Every rank

@@ -353,6 +353,14 @@ class Peer:
         if check_status:
             self.check(stream)
 
+    def allreduce_pipelined(self, cur_ptr: int | None, prev_ptr: int | None, elems: int, stream=None,
+                            local_ranks: int = 64, local_side: int = 8, local_algo: int = SWING) -> None:
+        """The hierarchical step pipelined across consecutive buckets (k_hier_x):
+        finishes prev (the bucket the previous call started) and starts cur.
+        K buckets = K + 1 calls: (b0, None), (b1, b0), ..., (None, b_{K-1})."""
+        check(lib.allred_peer_allreduce_pipelined(self._h, cur_ptr or None, prev_ptr or None, elems, local_ranks,
+                                                  local_side, local_algo, _stream_ptr(stream)), "peer_allreduce_pipelined")
+
     def dist_allreduce(self, desc: DistDesc, buf_ptr: int, workspace_ptr: int | None = None, stream=None,
                        check_status: bool = False) -> None:
         """dist_allreduce's program (same desc, same bits) over the peer windows."""

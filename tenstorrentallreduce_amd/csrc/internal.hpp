@@ -135,6 +135,12 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
 int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                      size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                      void* stream);
+// the hierarchical step across consecutive buckets (k_hier_x): finishes `prev` (may be null)
+// and starts `cur` (may be null) in one launch; llc / llp: every GPU's LL area of cur's /
+// prev's parity; ALLRED_ERR_UNSUPPORTED beyond kHierXMaxTiles tiles per workgroup
+int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
+                  uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
+                  uint32_t* status, unsigned max_grid, void* stream);
 // allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * n / 8
 int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
                        uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream);

@@ -59,6 +59,9 @@ struct allred_peer {
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
+    // allred_peer_allreduce_pipelined: a bucket started (its partials pushed) and not yet finished
+    bool pipe_pending = false;
+    uint32_t pipe_k = 0;            // that bucket's call number (epoch pipe_k + 1, LL parity pipe_k & 1)
 };
 
 extern "C" {
@@ -182,9 +185,43 @@ void parity_windows(allred_peer* p, uint16_t** wins) {
 
 }  // namespace
 
+int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* prev, uint64_t elems, int local_ranks,
+                                    int local_side, int local_algo, void* stream) {
+    if (!p || !p->connected || (!cur && !prev)) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)elems;
+    if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
+    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * 128 > p->ll_box_words)
+        return ALLRED_ERR_UNSUPPORTED;
+    // prev must be the bucket the previous call started; a started bucket must be finished next
+    if (prev ? (!p->pipe_pending || p->pipe_k + 1u != p->calls) : p->pipe_pending) return ALLRED_ERR_ARG;
+    const uint8_t* order = nullptr;
+    int st = local_tree_order(local_algo, local_side, local_ranks, &order);
+    if (st != ALLRED_OK) return st;
+    const uint32_t kc = p->calls, kp = p->pipe_k;
+    uint64_t* llc[ALLRED_MAX_NODES];
+    uint64_t* llp[ALLRED_MAX_NODES];
+    for (int q = 0; q < p->nranks; ++q) {
+        llc[q] = p->peer_ll[q] + (kc & 1u) * 2 * p->ll_box_words;
+        llp[q] = p->peer_ll[q] + (kp & 1u) * 2 * p->ll_box_words;
+    }
+    st = launch_hier_x(cur, prev, n, order, cur ? llc : nullptr, prev ? llp : nullptr, p->nranks, p->rank, n,
+                       p->ll_box_words, kc + 1u, kp + 1u, p->status, p->max_groups, stream);
+    if (st != ALLRED_OK) return st;
+    if (cur) {
+        p->pipe_k = kc;
+        p->pipe_pending = true;
+        ++p->calls;
+    } else {
+        p->pipe_pending = false;
+    }
+    p->last_all_peer = true;
+    return ALLRED_OK;
+}
+
 int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream) {
     if (!p || !buf || !p->connected) return ALLRED_ERR_ARG;
+    if (p->pipe_pending) return ALLRED_ERR_ARG;   // finish the pipelined sequence first
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     uint16_t* bucket = buf;
@@ -257,7 +294,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
 int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16_t* buf, void* workspace,
                                void* stream) {
     if (!p || !d || !buf || !p->connected) return ALLRED_ERR_ARG;
-    if (d->total_nodes != p->nranks) return ALLRED_ERR_ARG;
+    if (d->total_nodes != p->nranks || p->pipe_pending) return ALLRED_ERR_ARG;
     const size_t n = (size_t)d->elems;
     if (d->variant == ALLRED_MEM) {
         uint16_t* ws = workspace ? static_cast<uint16_t*>(workspace) + n : nullptr;  // dist workspace layout

@@ -756,6 +756,150 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
     }
 }
 
+// ---- hierarchical step across consecutive buckets ----------------------------
+// k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
+// hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
+// (cur 0, -), (cur 1, prev 0), ..., (-, prev K-1)).  Within one bucket the
+// read phase (tree -> partial) must finish on every GPU before its write phase
+// (result -> 64 rank rows) can start, so k_hier_ll reads only, then writes only
+// (17.6 us at W = 1 vs 14.1 for the fused one-GPU pass).  Across buckets there
+// is no such dependency: this launch streams cur's tiles in (LDS-DMA, two
+// tiles ahead, tree, partial pushed to the tile's owner) while writing prev's
+// tiles out, interleaved op by op as in k_tree_lds_lag.  Order in a launch:
+//   L(cur 0), L(cur 1) issued (HBM busy from the start), then prev's results
+//            of this workgroup's tiles polled into LDS (the owners pushed them
+//            at the end of the previous launch)
+//   loop j:  A(cur j) [tree, partial -> owner] | S(prev j) stores interleaved
+//            with L(cur j+2)
+//   R(cur)   the tiles of cur this GPU owns: the W partials (pushed during
+//            this launch's loops) polled, summed (fp32, owner first, one
+//            rounding), the result pushed to every GPU's box
+// Up to kHierXMaxTiles tiles per workgroup (results staged in LDS).  Every poll
+// waits for work that waits on nothing of the poller (the results: the owners'
+// previous launches; R(cur): every GPU's loop of this launch, which polls only
+// results of the previous launch), and the grid is resident, so every wait is
+// satisfied.
+constexpr int kHierXMaxTiles = 8;   // lanes (j, c) of the whole workgroup serve tile j
+
+__global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
+                                                   uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
+                                                   LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
+                                                   uint64_t box_words, uint32_t ecur, uint32_t eprev,
+                                                   uint32_t* status) {
+    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
+    __shared__ __attribute__((aligned(16))) uint4 res[kHierXMaxTiles][TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
+                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
+    };
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    wait_vm<0>();   // the order bytes
+    if (cur && mine > 0) issue(tile_of(0), 0);
+    if (cur && mine > 1) issue(tile_of(1), 1);
+    // ---- prev's results of this workgroup's tiles -> LDS: lane (j, c) (32 j + c)
+    // serves tile j, column c.  The owners pushed them at the end of the previous
+    // launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep HBM busy.
+    const int jr = threadIdx.x / TV;
+    if (prev && jr < kHierXMaxTiles && jr < mine) {
+        const uint64_t* at = lpv.ll[me] + box_words + tile_of(jr) * 128 + c * 4;
+        uint64_t wd[4];
+        ll_load(at, wd);
+        res[jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+    }
+    lds_barrier();   // order bytes and results in LDS
+    for (int j = 0; j < mine; ++j) {
+        if (cur) {   // ---- A(cur j)
+            // after L(j): S(j-2)'s last op, L(j+1), S(j-1) (+ wave 0's partial pushes: waits a little longer)
+            wait_any((j >= 2 && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && prev ? OPS : 0));
+            lds_barrier();   // tile j is in LDS
+            const uint4* tile = buf[j & 1];
+            const uint8_t* ord = ord_lds + RPW * w + LPL * q;
+            uint4 x[LPL];
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+            for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+            if (q == 0) part[j & 1][w * TV + c] = pw;
+            lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
+            if (w == 0 && q == 0) {
+                const uint64_t t = tile_of(j);
+                const int o = owner_of(t);
+                const uint4* pp = part[j & 1];
+                const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+                ll_put(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, pr, ecur);
+            }
+        }
+        // ---- cur's tile j+2 in, prev's tile j out, interleaved op by op
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(j);
+        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+        const uint4 rv = prev ? res[j][c] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            if (cur && j + 2 < mine)
+                lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
+                          bl + (uint32_t)(RPI * k * TV * 16));
+            if (prev) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
+        }
+    }
+    // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
+    // partial (during this launch's loop): W partials summed (fp32, owner first,
+    // one rounding), the result pushed to every GPU's box for the next launch.
+    if (cur && jr < kHierXMaxTiles && jr < mine) {
+        const uint64_t t = tile_of(jr);
+        if (owner_of(t) == me) {
+            const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
+            uint64_t wr[kLLMaxGpus][4];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c * 4, wr[src]);
+            uint4 y[kLLMaxGpus];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W)
+                    y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
+                                                     : ll_get(lc.ll[me] + (lr * W + src) * 128 + c * 4, ecur, status);
+            uint4 s0 = y[0];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src == me) s0 = y[src];
+            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+#pragma unroll
+            for (int qq = 0; qq < kLLMaxGpus; ++qq) {
+                if (qq >= W || qq == me) continue;
+                a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
+                a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
+                a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
+                a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
+            }
+            uint4 o;
+            o.x = pack_rne(a[0], a[1]);
+            o.y = pack_rne(a[2], a[3]);
+            o.z = pack_rne(a[4], a[5]);
+            o.w = pack_rne(a[6], a[7]);
+#pragma unroll
+            for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c * 4, o, ecur);
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_peer_mem_ll: allred_mem_2D across GPUs for small buckets with LL hand-offs
 // (the flat counterpart of k_hier_ll).  A: every vector is pushed as four
@@ -993,6 +1137,27 @@ int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uin
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_pipe, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
                        me, ntiles, ntiles / nranks, box_words, epoch, status);
+    return peer_last_error();
+}
+
+int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
+                  uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
+                  uint32_t* status, unsigned max_grid, void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
+        (!cur && !prev) || (cur && !aligned16(cur)) || (prev && !aligned16(prev)))
+        return ALLRED_ERR_ARG;
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
+    if ((ntiles + grid - 1) / grid > (uint64_t)kHierXMaxTiles) return ALLRED_ERR_UNSUPPORTED;
+    LLPtrs lc{}, lp{};
+    for (int q = 0; q < nranks; ++q) {
+        lc.ll[q] = llc ? llc[q] : nullptr;
+        lp.ll[q] = llp ? llp[q] : nullptr;
+    }
+    hipLaunchKernelGGL(k_hier_x, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, prev, stride, order, lc, lp,
+                       nranks, me, ntiles, ntiles / nranks, box_words, ecur, eprev, status);
     return peer_last_error();
 }
 

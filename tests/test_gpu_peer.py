@@ -108,7 +108,10 @@ def worker(rank, world, port, q):
         for mi, (mode, limit, ll, cap) in enumerate((("hier_one_kernel", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
                                                      ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1),
-                                                     ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2))):
+                                                     ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2),
+                                                     ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1))):
+            if cap < 0:   # k_hier_x takes at most 8 tiles per workgroup
+                cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
             peer.set_max_groups(cap)
@@ -118,8 +121,14 @@ def worker(rank, world, port, q):
                         for r in range(world)]
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
-                peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+                if mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
+                    peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
+                                             torch.cuda.current_stream())
+                else:
+                    peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
+            if mode.startswith("hier_x"):
+                peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
             torch.cuda.synchronize()
             for rep, (data, buf, _) in enumerate(runs):
                 partials = []
@@ -346,6 +355,59 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
         assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.set_hier_ll(0)
+        peer.close()
+
+
+@pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 4), (256 * 5, 0, 3), (256 * 40, 5, 2), (327680, 160, 1)])
+def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
+    """One GPU (W = 1), 64 local ranks: a sequence of buckets through the
+    pipelined hierarchical step (k_hier_x: each launch finishes the previous
+    bucket while it reads the next), buckets + 1 calls, every bucket bit-exact
+    vs the oracle (tree of local rank 0, the mem_2D sum of one partial, rows
+    overwritten with it); full and capped grids (up to 8 tiles per workgroup).
+    Protocol errors: a prev that is not the pending bucket, another peer call
+    while a bucket is pending, finishing with nothing pending."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import tenstorrentallreduce_amd as t
+    from tenstorrentallreduce_amd import _lib
+    import oracle
+    local = 64
+    peer = t.Peer(1, 0, 0, 2 * n)
+    peer.connect([peer.handle()])
+    try:
+        peer.set_max_groups(cap)
+        data, want = [], []
+        for b in range(buckets):
+            d = np.random.default_rng(1300 + b).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+            loc = [x.copy() for x in d]
+            oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+            data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
+            want.append(loc[0])
+        s = torch.cuda.current_stream()
+        for _ in range(2):   # twice: the second sequence reuses both LL parities
+            bufs = [x.clone() for x in data]
+            prev = None
+            for b in bufs:
+                peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
+                prev = b.data_ptr()
+            peer.allreduce_pipelined(None, prev, n, s)
+            torch.cuda.synchronize()
+            for i, (b, w) in enumerate(zip(bufs, want)):
+                bad = int((b.cpu().numpy().view(np.uint16) != w[None, :]).sum())
+                assert bad == 0, (i, bad)
+        assert peer.status() & t.PEER_TIMEOUT == 0
+        x = data[0].clone()
+        peer.allreduce_pipelined(x.data_ptr(), None, n, s)
+        with pytest.raises(_lib.AllredError):   # another call while a bucket is pending
+            peer.allreduce(x.data_ptr(), n, s, local, 8, t.SWING, x.data_ptr())
+        with pytest.raises(_lib.AllredError):   # a second start without finishing the first
+            peer.allreduce_pipelined(x.data_ptr(), None, n, s)
+        peer.allreduce_pipelined(None, x.data_ptr(), n, s)
+        with pytest.raises(_lib.AllredError):   # nothing pending
+            peer.allreduce_pipelined(None, x.data_ptr(), n, s)
+        torch.cuda.synchronize()
+    finally:
         peer.close()
 
 

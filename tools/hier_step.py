@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
 x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_oneshot,
-k_hier_ll and k_hier_pipe — the N > 1 bench's candidates with the cross-GPU
+k_hier_ll, k_hier_pipe and k_hier_x (buckets pipelined: K buckets in K + 1
+launches, the timed region includes the last bucket's finishing launch) — the N > 1 bench's candidates with the cross-GPU
 hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
 kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
 arms interleaved.   python tools/hier_step.py [steps] [rounds]"""
@@ -9,6 +10,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -24,9 +26,33 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
-res = {k: [] for k in arms}
+res = {k: [] for k in list(arms) + ["hier_x"]}
+host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
+SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+
+def pipelined(k):   # k buckets in k + 1 calls (k_hier_x): each call finishes the previous bucket
+    prev = None
+    for i in range(k):
+        cur = sets[i % NS].data_ptr()
+        peer.allreduce_pipelined(cur, prev, n, s)
+        prev = cur
+    peer.allreduce_pipelined(None, prev, n, s)
+
+
 for _ in range(rounds):
+    pipelined(20)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s):
+        torch.cuda._sleep(SPIN)
+    e0.record(s)
+    h0 = time.perf_counter()
+    pipelined(steps)
+    host["hier_x"].append(round((time.perf_counter() - h0) * 1e6 / steps, 2))
+    e1.record(s)
+    torch.cuda.synchronize()
+    res["hier_x"].append(round(e0.elapsed_time(e1) * 1e3 / steps, 3))
     for name, (limit, ll) in arms.items():
         peer.set_oneshot_max(limit)
         peer.set_hier_ll(ll)
@@ -34,10 +60,12 @@ for _ in range(rounds):
             peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
-            torch.cuda._sleep(200000)
+            torch.cuda._sleep(SPIN)
         e0.record(s)
+        h0 = time.perf_counter()
         for i in range(steps):
             peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
+        host[name].append(round((time.perf_counter() - h0) * 1e6 / steps, 2))
         e1.record(s)
         torch.cuda.synchronize()
         res[name].append(round(e0.elapsed_time(e1) * 1e3 / steps, 3))
@@ -45,4 +73,5 @@ status = peer.status()
 peer.close()
 print(json.dumps({"W": 1, "bytes_per_rank": n * 2, "ranks": P, "sets": NS, "steps": steps,
                   "us_per_step": res, "median": {k: statistics.median(v) for k, v in res.items()},
+                  "host_us_per_call": host, "spin_cycles": SPIN,
                   "peer_status": status}))
