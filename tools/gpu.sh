@@ -10,6 +10,7 @@
 #                        then FETCH_SIZE and WRITE_SIZE in separate --pmc passes
 #   ab <v> "<tiles>" <tune a> <tune b> ...   tools/ab_fused.py arms interleaved (ALLRED_TUNE per arm)
 #   skew ["<pads>"]      rank-row skew A/B of the config-2 fused pass
+#   pmc_lo               PMC traffic of the fused LO pass, rocprofv3 stats of the schedule forms
 #   share <n>            the N > 1 bench path rehearsed with n ranks on the one GPU
 #                        (bench.py --share-gpu: peer transports, no RCCL; numbers mean nothing)
 set -o pipefail
@@ -72,6 +73,21 @@ for r in rows:
 for k, v in by.items():
     print(k, sorted(v))
 EOF
+    ;;
+pmc_lo)
+    # HBM traffic (FETCH_SIZE / WRITE_SIZE, separate passes) of the fused Swing LO (k_lo_dag_reg)
+    # and rocprofv3 stats of the schedule forms (k_steps_pipe) at config 2 -> gpurun_out/pmc_lo
+    out=gpurun_out/pmc_lo
+    mkdir -p "$out"
+    export AB_EAGER=1 AB_SETS=32
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -d "$out/lo_fetch" -o run -- \
+        python3 tools/ab_fused.py lo 320 100 > /dev/null 2> "$out/e1" &&
+    timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -f csv -d "$out/lo_write" -o run -- \
+        python3 tools/ab_fused.py lo 320 100 > /dev/null 2> "$out/e2" &&
+    AB_EXEC=steps timeout -s KILL 120 rocprofv3 --kernel-trace --stats -f csv -d "$out/steps_trace" -o run -- \
+        python3 tools/ab_fused.py bo 5 200 > "$out/steps_bo.json" 2> "$out/e3" &&
+    AB_EXEC=steps timeout -s KILL 120 rocprofv3 --kernel-trace --stats -f csv -d "$out/steps_lo_trace" -o run -- \
+        python3 tools/ab_fused.py lo 320 200 > "$out/steps_lo.json" 2> "$out/e4"
     ;;
 skew)
     # skew "<pads in elements>": rank-row skew A/B of the config-2 fused pass (stride = n + pad)
