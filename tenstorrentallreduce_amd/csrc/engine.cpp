@@ -28,6 +28,7 @@
 #include <utility>
 #include <vector>
 
+#include "device_guard.hpp"
 #include "internal.hpp"
 
 using namespace tsa;
@@ -65,21 +66,6 @@ struct allred_plan {
 namespace {
 
 int popcount64(uint64_t x) { return __builtin_popcountll(x); }
-
-// switches the calling thread to `device` (>= 0) for the scope, then back
-struct DeviceGuard {
-    int prev = -1;
-    bool ok = true;
-    explicit DeviceGuard(int device) {
-        if (device < 0) return;
-        if (hipGetDevice(&prev) != hipSuccess) { ok = false; prev = -1; return; }
-        if (prev == device) { prev = -1; return; }
-        if (hipSetDevice(device) != hipSuccess) { ok = false; prev = -1; }
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
 
 void free_plan(allred_plan* p) {
     if (!p) return;

@@ -25,6 +25,7 @@
 
 #include <cstring>
 
+#include "device_guard.hpp"
 #include "internal.hpp"
 
 using namespace tsa;
@@ -147,6 +148,8 @@ int allred_peer_handle(allred_peer* p, uint8_t* out) {
 
 int allred_peer_connect(allred_peer* p, const uint8_t* all) {
     if (!p || !all || p->connected) return ALLRED_ERR_ARG;
+    DeviceGuard guard(p->device);   // the peers' windows are mapped for this peer's device
+    if (!guard.ok) return ALLRED_ERR_HIP;
     for (int q = 0; q < p->nranks; ++q) {
         if (q == p->rank) {
             p->peer_win[q][0] = p->win[0];
