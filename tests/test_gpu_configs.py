@@ -98,7 +98,7 @@ def test_config5_reference_inputs(n):
                                          (t.RECDUB, (2, 2), 1024), (t.SWING_1D, (1, 16), 16 * 8 * 33),
                                          (t.SWING, (1, 1), 64), (t.SWING, (4, 8), 8 * 256 * 3),
                                          (t.SWING, (8, 32), 32 * 256 * 3), (t.RECDUB, (4, 16), 16 * 256 * 5),
-                                         (t.SWING_1D, (1, 16), 16 * 256 * 2)])
+                                         (t.SWING_1D, (1, 16), 16 * 256 * 2), (t.SWING, (8, 64), 1 << 20)])
 def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form):
     """The schedule form as one pipelined launch (k_steps_pipe, steps_form 0:
     whole 512-byte units of 8..64 ranks staged into LDS two ahead, the step
