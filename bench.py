@@ -221,10 +221,10 @@ def bench_single(args) -> dict:
     torch.cuda.synchronize()
     hot_ms = e0.elapsed_time(e1) / args.steps
 
-    # host-staged end to end (buckets start and end in pinned host memory): the
-    # reference program surface, H2D of all 64 buckets + allreduce + D2H
-    # reference program surface, H2D of all 64 buckets + allreduce + D2H (one DMA each way) ...
-    # ("dma") and the fused kernel reading / writing the pinned host buckets in place ("zerocopy")
+    # host-staged end to end (buckets start and end in pinned host memory), the
+    # reference program surface: H2D of all 64 buckets + allreduce + D2H, one DMA
+    # each way ("dma"), or the fused kernel reading / writing the pinned host
+    # buckets in place ("zerocopy")
     argv = ["allred_BO_2D", "1", "1", str(SIDE), "13", str(TILES), "32", "0", "1"]
     e2e = {}
     for mode in ("zerocopy", "dma"):
