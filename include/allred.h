@@ -231,6 +231,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     its step, so an element the transport never delivered surfaces as NaN in the
  *                     result instead of stale data.  Same result bits on a correct run.  (The
  *                     reference has no invariant or race checking)
+ *   fused_chunk_tiles 1280: the persistent fused 64-rank passes run a bucket of T 256-element
+ *                     tiles as max(1, round(T / 1280)) launches over consecutive tile ranges
+ *                     (0 = one launch); allred_plan_launches counts them
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

@@ -561,7 +561,9 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
     }
     // workspace and launch count per execute
     if (desc->exec == ALLRED_EXEC_FUSED) {
-        p->launches = 1;
+        // 64 ranks from 1024 whole tiles: the persistent passes, in launches of
+        // about fused_chunk_tiles tiles (the value when the plan is made)
+        p->launches = total == 64 && n % 256 == 0 && n / 256 >= 1024 ? (int)fused_chunk_launches(n / 256) : 1;
     } else if (p->steps_persistent) {
         p->launches = steps ? 1 : 0;
     } else if (desc->variant == ALLRED_BO) {

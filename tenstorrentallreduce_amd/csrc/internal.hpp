@@ -39,7 +39,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 // Kernel-form switches between bit-identical forms; defaults = the product forms.
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
-    lo_dag_reg_min_tiles, check,
+    lo_dag_reg_min_tiles, check, fused_chunk_tiles,
     count
 };
 int64_t tune(Tune key);
@@ -52,6 +52,8 @@ constexpr int kMaxAddSegs = 64;
 int launch_bf16_add_segs(uint16_t* dst, const uint16_t* src, const uint64_t* off, const uint64_t* len, int nsegs,
                          void* stream);
 // host_memory: the ranks live in pinned host memory (zero-copy) -> pipelined form
+// launches of one persistent fused pass over `tiles` 256-element tiles (fused_chunk_tiles)
+uint64_t fused_chunk_launches(uint64_t tiles);
 int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
                       bool host_memory = false);
 // dag: the interned LO DAG of a 64-rank schedule (engine.cpp lo_dag), or null

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 template <int P>
 __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ order, uint64_t block_vec,
-                                                         uint64_t ntiles) {
+                                                         uint64_t t0, uint64_t ntiles) {
     constexpr int NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     static_assert(OPS >= 1 && 3 * OPS <= 63, "vmcnt is 6 bits");
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
     };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto tile_of = [&](int j) { return t0 + blockIdx.x + (uint64_t)j * G; };   // tiles t0 .. t0 + ntiles - 1
     if (mine > 0) issue(tile_of(0), 0);
     if (mine > 1) issue(tile_of(1), 1);
     for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += 64 * NW)
@@ -586,7 +586,7 @@ __device__ __forceinline__ void lo_dag_eval(float* v, std::integer_sequence<int,
 
 template <class D>
 __global__ __launch_bounds__(kBlock) void k_lo_dag_reg(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                       uint64_t ntiles) {
+                                                       uint64_t t0, uint64_t ntiles) {
     constexpr int P = D::P, F = D::F, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI;
     static_assert(OPS >= 1 && 3 * OPS <= 63, "vmcnt is 6 bits");
     static_assert(NW * 64 == 256 && TV * 8 == 256, "one element of the 256-element tile per thread");
@@ -611,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void k_lo_dag_reg(uint16_t* __restrict__ ra
     }
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto tile_of = [&](int j) { return t0 + blockIdx.x + (uint64_t)j * G; };
     auto issue = [&](uint64_t t, int b) {
 #pragma unroll
         for (int k = 0; k < OPS; ++k)
@@ -719,7 +719,7 @@ __global__ __launch_bounds__(128) void k_mem_lds(uint16_t* __restrict__ ranks, u
 // ---------------------------------------------------------------------------
 template <bool ACC16 = false>
 __global__ __launch_bounds__(kBlock) void k_mem_lds_lag(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                        uint64_t block_vec, uint64_t ntiles) {
+                                                        uint64_t block_vec, uint64_t t0, uint64_t ntiles) {
     constexpr int P = 64, TV = 32, RPW = 16, OPS = 8;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 resb[2][TV];
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_mem_lds_lag(uint16_t* __restrict__ r
     };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto tile_of = [&](int j) { return t0 + blockIdx.x + (uint64_t)j * G; };
     if (mine > 0) issue(tile_of(0), 0);
     if (mine > 1) issue(tile_of(1), 1);
     uint4 prev = make_uint4(0, 0, 0, 0);
@@ -1378,6 +1378,25 @@ int launch_bf16_add_segs(uint16_t* dst, const uint16_t* src, const uint64_t* off
     return last_error();
 }
 
+uint64_t fused_chunk_launches(uint64_t tiles) {
+    const uint64_t chunk = (uint64_t)tune(Tune::fused_chunk_tiles);
+    const uint64_t nl = chunk ? (tiles + chunk / 2) / chunk : 1;
+    return nl < 1 ? 1 : nl;
+}
+
+// The persistent lagged passes (k_tree_lds_lag, k_lo_dag_reg, k_mem_lds_lag)
+// on large buckets: a sequence of launches over tile ranges a .. b-1 of about
+// fused_chunk_tiles tiles each (1280 = config 2's 2.5 tiles per workgroup).
+// Each launch opens with two tiles' loads on every workgroup — most of its
+// reads in one burst before its first store — while one launch over many
+// tiles per workgroup interleaves reads and writes throughout: 5.6-5.7 vs
+// 5.0-5.5 TB/s at 1.3-5.2 MB per rank (profiles/r02_fused_chunk_ab.txt).
+template <class F>
+void for_each_chunk(uint64_t tiles, F&& launch) {
+    const uint64_t nl = fused_chunk_launches(tiles);
+    for (uint64_t l = 0; l < nl; ++l) launch(tiles * l / nl, tiles * (l + 1) / nl);
+}
+
 int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
                       bool host_memory) {
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
@@ -1389,8 +1408,10 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
     // per CU (14.2-14.3 us vs 15.3 for k_tree_lds_pipe and 16.2 for one tile
     // per workgroup)
     if (whole_tiles && !host_memory && total == 64 && form == 0 && tiles >= 1024) {
-        hipLaunchKernelGGL((k_tree_lds_lag<64>), dim3(persistent_grid(tiles, 512)), dim3(kBlock), 0, st, ranks, stride,
-                           order, bv, tiles);
+        for_each_chunk(tiles, [&](uint64_t a, uint64_t b) {
+            hipLaunchKernelGGL((k_tree_lds_lag<64>), dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, ranks,
+                               stride, order, bv, a, b - a);
+        });
         return last_error();
     }
     // pinned host buckets (zero-copy: PCIe-bound, 32 workgroups keep both link
@@ -1412,11 +1433,13 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
 int launch_lo_dag_reg(uint16_t* ranks, uint64_t stride, size_t n, int algo, int side, int total, void* stream) {
     if (n % 256 || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_UNSUPPORTED;
     const uint64_t tiles = n / 256;
-    const dim3 grid(persistent_grid(tiles, 512));
     hipStream_t st = (hipStream_t)stream;
 #define TSA_X(D, A, S, T)                                                                             \
     if (algo == (A) && total == (T) && ((A) == ALLRED_SWING_1D || side == (S))) {                      \
-        hipLaunchKernelGGL(k_lo_dag_reg<D>, grid, dim3(kBlock), 0, st, ranks, stride, tiles);          \
+        for_each_chunk(tiles, [&](uint64_t a, uint64_t b) {                                           \
+            hipLaunchKernelGGL(k_lo_dag_reg<D>, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, \
+                               ranks, stride, a, b - a);                                              \
+        });                                                                                           \
         return last_error();                                                                          \
     }
     TSA_LO_DAGS(TSA_X)
@@ -1619,8 +1642,10 @@ int mem_fused_impl(uint16_t* ranks, uint64_t stride, uint64_t nv, int total, hip
     const uint64_t bv = nv / total, tiles = nv / 32;
     if (bv % 32 == 0 && total == 64 && tiles >= 1024 && fused_form() == 0) {
         // persistent, stores one iteration late (k_tree_lds_lag's schedule)
-        hipLaunchKernelGGL((k_mem_lds_lag<ACC16>), dim3(persistent_grid(tiles, 512)), dim3(kBlock), 0, st, ranks,
-                           stride, bv, tiles);
+        for_each_chunk(tiles, [&](uint64_t a, uint64_t b) {
+            hipLaunchKernelGGL((k_mem_lds_lag<ACC16>), dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, ranks,
+                               stride, bv, a, b - a);
+        });
         return last_error();
     }
     if (bv % 32 == 0 && total >= 4 && fused_form() != 1) {

@@ -33,6 +33,7 @@ const Key kKeys[] = {
     {"lo_dag_reg", 1, 0, 1},          // non-rank-uniform Swing fused LO: build-time DAG in registers
     {"lo_dag_reg_min_tiles", 64, 1, 1ll << 40},   // 256-element tiles per rank (64: 32 kB)
     {"check", 0, 0, 1},               // N > 1 programs: verify against the partners', poison receive regions
+    {"fused_chunk_tiles", 1280, 0, 1ll << 40},   // persistent fused passes: tiles per launch (0: one launch)
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

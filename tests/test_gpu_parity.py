@@ -168,6 +168,32 @@ def test_fused_persistent_forms_bit_exact_config2_size(algo, variant):
     assert (got == np.stack(want)).all()
 
 
+@pytest.mark.parametrize("variant", ["bo", "lo", "mem"])
+def test_fused_chunked_launches_bit_exact(variant):
+    """Large buckets run the persistent fused passes as consecutive tile-range
+    launches (fused_chunk_tiles, default 1280): 3,904 tiles = three launches
+    of 1,301 / 1,301 / 1,302 tiles (ragged), 1.9 MB per rank — against one
+    launch over every tile and against the oracle, bit-exact; config 2 stays
+    one launch."""
+    side, total, n = 8, 64, 3904 * 256
+    v = {"bo": t.BO, "lo": t.LO, "mem": t.MEM}[variant]
+    ranks = rand_ranks(total, n, seed=41 + v)
+    stride = t.preferred_rank_stride(n)
+    plan = t.Plan(t.SWING, v, side, n, total, t.EXEC_FUSED)
+    assert plan.launches == 3
+    plan.close()
+    plan = t.Plan(t.SWING, v, side, 327680, total, t.EXEC_FUSED)
+    assert plan.launches == 1
+    plan.close()
+    got = run_plan(t.SWING, v, side, total, ranks, t.EXEC_FUSED, stride=stride)
+    with t.tuned(fused_chunk_tiles=0):
+        one = run_plan(t.SWING, v, side, total, ranks, t.EXEC_FUSED, stride=stride)
+    assert (got == one).all()
+    want = [r.copy() for r in ranks]
+    oracle.allreduce(variant, t.SWING, side, want, total)
+    assert (got == np.stack(want)).all()
+
+
 @pytest.mark.parametrize("exec_mode", [t.EXEC_STEPS, t.EXEC_FUSED])
 def test_plan_padded_stride(exec_mode):
     side, total, n = 8, 64, 64 * 8 * 3
