@@ -5,7 +5,7 @@ k_hier_ll, k_hier_pipe and k_hier_x (buckets pipelined: K buckets in K + 1
 launches, the timed region includes the last bucket's finishing launch) — the N > 1 bench's candidates with the cross-GPU
 hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
 kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
-arms interleaved.   python tools/hier_step.py [steps] [rounds]"""
+arms interleaved.   python tools/hier_step.py [steps] [rounds]   (HIER_CAP: grid cap)"""
 import json
 import os
 import statistics
@@ -24,6 +24,7 @@ sets = [torch.randint(0x3F80, 0x42C8, (P, n), dtype=torch.int16, device="cuda") 
 ws = torch.empty(n, dtype=torch.int16, device="cuda")
 peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
+peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
 res = {k: [] for k in list(arms) + ["hier_x"]}
