@@ -268,7 +268,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         if (st != ALLRED_OK) return st;
     }
     const uint64_t ll_area = 2 * p->ll_box_words;   // LL words of one parity
-    if (p->mem_ll_max && n * 2 <= p->mem_ll_max && p->nranks <= 8 && p->flags_uncached && (n / 8) * 8 <= ll_area) {
+    if (p->mem_ll_max && n * 2 <= p->mem_ll_max && p->nranks <= 8 && p->flags_uncached && (n / 8 + 31) / 32 * 32 * 8 <= ll_area) {
         // small buckets: LL pushes, two one-way trips (k_peer_mem_ll); same bits
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * ll_area;
@@ -316,7 +316,7 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
     }
     const uint64_t ll_area = 2 * p->ll_box_words;   // LL words of one parity
     if (prog.S > 0 && prog.lo && prog.C == 1 && p->lo_ll_max && n * 2 <= p->lo_ll_max && p->nranks <= 8 &&
-        p->flags_uncached && (n / 8) * 4 * (uint64_t)prog.S <= ll_area) {
+        p->flags_uncached && (n / 8 + 31) / 32 * 32 * 4 * (uint64_t)prog.S <= ll_area) {
         // small LO buckets: LL pushes, one one-way trip per step (k_peer_lo_ll); same bits
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * ll_area;

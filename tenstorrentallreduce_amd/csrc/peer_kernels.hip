@@ -470,22 +470,34 @@ struct LLPtrs {
     uint64_t* ll[kLLMaxGpus];   // GPU q's LL area, this parity: [inbox: tiles x 128 words][result box: same]
 };
 
+// LL slot layout: 32 consecutive slots (16 data bytes each) form a group of 128
+// words, word k of slot i of the group at k * 32 + i.  Lanes serving consecutive
+// slots therefore write (and poll) 256 contiguous bytes per instruction — whole
+// 128-byte lines over xGMI — instead of one 8-byte word every 32 bytes.
+constexpr int kLLGroup = 32;
+__device__ __forceinline__ uint64_t* ll_slot(uint64_t* base, uint64_t s) {
+    return base + (s / kLLGroup) * (4 * kLLGroup) + s % kLLGroup;
+}
+__device__ __forceinline__ const uint64_t* ll_slot(const uint64_t* base, uint64_t s) {
+    return base + (s / kLLGroup) * (4 * kLLGroup) + s % kLLGroup;
+}
+
 __device__ __forceinline__ void ll_put(uint64_t* dst, uint4 v, uint32_t e) {
     const uint64_t hi = (uint64_t)e << 32;
-    __hip_atomic_store(dst + 0, hi | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(dst + 1, hi | v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(dst + 2, hi | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(dst + 3, hi | v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 0 * kLLGroup, hi | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 1 * kLLGroup, hi | v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 2 * kLLGroup, hi | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(dst + 3 * kLLGroup, hi | v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // poll 4 LL words until all carry epoch e (bounded: status bit 0 on timeout)
 __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_t* status) {
     uint64_t w0, w1, w2, w3;
     for (uint64_t spin = 0;; ++spin) {
-        w0 = __hip_atomic_load(src + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        w1 = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        w2 = __hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        w3 = __hip_atomic_load(src + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w0 = __hip_atomic_load(src + 0 * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w1 = __hip_atomic_load(src + 1 * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w2 = __hip_atomic_load(src + 2 * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        w3 = __hip_atomic_load(src + 3 * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if ((uint32_t)(w0 >> 32) == e && (uint32_t)(w1 >> 32) == e && (uint32_t)(w2 >> 32) == e &&
             (uint32_t)(w3 >> 32) == e)
             break;
@@ -546,7 +558,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         if (w == 0 && h == 0) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-            ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, res, epoch);
+            ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, res, epoch);
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
@@ -557,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         if (owner_of(t) != me) continue;
         const uint64_t li = t - (uint64_t)me * tiles_per_owner;
         const int q = threadIdx.x >> 5;   // source GPU of this lane's slot
-        if (q < W) xs[q * 32 + c] = ll_get(my_ll + (li * W + q) * 128 + c * 4, epoch, status);
+        if (q < W) xs[q * 32 + c] = ll_get(my_ll + (li * W + q) * 128 + c, epoch, status);
         __syncthreads();
         if (threadIdx.x < 32) {
             const uint4 s0 = xs[me * 32 + c];
@@ -578,7 +590,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             xs[8 * 32 + c] = o;
         }
         __syncthreads();
-        if (q < W) ll_put(lp.ll[q] + box_words + t * 128 + c * 4, xs[8 * 32 + c], epoch);
+        if (q < W) ll_put(lp.ll[q] + box_words + t * 128 + c, xs[8 * 32 + c], epoch);
         __syncthreads();   // xs is reused by the next owned tile
     }
     // ---- B: my result box -> the 64 rank rows, 4 tiles at a time
@@ -586,7 +598,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     for (int j0 = 0; j0 < mine; j0 += BB) {
         const int nb = mine - j0 < BB ? mine - j0 : BB;
         const int b = threadIdx.x >> 5;
-        if (b < nb) xs[16 * 32 + b * 32 + c] = ll_get(my_ll + box_words + tile_of(j0 + b) * 128 + c * 4, epoch, status);
+        if (b < nb) xs[16 * 32 + b * 32 + c] = ll_get(my_ll + box_words + tile_of(j0 + b) * 128 + c, epoch, status);
         __syncthreads();
         uint4 res[BB];
 #pragma unroll
@@ -632,7 +644,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
 // work to arrive in.
 __device__ __forceinline__ void ll_load(const uint64_t* src, uint64_t (&wd)[4]) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ bool ll_fresh(const uint64_t (&wd)[4], uint32_t e) {
     return (uint32_t)(wd[0] >> 32) == e && (uint32_t)(wd[1] >> 32) == e && (uint32_t)(wd[2] >> 32) == e &&
@@ -685,9 +697,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
                 const uint64_t lr = tile_of(j - 1) - (uint64_t)me * tiles_per_owner;
 #pragma unroll
                 for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) ll_load(my_ll + (lr * W + src) * 128 + c * 4, wr[src]);
+                    if (src < W) ll_load(my_ll + (lr * W + src) * 128 + c, wr[src]);
             }
-            if (do_b) ll_load(my_ll + box_words + tile_of(j - 2) * 128 + c * 4, wb);
+            if (do_b) ll_load(my_ll + box_words + tile_of(j - 2) * 128 + c, wb);
         }
         if (j < mine) {   // ---- A(j): every wave reduces
             lds_barrier();   // tile j is in LDS
@@ -707,7 +719,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4 pr = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-                ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, pr, epoch);
+                ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, epoch);
             }
         }
         if (!mp) continue;
@@ -717,7 +729,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src) {
                 if (src >= W) continue;
-                const uint64_t* at = my_ll + (lr * W + src) * 128 + c * 4;
+                const uint64_t* at = my_ll + (lr * W + src) * 128 + c;
                 y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(at, epoch, status);
             }
             uint4 s0 = y[0];
@@ -740,10 +752,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
             o.w = pack_rne(a[6], a[7]);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c * 4, o, epoch);
+                if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c, o, epoch);
         }
         uint4 res = make_uint4(0, 0, 0, 0);
-        if (do_b) res = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + tile_of(j - 2) * 128 + c * 4, epoch, status);
+        if (do_b) res = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + tile_of(j - 2) * 128 + c, epoch, status);
         // tile j+2's loads and tile j-2's stores, interleaved op by op (both of this parity)
         const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 2);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
@@ -815,7 +827,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     // launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep HBM busy.
     const int jr = threadIdx.x / TV;
     if (prev && jr < kHierXMaxTiles && jr < mine) {
-        const uint64_t* at = lpv.ll[me] + box_words + tile_of(jr) * 128 + c * 4;
+        const uint64_t* at = lpv.ll[me] + box_words + tile_of(jr) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
         res[jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
@@ -843,7 +855,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
-                ll_put(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c * 4, pr, ecur);
+                ll_put(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur);
             }
         }
         // ---- cur's tile j+2 in, prev's tile j out, interleaved op by op
@@ -868,13 +880,13 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c * 4, wr[src]);
+                if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
             uint4 y[kLLMaxGpus];
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src)
                 if (src < W)
                     y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
-                                                     : ll_get(lc.ll[me] + (lr * W + src) * 128 + c * 4, ecur, status);
+                                                     : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
             uint4 s0 = y[0];
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src)
@@ -895,7 +907,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             o.w = pack_rne(a[6], a[7]);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c * 4, o, ecur);
+                if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
         }
     }
 }
@@ -909,15 +921,18 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // bits of k_peer_oneshot), and pushes the result into every GPU's box; B:
 // every GPU polls its box and writes its bucket.  Two one-way trips, no flag,
 // no remote read.  A never waits and the grid is resident (<= 128 groups), so
-// every wait of R and B is reached.  LL layout of the call's parity:
-// [inbox: owned vectors][W][4 words], then [box: vectors][4 words].
+// every wait of R and B is reached.  LL slots of the call's parity (ll_slot
+// groups): [inbox: slot q * bv + u = vector u of my block from GPU q], then,
+// from the next whole group, [box: slot v = vector v of the bucket].
 // ---------------------------------------------------------------------------
+__host__ __device__ constexpr uint64_t ll_padded(uint64_t slots) { return (slots + 31) / 32 * 32; }
+
 __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me, uint16_t* __restrict__ bucket,
                                                         uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status) {
     const uint64_t gt = gtid(), GT = gthreads();
     uint4* bk = reinterpret_cast<uint4*>(bucket);
     uint64_t* const my_ll = lp.ll[me];
-    const uint64_t box = nv * 4;
+    const uint64_t box = ll_padded(nv) * 4;   // words
     for (uint64_t v = gt; v < nv; v += GT) {   // A
         const int o = (int)(v / bv);
         // the owner's area by an unrolled select over the (scalar) kernarg pointers: a
@@ -926,19 +941,20 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
 #pragma unroll
         for (int q = 1; q < kLLMaxGpus; ++q)
             if (o == q) dst = lp.ll[q];
-        ll_put(dst + ((v - (uint64_t)o * bv) * W + me) * 4, ld_nt(bk + v), epoch);
+        ll_put(ll_slot(dst, (uint64_t)me * bv + (v - (uint64_t)o * bv)), ld_nt(bk + v), epoch);
     }
     for (uint64_t u = gt; u < bv; u += GT) {   // R: my block
-        const uint64_t* slots = my_ll + u * W * 4;
         uint4 y[kLLMaxGpus];
         for (uint64_t spin = 0;; ++spin) {
             uint64_t wv[kLLMaxGpus][4];
 #pragma unroll
-            for (int q = 0; q < kLLMaxGpus; ++q)
+            for (int q = 0; q < kLLMaxGpus; ++q) {
+                const uint64_t* slot = ll_slot(my_ll, (uint64_t)(q < W ? q : 0) * bv + u);
 #pragma unroll
                 for (int e = 0; e < 4; ++e)
-                    wv[q][e] = q < W ? __hip_atomic_load(slots + q * 4 + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                    wv[q][e] = q < W ? __hip_atomic_load(slot + e * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                                      : (uint64_t)epoch << 32;
+            }
             uint32_t bad = 0;
 #pragma unroll
             for (int q = 0; q < kLLMaxGpus; ++q) {
@@ -967,9 +983,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
         }
         const uint4 r = make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
         const uint64_t v = (uint64_t)me * bv + u;
-        for (int q = 0; q < W; ++q) ll_put(lp.ll[q] + box + v * 4, r, epoch);
+        for (int q = 0; q < W; ++q) ll_put(ll_slot(lp.ll[q] + box, v), r, epoch);
     }
-    for (uint64_t v = gt; v < nv; v += GT) st_nt(bk + v, ll_get(my_ll + box + v * 4, epoch, status));   // B
+    for (uint64_t v = gt; v < nv; v += GT) st_nt(bk + v, ll_get(ll_slot(my_ll + box, v), epoch, status));   // B
 }
 
 // ---------------------------------------------------------------------------
@@ -979,10 +995,11 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
 // partner p_k's step-k slot, then polls its OWN step-k slot until the four
 // words of p_k carry the epoch, and adds (one bf16 rounding, the same add as
 // every LO form).  Per step one one-way xGMI trip instead of k_peer_sched's
-// progress flag + remote read round trip; no window, no flag area.  Slots
-// [step][vector][4 words] in the LL area of the call's parity; call k+2 may
-// reuse a parity because finishing call k+1 needs every rank to have started
-// it (the partners of all steps reach every rank of the schedule).
+// progress flag + remote read round trip; no window, no flag area.  Slot of
+// step k, vector v: k * ll_padded(nv) + v (ll_slot groups) in the LL area of
+// the call's parity; call k+2 may reuse a parity because finishing call k+1
+// needs every rank to have started it (the partners of all steps reach every
+// rank of the schedule).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
                                                        uint64_t nv, uint32_t epoch, uint32_t* status) {
@@ -991,10 +1008,11 @@ __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, i
     uint4* bk = reinterpret_cast<uint4*>(bucket);
     uint4 cur = ld_nt(bk + v);
     const uint64_t* mine = lp.ll[me];
+    const uint64_t per_step = ll_padded(nv);   // slots
     for (int k = 0; k < pr.S; ++k) {
         const int p = pr.peer[0][k];
-        ll_put(lp.ll[p] + ((uint64_t)k * nv + v) * 4, cur, epoch);
-        cur = add8(cur, ll_get(mine + ((uint64_t)k * nv + v) * 4, epoch, status));
+        ll_put(ll_slot(lp.ll[p], (uint64_t)k * per_step + v), cur, epoch);
+        cur = add8(cur, ll_get(ll_slot(mine, (uint64_t)k * per_step + v), epoch, status));
     }
     st_nt(bk + v, cur);
 }
@@ -1062,7 +1080,7 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
 int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
                        uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream) {
     const uint64_t nv = n / 8;
-    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > kLLMaxGpus || 8 * nv > area_words)
+    if (n % (8 * (size_t)nranks) || !aligned16(bucket) || nranks > kLLMaxGpus || 8 * ll_padded(nv) > area_words)
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
@@ -1078,7 +1096,7 @@ int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket,
                       uint64_t area_words, uint32_t epoch, uint32_t* status, void* stream) {
     const uint64_t nv = n / 8;
     if (n % 8 || !aligned16(bucket) || nranks > kLLMaxGpus || !prog.lo || prog.C != 1 ||
-        nv * 4 * (uint64_t)prog.S > area_words)
+        ll_padded(nv) * 4 * (uint64_t)prog.S > area_words)
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
