@@ -574,6 +574,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   peer_hier_pipe  the same LL hand-offs on the lagged-store pipeline (k_hier_pipe)
     #   peer_hier_x   the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
     #                 reads bucket i+1 while it writes bucket i; the last flush is timed)
+    #   peer_hier_x2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
+    #                 owned tiles, writes bucket i-2; every poll waits for the previous launch)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -585,18 +587,30 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
 
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
+    pend2 = [False]   # peer_hier_x2: buckets started and not yet finished (flush() finishes them)
 
     def flush():
         if pend[0] is not None:
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
+        if pend2[0]:
+            peer.allreduce_pipelined2(None, ELEMS, stream)
+            pend2[0] = False
 
     def run(kind, b, fresh=False):
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
         if kind == "peer_hier_x":   # buckets pipelined: this call finishes the previous one
+            if pend2[0]:
+                flush()
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
             pend[0] = b.data_ptr()
+            return
+        if kind == "peer_hier_x2":   # two deep: this call writes the bucket started two calls ago
+            if pend[0] is not None:
+                flush()
+            peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
+            pend2[0] = True
             return
         flush()
         if kind == "rccl":
@@ -622,7 +636,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         ref = small.clone()
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
-        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe", "peer_hier_x"):
+        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe", "peer_hier_x", "peer_hier_x2"):
             note(rank, f"verify: {kind}")
             try:   # the same calls on every rank: a raised status is raised everywhere
                 x = small.clone()
@@ -682,7 +696,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     e0.record(stream)
     for i in range(args.steps):
         step(i)
-    flush()   # peer_hier_x: the last bucket's finishing launch is part of the K steps' time
+    flush()   # peer_hier_x / _x2: the finishing launch is part of the K steps' time
     e1.record(stream)
     torch.cuda.synchronize()
     dist.barrier()
@@ -793,7 +807,7 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
     one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
-                  "peer_hier_x": "k_hier_x"}
+                  "peer_hier_x": "k_hier_x", "peer_hier_x2": "k_hier_x2"}
     if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
         roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
@@ -811,6 +825,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
            "peer_hier_x": "ONE kernel per bucket, consecutive buckets pipelined (K buckets in K + 1 launches, all "
                           "inside the timed region): on-GPU tree reduce of bucket i+1 while bucket i's rows are written, "
                           "mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
+           "peer_hier_x2": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
+                           "timed region): launch i reads bucket i, sums bucket i-1's owned tiles and writes bucket "
+                           "i-2's rows, mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     return {

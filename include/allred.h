@@ -379,6 +379,19 @@ int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int 
  * No reference counterpart (the reference runs one vector per program). */
 int allred_peer_allreduce_pipelined(allred_peer* peer, uint16_t* cur, uint16_t* prev, uint64_t elems,
                                     int local_ranks, int local_side, int local_algo, void* stream);
+/* The same step TWO buckets deep (k_hier_x2): the call with cur starts it
+ * (tree, partials pushed to the owners), sums the owned tiles of the bucket
+ * the previous call started and writes the rank rows of the bucket started
+ * two calls earlier; cur == NULL (flush) finishes every pending bucket in one
+ * launch.  K buckets = K + 1 calls: b0, b1, ..., b_{K-1}, NULL.  A bucket's
+ * rows are final, in stream order, after the call that started the bucket
+ * two calls later (or the flush); keep it alive until then.  Every poll of a
+ * launch waits for pushes of the previous launch on the other GPUs, so a GPU
+ * up to one launch late stalls nobody.  Same bits, arguments and limits as
+ * allred_peer_allreduce_pipelined; the two sequences do not mix.
+ * No reference counterpart. */
+int allred_peer_allreduce_pipelined2(allred_peer* peer, uint16_t* cur, uint64_t elems, int local_ranks,
+                                     int local_side, int local_algo, void* stream);
 /* Buckets of at most `bytes` (default 4 MiB) run as one kernel (per-workgroup
  * flags, no kernel boundaries); larger ones as copy / barrier / reduce-scatter /
  * barrier / all-gather launches.  Same result bits either way.  Every rank

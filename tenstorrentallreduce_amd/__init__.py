@@ -361,6 +361,15 @@ class Peer:
         check(lib.allred_peer_allreduce_pipelined(self._h, cur_ptr or None, prev_ptr or None, elems, local_ranks,
                                                   local_side, local_algo, _stream_ptr(stream)), "peer_allreduce_pipelined")
 
+    def allreduce_pipelined2(self, cur_ptr: int | None, elems: int, stream=None, local_ranks: int = 64,
+                             local_side: int = 8, local_algo: int = SWING) -> None:
+        """The same step two buckets deep (k_hier_x2): starts cur, sums the owned
+        tiles of the previous call's bucket, writes the rows of the bucket started
+        two calls earlier; cur None finishes everything pending.  K buckets = K + 1
+        calls: b0, b1, ..., b_{K-1}, None."""
+        check(lib.allred_peer_allreduce_pipelined2(self._h, cur_ptr or None, elems, local_ranks, local_side,
+                                                   local_algo, _stream_ptr(stream)), "peer_allreduce_pipelined2")
+
     def dist_allreduce(self, desc: DistDesc, buf_ptr: int, workspace_ptr: int | None = None, stream=None,
                        check_status: bool = False) -> None:
         """dist_allreduce's program (same desc, same bits) over the peer windows."""

@@ -157,6 +157,7 @@ SIGNATURES = [
     ("allred_peer_connect", C.c_int, [_P, _P]),
     ("allred_peer_allreduce", C.c_int, [_P, _u16p, C.c_uint64, C.c_int, C.c_int, C.c_int, _P, _P]),
     ("allred_peer_allreduce_pipelined", C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, _P]),
+    ("allred_peer_allreduce_pipelined2", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_peer_set_oneshot_max", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_set_hier_ll", C.c_int, [_P, C.c_int]),
     ("allred_peer_set_max_groups", C.c_int, [_P, C.c_uint32]),

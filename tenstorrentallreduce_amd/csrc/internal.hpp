@@ -143,7 +143,15 @@ int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uin
 int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
                   uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
                   uint32_t* status, unsigned max_grid, void* stream);
-// allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * n / 8
+// the same step two buckets deep (k_hier_x2): starts `cur`, sums the owned tiles of the bucket
+// the previous launch started (llm non-null: its parity's LL areas), writes `old` (started two
+// launches ago; llo: its parity); the flush launch (cur null) also writes that middle bucket
+// `fin` from its results
+int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
+                   uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
+                   uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
+                   unsigned max_grid, void* stream);
+// allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * (n / 8 rounded up to 32)
 int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
                        uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream);
 // the one-channel LO program with LL pushes (k_peer_lo_ll): ll[q] = GPU q's LL area of this

@@ -63,6 +63,12 @@ struct allred_peer {
     // allred_peer_allreduce_pipelined: a bucket started (its partials pushed) and not yet finished
     bool pipe_pending = false;
     uint32_t pipe_k = 0;            // that bucket's call number (epoch pipe_k + 1, LL parity pipe_k & 1)
+    // allred_peer_allreduce_pipelined2: up to two started, unfinished buckets, older
+    // first; with two, the older one's owned tiles are summed already
+    int x2_n = 0;
+    uint16_t* x2_buf[2] = {};
+    uint32_t x2_k[2] = {};          // their call numbers
+    uint64_t x2_elems = 0;          // the sequence's bucket size
 };
 
 extern "C" {
@@ -190,7 +196,7 @@ void parity_windows(allred_peer* p, uint16_t** wins) {
 
 int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* prev, uint64_t elems, int local_ranks,
                                     int local_side, int local_algo, void* stream) {
-    if (!p || !p->connected || (!cur && !prev)) return ALLRED_ERR_ARG;
+    if (!p || !p->connected || (!cur && !prev) || p->x2_n) return ALLRED_ERR_ARG;
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * 128 > p->ll_box_words)
@@ -221,10 +227,58 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
     return ALLRED_OK;
 }
 
+int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t elems, int local_ranks, int local_side,
+                                     int local_algo, void* stream) {
+    if (!p || !p->connected || p->pipe_pending) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)elems;
+    if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
+    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * 128 > p->ll_box_words)
+        return ALLRED_ERR_UNSUPPORTED;
+    if ((p->x2_n > 0 && n != p->x2_elems) || (!cur && p->x2_n == 0)) return ALLRED_ERR_ARG;
+    const uint8_t* order = nullptr;
+    int st = local_tree_order(local_algo, local_side, local_ranks, &order);
+    if (st != ALLRED_OK) return st;
+    auto area = [&](uint32_t k, uint64_t** ll) {   // every GPU's LL area of call k's parity
+        for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (k & 1u) * 2 * p->ll_box_words;
+    };
+    // mid: the newest pending bucket (its owned tiles are summed by this launch);
+    // old: the older one when two are pending (its rows are written by this launch)
+    const bool has_old = p->x2_n == 2;
+    const uint32_t kc = p->calls, km = p->x2_k[p->x2_n - 1 < 0 ? 0 : p->x2_n - 1], ko = p->x2_k[0];
+    uint64_t* llc[ALLRED_MAX_NODES];
+    uint64_t* llm[ALLRED_MAX_NODES];
+    uint64_t* llo[ALLRED_MAX_NODES];
+    area(kc, llc);
+    area(km, llm);
+    area(ko, llo);
+    uint16_t* old = has_old ? p->x2_buf[0] : nullptr;
+    uint16_t* fin = !cur ? p->x2_buf[p->x2_n - 1] : nullptr;
+    st = launch_hier_x2(cur, old, fin, n, order, cur ? llc : nullptr, p->x2_n > 0 ? llm : nullptr,
+                        has_old ? llo : nullptr, p->nranks, p->rank, n, p->ll_box_words, kc + 1u, km + 1u, ko + 1u,
+                        p->status, p->max_groups, stream);
+    if (st != ALLRED_OK) return st;
+    if (!cur) {   // flushed: nothing pending
+        p->x2_n = 0;
+    } else {
+        if (has_old) {   // old done: mid becomes the older pending bucket
+            p->x2_buf[0] = p->x2_buf[1];
+            p->x2_k[0] = p->x2_k[1];
+            p->x2_n = 1;
+        }
+        p->x2_buf[p->x2_n] = cur;
+        p->x2_k[p->x2_n] = kc;
+        ++p->x2_n;
+        p->x2_elems = n;
+        ++p->calls;
+    }
+    p->last_all_peer = true;
+    return ALLRED_OK;
+}
+
 int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream) {
     if (!p || !buf || !p->connected) return ALLRED_ERR_ARG;
-    if (p->pipe_pending) return ALLRED_ERR_ARG;   // finish the pipelined sequence first
+    if (p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;   // finish the pipelined sequence first
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     uint16_t* bucket = buf;
@@ -297,7 +351,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
 int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16_t* buf, void* workspace,
                                void* stream) {
     if (!p || !d || !buf || !p->connected) return ALLRED_ERR_ARG;
-    if (d->total_nodes != p->nranks || p->pipe_pending) return ALLRED_ERR_ARG;
+    if (d->total_nodes != p->nranks || p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;
     const size_t n = (size_t)d->elems;
     if (d->variant == ALLRED_MEM) {
         uint16_t* ws = workspace ? static_cast<uint16_t*>(workspace) + n : nullptr;  // dist workspace layout

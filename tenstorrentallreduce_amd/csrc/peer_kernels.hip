@@ -912,6 +912,163 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     }
 }
 
+// the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
+// first then ascending, one rounding (allred_mem_2D semantics, k_peer_oneshot's bits)
+__device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, int me) {
+    uint4 s0 = y[0];
+#pragma unroll
+    for (int src = 0; src < kLLMaxGpus; ++src)
+        if (src == me) s0 = y[src];
+    float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+#pragma unroll
+    for (int qq = 0; qq < kLLMaxGpus; ++qq) {
+        if (qq >= W || qq == me) continue;
+        a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
+        a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
+        a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
+        a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
+    }
+    return make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
+}
+
+// ---- hierarchical step, two-deep bucket pipeline ----------------------------
+// k_hier_x2: launch i starts bucket i (cur: tree -> partial pushed to the
+// tile's owner), sums the owned tiles of bucket i-1 (mid: its W partials were
+// pushed during launch i-1 -> the result is pushed to every GPU) and writes
+// bucket i-2 (old: its results were pushed during launch i-1).  Every poll of
+// launch i waits for pushes of launch i-1, never for one of its own launch, so
+// a GPU that starts its launch late (launch jitter, a slower peer) costs the
+// others nothing as long as it is less than a launch behind; k_hier_x (one
+// bucket deep) polls at the end of every launch for partials pushed during it.
+// Order in a launch:
+//   L(cur 0), L(cur 1) issued (HBM busy from the start); the polls of mid's
+//            owned partials and of old's results of this workgroup's tiles, all
+//            in flight together; mid's owned sums pushed to every GPU's box
+//   loop j:  A(cur j) [tree, partial -> owner] | S(old j) stores interleaved
+//            with L(cur j+2)
+//   fin:     (the flush launch, cur null) mid's results — pushed by the owned
+//            sums at the start of every GPU's flush launch — polled, mid's rows
+//            written
+// Hand-offs per tile are ordered by the workgroup that serves the tile on every
+// GPU (the same index): GPU g polls old = bucket i-2's result of tile t before
+// it pushes bucket i's partial of t, and the owner reads bucket i's partials of
+// t (launch i+1) before it pushes bucket i's result of t, so LL parity k & 1
+// (inbox and box) is reused only after its previous reader is done.
+// Same bits as k_hier_ll / k_hier_x; at most kHierXMaxTiles tiles per workgroup.
+__global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
+                                                    uint16_t* __restrict__ fin, uint64_t stride,
+                                                    const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
+                                                    int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
+                                                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
+                                                    int has_mid, uint32_t* status) {
+    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
+    __shared__ __attribute__((aligned(16))) uint4 res[kHierXMaxTiles][TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
+                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
+    };
+    // rows of tile j of bucket `dst` from res[j] (lanes of wave w, half q: rows RPW w + q + RPI k)
+    auto store_rows = [&](uint16_t* dst, int j) {
+        const uint4 rv = res[j][c];
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            st_nt(reinterpret_cast<uint4*>(dst + row_off + (uint64_t)(RPI * k) * stride) + tile_of(j) * TV + c, rv);
+    };
+    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
+    wait_vm<0>();   // the order bytes
+    if (cur && mine > 0) issue(tile_of(0), 0);
+    if (cur && mine > 1) issue(tile_of(1), 1);
+    // ---- lane (jr, c) (32 jr + c) serves tile jr of this workgroup, column c
+    const int jr = threadIdx.x / TV;
+    const bool act = jr < kHierXMaxTiles && jr < mine;
+    const uint64_t tr = tile_of(jr);
+    const bool rmid = has_mid && act && owner_of(tr) == me;
+    const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
+    uint64_t wr[kLLMaxGpus][4], wo[4];
+    if (rmid) {
+#pragma unroll
+        for (int src = 0; src < kLLMaxGpus; ++src)
+            if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
+    }
+    if (old && act) ll_load(lo.ll[me] + box_words + tr * 128 + c, wo);
+    if (rmid) {   // mid's owned sums -> every GPU's box
+        uint4 y[kLLMaxGpus];
+#pragma unroll
+        for (int src = 0; src < kLLMaxGpus; ++src)
+            if (src < W)
+                y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
+                                                 : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
+        const uint4 o = owner_sum(y, W, me);
+#pragma unroll
+        for (int dst = 0; dst < kLLMaxGpus; ++dst)
+            if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
+    }
+    if (old && act) res[jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tr * 128 + c, eold, status);
+    // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
+    // (the polls before them have returned, and with them both tiles' loads)
+    const int pushed = __ballot(rmid) != 0 ? 4 * W : 0;
+    lds_barrier();   // order bytes and old's results in LDS
+    for (int j = 0; j < mine; ++j) {
+        if (cur) {   // ---- A(cur j)
+            // after L(j): S(j-2)'s last op, L(j+1), S(j-1), this wave's owned-sum pushes
+            // (j < 2) (+ wave 0's partial pushes: waits a little longer)
+            wait_any((j >= 2 && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && old ? OPS : 0) +
+                     (j < 2 ? pushed : 0));
+            lds_barrier();   // tile j is in LDS
+            const uint4* tile = buf[j & 1];
+            const uint8_t* ord = ord_lds + RPW * w + LPL * q;
+            uint4 x[LPL];
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+            for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+            if (q == 0) part[j & 1][w * TV + c] = pw;
+            lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
+            if (w == 0 && q == 0) {
+                const uint64_t t = tile_of(j);
+                const int o = owner_of(t);
+                const uint4* pp = part[j & 1];
+                const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+                ll_put(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur);
+            }
+        }
+        // ---- cur's tile j+2 in, old's tile j out, interleaved op by op
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(j);
+        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+        const uint4 rv = old ? res[j][c] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            if (cur && j + 2 < mine)
+                lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
+                          bl + (uint32_t)(RPI * k * TV * 16));
+            if (old) st_nt(reinterpret_cast<uint4*>(old + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
+        }
+    }
+    if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
+        __syncthreads();   // every wave has read old's results out of res
+        if (act) res[jr][c] = ll_get(lm.ll[me] + box_words + tr * 128 + c, emid, status);
+        lds_barrier();
+        for (int j = 0; j < mine; ++j) store_rows(fin, j);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // k_peer_mem_ll: allred_mem_2D across GPUs for small buckets with LL hand-offs
 // (the flat counterpart of k_hier_ll).  A: every vector is pushed as four
@@ -1176,6 +1333,30 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     }
     hipLaunchKernelGGL(k_hier_x, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, prev, stride, order, lc, lp,
                        nranks, me, ntiles, ntiles / nranks, box_words, ecur, eprev, status);
+    return peer_last_error();
+}
+
+int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
+                   uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
+                   uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
+                   unsigned max_grid, void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
+        (!cur && !old && !fin) || (cur && !llc) || (old && !llo) || (fin && (cur || !llm)) ||
+        (cur && !aligned16(cur)) || (old && !aligned16(old)) || (fin && !aligned16(fin)))
+        return ALLRED_ERR_ARG;
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
+    if ((ntiles + grid - 1) / grid > (uint64_t)kHierXMaxTiles) return ALLRED_ERR_UNSUPPORTED;
+    LLPtrs lc{}, lm{}, lo{};
+    for (int q = 0; q < nranks; ++q) {
+        lc.ll[q] = llc ? llc[q] : nullptr;
+        lm.ll[q] = llm ? llm[q] : nullptr;
+        lo.ll[q] = llo ? llo[q] : nullptr;
+    }
+    hipLaunchKernelGGL(k_hier_x2, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc,
+                       lm, lo, nranks, me, ntiles, ntiles / nranks, box_words, ecur, emid, eold, llm ? 1 : 0, status);
     return peer_last_error();
 }
 

@@ -101,33 +101,39 @@ def worker(rank, world, port, q):
             fails.append(("hier", 0, 1))
         # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form
         # (k_hier_oneshot, per-tile flags), the LL push form (k_hier_ll), its
-        # pipelined form (k_hier_pipe) and the launch form, two calls back to back each (then LL once more after the
-        # launch form: its LL boxes must not accept the older calls' words)
+        # pipelined form (k_hier_pipe), the launch form and the bucket pipelines (k_hier_x, k_hier_x2), two or
+        # three calls back to back each (then LL once more after the launch form: its LL boxes must not accept
+        # the older calls' words)
         local, m = 64, 256 * world * 3
         # in full and capped grids (a capped grid gives every workgroup many tiles)
         for mi, (mode, limit, ll, cap) in enumerate((("hier_one_kernel", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
                                                      ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1),
                                                      ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2),
-                                                     ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1))):
-            if cap < 0:   # k_hier_x takes at most 8 tiles per workgroup
+                                                     ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
+                                                     ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1))):
+            if cap < 0:   # k_hier_x / k_hier_x2 take at most 8 tiles per workgroup
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
             peer.set_max_groups(cap)
             runs = []
-            for rep in range(2):
+            for rep in range(3 if mode.startswith("hier_x2") else 2):   # x2: one launch with cur, mid and old
                 data = [np.random.default_rng(700 + 100 * mi + 10 * rep + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
                         for r in range(world)]
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
-                if mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
+                if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
+                    peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
+                elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
                     peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
                                              torch.cuda.current_stream())
                 else:
                     peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
-            if mode.startswith("hier_x"):
+            if mode.startswith("hier_x2"):
+                peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
+            elif mode.startswith("hier_x"):
                 peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
             torch.cuda.synchronize()
             for rep, (data, buf, _) in enumerate(runs):
@@ -502,3 +508,60 @@ def test_config3_config5_eight_processes():
     for rank, fails, status in results:
         assert fails == [], (rank, fails)
         assert status == 0, (rank, status)
+
+
+@pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 5), (327680, 0, 1), (256 * 5, 0, 2), (256 * 40, 5, 3),
+                                           (327680, 160, 4)])
+def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
+    """One GPU (W = 1), 64 local ranks: a sequence of buckets through the
+    two-deep pipelined hierarchical step (k_hier_x2: launch i starts bucket i,
+    sums bucket i-1's owned tiles and writes bucket i-2), buckets + 1 calls
+    (1 bucket: the flush sums and writes it; 2: the flush writes both), every
+    bucket bit-exact vs the oracle; full and capped grids (up to 8 tiles per
+    workgroup), the sequence twice (both LL parities reused).  Protocol errors:
+    another peer call or the one-deep pipeline while buckets are pending, a
+    different bucket size mid-sequence, a flush with nothing pending."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import tenstorrentallreduce_amd as t
+    from tenstorrentallreduce_amd import _lib
+    import oracle
+    local = 64
+    peer = t.Peer(1, 0, 0, 2 * n)
+    peer.connect([peer.handle()])
+    try:
+        peer.set_max_groups(cap)
+        data, want = [], []
+        for b in range(buckets):
+            d = np.random.default_rng(2300 + b).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+            loc = [x.copy() for x in d]
+            oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+            data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
+            want.append(loc[0])
+        s = torch.cuda.current_stream()
+        for _ in range(2):
+            bufs = [x.clone() for x in data]
+            for b in bufs:
+                peer.allreduce_pipelined2(b.data_ptr(), n, s)
+            peer.allreduce_pipelined2(None, n, s)
+            torch.cuda.synchronize()
+            for i, (b, w) in enumerate(zip(bufs, want)):
+                bad = int((b.cpu().numpy().view(np.uint16) != w[None, :]).sum())
+                assert bad == 0, (i, bad)
+        assert peer.status() & t.PEER_TIMEOUT == 0
+        x = data[0].clone()
+        peer.allreduce_pipelined2(x.data_ptr(), n, s)
+        with pytest.raises(_lib.AllredError):   # another call while a bucket is pending
+            peer.allreduce(x.data_ptr(), n, s, local, 8, t.SWING, x.data_ptr())
+        with pytest.raises(_lib.AllredError):   # the one-deep pipeline does not mix in
+            peer.allreduce_pipelined(x.data_ptr(), None, n, s)
+        if n % (2 * 256) == 0:
+            with pytest.raises(_lib.AllredError):   # another bucket size mid-sequence
+                peer.allreduce_pipelined2(x.data_ptr(), n // 2, s)
+        peer.allreduce_pipelined2(None, n, s)
+        with pytest.raises(_lib.AllredError):   # nothing pending
+            peer.allreduce_pipelined2(None, n, s)
+        torch.cuda.synchronize()
+        assert (x.cpu().numpy().view(np.uint16) == want[0][None, :]).all()
+    finally:
+        peer.close()

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
 x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_oneshot,
-k_hier_ll, k_hier_pipe and k_hier_x (buckets pipelined: K buckets in K + 1
-launches, the timed region includes the last bucket's finishing launch) — the N > 1 bench's candidates with the cross-GPU
+k_hier_ll, k_hier_pipe, k_hier_x and k_hier_x2 (buckets pipelined one / two
+deep: K buckets in K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
 hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
 kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
 arms interleaved.   python tools/hier_step.py [steps] [rounds]   (HIER_CAP: grid cap)"""
@@ -27,33 +27,40 @@ peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
-res = {k: [] for k in list(arms) + ["hier_x"]}
+res = {k: [] for k in list(arms) + ["hier_x", "hier_x2"]}
 host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
 SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
-def pipelined(k):   # k buckets in k + 1 calls (k_hier_x): each call finishes the previous bucket
+def pipelined(k, deep):   # k buckets in k + 1 calls: k_hier_x (each call finishes the previous bucket) / k_hier_x2
     prev = None
     for i in range(k):
         cur = sets[i % NS].data_ptr()
-        peer.allreduce_pipelined(cur, prev, n, s)
+        if deep:
+            peer.allreduce_pipelined2(cur, n, s)
+        else:
+            peer.allreduce_pipelined(cur, prev, n, s)
         prev = cur
-    peer.allreduce_pipelined(None, prev, n, s)
+    if deep:
+        peer.allreduce_pipelined2(None, n, s)
+    else:
+        peer.allreduce_pipelined(None, prev, n, s)
 
 
 for _ in range(rounds):
-    pipelined(20)
-    torch.cuda.synchronize()
-    with torch.cuda.stream(s):
-        torch.cuda._sleep(SPIN)
-    e0.record(s)
-    h0 = time.perf_counter()
-    pipelined(steps)
-    host["hier_x"].append(round((time.perf_counter() - h0) * 1e6 / steps, 2))
-    e1.record(s)
-    torch.cuda.synchronize()
-    res["hier_x"].append(round(e0.elapsed_time(e1) * 1e3 / steps, 3))
+    for name, deep in (("hier_x", False), ("hier_x2", True)):
+        pipelined(20, deep)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(SPIN)
+        e0.record(s)
+        h0 = time.perf_counter()
+        pipelined(steps, deep)
+        host[name].append(round((time.perf_counter() - h0) * 1e6 / steps, 2))
+        e1.record(s)
+        torch.cuda.synchronize()
+        res[name].append(round(e0.elapsed_time(e1) * 1e3 / steps, 3))
     for name, (limit, ll) in arms.items():
         peer.set_oneshot_max(limit)
         peer.set_hier_ll(ll)
