@@ -507,6 +507,38 @@ __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_
     return make_uint4((uint32_t)w0, (uint32_t)w1, (uint32_t)w2, (uint32_t)w3);
 }
 
+// one poll of an LL slot without waiting (k_hier_pipe / k_hier_x / k_hier_x2 / k_hier_ll R)
+__device__ __forceinline__ void ll_load(const uint64_t* src, uint64_t (&wd)[4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool ll_fresh(const uint64_t (&wd)[4], uint32_t e) {
+    return (uint32_t)(wd[0] >> 32) == e && (uint32_t)(wd[1] >> 32) == e && (uint32_t)(wd[2] >> 32) == e &&
+           (uint32_t)(wd[3] >> 32) == e;
+}
+__device__ __forceinline__ uint4 ll_data(const uint64_t (&wd)[4]) {
+    return make_uint4((uint32_t)wd[0], (uint32_t)wd[1], (uint32_t)wd[2], (uint32_t)wd[3]);
+}
+
+// the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
+// first then ascending, one rounding (allred_mem_2D semantics, k_peer_oneshot's bits)
+__device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, int me) {
+    uint4 s0 = y[0];
+#pragma unroll
+    for (int src = 0; src < kLLMaxGpus; ++src)
+        if (src == me) s0 = y[src];
+    float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
+#pragma unroll
+    for (int qq = 0; qq < kLLMaxGpus; ++qq) {
+        if (qq >= W || qq == me) continue;
+        a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
+        a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
+        a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
+        a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
+    }
+    return make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
+}
+
 __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
@@ -562,36 +594,29 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
-    uint4* xs = buf[0];   // [8 GPUs][32 columns] partials, then [32] results / [4][32] B rows
-    // ---- R: the tiles I own: W partials from my inbox -> every GPU's result box
-    for (int j = 0; j < mine; ++j) {
-        const uint64_t t = tile_of(j);
+    uint4* xs = buf[0];   // [4][32] B rows
+    // ---- R: the tiles I own, 8 at a time: lane (jr, c) polls the W partials of
+    // tile jr's column c from my inbox (all in flight at once), sums them and
+    // pushes the result to every GPU's box — one poll round trip per 8 tiles
+    for (int j0 = 0; j0 < mine; j0 += 8) {
+        const int jr = j0 + (int)(threadIdx.x >> 5);
+        if (jr >= mine) break;
+        const uint64_t t = tile_of(jr);
         if (owner_of(t) != me) continue;
         const uint64_t li = t - (uint64_t)me * tiles_per_owner;
-        const int q = threadIdx.x >> 5;   // source GPU of this lane's slot
-        if (q < W) xs[q * 32 + c] = ll_get(my_ll + (li * W + q) * 128 + c, epoch, status);
-        __syncthreads();
-        if (threadIdx.x < 32) {
-            const uint4 s0 = xs[me * 32 + c];
-            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
-            for (int qq = 0; qq < W; ++qq) {
-                if (qq == me) continue;
-                const uint4 y = xs[qq * 32 + c];
-                a[0] += lo_f(y.x); a[1] += hi_f(y.x);
-                a[2] += lo_f(y.y); a[3] += hi_f(y.y);
-                a[4] += lo_f(y.z); a[5] += hi_f(y.z);
-                a[6] += lo_f(y.w); a[7] += hi_f(y.w);
-            }
-            uint4 o;
-            o.x = pack_rne(a[0], a[1]);
-            o.y = pack_rne(a[2], a[3]);
-            o.z = pack_rne(a[4], a[5]);
-            o.w = pack_rne(a[6], a[7]);
-            xs[8 * 32 + c] = o;
-        }
-        __syncthreads();
-        if (q < W) ll_put(lp.ll[q] + box_words + t * 128 + c, xs[8 * 32 + c], epoch);
-        __syncthreads();   // xs is reused by the next owned tile
+        uint64_t wr[kLLMaxGpus][4];
+#pragma unroll
+        for (int src = 0; src < kLLMaxGpus; ++src)
+            if (src < W) ll_load(my_ll + (li * W + src) * 128 + c, wr[src]);
+        uint4 y[kLLMaxGpus];
+#pragma unroll
+        for (int src = 0; src < kLLMaxGpus; ++src)
+            if (src < W)
+                y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(my_ll + (li * W + src) * 128 + c, epoch, status);
+        const uint4 o = owner_sum(y, W, me);
+#pragma unroll
+        for (int dst = 0; dst < kLLMaxGpus; ++dst)
+            if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c, o, epoch);
     }
     // ---- B: my result box -> the 64 rank rows, 4 tiles at a time
     constexpr int BB = 4;
@@ -642,18 +667,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
 // R(j-2) before B(j-2)), and the grid is resident, so every wait is reached
 // and satisfied; the hand-offs have one (R) and two (B) iterations of local
 // work to arrive in.
-__device__ __forceinline__ void ll_load(const uint64_t* src, uint64_t (&wd)[4]) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ bool ll_fresh(const uint64_t (&wd)[4], uint32_t e) {
-    return (uint32_t)(wd[0] >> 32) == e && (uint32_t)(wd[1] >> 32) == e && (uint32_t)(wd[2] >> 32) == e &&
-           (uint32_t)(wd[3] >> 32) == e;
-}
-__device__ __forceinline__ uint4 ll_data(const uint64_t (&wd)[4]) {
-    return make_uint4((uint32_t)wd[0], (uint32_t)wd[1], (uint32_t)wd[2], (uint32_t)wd[3]);
-}
-
 __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                       const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                       uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
@@ -732,24 +745,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
                 const uint64_t* at = my_ll + (lr * W + src) * 128 + c;
                 y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(at, epoch, status);
             }
-            uint4 s0 = y[0];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src == me) s0 = y[src];
-            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
-#pragma unroll
-            for (int qq = 0; qq < kLLMaxGpus; ++qq) {
-                if (qq >= W || qq == me) continue;
-                a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
-                a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
-                a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
-                a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
-            }
-            uint4 o;
-            o.x = pack_rne(a[0], a[1]);
-            o.y = pack_rne(a[2], a[3]);
-            o.z = pack_rne(a[4], a[5]);
-            o.w = pack_rne(a[6], a[7]);
+            const uint4 o = owner_sum(y, W, me);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
                 if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c, o, epoch);
@@ -887,48 +883,12 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                 if (src < W)
                     y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
                                                      : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
-            uint4 s0 = y[0];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src == me) s0 = y[src];
-            float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
-#pragma unroll
-            for (int qq = 0; qq < kLLMaxGpus; ++qq) {
-                if (qq >= W || qq == me) continue;
-                a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
-                a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
-                a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
-                a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
-            }
-            uint4 o;
-            o.x = pack_rne(a[0], a[1]);
-            o.y = pack_rne(a[2], a[3]);
-            o.z = pack_rne(a[4], a[5]);
-            o.w = pack_rne(a[6], a[7]);
+            const uint4 o = owner_sum(y, W, me);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
                 if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
         }
     }
-}
-
-// the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
-// first then ascending, one rounding (allred_mem_2D semantics, k_peer_oneshot's bits)
-__device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, int me) {
-    uint4 s0 = y[0];
-#pragma unroll
-    for (int src = 0; src < kLLMaxGpus; ++src)
-        if (src == me) s0 = y[src];
-    float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y), lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
-#pragma unroll
-    for (int qq = 0; qq < kLLMaxGpus; ++qq) {
-        if (qq >= W || qq == me) continue;
-        a[0] += lo_f(y[qq].x); a[1] += hi_f(y[qq].x);
-        a[2] += lo_f(y[qq].y); a[3] += hi_f(y[qq].y);
-        a[4] += lo_f(y[qq].z); a[5] += hi_f(y[qq].z);
-        a[6] += lo_f(y[qq].w); a[7] += hi_f(y[qq].w);
-    }
-    return make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
 }
 
 // ---- hierarchical step, two-deep bucket pipeline ----------------------------
