@@ -42,6 +42,11 @@ __global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, 
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
 }
 
+// kSchedU vectors per thread in flight per loop trip of the copy / add loops
+// that read peers' windows over xGMI: a remote read's latency is paid once per
+// kSchedU vectors instead of once per vector
+constexpr int kSchedU = 4;
+
 // reduce-scatter: block `me` of every window, owner first then ranks in order
 // (fp32, one rounding), written to my window (peers gather it) and to my bucket
 __global__ __launch_bounds__(kBlock) void k_peer_rs(PeerPtrs pp, int nranks, int me, uint16_t* __restrict__ bucket,
@@ -81,8 +86,16 @@ __global__ __launch_bounds__(kBlock) void k_peer_ag(PeerPtrs pp, int me, uint16_
     const int q = blockIdx.y;
     if (q == me) return;
     const uint64_t off = (uint64_t)q * blk_vec;
-    for (uint64_t v = gtid(); v < blk_vec; v += gthreads())
-        st_nt(reinterpret_cast<uint4*>(bucket) + off + v, ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + off + v));
+    const uint64_t G = gthreads();
+    for (uint64_t v = gtid(); v < blk_vec; v += kSchedU * G) {
+        uint4 y[kSchedU];
+#pragma unroll
+        for (int u = 0; u < kSchedU; ++u)
+            if (v + u * G < blk_vec) y[u] = ld_nt(reinterpret_cast<const uint4*>(pp.win[q]) + off + v + u * G);
+#pragma unroll
+        for (int u = 0; u < kSchedU; ++u)
+            if (v + u * G < blk_vec) st_nt(reinterpret_cast<uint4*>(bucket) + off + v + u * G, y[u]);
+    }
 }
 
 // ---- one-kernel form (latency regime) --------------------------------------
@@ -233,10 +246,22 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
             const bool last = k == S - 1;
             for (uint64_t m = pr.recv[c][k]; m; m &= m - 1) {
                 const int b = __builtin_ctzll(m);
-                for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) {
-                    const uint4 o = add8(ld_nt(mine + v), ld_nt(theirs + v));
-                    st_nt(mine + v, o);
-                    if (last) st_nt(bk + v, o);
+                const uint64_t end = cb + b * blk + hi;
+                for (uint64_t v = cb + b * blk + lo + tid; v < end; v += kSchedU * kBlock) {
+                    uint4 x[kSchedU], y[kSchedU];
+#pragma unroll
+                    for (int u = 0; u < kSchedU; ++u)
+                        if (v + u * kBlock < end) {
+                            x[u] = ld_nt(mine + v + u * kBlock);
+                            y[u] = ld_nt(theirs + v + u * kBlock);
+                        }
+#pragma unroll
+                    for (int u = 0; u < kSchedU; ++u)
+                        if (v + u * kBlock < end) {
+                            const uint4 o = add8(x[u], y[u]);
+                            st_nt(mine + v + u * kBlock, o);
+                            if (last) st_nt(bk + v + u * kBlock, o);
+                        }
                 }
             }
             sched_signal(pp, pr, c, me, slot, base + 2 + k);
@@ -249,10 +274,18 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
             const bool keep = t < S - 1;  // later partners read these blocks from my window
             for (uint64_t m = pr.send[c][i]; m; m &= m - 1) {
                 const int b = __builtin_ctzll(m);
-                for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) {
-                    const uint4 y = ld_nt(theirs + v);
-                    if (keep) st_nt(mine + v, y);
-                    st_nt(bk + v, y);
+                const uint64_t end = cb + b * blk + hi;
+                for (uint64_t v = cb + b * blk + lo + tid; v < end; v += kSchedU * kBlock) {
+                    uint4 y[kSchedU];
+#pragma unroll
+                    for (int u = 0; u < kSchedU; ++u)
+                        if (v + u * kBlock < end) y[u] = ld_nt(theirs + v + u * kBlock);
+#pragma unroll
+                    for (int u = 0; u < kSchedU; ++u)
+                        if (v + u * kBlock < end) {
+                            if (keep) st_nt(mine + v + u * kBlock, y[u]);
+                            st_nt(bk + v + u * kBlock, y[u]);
+                        }
                 }
             }
             if (keep) sched_signal(pp, pr, c, me, slot, base + 2 + pos);
@@ -272,7 +305,18 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
         const uint4* a = mine + (k & 1) * half_vec;
         const uint4* b = reinterpret_cast<const uint4*>(pp.win[p]) + (k & 1) * half_vec;
         uint4* dst = last ? bk : mine + ((k + 1) & 1) * half_vec;
-        for (uint64_t v = lo + tid; v < hi; v += kBlock) st_nt(dst + v, add8(ld_nt(a + v), ld_nt(b + v)));
+        for (uint64_t v = lo + tid; v < hi; v += kSchedU * kBlock) {
+            uint4 x[kSchedU], y[kSchedU];
+#pragma unroll
+            for (int u = 0; u < kSchedU; ++u)
+                if (v + u * kBlock < hi) {
+                    x[u] = ld_nt(a + v + u * kBlock);
+                    y[u] = ld_nt(b + v + u * kBlock);
+                }
+#pragma unroll
+            for (int u = 0; u < kSchedU; ++u)
+                if (v + u * kBlock < hi) st_nt(dst + v + u * kBlock, add8(x[u], y[u]));
+        }
         if (!last) sched_signal(pp, pr, c, me, slot, base + 2 + k);
     }
 }
