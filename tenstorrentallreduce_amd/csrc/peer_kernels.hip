@@ -638,41 +638,49 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
-    uint4* xs = buf[0];   // [4][32] B rows
-    // ---- R: the tiles I own, 8 at a time: lane (jr, c) polls the W partials of
-    // tile jr's column c from my inbox (all in flight at once), sums them and
-    // pushes the result to every GPU's box — one poll round trip per 8 tiles
-    for (int j0 = 0; j0 < mine; j0 += 8) {
-        const int jr = j0 + (int)(threadIdx.x >> 5);
-        if (jr >= mine) break;
-        const uint64_t t = tile_of(jr);
-        if (owner_of(t) != me) continue;
-        const uint64_t li = t - (uint64_t)me * tiles_per_owner;
-        uint64_t wr[kLLMaxGpus][4];
-#pragma unroll
-        for (int src = 0; src < kLLMaxGpus; ++src)
-            if (src < W) ll_load(my_ll + (li * W + src) * 128 + c, wr[src]);
-        uint4 y[kLLMaxGpus];
-#pragma unroll
-        for (int src = 0; src < kLLMaxGpus; ++src)
-            if (src < W)
-                y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(my_ll + (li * W + src) * 128 + c, epoch, status);
-        const uint4 o = owner_sum(y, W, me);
-#pragma unroll
-        for (int dst = 0; dst < kLLMaxGpus; ++dst)
-            if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c, o, epoch);
-    }
-    // ---- B: my result box -> the 64 rank rows, 4 tiles at a time
-    constexpr int BB = 4;
+    uint4* xs = buf[0];   // [8][32] results of a batch
+    // ---- R + B, 8 tiles at a time; lane (jr, c) serves tile jr of the batch, column c.
+    // R: for a tile I own, the W partials of its column are polled from my inbox
+    // (all in flight at once), summed and pushed to every OTHER GPU's box; the
+    // result stays in the lane.  B: every other tile's result is polled from my
+    // box, then the batch's 64 rank rows are written.  One poll round trip per
+    // batch for the owned tiles and one for the others; at W = 1 every tile is
+    // owned and B polls nothing.  B(batch k) waits only for R(batch k) of the
+    // owners (the same workgroup index there), which waits only for A.
+    constexpr int BB = 8;
     for (int j0 = 0; j0 < mine; j0 += BB) {
         const int nb = mine - j0 < BB ? mine - j0 : BB;
         const int b = threadIdx.x >> 5;
-        if (b < nb) xs[16 * 32 + b * 32 + c] = ll_get(my_ll + box_words + tile_of(j0 + b) * 128 + c, epoch, status);
+        const uint64_t t = tile_of(j0 + b);
+        const bool own = b < nb && owner_of(t) == me;
+        uint4 val = make_uint4(0, 0, 0, 0);
+        if (own) {
+            const uint64_t li = t - (uint64_t)me * tiles_per_owner;
+            uint64_t wr[kLLMaxGpus][4];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W) ll_load(my_ll + (li * W + src) * 128 + c, wr[src]);
+            uint4 y[kLLMaxGpus];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W)
+                    y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(my_ll + (li * W + src) * 128 + c, epoch, status);
+            val = owner_sum(y, W, me);
+#pragma unroll
+            for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                if (dst < W && dst != me) ll_put(lp.ll[dst] + box_words + t * 128 + c, val, epoch);
+        }
+        // every owned-tile push of this wave is issued before any of its result polls:
+        // a wave holds owned and other tiles, and a poll spinning ahead of the wave's
+        // own pushes could wait (circularly) for a GPU whose wave waits for those pushes
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (!own && b < nb) val = ll_get(my_ll + box_words + t * 128 + c, epoch, status);
+        if (b < nb) xs[b * 32 + c] = val;
         __syncthreads();
         uint4 res[BB];
 #pragma unroll
         for (int bb = 0; bb < BB; ++bb)
-            if (bb < nb) res[bb] = xs[16 * 32 + bb * 32 + c];
+            if (bb < nb) res[bb] = xs[bb * 32 + c];
         __syncthreads();   // xs is reused by the next batch
 #pragma unroll
         for (int bb = 0; bb < BB; ++bb) {
