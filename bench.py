@@ -576,6 +576,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #                 reads bucket i+1 while it writes bucket i; the last flush is timed)
     #   peer_hier_x2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
     #                 owned tiles, writes bucket i-2; every poll waits for the previous launch)
+    #   peer_hier_x2t the same with bucket i-1's owned sums at the END of launch i (tune
+    #                 hier_x2_tail: its polls never wait; the result polls wait like k_hier_x's)
     # A peer candidate runs only once verified on THIS machine: on small-integer
     # inputs (every sum exact, so every reduction order agrees) its bits must equal
     # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
@@ -587,13 +589,21 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
 
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
-    pend2 = [False]   # peer_hier_x2: buckets started and not yet finished (flush() finishes them)
+    pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
+
+    tail = [None]
+
+    def x2_tail(on):   # the host-side switch between the two k_hier_x2 forms, read at launch
+        if tail[0] != on:
+            t.tune("hier_x2_tail", int(on))
+            tail[0] = on
 
     def flush():
         if pend[0] is not None:
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
         if pend2[0]:
+            x2_tail(pend2[0] == "peer_hier_x2t")
             peer.allreduce_pipelined2(None, ELEMS, stream)
             pend2[0] = False
 
@@ -606,11 +616,12 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
             pend[0] = b.data_ptr()
             return
-        if kind == "peer_hier_x2":   # two deep: this call writes the bucket started two calls ago
-            if pend[0] is not None:
+        if kind in ("peer_hier_x2", "peer_hier_x2t"):   # two deep: this call writes the bucket started two calls ago
+            if pend[0] is not None or (pend2[0] and pend2[0] != kind):
                 flush()
+            x2_tail(kind == "peer_hier_x2t")
             peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
-            pend2[0] = True
+            pend2[0] = kind
             return
         flush()
         if kind == "rccl":
@@ -636,7 +647,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         ref = small.clone()
         note(rank, f"verify: {base} on small integers")
         run(base, ref, fresh=True)
-        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe", "peer_hier_x", "peer_hier_x2"):
+        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe", "peer_hier_x", "peer_hier_x2",
+                     "peer_hier_x2t"):
             note(rank, f"verify: {kind}")
             try:   # the same calls on every rank: a raised status is raised everywhere
                 x = small.clone()
@@ -807,7 +819,7 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
     one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
-                  "peer_hier_x": "k_hier_x", "peer_hier_x2": "k_hier_x2"}
+                  "peer_hier_x": "k_hier_x", "peer_hier_x2": "k_hier_x2", "peer_hier_x2t": "k_hier_x2<TAIL>"}
     if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
         roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
@@ -828,6 +840,10 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
            "peer_hier_x2": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
                            "timed region): launch i reads bucket i, sums bucket i-1's owned tiles and writes bucket "
                            "i-2's rows, mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
+           "peer_hier_x2t": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
+                            "timed region): launch i reads bucket i, writes bucket i-2's rows and at its end sums "
+                            "bucket i-1's owned tiles, mem_2D one-shot across GPUs with LL pushes into peer-mapped "
+                            "xGMI windows",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     return {

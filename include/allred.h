@@ -234,6 +234,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   fused_chunk_tiles 1280: the persistent fused 64-rank passes run a bucket of T 256-element
  *                     tiles as max(1, round(T / 1280)) launches over consecutive tile ranges
  *                     (0 = one launch); allred_plan_launches counts them
+ *   hier_x2_tail      0; 1: k_hier_x2 (allred_peer_allreduce_pipelined2) sums the owned tiles of
+ *                     the middle bucket at the end of each launch instead of its start
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

@@ -967,6 +967,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // t (launch i+1) before it pushes bucket i's result of t, so LL parity k & 1
 // (inbox and box) is reused only after its previous reader is done.
 // Same bits as k_hier_ll / k_hier_x; at most kHierXMaxTiles tiles per workgroup.
+template <bool TAIL>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
@@ -1010,14 +1011,12 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     const uint64_t tr = tile_of(jr);
     const bool rmid = has_mid && act && owner_of(tr) == me;
     const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
-    uint64_t wr[kLLMaxGpus][4], wo[4];
-    if (rmid) {
+    // mid's owned sums: polls of its W partials, owner sum, pushed to every GPU's box
+    auto owned_sums = [&]() {
+        uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
         for (int src = 0; src < kLLMaxGpus; ++src)
             if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
-    }
-    if (old && act) ll_load(lo.ll[me] + box_words + tr * 128 + c, wo);
-    if (rmid) {   // mid's owned sums -> every GPU's box
         uint4 y[kLLMaxGpus];
 #pragma unroll
         for (int src = 0; src < kLLMaxGpus; ++src)
@@ -1028,11 +1027,14 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
             if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
-    }
+    };
+    uint64_t wo[4];
+    if (old && act) ll_load(lo.ll[me] + box_words + tr * 128 + c, wo);
+    if (!TAIL && rmid) owned_sums();
     if (old && act) res[jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tr * 128 + c, eold, status);
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
     // (the polls before them have returned, and with them both tiles' loads)
-    const int pushed = __ballot(rmid) != 0 ? 4 * W : 0;
+    const int pushed = !TAIL && __ballot(rmid) != 0 ? 4 * W : 0;
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
@@ -1073,6 +1075,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             if (old) st_nt(reinterpret_cast<uint4*>(old + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
         }
     }
+    if (TAIL && rmid) owned_sums();   // TAIL: mid's partials arrived during the launch i-1
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
         __syncthreads();   // every wave has read old's results out of res
         if (act) res[jr][c] = ll_get(lm.ll[me] + box_words + tr * 128 + c, emid, status);
@@ -1367,8 +1370,9 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         lm.ll[q] = llm ? llm[q] : nullptr;
         lo.ll[q] = llo ? llo[q] : nullptr;
     }
-    hipLaunchKernelGGL(k_hier_x2, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc,
-                       lm, lo, nranks, me, ntiles, ntiles / nranks, box_words, ecur, emid, eold, llm ? 1 : 0, status);
+    hipLaunchKernelGGL(tune(Tune::hier_x2_tail) ? k_hier_x2<true> : k_hier_x2<false>, dim3(grid), dim3(kBlock), 0,
+                       (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
+                       box_words, ecur, emid, eold, llm ? 1 : 0, status);
     return peer_last_error();
 }
 

@@ -111,7 +111,8 @@ def worker(rank, world, port, q):
                                                      ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1),
                                                      ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
-                                                     ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1))):
+                                                     ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
+                                                     ("hier_x2_tail", 0, 0, 0))):
             if cap < 0:   # k_hier_x / k_hier_x2 take at most 8 tiles per workgroup
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
@@ -124,7 +125,8 @@ def worker(rank, world, port, q):
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
-                    peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
+                    with t.tuned(hier_x2_tail=int(mode == "hier_x2_tail")):
+                        peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
                     peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
                                              torch.cuda.current_stream())
@@ -132,7 +134,8 @@ def worker(rank, world, port, q):
                     peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
-                peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
+                with t.tuned(hier_x2_tail=int(mode == "hier_x2_tail")):
+                    peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
                 peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
             torch.cuda.synchronize()
@@ -539,15 +542,16 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for _ in range(2):
-            bufs = [x.clone() for x in data]
-            for b in bufs:
-                peer.allreduce_pipelined2(b.data_ptr(), n, s)
-            peer.allreduce_pipelined2(None, n, s)
-            torch.cuda.synchronize()
+        for rep in range(4):   # owned sums at the start (0, 1) / the end (2, 3) of a launch
+            with t.tuned(hier_x2_tail=rep // 2):
+                bufs = [x.clone() for x in data]
+                for b in bufs:
+                    peer.allreduce_pipelined2(b.data_ptr(), n, s)
+                peer.allreduce_pipelined2(None, n, s)
+                torch.cuda.synchronize()
             for i, (b, w) in enumerate(zip(bufs, want)):
                 bad = int((b.cpu().numpy().view(np.uint16) != w[None, :]).sum())
-                assert bad == 0, (i, bad)
+                assert bad == 0, (rep, i, bad)
         assert peer.status() & t.PEER_TIMEOUT == 0
         x = data[0].clone()
         peer.allreduce_pipelined2(x.data_ptr(), n, s)
