@@ -236,6 +236,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     (0 = one launch); allred_plan_launches counts them
  *   hier_x2_tail      0; 1: k_hier_x2 (allred_peer_allreduce_pipelined2) sums the owned tiles of
  *                     the middle bucket at the end of each launch instead of its start
+ *   lo_tree_min_tiles 64: a 64-rank rank-uniform LO plan (every RecDub schedule) takes the BO tree
+ *                     pass from this many 256-element tiles per rank, the register butterfly below
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

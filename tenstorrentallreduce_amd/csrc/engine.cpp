@@ -518,7 +518,10 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
             }
         }
     }
+    // rank-uniform LO = the BO tree pass; at 64 ranks below lo_tree_min_tiles tiles per rank
+    // (32 kB) the register butterfly is faster (2 kB: 2.9 vs 3.5 us, profiles/r02_sweep.jsonl)
     p->lo_tree = desc->variant == ALLRED_LO && n % (8 * (size_t)total) == 0 && tune(Tune::lo_tree) &&
+                 (total != 64 || n >= (uint64_t)tune(Tune::lo_tree_min_tiles) * 256) &&
                  lo_rank_uniform(p->sched, total);
     std::vector<uint8_t> order(&p->sched.tree_order[0][0],
                                &p->sched.tree_order[0][0] + ALLRED_MAX_NODES * ALLRED_MAX_NODES);

@@ -35,6 +35,7 @@ const Key kKeys[] = {
     {"check", 0, 0, 1},               // N > 1 programs: verify against the partners', poison receive regions
     {"fused_chunk_tiles", 1280, 0, 1ll << 40},   // persistent fused passes: tiles per launch (0: one launch)
     {"hier_x2_tail", 0, 0, 1},        // k_hier_x2: owned sums at the end of the launch instead of its start
+    {"lo_tree_min_tiles", 64, 0, 1ll << 40},   // 64-rank rank-uniform LO: tree pass from this many 256-element tiles
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

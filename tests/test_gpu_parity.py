@@ -276,22 +276,36 @@ def test_fused_lo_register_dag(algo, grid, n, pad):
 
 @pytest.mark.parametrize("lo_tree", [1, 0])
 @pytest.mark.parametrize("algo,grid,n", [
-    (t.RECDUB, (8, 64), 327680), (t.RECDUB, (8, 64), 1024 * 16), (t.RECDUB, (4, 16), 1024 * 64),
+    (t.RECDUB, (8, 64), 327680), (t.RECDUB, (8, 64), 1024 * 16), (t.RECDUB, (8, 64), 1024 * 2),
+    (t.RECDUB, (4, 16), 1024 * 64),
     (t.RECDUB, (2, 4), 1024), (t.SWING, (4, 16), 1024 * 64), (t.SWING, (2, 4), 1024),
     (t.RECDUB_1D, (8, 64), 1024 * 64), (t.SWING_1D, (2, 4), 1024 * 8)])
 def test_fused_lo_rank_uniform_tree_route(algo, grid, n, lo_tree):
     """Schedules whose LO trees are all the same up to child swaps (every RecDub,
     Swing up to 16 ranks) run the fused LO as the BO tree pass (engine.cpp
-    lo_rank_uniform); tune lo_tree=0 keeps the butterfly.  Both against the
-    oracle's butterfly, bit-exact."""
+    lo_rank_uniform); tune lo_tree=0 keeps the butterfly, lo_tree_min_tiles=0
+    takes the tree route at every size (by default 64-rank buckets below 64
+    tiles keep the butterfly).  Both against the oracle's butterfly, bit-exact."""
     side, total = grid
     ranks = rand_ranks(total, n, seed=29 + total + algo)
-    with t.tuned(lo_tree=lo_tree):
+    with t.tuned(lo_tree=lo_tree, lo_tree_min_tiles=0 if lo_tree else 64):
         got = run_plan(algo, t.LO, side, total, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
     want = [r.copy() for r in ranks]
     oracle.allreduce("lo", algo, side, want, total)
     assert (got == np.stack(want)).all()
     assert (got == got[0]).all()
+
+
+@pytest.mark.parametrize("n", [1024, 1024 * 8, 1024 * 64])
+def test_fused_lo_recdub_default_route(n):
+    """64-rank RecDub LO with the default lo_tree_min_tiles (64): the register
+    butterfly below 32 kB per rank, the tree pass from there; bit-exact vs the
+    oracle either way."""
+    ranks = rand_ranks(64, n, seed=41)
+    got = run_plan(t.RECDUB, t.LO, 8, 64, ranks, t.EXEC_FUSED, stride=t.preferred_rank_stride(n))
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("lo", t.RECDUB, 8, want, 64)
+    assert (got == np.stack(want)).all()
 
 
 def test_config1_known_answer():

@@ -5,7 +5,10 @@ The reference's timing_taker.py sweep (python/timing_taker.py:121-126):
   BO / mem sizes 1..5 tiles per block (128 kB .. 640 kB per rank)
 on the 8x8 grid, every variant in both execution forms (schedule steps /
 fused).  One JSON line per point: us per allreduce (median of rounds), GB/s
-of rank bytes, HBM GB/s of the form's algorithmic traffic.
+of rank bytes, HBM GB/s of the form's algorithmic traffic.  From 128 kB per
+rank the rotating bucket sets total >= 1 GiB (cold HBM); below, 4 warm sets
+(the latency regime).  The timed launches are queued behind a spin kernel, so
+small buckets measure back-to-back GPU time, not the host's launch rate.
 """
 import json
 import os
@@ -19,12 +22,14 @@ import torch  # noqa: E402
 import tenstorrentallreduce_amd as t  # noqa: E402
 
 SIDE, RANKS = 8, 64
+SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))
 
 
-def alg_bytes(variant, exec_mode, n, steps=6):
+def alg_bytes(variant, exec_mode, n, launches, steps=6):
     P, b = RANKS, 2
-    if exec_mode == t.EXEC_FUSED:
-        return 2 * P * n * b
+    if exec_mode == t.EXEC_FUSED or (variant != t.MEM and launches == 1):
+        return 2 * P * n * b   # one HBM pass (the round-2 schedule form reads and writes every rank row once)
+    # round 1's one launch per step (allred_tune_set("steps_form", 1))
     if variant == t.BO:  # RS: 3 x (P * n/2^(k+1)) per step; AG: 2 x same
         return sum(5 * P * (n >> (k + 1)) * b for k in range(steps))
     if variant == t.LO:
@@ -35,7 +40,11 @@ def alg_bytes(variant, exec_mode, n, steps=6):
 def time_plan(variant, algo, exec_mode, n, reps, rounds=5):
     dev = torch.device("cuda:0")
     stride = t.preferred_rank_stride(n)
-    sets = 4
+    # bandwidth regime (>= 128 kB per rank): rotating sets of >= 1 GiB in all (cold HBM, the
+    # 256 MiB MALL cannot hold them); latency regime (smaller): 4 sets, warm as in a loop
+    # re-reducing one small bucket
+    set_bytes = RANKS * stride * 2
+    sets = 4 if n * 2 < (128 << 10) else max(4, -(-(1 << 30) // set_bytes))
     bufs = [torch.full((RANKS, stride), 0x3F80, dtype=torch.int16, device=dev) for _ in range(sets)]
     plan = t.Plan(algo, variant, SIDE, n, RANKS, exec_mode)
     ws = torch.empty(max(plan.workspace_bytes, 16), dtype=torch.uint8, device=dev)
@@ -45,6 +54,8 @@ def time_plan(variant, algo, exec_mode, n, reps, rounds=5):
     for _ in range(rounds):
         for i in range(3):
             plan.execute(bufs[i % sets].data_ptr(), stride, ws.data_ptr(), st)
+        with torch.cuda.stream(st):   # the GPU busy while the host queues the reps: GPU time, not launch rate
+            torch.cuda._sleep(SPIN)
         e0.record(st)
         for i in range(reps):
             plan.execute(bufs[i % sets].data_ptr(), stride, ws.data_ptr(), st)
@@ -72,7 +83,7 @@ def main():
             for exec_mode in (t.EXEC_STEPS, t.EXEC_FUSED):
                 reps = 200 if n * RANKS * 2 < (64 << 20) else 50
                 us, launches = time_plan(variant, algo, exec_mode, n, reps)
-                ab = alg_bytes(variant, exec_mode, n)
+                ab = alg_bytes(variant, exec_mode, n, launches)
                 print(json.dumps({
                     "variant": names[variant], "algo": "swing" if algo == t.SWING else "recdub",
                     "exec": "fused" if exec_mode == t.EXEC_FUSED else "steps", "tiles_arg": tiles_arg,
