@@ -420,7 +420,7 @@ def roofline_xgmi(extras: dict, world: int) -> dict | None:
     GPU's egress = (p - 1) links x the MEASURED per-direction link rate
     (link_probe), with the spec rate (76.8 GB/s per direction) beside it."""
     arms = {k: v for k, v in extras.items() if "config4_swing_bo_1GiB_all_links" in k and isinstance(v, dict)
-            and "busbw_GBps" in v}
+            and "busbw_GBps" in v and not v.get("peer_timeout")}
     if not arms or world < 2:
         return None
     name = max(arms, key=lambda k: arms[k]["busbw_GBps"])
@@ -517,6 +517,9 @@ def xgmi_arm(out, comm, peer, world, dev, stream, side, total, name, algo, varia
     if peer is not None:
         ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
         out["peer_" + name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+        torch.cuda.synchronize()
+        if peer.status() & t.PEER_TIMEOUT:   # sticky: this arm (or an earlier one) timed out, the numbers are void
+            out["peer_" + name]["peer_timeout"] = True
         if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
             peer.set_lo_ll_max(0)
             ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)

@@ -415,8 +415,10 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * writes tile j-2).  (The specialised-wave form of round 1 lives in
  * tools/ubench/ws_trace.hip: 27-38 us vs 18 at W = 1, never a candidate.) */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
-/* Caps the grid of the hierarchical one-kernel forms at `groups` workgroups
- * (0 = default: 512, two per CU, the whole grid resident on a GPU of its own).
+/* Caps the grid of the hierarchical one-kernel forms, k_peer_mem_ll and the
+ * scheduled form (allred_peer_dist_allreduce) at `groups` workgroups (0 =
+ * default: 512 for the hierarchical forms, two per CU, 256 for the scheduled
+ * form; the whole grid resident on a GPU of its own).
  * Their workgroups wait for each other across processes, so when several
  * processes share one GPU (rehearsals) the sum of their grids must fit at once:
  * groups <= 512 / processes.  Same result bits at any cap. */

@@ -121,7 +121,8 @@ int launch_peer_allreduce(uint16_t* const* wins, uint32_t* const* flags, int nra
 int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epoch, uint32_t* status, void* stream);
 // the scheduled form: one launch; flag values base_epoch + 1 .. base_epoch + 2S + 1
 int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
-                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, void* stream);
+                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, unsigned max_groups,
+                      void* stream);
 // hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast.
 // wins[q] = GPU q's window for this parity ([partial n][result n]); hflags[q]: [tiles][nranks + 1]
 int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,

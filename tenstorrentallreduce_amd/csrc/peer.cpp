@@ -388,7 +388,7 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
             if (st != ALLRED_OK) return st;
         }
         st = launch_peer_sched(wins, p->peer_flags, p->rank, bucket, prog, p->max_elems / 2 / 8, p->seq, p->status,
-                               stream);
+                               p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         p->seq += 2u * (uint32_t)prog.S + 2u;
         ++p->calls;

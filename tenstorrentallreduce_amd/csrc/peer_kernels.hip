@@ -1226,7 +1226,7 @@ int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epo
 }
 
 int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
-                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, void* stream) {
+                      uint64_t half_vec, uint32_t base_epoch, uint32_t* status, unsigned max_groups, void* stream) {
     if (!aligned16(bucket) || prog.N > ALLRED_MAX_NODES || prog.C < 1 || prog.C > kPeerMaxChannels ||
         prog.S > kPeerMaxSteps)
         return ALLRED_ERR_ARG;
@@ -1241,7 +1241,10 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
         if (u > per) per = u;
     }
     uint64_t gc = (per + kBlock - 1) / kBlock;
-    const uint64_t gmax = kPeerSchedMaxGroups / prog.C;
+    // workgroup g waits for workgroup g of its partners: every GPU's grid must be resident
+    // at once (max_groups < kPeerSchedMaxGroups when processes share one GPU)
+    const uint64_t cap = max_groups && max_groups < kPeerSchedMaxGroups ? max_groups : kPeerSchedMaxGroups;
+    const uint64_t gmax = cap / prog.C > 0 ? cap / prog.C : 1;
     if (gc > gmax) gc = gmax;
     if (gc < 1) gc = 1;
     hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
