@@ -674,24 +674,31 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         // a wave holds owned and other tiles, and a poll spinning ahead of the wave's
         // own pushes could wait (circularly) for a GPU whose wave waits for those pushes
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (!own && b < nb) val = ll_get(my_ll + box_words + t * 128 + c, epoch, status);
-        if (b < nb) xs[b * 32 + c] = val;
+        // the other GPUs' results: polls issued now, taken after the owned tiles' rows
+        // have gone out (their xGMI round trip overlaps those stores)
+        uint64_t wb[4];
+        if (!own && b < nb) ll_load(my_ll + box_words + t * 128 + c, wb);
+        if (own) xs[b * 32 + c] = val;
         __syncthreads();
-        uint4 res[BB];
+        auto store_batch = [&](bool owned) {   // the rows of the batch's owned / other tiles
 #pragma unroll
-        for (int bb = 0; bb < BB; ++bb)
-            if (bb < nb) res[bb] = xs[bb * 32 + c];
-        __syncthreads();   // xs is reused by the next batch
+            for (int bb = 0; bb < BB; ++bb) {
+                if (bb >= nb) break;
+                if ((owner_of(tile_of(j0 + bb)) == me) != owned) continue;
+                const uint4 rv = xs[bb * 32 + c];
+                const uint64_t v0 = tile_of(j0 + bb) * TV;
 #pragma unroll
-        for (int bb = 0; bb < BB; ++bb) {
-            if (bb >= nb) break;
-            const uint64_t v0 = tile_of(j0 + bb) * TV;
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                const int r = RPW * w + 2 * k + h;
-                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res[bb]);
+                for (int k = 0; k < OPS; ++k) {
+                    const int r = RPW * w + 2 * k + h;
+                    st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, rv);
+                }
             }
-        }
+        };
+        store_batch(true);
+        if (!own && b < nb) xs[b * 32 + c] = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + t * 128 + c, epoch, status);
+        __syncthreads();
+        store_batch(false);
+        __syncthreads();   // xs is reused by the next batch
     }
 }
 
