@@ -607,19 +607,38 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    // The workgroup's tiles are blockIdx.x + kG (tile_of, also the R / B batches of 8,
+    // identical on every GPU: B of batch i waits only for R of batch i of the owners).
+    // A reduces them in a different order (tile_a): within each batch of 8, the tiles
+    // other GPUs own first, its own tiles last — the owned ones form the run
+    // k0 <= k < k1.  Every GPU reduces the tiles it does not own first, so an owner
+    // finds the remote partials of its tiles already arrived, and the result leaves
+    // after one xGMI trip (natural order: remote partials of the last tiles arrive one
+    // trip after the owner's own, then the result needs a second).  At W = 1 nothing moves.
+    auto tile_of = [&](int k) { return blockIdx.x + (uint64_t)k * G; };
+    auto count_below = [&](uint64_t t0) {   // the workgroup's tiles below tile index t0
+        return t0 <= blockIdx.x ? 0 : (int)min((uint64_t)mine, (t0 - blockIdx.x + G - 1) / G);
+    };
+    const int k0 = count_below((uint64_t)me * tiles_per_owner), k1 = count_below((uint64_t)(me + 1) * tiles_per_owner);
+    auto tile_a = [&](int j) {
+        const int lo = j & ~7, hi = lo + 8 < mine ? lo + 8 : mine;
+        const int a0 = k0 < lo ? lo : (k0 > hi ? hi : k0), a1 = k1 < lo ? lo : (k1 > hi ? hi : k1);
+        const int p = j - lo, below = a0 - lo, above = hi - a1;
+        const int k = p < below ? lo + p : (p < below + above ? a1 + (p - below) : a0 + (p - below - above));
+        return tile_of(k);
+    };
     auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
     uint64_t* const my_ll = lp.ll[me];
     // ---- A: local trees, partials pushed to their owners
-    if (mine > 0) issue(tile_of(0), 0);
+    if (mine > 0) issue(tile_a(0), 0);
     for (int j = 0; j < mine; ++j) {
         // in flight after tile j's loads: wave 0's four LL stores of tile j-1
         // (wave-uniform branch: vmcnt is per wave)
         if (j > 0 && w == 0) wait_vm<4>(); else wait_vm<0>();
         lds_barrier();
-        if (j + 1 < mine) issue(tile_of(j + 1), (j + 1) & 1);
+        if (j + 1 < mine) issue(tile_a(j + 1), (j + 1) & 1);
         const uint4* tile = buf[j & 1];
-        const uint64_t t = tile_of(j);
+        const uint64_t t = tile_a(j);
         const uint8_t* ord = ord_lds + RPW * w + LPL * h;
         uint4 x[LPL];
 #pragma unroll
