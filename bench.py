@@ -553,11 +553,6 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             if comm is not None:
                 comm.close()
             comm, comm_err = None, comm_err or "failed on another rank"
-    note(rank, f"world {world}, device {dev_index}: opening peer windows")
-    peer, peer_err = open_peer(rank, world, dev_index, (1 << 30) // 2)   # windows for 1 GiB buckets
-    note(rank, f"peer windows: {'ok' if peer is not None else peer_err}")
-    if peer is not None and args.share_gpu:
-        peer.set_max_groups(512 // world)   # every rank's one-kernel grid resident at once
     stream = torch.cuda.Stream(device=dev)
     desc = t.dist_desc(t.SWING, t.BO, side, total, ELEMS, local_ranks=RANKS, local_side=SIDE, local_algo=t.SWING)
     # rotating bucket sets as at N = 1 (every step streams its 64 ranks from HBM)
@@ -568,6 +563,69 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     torch.cuda.synchronize()
     ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)
     partial = torch.empty(ELEMS, dtype=torch.int16, device=dev)
+    t_start = time.perf_counter()
+
+    def timed_steps(step_fn, after=None):   # the K steps behind a spin kernel, max over ranks (ms per step)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(200000)
+        e0.record(stream)
+        for i in range(args.steps):
+            step_fn(i)
+        if after is not None:
+            after()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
+        dist.all_reduce(ms, op=dist.ReduceOp.MAX)
+        return ms.item() / args.steps
+
+    def local_phases_ms():   # tree reduce of the 64 ranks + broadcast: the HBM kernels alone
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(args.steps):
+            b = bufs[i % len(bufs)]
+            t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, partial.data_ptr(), stream)
+            t.broadcast(b.data_ptr(), ELEMS, ELEMS, RANKS, partial.data_ptr(), stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / args.steps
+
+    # A measured RCCL line before the peer windows are touched: if opening, verifying
+    # or timing them hangs on an untried machine (the peer waits are bounded, an IPC
+    # open is not), rank 0 prints this line after --peer-timeout s and every rank
+    # leaves, so the driver still gets its one JSON line.
+    peer_guard = None
+    if comm is not None:
+        note(rank, "fallback headline over RCCL")
+        for i in range(args.warmup):
+            t.dist_allreduce(comm, desc, bufs[i % len(bufs)].data_ptr(), ws.data_ptr(), stream)
+        fb_ms = timed_steps(lambda i: t.dist_allreduce(comm, desc, bufs[i % len(bufs)].data_ptr(), ws.data_ptr(),
+                                                       stream))
+        fb_local = local_phases_ms()
+
+        def peer_give_up():
+            if rank == 0:
+                emit(multi_line(args, world, "rccl", fb_ms, fb_local, time.perf_counter() - t_start,
+                                {"headline_transport": "rccl", "peer_error":
+                                 f"peer setup / verification / timing did not finish within {args.peer_timeout:g} s"}))
+            os._exit(0)
+
+        peer_guard = threading.Timer(args.peer_timeout + (0 if rank == 0 else 10), peer_give_up)
+        peer_guard.daemon = True
+        peer_guard.start()
+    note(rank, f"world {world}, device {dev_index}: opening peer windows")
+    peer, peer_err = open_peer(rank, world, dev_index, (1 << 30) // 2)   # windows for 1 GiB buckets
+    note(rank, f"peer windows: {'ok' if peer is not None else peer_err}")
+    if peer is not None and args.share_gpu:
+        peer.set_max_groups(512 // world)   # every rank's one-kernel grid resident at once
 
     # Inter-GPU transport, three candidates for the hierarchical step:
     #   rccl        tree -> 2D Swing BO over RCCL -> broadcast (3 launches + RCCL groups)
@@ -700,25 +758,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     for i in range(args.warmup):
         step(i)
     flush()
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    with torch.cuda.stream(stream):
-        torch.cuda._sleep(200000)   # GPU busy while the host submits the steps (as at N = 1)
-    e0.record(stream)
-    for i in range(args.steps):
-        step(i)
-    flush()   # peer_hier_x / _x2: the finishing launch is part of the K steps' time
-    e1.record(stream)
-    torch.cuda.synchronize()
-    dist.barrier()
+    # peer_hier_x / _x2: the finishing launch is part of the K steps' time
+    ms_per_step = timed_steps(step, after=flush)
     wall = time.perf_counter() - t0
-    ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
-    dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-    ms_per_step = ms.item() / args.steps
     peer_timeout = False
     if transport != "rccl" and peer is not None:
         # a timed-out peer wait means wrong bytes: such a number is never the headline
@@ -732,32 +775,14 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             transport = "rccl"
             for i in range(args.warmup):
                 step(i)
-            torch.cuda.synchronize()
-            dist.barrier()
-            e0.record(stream)
-            for i in range(args.steps):
-                step(i)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            dist.barrier()
-            ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
-            dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-            ms_per_step = ms.item() / args.steps
+            ms_per_step = timed_steps(step)
     if peer is not None:   # defaults again for the extras below
         peer.set_oneshot_max(4 << 20)
         peer.set_hier_ll(0)
         mode[0] = None
-
-    # local phases alone (tree reduce of 64 ranks + broadcast): the HBM kernels
-    torch.cuda.synchronize()
-    e0.record(stream)
-    for i in range(args.steps):
-        b = bufs[i % len(bufs)]
-        t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, partial.data_ptr(), stream)
-        t.broadcast(b.data_ptr(), ELEMS, ELEMS, RANKS, partial.data_ptr(), stream)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    local_ms = e0.elapsed_time(e1) / args.steps
+    local_ms = local_phases_ms()
+    if peer_guard is not None:   # the headline is measured: the extras have their own watchdog
+        peer_guard.cancel()
 
     extras = {"headline_transport": transport, "peer_verified": verify, "transport_quick_ms": quick,
               "peer_timeout_in_timed_loop": peer_timeout}
@@ -892,6 +917,8 @@ def main():
                     help="N = 1: back-to-back replays of the K timed steps; ms_per_step = median replay / K")
     ap.add_argument("--no-cpu-baseline", dest="cpu", action="store_false")
     ap.add_argument("--no-extras", dest="extras", action="store_false")
+    ap.add_argument("--peer-timeout", type=float, default=240.0,
+                    help="N > 1: seconds the peer-window phase may take before the RCCL-measured line is printed")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the extras may take before the headline line is printed without them")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
