@@ -618,7 +618,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                                  f"peer setup / verification / timing did not finish within {args.peer_timeout:g} s"}))
             os._exit(0)
 
-        peer_guard = threading.Timer(args.peer_timeout + (0 if rank == 0 else 10), peer_give_up)
+        # every rank's timer started after the same barrier: all leave together (no rank is left
+        # to fail in a collective of a rank that is gone)
+        peer_guard = threading.Timer(args.peer_timeout, peer_give_up)
         peer_guard.daemon = True
         peer_guard.start()
     note(rank, f"world {world}, device {dev_index}: opening peer windows")
