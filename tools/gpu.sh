@@ -13,6 +13,8 @@
 #   pmc_lo               PMC traffic of the fused LO pass, rocprofv3 stats of the schedule forms
 #   share <n>            the N > 1 bench path rehearsed with n ranks on the one GPU
 #                        (bench.py --share-gpu: peer transports, no RCCL; numbers mean nothing)
+#   hier [steps rounds]  tools/hier_step.py: the hierarchical step's forms on one GPU (W = 1)
+#   sweep                tools/sweep.py: every variant and form over the reference's size sweep
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
@@ -116,8 +118,20 @@ share)
     cat gpurun_out/share_n$n.json
     exit $rc
     ;;
+hier)
+    timeout -k 10 300 python tools/hier_step.py ${1:-100} ${2:-3} > gpurun_out/hier_step.json 2> gpurun_out/hier_step.err
+    rc=$?
+    cat gpurun_out/hier_step.json
+    exit $rc
+    ;;
+sweep)
+    timeout -k 10 500 python -u tools/sweep.py > gpurun_out/sweep.jsonl 2> gpurun_out/sweep.err
+    rc=$?
+    tail -2 gpurun_out/sweep.err
+    exit $rc
+    ;;
 *)
-    echo "usage: $0 test|smoke|bench|prof|share" >&2
+    echo "usage: $0 test|smoke|bench|prof|ab|skew|pmc_lo|share|hier|sweep" >&2
     exit 2
     ;;
 esac
