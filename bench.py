@@ -629,7 +629,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     if peer is not None and args.share_gpu:
         peer.set_max_groups(512 // world)   # every rank's one-kernel grid resident at once
 
-    # Inter-GPU transport, three candidates for the hierarchical step:
+    # Inter-GPU transport: the candidates for the hierarchical step
     #   rccl        tree -> 2D Swing BO over RCCL -> broadcast (3 launches + RCCL groups)
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
