@@ -480,6 +480,8 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
             ("config4_swing_bo_1GiB_one_link", t.SWING, t.BO, 1 << 30, 2, 1, 1),
             ("swing_bo_256MiB_all_links", t.SWING, t.BO, 256 << 20, 5, 0, 1),
             ("config3_recdub_bo_640kB", t.RECDUB, t.BO, ELEMS * 2, 50, 0, 1),
+            # the same bucket spread over every link (link-spreading channels; auto uses one below 1 MiB)
+            ("config3_recdub_bo_640kB_all_links", t.RECDUB, t.BO, ELEMS * 2, 50, world - 1, 1),
             ("hierarchical_all_links", t.SWING, t.BO, ELEMS * 2, 50, world - 1, RANKS),
             ("hierarchical_lo_partial", t.SWING, t.LO, ELEMS * 2, 50, 1, RANKS)]
     # BASELINE config 5: flat 2D Swing LO, 2 kB .. 128 kB per GPU (latency regime)
