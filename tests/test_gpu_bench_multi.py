@@ -1,0 +1,47 @@
+"""The N > 1 bench path end to end on one GPU: bench.py under torchrun with two
+ranks sharing cuda:0 (--share-gpu: peer transports only, RCCL refuses two ranks
+on one device).  Checks the driver's contract on the line rank 0 prints — one
+JSON line, the BASELINE metric, n_gpus, the weak-scaling value from its own
+ms_per_step, a transport that was verified on this machine, no peer timeout —
+not the numbers (a shared GPU measures nothing).  The 8-GPU run is the
+driver's; this keeps the code path it takes exercised on every GPU run."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_bench_two_ranks_share_gpu():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--share-gpu", "--steps", "10", "--warmup", "2", "--no-extras"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["metric"] == bench.METRIC and d["n_gpus"] == 2 and d["steps"] == 10 and d["scaling"] == "weak"
+    world_bytes = 2 * bench.RANKS * bench.ELEMS * 2
+    assert d["value"] == pytest.approx(world_bytes / (d["ms_per_step"] * 1e-3) / 1e9, rel=1e-3)
+    x = d["xgmi"]
+    transport = d["config"]["transport"]
+    assert transport == x["headline_transport"]
+    assert transport == "peer_launches" or x["peer_verified"].get(transport) is True
+    assert x["peer_timeout_in_timed_loop"] is False and x["peer_status"] & 1 == 0
+    assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
