@@ -567,5 +567,15 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             peer.allreduce_pipelined2(None, n, s)
         torch.cuda.synchronize()
         assert (x.cpu().numpy().view(np.uint16) == want[0][None, :]).all()
+        # one-launch calls right after a sequence (LL parities and epochs continue)
+        peer.set_hier_ll(1)
+        ys = [data[i % buckets].clone() for i in range(3)]
+        ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
+        for y in ys:
+            peer.allreduce(y.data_ptr(), n, s, local, 8, t.SWING, ws.data_ptr())
+        torch.cuda.synchronize()
+        for i, y in enumerate(ys):
+            assert (y.cpu().numpy().view(np.uint16) == want[i % buckets][None, :]).all(), i
+        assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.close()
