@@ -909,8 +909,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     lds_barrier();   // order bytes and results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
-            // after L(j): S(j-2)'s last op, wave 0's partial push of tile j-1 (uncached stores whose
-            // acknowledgement is slow: waiting for them would stall wave 0 and the barrier), L(j+1), S(j-1)
+            // after L(j): S(j-2)'s last op, wave 0's partial push of tile j-1, L(j+1), S(j-1)
             wait_any((j >= 2 && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && prev ? OPS : 0) +
                      (w == 0 && j >= 1 ? 4 : 0));
             lds_barrier();   // tile j is in LDS
