@@ -534,6 +534,12 @@ __device__ __forceinline__ void ll_put(uint64_t* dst, uint4 v, uint32_t e) {
     __hip_atomic_store(dst + 3 * kLLGroup, hi | v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// word k of an LL slot (the four waves of a workgroup push one word each)
+__device__ __forceinline__ void ll_put_word(uint64_t* dst, uint4 v, uint32_t e, int k) {
+    const uint32_t d = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+    __hip_atomic_store(dst + k * kLLGroup, ((uint64_t)e << 32) | d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // poll 4 LL words until all carry epoch e (bounded: status bit 0 on timeout)
 __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_t* status) {
     uint64_t w0, w1, w2, w3;
@@ -632,9 +638,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     // ---- A: local trees, partials pushed to their owners
     if (mine > 0) issue(tile_a(0), 0);
     for (int j = 0; j < mine; ++j) {
-        // in flight after tile j's loads: wave 0's four LL stores of tile j-1
-        // (wave-uniform branch: vmcnt is per wave)
-        if (j > 0 && w == 0) wait_vm<4>(); else wait_vm<0>();
+        // in flight after tile j's loads: this wave's LL store of tile j-1
+        if (j > 0) wait_vm<1>(); else wait_vm<0>();
         lds_barrier();
         if (j + 1 < mine) issue(tile_a(j + 1), (j + 1) & 1);
         const uint4* tile = buf[j & 1];
@@ -650,10 +655,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
         if (h == 0) part[w * TV + c] = pw;
         lds_barrier();
-        if (w == 0 && h == 0) {
+        if (h == 0) {   // the partial -> its owner's inbox, wave w writing word w
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-            ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, res, epoch);
+            ll_put_word(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, res, epoch, w);
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
@@ -909,9 +914,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     lds_barrier();   // order bytes and results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
-            // after L(j): S(j-2)'s last op, wave 0's partial push of tile j-1, L(j+1), S(j-1)
+            // after L(j): S(j-2)'s last op, this wave's partial word of tile j-1, L(j+1), S(j-1)
             wait_any((j >= 2 && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && prev ? OPS : 0) +
-                     (w == 0 && j >= 1 ? 4 : 0));
+                     (j >= 1 ? 1 : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -925,12 +930,12 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            if (w == 0 && q == 0) {
+            if (q == 0) {   // the partial -> its owner's inbox, wave w writing word w
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
-                ll_put(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur);
+                ll_put_word(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur, w);
             }
         }
         // ---- cur's tile j+2 in, prev's tile j out, interleaved op by op
@@ -1065,10 +1070,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
-            // after L(j): S(j-2)'s last op, wave 0's partial push of tile j-1, L(j+1), S(j-1),
+            // after L(j): S(j-2)'s last op, this wave's partial word of tile j-1, L(j+1), S(j-1),
             // this wave's owned-sum pushes (j < 2)
             wait_any((j >= 2 && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && old ? OPS : 0) +
-                     (w == 0 && j >= 1 ? 4 : 0) + (j < 2 ? pushed : 0));
+                     (j >= 1 ? 1 : 0) + (j < 2 ? pushed : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -1082,12 +1087,12 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            if (w == 0 && q == 0) {
+            if (q == 0) {   // the partial -> its owner's inbox, wave w writing word w
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
-                ll_put(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur);
+                ll_put_word(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur, w);
             }
         }
         // ---- cur's tile j+2 in, old's tile j out, interleaved op by op
