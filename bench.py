@@ -743,10 +743,14 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 candidates.append(kind)
         del small, ref
     quick = {}
+    # each candidate timed the way the headline is: K steps with the pipelined forms'
+    # finishing launch inside (it weighs 1/K per step), median of three
+    qk = max(args.steps, 10)
     for kind in candidates:
         note(rank, f"quick timing: {kind}")
         it = iter(range(1 << 30))
-        quick[kind] = round(timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), 50, stream, after=flush), 4)
+        quick[kind] = round(statistics.median(
+            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush) for _ in range(3)), 4)
     transport = min(candidates, key=lambda k: quick[k])
 
     def step(i):
