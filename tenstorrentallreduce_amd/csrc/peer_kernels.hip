@@ -666,8 +666,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     // ---- R + B, 8 tiles at a time; lane (jr, c) serves tile jr of the batch, column c.
     // R: for a tile I own, the W partials of its column are polled from my inbox
     // (all in flight at once), summed and pushed to every OTHER GPU's box; the
-    // result stays in the lane.  B: every other tile's result is polled from my
-    // box, then the batch's 64 rank rows are written.  One poll round trip per
+    // result stays in the lane.  B: the owned tiles' 64 rank rows are written while
+    // every other tile's result is polled from my box, then those tiles' rows.  One poll round trip per
     // batch for the owned tiles and one for the others; at W = 1 every tile is
     // owned and B polls nothing.  B(batch k) waits only for R(batch k) of the
     // owners (the same workgroup index there), which waits only for A.
