@@ -258,8 +258,9 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_pipe(uint16_t* __restrict__
 // stores thus always queue behind the next tile's loads and a wave never
 // waits for a store before a load.  Issue order per wave: L0 L1 | L2 | L3 S0 |
 // L4 S1 | ..., so after tile j's loads come tile j+1's loads and the stores of
-// tiles j-2 and j-3.  The first two tiles' loads go out before the 4 KiB tree
-// order table is staged.  Measured arms (the table first, an LDS-counter
+// tiles j-2 and j-3.  The 4 KiB tree order table's load goes out first, then
+// the first two tiles' loads, and only the table's load is waited for before
+// it is staged into LDS.  Measured arms (the table first, an LDS-counter
 // barrier, 2 / 8 waves, 1 KiB rows, other interleave orders) and their
 // numbers: DESIGN.md §4, tools/ubench/fused_ab.hip.
 // ---------------------------------------------------------------------------
@@ -286,11 +287,17 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     auto tile_of = [&](int j) { return t0 + blockIdx.x + (uint64_t)j * G; };   // tiles t0 .. t0 + ntiles - 1
+    // the 4 KiB order table (16 bytes per thread) is loaded ahead of the first two tiles
+    // and waited for exactly, so tile 0's tree waits for tile 0 only, not for tile 1 too
+    // (a compiler-issued load would be followed by vmcnt(0): it cannot see the LDS-DMA ops)
+    static_assert(P * ALLRED_MAX_NODES == 16 * 64 * NW, "one 16-byte load per thread");
+    u32x4 ov;
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ov) : "v"(reinterpret_cast<const uint4*>(order) + threadIdx.x) : "memory");
     if (mine > 0) issue(tile_of(0), 0);
     if (mine > 1) issue(tile_of(1), 1);
-    for (int i = threadIdx.x; i < P * ALLRED_MAX_NODES / 16; i += 64 * NW)
-        reinterpret_cast<uint4*>(ord_lds)[i] = reinterpret_cast<const uint4*>(order)[i];
-    __syncthreads();
+    if (mine > 1) wait_vm<2 * OPS>(); else if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
+    reinterpret_cast<u32x4*>(ord_lds)[threadIdx.x] = ov;
+    lds_barrier();
     uint4 prev = make_uint4(0, 0, 0, 0);
     for (int j = 0; j < mine; ++j) {
         // after L(j): the last op of S(j-3) (interleaved with L(j)), L(j+1), S(j-2)
