@@ -296,6 +296,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
     if (mine > 0) issue(tile_of(0), 0);
     if (mine > 1) issue(tile_of(1), 1);
     if (mine > 1) wait_vm<2 * OPS>(); else if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
+    asm volatile("" : "+v"(ov));   // no use of ov may move above the wait
     reinterpret_cast<u32x4*>(ord_lds)[threadIdx.x] = ov;
     lds_barrier();
     uint4 prev = make_uint4(0, 0, 0, 0);

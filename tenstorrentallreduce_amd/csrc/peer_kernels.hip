@@ -570,6 +570,16 @@ __device__ __forceinline__ uint4 ll_data(const uint64_t (&wd)[4]) {
     return make_uint4((uint32_t)wd[0], (uint32_t)wd[1], (uint32_t)wd[2], (uint32_t)wd[3]);
 }
 
+// the 64-byte tree order, one byte per lane of wave 0, loaded by inline asm: the
+// compiler would follow its own load with vmcnt(0) before staging it, so the
+// tiles' LDS-DMA loads (invisible to it) would wait behind the order's round
+// trip; here they go out right behind it and only the byte is waited for
+__device__ __forceinline__ uint32_t order_byte_load(const uint8_t* order, int lane) {
+    uint32_t b;
+    asm volatile("global_load_ubyte %0, %1, off" : "=v"(b) : "v"(order + lane) : "memory");
+    return b;
+}
+
 // the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
 // first then ascending, one rounding (allred_mem_2D semantics, k_peer_oneshot's bits)
 __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, int me) {
@@ -599,8 +609,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 31, h = lane >> 5;
-    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
-    __syncthreads();
+    uint32_t ob = 0;
+    if (w == 0) ob = order_byte_load(order, lane);
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
     auto issue = [&](uint64_t t, int b) {
@@ -622,10 +632,11 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     // after one xGMI trip (natural order: remote partials of the last tiles arrive one
     // trip after the owner's own, then the result needs a second).  At W = 1 nothing moves.
     auto tile_of = [&](int k) { return blockIdx.x + (uint64_t)k * G; };
-    auto count_below = [&](uint64_t t0) {   // the workgroup's tiles below tile index t0
-        return t0 <= blockIdx.x ? 0 : (int)min((uint64_t)mine, (t0 - blockIdx.x + G - 1) / G);
+    auto count_below = [&](uint32_t t0) {   // the workgroup's tiles below tile index t0 (32-bit: < 2^20 tiles)
+        return t0 <= blockIdx.x ? 0 : (int)min((uint32_t)mine, (t0 - blockIdx.x + (uint32_t)G - 1) / (uint32_t)G);
     };
-    const int k0 = count_below((uint64_t)me * tiles_per_owner), k1 = count_below((uint64_t)(me + 1) * tiles_per_owner);
+    const uint32_t tpo32 = (uint32_t)tiles_per_owner;
+    const int k0 = count_below((uint32_t)me * tpo32), k1 = count_below((uint32_t)(me + 1) * tpo32);
     auto tile_a = [&](int j) {
         const int lo = j & ~7, hi = lo + 8 < mine ? lo + 8 : mine;
         const int a0 = k0 < lo ? lo : (k0 > hi ? hi : k0), a1 = k1 < lo ? lo : (k1 > hi ? hi : k1);
@@ -637,6 +648,11 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     uint64_t* const my_ll = lp.ll[me];
     // ---- A: local trees, partials pushed to their owners
     if (mine > 0) issue(tile_a(0), 0);
+    if (w == 0) {   // the order byte (tile 0's loads may stay in flight); read after the loop's barrier
+        if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
+        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
+        ord_lds[lane] = (uint8_t)ob;
+    }
     for (int j = 0; j < mine; ++j) {
         // in flight after tile j's loads: this wave's LL store of tile j-1
         if (j > 0) wait_vm<1>(); else wait_vm<0>();
@@ -775,9 +791,14 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
         for (int k = 0; k < OPS; ++k)
             lds_dma16(reinterpret_cast<const uint4*>(row(k)) + t * TV + c, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
     };
-    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
-    wait_vm<0>();
+    uint32_t ob = 0;
+    if (w == 0) ob = order_byte_load(order, lane);
     if (mine > par) issue(tile_of(par), par);   // tile 0 by waves 0-1, tile 1 by waves 2-3
+    if (w == 0) {   // the order byte (tile 0's loads may stay in flight); read after the loop's barrier
+        if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
+        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
+        ord_lds[lane] = (uint8_t)ob;
+    }
     for (int j = 0; j < mine + 2; ++j) {
         const bool mp = par == (j & 1);   // this wave serves tile j's parity (wave-uniform)
         const bool own_r = j >= 1 && j - 1 < mine && owner_of(tile_of(j - 1)) == me;   // workgroup-uniform
@@ -897,10 +918,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
                       wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
     };
-    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
-    wait_vm<0>();   // the order bytes
+    uint32_t ob = 0;
+    if (w == 0) ob = order_byte_load(order, lane);
     if (cur && mine > 0) issue(tile_of(0), 0);
     if (cur && mine > 1) issue(tile_of(1), 1);
+    if (w == 0) {   // the order byte only (the tiles' loads stay in flight)
+        wait_any((cur && mine > 0 ? OPS : 0) + (cur && mine > 1 ? OPS : 0));
+        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
+        ord_lds[lane] = (uint8_t)ob;
+    }
     // ---- prev's results of this workgroup's tiles -> LDS: lane (j, c) (32 j + c)
     // serves tile j, column c.  The owners pushed them at the end of the previous
     // launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep HBM busy.
@@ -1033,10 +1059,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         for (int k = 0; k < OPS; ++k)
             st_nt(reinterpret_cast<uint4*>(dst + row_off + (uint64_t)(RPI * k) * stride) + tile_of(j) * TV + c, rv);
     };
-    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
-    wait_vm<0>();   // the order bytes
+    uint32_t ob = 0;
+    if (w == 0) ob = order_byte_load(order, lane);
     if (cur && mine > 0) issue(tile_of(0), 0);
     if (cur && mine > 1) issue(tile_of(1), 1);
+    if (w == 0) {   // the order byte only (the tiles' loads stay in flight)
+        wait_any((cur && mine > 0 ? OPS : 0) + (cur && mine > 1 ? OPS : 0));
+        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
+        ord_lds[lane] = (uint8_t)ob;
+    }
     // ---- lane (jr, c) (32 jr + c) serves tile jr of this workgroup, column c
     const int jr = threadIdx.x / TV;
     const bool act = jr < kHierXMaxTiles && jr < mine;
