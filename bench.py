@@ -9,13 +9,18 @@ A step is one allreduce of device-resident bf16 buckets:
          655,360 B (5 tiles per block) in one MI355X's HBM, executed as the
          one-pass fused HIP kernel (k_tree_lds_lag<64>, bit-exact with the
          12-step schedule).  32 rotating bucket sets (1.3 GB, 5x the 256 MiB Infinity
-         Cache) so every step streams from HBM; the K steps are replayed from
-         a captured HIP graph.
+         Cache) so every step streams from HBM; K < 100 steps are eager launches
+         behind a spin kernel, K >= 100 replays of a captured HIP graph
+         (DESIGN.md §6); ms_per_step = the median of 5 repetitions / K.
+         Beside it: the tile-sum (k_add) at 256 MiB and 1 GiB with its own roofline.
   N > 1  weak scaling: every GPU holds its own 64 x 640 kB ranks (same set
          rotation); on-GPU tree reduce -> 2D Swing BO between the N GPUs (grid
          (2,2), (2,4), (4,8)) over RCCL/xGMI or peer-mapped windows, or the
          one-kernel hierarchical form -> back to the 64 ranks; the transport
-         is the fastest one verified bit-exact on the machine running it.
+         is the fastest one verified on the machine running it (exact sums and
+         the reference's closed form, verify_transport), median of 3
+         repetitions; every xGMI arm (configs 3-5) is verified before it is
+         timed, and the CPU loopback of configs 3-5 is timed beside it.
 value = bytes of all ranks' buckets allreduced per second, whole job (GB/s, 1e9).
 Rank 0 prints ONE JSON line.  See DESIGN.md §Measurement for every field.
 """
@@ -119,6 +124,49 @@ def pmc_traffic(kernel: str):
         return e["hbm_bytes_per_launch"] if e.get("template") == kernel else None
     except Exception:
         return None
+
+
+def tilesum(stream, steps: int, reps: int) -> dict:
+    """The local tile-sum (north_star: >= 70 % of per-GPU HBM peak): dst += src
+    in bf16 through allred_bf16_add (k_add, the per-step add of
+    allred_BO_2D/kernels/compute_kernel.cpp:53-60 over a whole bucket) at 256 MiB
+    and 1 GiB.  Checked once against the torch fp32 reference of the same op
+    (fp32 add, RNE to bf16), then timed: R repetitions of K back-to-back adds,
+    median; algorithmic bytes 3 * n * 2 (two reads, one write) per launch."""
+    out = {}
+    for nbytes in (256 << 20, 1 << 30):
+        n = nbytes // 2
+        g = torch.Generator(device="cuda:0").manual_seed(nbytes & 0xFFFF)
+        dst = (torch.rand(n, generator=g, device="cuda:0") * 100).to(torch.bfloat16)
+        src = (torch.rand(n, generator=g, device="cuda:0") * 100).to(torch.bfloat16)
+        want = (dst.float() + src.float()).to(torch.bfloat16)
+        torch.cuda.synchronize()
+        t.bf16_add(dst.data_ptr(), src.data_ptr(), n, stream)
+        torch.cuda.synchronize()
+        ok = torch.equal(dst.view(torch.int16), want.view(torch.int16))
+        del want
+        k = max(5, min(steps, 50))
+        with torch.cuda.stream(stream):
+            for _ in range(3):
+                t.bf16_add(dst.data_ptr(), src.data_ptr(), n, stream)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+        torch.cuda.synchronize()
+        ev[0].record(stream)
+        for r in range(reps):
+            for _ in range(k):
+                t.bf16_add(dst.data_ptr(), src.data_ptr(), n, stream)
+            ev[r + 1].record(stream)
+        torch.cuda.synchronize()
+        ms = statistics.median(ev[r].elapsed_time(ev[r + 1]) for r in range(reps)) / k
+        alg = 3 * nbytes
+        ach = alg / (ms * 1e-3) / 1e9
+        out[f"{nbytes >> 20}MiB"] = {
+            "ms_per_add": round(ms, 5), "matches_torch_fp32": ok, "adds_per_repetition": k, "repetitions": reps,
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(f"k_add@{nbytes >> 20}MiB"),
+                         "kernel": "k_add", "algorithmic_bytes_per_launch": alg}}
+        del dst, src
+    return out
 
 
 def bench_single(args) -> dict:
@@ -285,6 +333,8 @@ def bench_single(args) -> dict:
                "us_per_allreduce": c1_us.get("graph", c1_us["eager"]), "us_eager_launches": c1_us["eager"],
                "known_answer_ok": c1_ok, "note": "back-to-back allreduces on one stream: launch-bound, no roofline"}
 
+    tsum = tilesum(stream, args.steps, reps)
+
     alg_bytes = 2 * RANKS * ELEMS * 2          # read every rank once, write every rank once
     achieved = alg_bytes / (ms_per_step * 1e-3) / 1e9
     out = {
@@ -316,6 +366,7 @@ def bench_single(args) -> dict:
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
         "host_staged": e2e,
         "config1": config1,
+        "tilesum": tsum,
         "prewarm_ms": round(prewarm_s * 1e3, 1),
         "host_wall_s": round(wall, 6),
     }
@@ -374,6 +425,114 @@ def agreed(ok: bool) -> bool:
     return bool(v.item())
 
 
+# ---------------------------------------------------------------- N > 1 verification
+# Every N > 1 transport is checked on the machine that times it, against values
+# that do not come from any transport (validate_result_vector's role,
+# allred_helper.cpp:18-120 / allred_helper.hpp:84-96):
+#   exact_sum    every global row (GPU g, local rank l) gets 0 / 1 bf16 values drawn
+#                from a hash of (seed, g * local + l, element) that every rank can
+#                evaluate for every row, so each rank computes the exact sum of all
+#                rows itself; counts stay <= 256, so every partial sum of every
+#                reduction order is exact in bf16 and every correct transport
+#                returns exactly that sum — a wrong, missing or doubled block shows.
+#   closed_form  the reference's own inputs (even-x rows src_1, odd-x rows src_0,
+#                allred_BO_2D.cpp:79-85), with the same a / b on every GPU.  On the
+#                XOR schedules of the GPU grids every level of every rank's tree
+#                combines two all-a / all-b / balanced groups, so the result is
+#                exactly RNE(a + b) * R / 2 for R rows (the reference's expected
+#                value, allred_helper.cpp:42-43, at error 0); mem_2D's fp32 sum
+#                with one rounding gives the same bits.
+MASK32 = 0xFFFFFFFF
+
+
+def _mix32(x: torch.Tensor) -> torch.Tensor:
+    """32-bit integer finaliser on int64 tensors (constants < 2^31: no product
+    leaves int64)"""
+    x = x ^ (x >> 16)
+    x = (x * 0x7FEB352D) & MASK32
+    x = x ^ (x >> 15)
+    x = (x * 0x2C1B3C6D) & MASK32
+    return x ^ (x >> 16)
+
+
+def exact_bits_(out: torch.Tensor, row: int, seed: int, chunk: int = 1 << 24) -> None:
+    """out (one row, int16 view of bf16) <- 1.0 with probability 1/4, else 0.0,
+    a function of (seed, global row id, element index) only"""
+    n = out.numel()
+    key = _mix32(torch.tensor([(row * 0x9E3779B1 + seed * 0x632BE5AB + 1) & MASK32], dtype=torch.int64))
+    key = key.to(out.device)
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        h = _mix32(torch.arange(s, e, dtype=torch.int64, device=out.device) ^ key)
+        out[s:e] = torch.where((h & 3) == 0, 0x3F80, 0).to(torch.int16)
+
+
+def exact_expected(rows: int, n: int, seed: int, dev) -> torch.Tensor:
+    """int16 view of bf16: the exact sum over global rows 0 .. rows-1"""
+    acc = torch.zeros(n, dtype=torch.int16, device=dev)
+    tmp = torch.empty(n, dtype=torch.int16, device=dev)
+    for r in range(rows):
+        exact_bits_(tmp, r, seed)
+        acc += (tmp != 0).to(torch.int16)
+    if int(acc.max()) > 256:   # bf16 holds every integer up to 256 (never hit: mean rows / 4)
+        raise RuntimeError("exact-sum inputs exceed 256 per element")
+    return acc.to(torch.float32).to(torch.bfloat16).view(torch.int16)
+
+
+def ref_pair(n: int, seed: int, dev):
+    """src_0 / src_1 of the reference convention, identical on every rank (same seed)"""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    a = (torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16)
+    b = (torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16)
+    return a, b
+
+
+def closed_form(a: torch.Tensor, b: torch.Tensor, rows: int) -> torch.Tensor:
+    """RNE(a + b) * rows / 2 (exact scaling by a power of two); one row: src_1 itself"""
+    if rows == 1:
+        return b.view(torch.int16)
+    return ((a.float() + b.float()).to(torch.bfloat16) * (rows // 2)).view(torch.int16)
+
+
+def verify_transport(run, buf: torch.Tensor, world: int, rank: int, local: int, local_side: int, side: int,
+                     seed: int, status=None) -> dict:
+    """run(buf) allreduces buf (local rows x n, in place) once; both checks, agreed
+    over ranks (MIN): {"exact_sum": bool, "closed_form": bool, "verified": bool}.
+    status(): nonzero when the transport itself reports a failure (peer timeout)."""
+    n = buf.shape[1]
+    rows = world * local
+    res = {}
+    for check in ("exact_sum", "closed_form"):
+        ok = True
+        try:
+            if check == "exact_sum":
+                for l in range(local):
+                    exact_bits_(buf[l], rank * local + l, seed)
+                want = exact_expected(rows, n, seed, buf.device)
+            else:
+                a, b = ref_pair(n, seed + 1, buf.device)
+                for l in range(local):   # x parity: the local grid's (hierarchical) or the GPU grid's (flat)
+                    x = (l % local_side) if local > 1 else (rank % side)
+                    buf[l].copy_((b if x % 2 == 0 else a).view(torch.int16))
+                want = closed_form(a, b, rows)
+                del a, b
+            if buf.is_cuda:
+                torch.cuda.synchronize(buf.device)
+            run(buf)
+            if buf.is_cuda:
+                torch.cuda.synchronize(buf.device)
+            ok = bool((buf == want[None, :]).all())
+            if status is not None and status():
+                ok = False
+            del want
+        except Exception as e:  # reported, never silently dropped: the check fails
+            print(f"[bench r{rank}] verify {check}: {e!r}", file=sys.stderr)
+            ok = False
+        res[check] = agreed(ok)
+    res["verified"] = res["exact_sum"] and res["closed_form"]
+    return res
+
+
 def open_peer(rank, world, local_rank, max_elems):
     """Peer windows (allred_peer_*), IPC handles exchanged over gloo.  Returns
     (peer, None) or (None, reason) — the same on every rank."""
@@ -410,28 +569,38 @@ def arm_stats(ms, nbytes, world, lo=False) -> dict:
     if lo:
         busbw = nbytes / sec / 1e9   # LO moves the whole bucket every step: report algbw
     return {"ms": round(ms, 4), "algbw_GBps": round(nbytes / sec / 1e9, 3), "busbw_GBps": round(busbw, 3),
-            "xgmi_frac": round(busbw / (max(1, world - 1) * XGMI_LINK_DIR_GBPS), 4)}
+            "xgmi_frac_spec": round(busbw / (max(1, world - 1) * XGMI_LINK_DIR_GBPS), 4)}
 
 
 def roofline_xgmi(extras: dict, world: int) -> dict | None:
     """The N > 1 xGMI roofline (north_star's >= 80 % target): the
     BASELINE config-4 arm (8-rank-grid Swing BO, 1 GiB of real bf16 per GPU, all
-    links), the faster of its RCCL and peer-window transports, busbw over the
-    GPU's egress = (p - 1) links x the MEASURED per-direction link rate
-    (link_probe), with the spec rate (76.8 GB/s per direction) beside it."""
+    links), the faster of its RCCL and peer-window transports among the arms
+    VERIFIED on this machine, busbw over the GPU's egress = (p - 1) links x the
+    MEASURED per-direction link rate (link_probe).  frac is null unless that
+    peak was measured and 0 < frac <= 1 (a shared-GPU rehearsal has no link to
+    measure: its numbers mean nothing); the spec-rate figure stays beside it."""
     arms = {k: v for k, v in extras.items() if "config4_swing_bo_1GiB_all_links" in k and isinstance(v, dict)
-            and "busbw_GBps" in v and not v.get("peer_timeout")}
-    if not arms or world < 2:
+            and "busbw_GBps" in v and v.get("verified") is True and not v.get("peer_timeout")}
+    if world < 2:
         return None
+    if not arms:
+        return {"bound": "xgmi", "achieved": None, "peak": None, "unit": "GB/s", "frac": None, "traffic": None,
+                "note": "no verified config-4 arm"}
     name = max(arms, key=lambda k: arms[k]["busbw_GBps"])
     bus = arms[name]["busbw_GBps"]
     probe = extras.get("link_probe", {})
     link = probe.get("GBps_per_direction") if isinstance(probe, dict) else None
     peak_spec = (world - 1) * XGMI_LINK_DIR_GBPS
-    peak = (world - 1) * link if link else peak_spec
-    return {"bound": "xgmi", "achieved": bus, "peak": round(peak, 2), "unit": "GB/s", "frac": round(bus / peak, 4),
-            "traffic": None, "arm": name, "bytes_per_gpu": 1 << 30, "links": world - 1,
-            "peak_source": "measured link_probe" if link else "spec (no RCCL link probe: --share-gpu)",
+    peak = (world - 1) * link if link else None
+    frac = bus / peak if peak else None
+    sane = frac is not None and 0 < frac <= 1
+    return {"bound": "xgmi", "achieved": bus, "peak": round(peak, 2) if peak else None, "unit": "GB/s",
+            "frac": round(frac, 4) if sane else None, "traffic": None, "arm": name, "bytes_per_gpu": 1 << 30,
+            "links": world - 1,
+            "peak_source": "measured link_probe (RCCL sendrecv, both directions at once)" if link
+                           else "not measured (no RCCL link probe: --share-gpu); frac null",
+            "frac_unbounded": round(frac, 4) if frac is not None and not sane else None,
             "peak_spec": peak_spec, "frac_spec": round(bus / peak_spec, 4),
             "achieved_def": "busbw = 2(p-1)/p * bytes_per_gpu / t"}
 
@@ -470,10 +639,11 @@ def link_probe(rank, world, dev) -> dict:
             "spec_GBps_per_direction": XGMI_LINK_DIR_GBPS, "pairs": "2i<->2i+1, both directions at once"}
 
 
-def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
+def xgmi_arms(comm, peer, world, rank, dev, stream, side, total) -> dict:
     """Flat / hierarchical inter-GPU allreduces (BASELINE configs 3-5 regimes),
     each through RCCL (allred_dist_allreduce) and through the peer windows
-    (allred_peer_dist_allreduce: same program, same bits, one kernel)."""
+    (allred_peer_dist_allreduce: same program, same bits, one kernel), each
+    verified on this machine before it is timed."""
     out = {}
     # BASELINE config 4: 8-rank Swing BO, 1 GiB per rank (all links = link-spreading channels; one link = plain)
     arms = [("config4_swing_bo_1GiB_all_links", t.SWING, t.BO, 1 << 30, 3, 0, 1),
@@ -494,7 +664,7 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
         # record it, agree, and go on with the next arm instead of losing the line
         err = None
         try:
-            xgmi_arm(out, comm, peer, world, dev, stream, side, total, *arm)
+            xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, *arm)
         except Exception as e:  # reported, never silently dropped
             err = repr(e)
         if not agreed(err is None):
@@ -503,36 +673,118 @@ def xgmi_arms(comm, peer, world, dev, stream, side, total) -> dict:
     return out
 
 
-def xgmi_arm(out, comm, peer, world, dev, stream, side, total, name, algo, variant, nbytes, reps, chans, local):
-    """One arm of xgmi_arms: its RCCL and peer-window timings into out."""
+def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo, variant, nbytes, reps, chans,
+             local):
+    """One arm of xgmi_arms: each transport verified (exact sums and the closed
+    form, verify_transport), then timed on real data (uniform [0,100) bf16 per
+    rank) into out[...] with its verdict beside the numbers."""
     n = nbytes // 2
     d2 = t.dist_desc(algo, variant, side, total, n, local_ranks=local, local_side=SIDE, local_algo=t.SWING,
                      channels=chans)
-    b2 = torch.empty((local, n), dtype=torch.int16, device=dev)   # real data: uniform [0,100) bf16
-    g = torch.Generator(device=dev).manual_seed(4000 + 17 * len(out) + torch.distributed.get_rank())
-    for r in range(local):
-        b2[r].copy_((torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16).view(torch.int16))
+    b2 = torch.empty((local, n), dtype=torch.int16, device=dev)
     w2 = torch.empty(max(16, t.dist_workspace_bytes(d2)), dtype=torch.uint8, device=dev)
+    seed = 5000 + 31 * len(out)
+
+    def timed(key, fn, lo, status=None):
+        v = verify_transport(fn, b2, world, rank, local, SIDE, side, seed, status=status)
+        g = torch.Generator(device=dev).manual_seed(4000 + 17 * len(out) + rank)
+        for r in range(local):   # real data for the timing
+            b2[r].copy_((torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16).view(torch.int16))
+        ms = timed_max(lambda: fn(b2), reps, stream)
+        out[key] = {**arm_stats(ms, nbytes, world, lo), "channels": chans, **v}
+
     if variant != t.MEM and comm is not None:
-        ms = timed_max(lambda: t.dist_allreduce(comm, d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-        out[name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+        timed(name, lambda b: t.dist_allreduce(comm, d2, b.data_ptr(), w2.data_ptr(), stream), variant == t.LO)
     if peer is not None:
-        ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-        out["peer_" + name] = {**arm_stats(ms, nbytes, world, variant == t.LO), "channels": chans}
+        def status():
+            return peer.status() & t.PEER_TIMEOUT
+
+        def peer_fn(b):
+            peer.dist_allreduce(d2, b.data_ptr(), w2.data_ptr(), stream)
+
+        timed("peer_" + name, peer_fn, variant == t.LO, status)
         torch.cuda.synchronize()
-        if peer.status() & t.PEER_TIMEOUT:   # sticky: this arm (or an earlier one) timed out, the numbers are void
+        if status():   # sticky: this arm (or an earlier one) timed out, the numbers are void
             out["peer_" + name]["peer_timeout"] = True
+            out["peer_" + name]["verified"] = False
         if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
             peer.set_lo_ll_max(0)
-            ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-            peer.set_lo_ll_max(256 << 10)
-            out["peer_sched_" + name] = {**arm_stats(ms, nbytes, world, True), "channels": chans}
+            try:
+                timed("peer_sched_" + name, peer_fn, True, status)
+            finally:
+                peer.set_lo_ll_max(256 << 10)
         if variant == t.MEM and nbytes <= (256 << 10):   # mem_2D without LL hand-offs (k_peer_oneshot)
             peer.set_mem_ll_max(0)
-            ms = timed_max(lambda: peer.dist_allreduce(d2, b2.data_ptr(), w2.data_ptr(), stream), reps, stream)
-            peer.set_mem_ll_max(256 << 10)
-            out["peer_oneshot_" + name] = {**arm_stats(ms, nbytes, world, False), "channels": chans}
+            try:
+                timed("peer_oneshot_" + name, peer_fn, False, status)
+            finally:
+                peer.set_mem_ll_max(256 << 10)
     del b2, w2
+
+
+def cpu_baseline_multi() -> dict:
+    """BASELINE configs 3, 4 and 5 in the oracle's loopback restatement (one forked
+    process per rank, shared-memory buffers, semaphore handshakes) on this host's
+    cores, 8 rank processes each (the 4x2 grid of the 8-GPU runs), as
+    python/timing_taker.py runs each config beside its device run; ~15-25 s of CPU
+    work in all.  value = config 3 (8 x 655,360 B over the median allreduce)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: the CPU baseline leg only
+    cores = min(8, cpu_cores())
+
+    def one(argv, budget_s, max_reps=400):
+        probe = oracle.loopback("bo", argv, reps=2, total=8, timeout=300)
+        reps = int(min(max_reps, max(3, budget_s / max(probe["median_s"], 1e-5))))
+        out = oracle.loopback("bo", argv, reps=reps, total=8, timeout=300)
+        nbytes = out["bytes_per_rank"]
+        return {"us_median": round(out["median_s"] * 1e6, 3), "reps": reps, "bytes_per_rank": nbytes,
+                "algbw_GBps": round(nbytes / out["median_s"] / 1e9, 4), "mismatches": out["mismatches"]}
+
+    res = {}
+    # config 3: allred_BO_2D 0 1 <4x2> 13 40 32 0 1 (RecDub BO, 40 tiles per block = 655,360 B per rank)
+    res["config3_recdub_bo_640kB"] = c3 = one([0, 1, 4, 13, 40, 32, 0, 1], 4.0)
+    # config 4 at a reduced bucket: 4096 tiles per block = 64 MiB per rank (1 GiB per rank
+    # would hold 8 GiB of shared buffers; the CPU rate is flat in the bandwidth regime)
+    res["config4_swing_bo_64MiB_reduced"] = one([1, 1, 4, 13, 4096, 32, 0, 1], 6.0, max_reps=5)
+    for tiles, kb in ((1, 2), (4, 8), (16, 32), (64, 128)):   # config 5: Swing LO 2 .. 128 kB
+        res[f"config5_swing_lo_{kb}kB"] = one([1, 1, 4, 13, tiles, 32, 0, 0], 2.0)
+    return {"value": round(8 * c3["bytes_per_rank"] / (c3["us_median"] * 1e-6) / 1e9, 4), "unit": "GB/s",
+            "cores": cores, "kind": "port",
+            "sample": ("oracle loopback, 8 forked rank processes per config (4x2 grid): config 3 RecDub BO "
+                       "640 kB, config 4 Swing BO at 64 MiB per rank (reduced from 1 GiB, <= 5 reps), "
+                       "config 5 Swing LO 2/8/32/128 kB; value = config 3, bytes of all 8 ranks / median time"),
+            "online_cpus": os.sysconf("SC_NPROCESSORS_ONLN"), "configs": res}
+
+
+def choose_transport(quick: dict, verify: dict):
+    """The fastest transport whose verdict is verified (None if none is)."""
+    ok = [k for k in quick if verify.get(k, {}).get("verified") is True]
+    return min(ok, key=lambda k: quick[k]) if ok else None
+
+
+def cli_config3(world: int) -> dict:
+    """BASELINE config 3 through the reference's own program surface on every GPU
+    of this node: bin/allred_BO_2D 0 1 4 13 40 32 0 1 with ALLRED_NODES=8 (the 4x2
+    grid) and ALLRED_GPUS = the GPUs this process sees (one device thread per GPU,
+    RCCL between them), every GPU's ranks checked with validate_result_vector."""
+    gpus = min(world, torch.cuda.device_count())
+    env = {"ALLRED_NODES": "8", "ALLRED_GPUS": str(gpus), "ALLRED_REPORT": "1", "ALLRED_CHECK_ALL": "1",
+           "ALLRED_STRICT": "1"}
+    argv = [0, 1, 4, 13, 40, 32, 0, 1]
+    p = t.run_cli("allred_BO_2D", argv, env=env, timeout=180)
+    rep = {}
+    for line in p.stderr.splitlines():
+        if line.startswith("{"):
+            rep = json.loads(line)
+    ok = p.returncode == 0 and "All values match!" in p.stdout and rep.get("mismatches") == 0
+    out = {"argv": " ".join(map(str, ["allred_BO_2D", *argv])), "env": env, "rc": p.returncode, "verified": ok,
+           "report": rep}
+    if rep.get("device_s"):
+        out["algbw_GBps"] = round(rep["bytes_per_rank"] / rep["device_s"] / 1e9, 3)
+        out["busbw_GBps"] = round(2 * 7 / 8 * rep["bytes_per_rank"] / rep["device_s"] / 1e9, 3)
+    if not ok:
+        out["stderr_tail"] = p.stderr[-400:]
+    return out
 
 
 def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
@@ -565,27 +817,33 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     torch.cuda.synchronize()
     ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)
     partial = torch.empty(ELEMS, dtype=torch.int16, device=dev)
+    vbuf = torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev)   # verification bucket
     t_start = time.perf_counter()
 
-    def timed_steps(step_fn, after=None):   # the K steps behind a spin kernel, max over ranks (ms per step)
+    def timed_steps(step_fn, after=None, reps=None):
+        """R repetitions of the K steps behind a spin kernel, an event between
+        consecutive ones; per repetition the max over ranks; returns (median ms
+        per step, every repetition's ms per step)"""
+        reps = reps or max(3, min(args.reps, 5))
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
         with torch.cuda.stream(stream):
             torch.cuda._sleep(200000)
-        e0.record(stream)
-        for i in range(args.steps):
-            step_fn(i)
-        if after is not None:
-            after()
-        e1.record(stream)
+        ev[0].record(stream)
+        for r in range(reps):
+            for i in range(args.steps):
+                step_fn(i)
+            if after is not None:
+                after()
+            ev[r + 1].record(stream)
         torch.cuda.synchronize()
         dist.barrier()
-        ms = torch.tensor([e0.elapsed_time(e1)], dtype=torch.float64)
+        ms = torch.tensor([ev[r].elapsed_time(ev[r + 1]) for r in range(reps)], dtype=torch.float64)
         dist.all_reduce(ms, op=dist.ReduceOp.MAX)
-        return ms.item() / args.steps
+        per = [m / args.steps for m in ms.tolist()]
+        return statistics.median(per), per
 
     def local_phases_ms():   # tree reduce of the 64 ranks + broadcast: the HBM kernels alone
         torch.cuda.synchronize()
@@ -600,39 +858,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / args.steps
 
-    # A measured RCCL line before the peer windows are touched: if opening, verifying
-    # or timing them hangs on an untried machine (the peer waits are bounded, an IPC
-    # open is not), rank 0 prints this line after --peer-timeout s and every rank
-    # leaves, so the driver still gets its one JSON line.
-    peer_guard = None
-    if comm is not None:
-        note(rank, "fallback headline over RCCL")
-        for i in range(args.warmup):
-            t.dist_allreduce(comm, desc, bufs[i % len(bufs)].data_ptr(), ws.data_ptr(), stream)
-        fb_ms = timed_steps(lambda i: t.dist_allreduce(comm, desc, bufs[i % len(bufs)].data_ptr(), ws.data_ptr(),
-                                                       stream))
-        fb_local = local_phases_ms()
-
-        def peer_give_up():
-            if rank == 0:
-                emit(multi_line(args, world, "rccl", fb_ms, fb_local, time.perf_counter() - t_start,
-                                {"headline_transport": "rccl", "peer_error":
-                                 f"peer setup / verification / timing did not finish within {args.peer_timeout:g} s"}))
-            os._exit(0)
-
-        # every rank's timer started after the same barrier: all leave together (no rank is left
-        # to fail in a collective of a rank that is gone)
-        peer_guard = threading.Timer(args.peer_timeout, peer_give_up)
-        peer_guard.daemon = True
-        peer_guard.start()
-    note(rank, f"world {world}, device {dev_index}: opening peer windows")
-    peer, peer_err = open_peer(rank, world, dev_index, (1 << 30) // 2)   # windows for 1 GiB buckets
-    note(rank, f"peer windows: {'ok' if peer is not None else peer_err}")
-    if peer is not None and args.share_gpu:
-        peer.set_max_groups(512 // world)   # every rank's one-kernel grid resident at once
-
     # Inter-GPU transport: the candidates for the hierarchical step
     #   rccl        tree -> 2D Swing BO over RCCL -> broadcast (3 launches + RCCL groups)
+    #   peer_launches  tree -> mem_2D across GPUs over peer windows (launches) -> broadcast
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
     #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
@@ -643,20 +871,17 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #                 owned tiles, writes bucket i-2; every poll waits for the previous launch)
     #   peer_hier_x2t the same with bucket i-1's owned sums at the END of launch i (tune
     #                 hier_x2_tail: its polls never wait; the result polls wait like k_hier_x's)
-    # A peer candidate runs only once verified on THIS machine: on small-integer
-    # inputs (every sum exact, so every reduction order agrees) its bits must equal
-    # the RCCL path's (the data movement is right), peer_swing must equal RCCL on
-    # the real inputs too (same program), and peer_hier must equal the launch form
-    # of the same semantics (tree + mem_2D + broadcast).  Then each candidate is
-    # timed briefly and the fastest is the headline transport.
-    ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
-
+    # Every transport runs only once verified on THIS machine (verify_transport: the
+    # exact sum of per-row 0/1 inputs and the reference's closed form, both computed
+    # without any transport); the one-kernel peer forms must also equal the launch
+    # form of the same semantics bit for bit on random real data, and peer_swing the
+    # RCCL program's.  Then each verified one is timed and the fastest is the headline.
+    peer_box = [None]
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
-
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
     pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
-
     tail = [None]
+    ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
     def x2_tail(on):   # the host-side switch between the two k_hier_x2 forms, read at launch
         if tail[0] != on:
@@ -664,6 +889,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             tail[0] = on
 
     def flush():
+        peer = peer_box[0]
         if pend[0] is not None:
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
@@ -673,6 +899,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             pend2[0] = False
 
     def run(kind, b, fresh=False):
+        peer = peer_box[0]
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
         if kind == "peer_hier_x":   # buckets pipelined: this call finishes the previous one
@@ -688,7 +915,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
             pend2[0] = kind
             return
-        flush()
+        if peer is not None:
+            flush()
         if kind == "rccl":
             t.dist_allreduce(comm, desc, b.data_ptr(), ws.data_ptr(), stream)
         elif kind == "peer_swing":
@@ -700,48 +928,83 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 mode[0] = kind
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
-    # the reference transport: RCCL, or (--share-gpu) the peer launch form
-    base = "rccl" if comm is not None else "peer_launches"
-    candidates, verify = [base], {}
-    if peer is None and comm is None:
-        raise RuntimeError("neither the RCCL communicator nor the peer windows could be opened"
-                           f" (rccl: {comm_err}, peer: {peer_err})")
-    if peer is not None:
-        small = torch.zeros_like(buf)
-        small[:4] = torch.randint(0, 2, (4, ELEMS), device=dev).to(torch.bfloat16).view(torch.int16)
-        ref = small.clone()
-        note(rank, f"verify: {base} on small integers")
-        run(base, ref, fresh=True)
-        for kind in ("peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe", "peer_hier_x", "peer_hier_x2",
-                     "peer_hier_x2t"):
-            note(rank, f"verify: {kind}")
-            try:   # the same calls on every rank: a raised status is raised everywhere
-                x = small.clone()
-                run(kind, x, fresh=True)
+    verify = {}
+
+    def check(kind, seed):
+        note(rank, f"verify: {kind}")
+        peer = peer_box[0]
+
+        def once(b):
+            run(kind, b, fresh=True)
+            if peer is not None:
                 flush()
-                torch.cuda.synchronize()
-                ok = torch.equal(x, ref)
+
+        status = (lambda: peer.status() & t.PEER_TIMEOUT) if kind != "rccl" else None
+        v = verify_transport(once, vbuf, world, rank, RANKS, SIDE, side, seed, status=status)
+        same_as = {"peer_swing": "rccl"}.get(kind, None if kind in ("rccl", "peer_launches") else "peer_launches")
+        if same_as == "rccl" and not verify.get("rccl", {}).get("verified"):
+            same_as = None   # --share-gpu: no RCCL to compare with (the Swing trees differ from mem_2D's)
+        if v["verified"] and same_as:   # random real data: bit-identical to the form of the same semantics
+            ok = False
+            try:
                 a, b2 = buf.clone(), buf.clone()
-                if kind == "peer_swing" and base == "rccl":
-                    run("rccl", a, fresh=True)
-                    run("peer_swing", b2)
-                elif kind == "peer_swing":   # --share-gpu: same semantics (Swing trees) only on small integers
-                    a = b2 = None
-                else:   # the one-kernel forms against the launch form of the same semantics
-                    run("peer_launches", a, fresh=True)
-                    run(kind, b2)
+                run(same_as, a, fresh=True)
+                run(kind, b2)
+                if peer is not None:
                     flush()
                 torch.cuda.synchronize()
-                ok = ok and (a is None or torch.equal(a, b2)) and (peer.status() & t.PEER_TIMEOUT) == 0
-                del x, a, b2
+                ok = torch.equal(a, b2) and not (status and status())
+                del a, b2
             except Exception as e:  # reported, never silently dropped: the candidate is not used
-                note(rank, f"verify: {kind} raised {e!r}")
-                verify[kind + "_error"] = repr(e)
-                ok = False
-            verify[kind] = agreed(ok)
-            if verify[kind]:
+                note(rank, f"verify: {kind} vs {same_as} raised {e!r}")
+            v["matches_" + same_as] = agreed(ok)
+            v["verified"] = v["matches_" + same_as]
+        verify[kind] = v
+        note(rank, f"verify: {kind} -> {v}")
+        return v["verified"]
+
+    # RCCL first, verified before any number of it is measured: the watchdog's
+    # fallback line below is only ever an RCCL number that passed both checks
+    rccl_ok = comm is not None and check("rccl", 9000)
+    peer_guard = None
+    if rccl_ok:
+        note(rank, "fallback headline over RCCL")
+        for i in range(args.warmup):
+            run("rccl", bufs[i % len(bufs)])
+        fb_ms, _ = timed_steps(lambda i: run("rccl", bufs[i % len(bufs)]))
+        fb_local = local_phases_ms()
+        FALLBACK_DONE.set()
+
+        def peer_give_up():
+            if rank == 0:
+                emit(multi_line(args, world, "rccl", fb_ms, fb_local, time.perf_counter() - t_start,
+                                {"headline_transport": "rccl", "transport_verified": dict(verify), "peer_error":
+                                 f"peer setup / verification / timing did not finish within {args.peer_timeout:g} s"}))
+            os._exit(0)
+
+        # every rank's timer started after the same barrier: all leave together; a rank
+        # whose own timer was cancelled first and then loses rank 0 exits cleanly too
+        # (FALLBACK_DONE, main())
+        peer_guard = threading.Timer(args.peer_timeout, peer_give_up)
+        peer_guard.daemon = True
+        peer_guard.start()
+    note(rank, f"world {world}, device {dev_index}: opening peer windows")
+    peer, peer_err = open_peer(rank, world, dev_index, (1 << 30) // 2)   # windows for 1 GiB buckets
+    peer_box[0] = peer
+    note(rank, f"peer windows: {'ok' if peer is not None else peer_err}")
+    if peer is not None and args.share_gpu:
+        peer.set_max_groups(512 // world)   # every rank's one-kernel grid resident at once
+    if peer is None and not rccl_ok:
+        raise RuntimeError("no verified transport: RCCL " + (comm_err or ("unverified" if comm else "absent")) +
+                           f", peer windows: {peer_err}")
+    candidates = ["rccl"] if rccl_ok else []
+    if peer is not None:
+        for i, kind in enumerate(("peer_launches", "peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe",
+                                  "peer_hier_x", "peer_hier_x2", "peer_hier_x2t")):
+            if check(kind, 9100 + 10 * i):
                 candidates.append(kind)
-        del small, ref
+    if not candidates:
+        raise RuntimeError(f"no transport passed verification on this machine: {verify}")
     quick = {}
     # each candidate timed the way the headline is: K steps with the pipelined forms'
     # finishing launch inside (it weighs 1/K per step), median of three
@@ -750,8 +1013,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         note(rank, f"quick timing: {kind}")
         it = iter(range(1 << 30))
         quick[kind] = round(statistics.median(
-            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush) for _ in range(3)), 4)
-    transport = min(candidates, key=lambda k: quick[k])
+            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush if peer else None)
+            for _ in range(3)), 4)
+    transport = choose_transport(quick, verify)
 
     def step(i):
         run(transport, bufs[i % len(bufs)])
@@ -765,10 +1029,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         step(i)
     for i in range(args.warmup):
         step(i)
-    flush()
+    if peer is not None:
+        flush()
     t0 = time.perf_counter()
-    # peer_hier_x / _x2: the finishing launch is part of the K steps' time
-    ms_per_step = timed_steps(step, after=flush)
+    # peer_hier_x / _x2: the finishing launch is part of each repetition's K steps
+    ms_per_step, rep_ms = timed_steps(step, after=flush if peer is not None else None)
     wall = time.perf_counter() - t0
     peer_timeout = False
     if transport != "rccl" and peer is not None:
@@ -777,13 +1042,13 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         dist.all_reduce(st0, op=dist.ReduceOp.MAX)
         peer_timeout = bool(st0.item())
         if peer_timeout:
-            if comm is None:
+            if not rccl_ok:
                 raise RuntimeError(f"peer transport {transport} timed out during the timed steps: no valid number")
             note(rank, f"{transport} timed out in the timed loop: timing the RCCL transport instead")
             transport = "rccl"
             for i in range(args.warmup):
                 step(i)
-            ms_per_step = timed_steps(step)
+            ms_per_step, rep_ms = timed_steps(step)
     if peer is not None:   # defaults again for the extras below
         peer.set_oneshot_max(4 << 20)
         peer.set_hier_ll(0)
@@ -791,9 +1056,12 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     local_ms = local_phases_ms()
     if peer_guard is not None:   # the headline is measured: the extras have their own watchdog
         peer_guard.cancel()
+    HEADLINE_DONE.set()
 
-    extras = {"headline_transport": transport, "peer_verified": verify, "transport_quick_ms": quick,
-              "peer_timeout_in_timed_loop": peer_timeout}
+    extras = {"headline_transport": transport, "transport_verified": verify, "transport_quick_ms": quick,
+              "peer_timeout_in_timed_loop": peer_timeout,
+              "timing": {"repetitions": len(rep_ms), "ms_per_step_per_repetition": [round(x, 6) for x in rep_ms],
+                         "ms_per_step": "median repetition (each: the K steps, max over ranks)"}}
     if peer_err:
         extras["peer_error"] = peer_err
     if comm_err:
@@ -817,11 +1085,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 emit(line(ex))
             os._exit(0)
 
-        HEADLINE_DONE.set()
         guard = threading.Timer(args.extras_timeout + (0 if rank == 0 else 10), give_up)
         guard.daemon = True
         guard.start()
-        extras.update(xgmi_arms(comm, peer if verify.get("peer_swing") else None, world, dev, stream, side, total))
+        extras.update(xgmi_arms(comm, peer if verify.get("peer_swing", {}).get("verified") else None, world, rank,
+                                dev, stream, side, total))
         if world > 1 and comm is not None:
             try:
                 extras["link_probe"] = link_probe(rank, world, dev)
@@ -840,28 +1108,55 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         peer.close()
     if comm is not None:
         comm.close()
+    del bufs, vbuf, ws
+    torch.cuda.synchronize()
+    # rank 0 alone (the others wait at the barrier): the reference's program surface
+    # across this node's GPUs (config 3), then the CPU baseline of configs 3-5
+    if rank == 0 and args.extras:
+        try:
+            extras["cli_config3"] = cli_config3(world)
+        except Exception as e:  # reported, never silently dropped
+            extras["cli_config3"] = {"error": repr(e), "verified": False}
+    cpu = None
+    if rank == 0 and args.cpu:
+        try:
+            cpu = cpu_baseline_multi()
+        except Exception as e:  # reported, never silently dropped
+            cpu = {"value": None, "error": repr(e)}
+    dist.barrier()
     if rank != 0:
         return None
-    return line(extras)
+    out = line(extras)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    return out
 
 
 # set once the N > 1 headline is measured: a rank that then loses its peers
 # (rank 0 gave up on the extras and left) exits cleanly instead of failing the job
 HEADLINE_DONE = threading.Event()
+# set once the RCCL fallback line is measured: rank 0's peer watchdog may then print
+# it and leave while this rank's own (already cancelled) timer did not fire
+FALLBACK_DONE = threading.Event()
+
+# the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
+ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
+              "peer_hier_x": "k_hier_x", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>"}
 
 
 def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> dict:
     """rank 0's JSON line of the N > 1 bench"""
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    one_launch = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
-                  "peer_hier_x": "k_hier_x", "peer_hier_x2": "k_hier_x2", "peer_hier_x2t": "k_hier_x2<TAIL>"}
-    if transport in one_launch:   # the step IS one launch: its HBM bytes over its time
-        roof = {"kernel": f"{one_launch[transport]} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
-                "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9}
+    if transport in ONE_LAUNCH:   # the step IS one launch: its HBM bytes over its time
+        kern = ONE_LAUNCH[transport]
+        roof = {"kernel": f"{kern} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
+                "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9, "traffic": pmc_traffic(kern)}
     else:
+        tr, bc = pmc_traffic("k_tree_lds_pipe<64, false>"), pmc_traffic("k_broadcast")
         roof = {"kernel": "k_tree_lds_pipe<64, false> + k_broadcast (local phases)",
-                "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9}
+                "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9,
+                "traffic": tr + bc if tr and bc else None}
     achieved = roof["achieved"]
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
            "peer_launches": "on-GPU tree reduce, mem_2D across GPUs over peer-mapped windows (launches), broadcast",
@@ -882,6 +1177,7 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                             "xGMI windows",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
+    v = extras.get("transport_verified", {}).get(transport, {})
     return {
         "metric": METRIC,
         "value": round(bytes_all / (ms_per_step * 1e-3) / 1e9, 3),
@@ -898,9 +1194,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
         "config": {"workload": f"config 2 per GPU (64 virtual ranks x 655,360 B, 8x8 Swing) x {world} GPUs: "
                                f"{via}; GPU grid {GRIDS[world]}",
                    "ranks": RANKS * world, "bytes_per_rank": ELEMS * 2, "parallelism": f"dp{world}",
-                   "transport": transport},
+                   "transport": transport, "verified": v.get("verified") is True},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None, "kernel": roof["kernel"],
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": roof["traffic"], "kernel": roof["kernel"],
                      "algorithmic_bytes_per_launch": roof["algorithmic_bytes_per_launch"],
                      "local_phases_ms": round(local_ms, 6)},
         "roofline_xgmi": roofline_xgmi(extras, world),
@@ -951,9 +1247,9 @@ def main():
         try:
             out = bench_multi(args, rank, world, local_rank, emit)
         except Exception as e:
-            if rank == 0 or not HEADLINE_DONE.is_set():
+            if rank == 0 or not (HEADLINE_DONE.is_set() or FALLBACK_DONE.is_set()):
                 raise
-            note(rank, f"extras ended by a peer's exit ({e!r}); rank 0 reports the headline")
+            note(rank, f"ended by a peer's exit ({e!r}); rank 0 reports the line")
             sys.stderr.flush()
             os._exit(0)
         dist.destroy_process_group()

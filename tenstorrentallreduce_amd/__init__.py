@@ -194,8 +194,12 @@ class Plan:
         self.total = total or side * side
         self.elems = elems_per_rank
         self.workspace_bytes = lib.allred_plan_workspace_bytes(h)
-        self.launches = lib.allred_plan_launches(h)
         self.stamp_words = lib.allred_plan_stamp_words(h)
+
+    @property
+    def launches(self) -> int:
+        """Kernel launches one execute enqueues now (fused plans: with the current tune keys)."""
+        return lib.allred_plan_launches(self._h)
 
     def execute(self, ranks_ptr: int, stride: int, workspace_ptr: int | None = None, stream=None,
                 stamps_ptr: int | None = None) -> None:

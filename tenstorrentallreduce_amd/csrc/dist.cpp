@@ -210,6 +210,7 @@ std::vector<Step> program(const allred_schedule& s, int rank, int variant, size_
 // the rank's program for desc, built once and cached (key: every desc field that
 // shapes it, the channel count actually used, the rank)
 using ProgKey = std::tuple<int, int, int, int, uint64_t, int, int>;
+constexpr size_t kMaxCachedPrograms = 1024;   // per-(desc, rank) programs / verdicts kept
 std::mutex g_prog_mu;
 std::map<ProgKey, std::shared_ptr<const std::vector<Step>>> g_progs;
 
@@ -218,6 +219,9 @@ std::shared_ptr<const std::vector<Step>> cached_program(const allred_dist_desc* 
     const ProgKey key{d->algo, d->variant, d->side_length, d->total_nodes, d->elems, C, rank};
     std::lock_guard<std::mutex> g(g_prog_mu);
     auto it = g_progs.find(key);
+    // bounded: a job cycling through many bucket sizes starts the cache afresh
+    // (programs in use stay alive through their shared_ptr)
+    if (it == g_progs.end() && g_progs.size() >= kMaxCachedPrograms) g_progs.clear();
     if (it == g_progs.end())
         it = g_progs.emplace(key, std::make_shared<const std::vector<Step>>(
                                       program(s, rank, d->variant, (size_t)d->elems, C))).first;
@@ -276,6 +280,7 @@ int verify_program(const allred_dist_desc* d, const allred_schedule& s, int rank
             if (all[i - 1].off + all[i - 1].len > all[i].off) st = ALLRED_ERR_SCHEDULE;
     }
     std::lock_guard<std::mutex> g(g_verified_mu);
+    if (g_verified.size() >= kMaxCachedPrograms) g_verified.clear();
     g_verified[key] = st;
     return st;
 }
@@ -441,6 +446,10 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
     int st = check_desc(d, &s);
     if (st != ALLRED_OK) return st;
     if (d->total_nodes != c->nranks) return ALLRED_ERR_ARG;
+    // the step adds (k_add_segs) take 16-byte aligned buckets: refuse before the
+    // first exchange, never between two RCCL groups (the partners would be left
+    // waiting in a step this rank never enters)
+    if (((uintptr_t)buf | (uintptr_t)workspace) % 16) return ALLRED_ERR_ARG;
     hipStream_t hs = (hipStream_t)stream;
     const size_t n = (size_t)d->elems;
     uint16_t* staging = static_cast<uint16_t*>(workspace);

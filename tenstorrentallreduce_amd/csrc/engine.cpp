@@ -565,8 +565,8 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
     // workspace and launch count per execute
     if (desc->exec == ALLRED_EXEC_FUSED) {
         // 64 ranks from 1024 whole tiles: the persistent passes, in launches of
-        // about fused_chunk_tiles tiles (the value when the plan is made)
-        p->launches = total == 64 && n % 256 == 0 && n / 256 >= 1024 ? (int)fused_chunk_launches(n / 256) : 1;
+        // about fused_chunk_tiles tiles (allred_plan_launches recounts at call time)
+        p->launches = (int)fused_launches(desc->variant, p->lo_tree, desc->algo, desc->side_length, n, total);
     } else if (p->steps_persistent) {
         p->launches = steps ? 1 : 0;
     } else if (desc->variant == ALLRED_BO) {
@@ -591,7 +591,15 @@ int allred_plan_destroy(allred_plan* plan) {
 
 size_t allred_plan_workspace_bytes(const allred_plan* plan) { return plan ? plan->ws_bytes : 0; }
 
-int allred_plan_launches(const allred_plan* plan) { return plan ? plan->launches : 0; }
+int allred_plan_launches(const allred_plan* plan) {
+    if (!plan) return 0;
+    // fused plans: what execute would enqueue now on device memory (the tune keys
+    // it reads at launch time included); pinned host buckets take one launch
+    if (plan->desc.exec == ALLRED_EXEC_FUSED)
+        return (int)fused_launches(plan->desc.variant, plan->lo_tree, plan->desc.algo, plan->desc.side_length, plan->n,
+                                   plan->total);
+    return plan->launches;
+}
 
 int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size_t cap, int* read_conflicts) {
     if (!out && cap) return ALLRED_ERR_ARG;

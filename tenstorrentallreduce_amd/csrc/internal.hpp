@@ -54,6 +54,7 @@ int launch_bf16_add_segs(uint16_t* dst, const uint16_t* src, const uint64_t* off
 // host_memory: the ranks live in pinned host memory (zero-copy) -> pipelined form
 // launches of one persistent fused pass over `tiles` 256-element tiles (fused_chunk_tiles)
 uint64_t fused_chunk_launches(uint64_t tiles);
+uint64_t fused_launches(int variant, bool lo_tree, int algo, int side, size_t n, int total);
 int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint8_t* order, void* stream,
                       bool host_memory = false);
 // dag: the interned LO DAG of a 64-rank schedule (engine.cpp lo_dag), or null

@@ -1392,6 +1392,25 @@ uint64_t fused_chunk_launches(uint64_t tiles) {
     return nl < 1 ? 1 : nl;
 }
 
+// Kernel launches one fused execute of device-resident buckets enqueues: the
+// same decisions launch_tree_fused (BO, rank-uniform LO), launch_lo_dag_reg /
+// launch_butterfly (other LO) and mem_fused_impl (MEM) take, with the tune
+// keys as they are now (allred_plan_launches asks at call time).
+uint64_t fused_launches(int variant, bool lo_tree, int algo, int side, size_t n, int total) {
+    const uint64_t nv = n / 8, tiles = nv / 32, bv = total > 0 ? nv / total : 0;
+    const bool big64 = total == 64 && nv % 32 == 0 && bv % 32 == 0 && tiles >= 1024;
+    if (variant == ALLRED_MEM) return big64 && fused_form() == 0 ? fused_chunk_launches(tiles) : 1;
+    if (variant == ALLRED_LO && !lo_tree) {
+        if (!tune(Tune::lo_dag_reg) || n % 256 || tiles < (uint64_t)tune(Tune::lo_dag_reg_min_tiles)) return 1;
+#define TSA_X(D, A, S, T) \
+    if (algo == (A) && total == (T) && ((A) == ALLRED_SWING_1D || side == (S))) return fused_chunk_launches(tiles);
+        TSA_LO_DAGS(TSA_X)
+#undef TSA_X
+        return 1;   // the butterfly forms: one launch
+    }
+    return big64 && fused_form() == 0 ? fused_chunk_launches(tiles) : 1;
+}
+
 // The persistent lagged passes (k_tree_lds_lag, k_lo_dag_reg, k_mem_lds_lag)
 // on large buckets: a sequence of launches over tile ranges a .. b-1 of about
 // fused_chunk_tiles tiles each (1280 = config 2's 2.5 tiles per workgroup).

@@ -63,6 +63,8 @@ struct allred_peer {
     // allred_peer_allreduce_pipelined: a bucket started (its partials pushed) and not yet finished
     bool pipe_pending = false;
     uint32_t pipe_k = 0;            // that bucket's call number (epoch pipe_k + 1, LL parity pipe_k & 1)
+    uint16_t* pipe_buf = nullptr;   // that bucket, and its size: the next call must finish exactly it
+    uint64_t pipe_elems = 0;
     // allred_peer_allreduce_pipelined2: up to two started, unfinished buckets, older
     // first; with two, the older one's owned tiles are summed already
     int x2_n = 0;
@@ -201,8 +203,12 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
     if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * 128 > p->ll_box_words)
         return ALLRED_ERR_UNSUPPORTED;
-    // prev must be the bucket the previous call started; a started bucket must be finished next
-    if (prev ? (!p->pipe_pending || p->pipe_k + 1u != p->calls) : p->pipe_pending) return ALLRED_ERR_ARG;
+    // prev must be the bucket the previous call started (same pointer, same size: the
+    // launch finishes prev with this call's tile count and owner split); a started
+    // bucket must be finished next
+    if (prev ? (!p->pipe_pending || p->pipe_k + 1u != p->calls || prev != p->pipe_buf || n != p->pipe_elems)
+             : p->pipe_pending)
+        return ALLRED_ERR_ARG;
     const uint8_t* order = nullptr;
     int st = local_tree_order(local_algo, local_side, local_ranks, &order);
     if (st != ALLRED_OK) return st;
@@ -219,9 +225,12 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
     if (cur) {
         p->pipe_k = kc;
         p->pipe_pending = true;
+        p->pipe_buf = cur;
+        p->pipe_elems = n;
         ++p->calls;
     } else {
         p->pipe_pending = false;
+        p->pipe_buf = nullptr;
     }
     p->last_all_peer = true;
     return ALLRED_OK;

@@ -30,7 +30,8 @@ def free_port() -> int:
 def test_bench_two_ranks_share_gpu():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--share-gpu", "--steps", "10", "--warmup", "2", "--no-extras"]
+           "--gpus", "2", "--share-gpu", "--steps", "10", "--warmup", "2", "--no-extras",
+           "--no-cpu-baseline"]
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
@@ -42,6 +43,12 @@ def test_bench_two_ranks_share_gpu():
     x = d["xgmi"]
     transport = d["config"]["transport"]
     assert transport == x["headline_transport"]
-    assert transport == "peer_launches" or x["peer_verified"].get(transport) is True
+    # the headline transport passed both independent checks on this machine
+    v = x["transport_verified"][transport]
+    assert v["verified"] is True and v["exact_sum"] is True and v["closed_form"] is True
+    assert d["config"]["verified"] is True
     assert x["peer_timeout_in_timed_loop"] is False and x["peer_status"] & 1 == 0
     assert d["roofline"]["bound"] == "hbm" and 0 < d["roofline"]["frac"] < 1
+    assert x["timing"]["repetitions"] >= 3   # median of >= 3 K-step repetitions
+    assert d["ms_per_step"] == pytest.approx(sorted(x["timing"]["ms_per_step_per_repetition"])[
+        len(x["timing"]["ms_per_step_per_repetition"]) // 2], rel=1e-3)

@@ -55,4 +55,9 @@ def test_single_rank_rccl_comm(local):
 
     t.dist_allreduce_host(desc, 0, host, scratch, no_exchange)
     assert np.array_equal(buf.cpu().numpy().view(np.uint16), host)
+    # a bucket or workspace off 16-byte alignment is refused before any exchange
+    with pytest.raises(t.AllredError):
+        t.dist_allreduce(comm, desc, buf.data_ptr() + 2, ws.data_ptr(), torch.cuda.current_stream())
+    with pytest.raises(t.AllredError):
+        t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr() + 8, torch.cuda.current_stream())
     comm.close()

@@ -181,7 +181,15 @@ def test_fused_chunked_launches_bit_exact(variant):
     stride = t.preferred_rank_stride(n)
     plan = t.Plan(t.SWING, v, side, n, total, t.EXEC_FUSED)
     assert plan.launches == 3
+    with t.tuned(fused_chunk_tiles=0):   # counted with the keys execute reads at launch time
+        assert plan.launches == 1
+    with t.tuned(fused_form=3):          # a forced single-launch form (the LO register DAG ignores it)
+        assert plan.launches == (3 if variant == "lo" else 1)
     plan.close()
+    if variant == "lo":   # 1D Swing at 64 ranks has no register DAG: the one-launch butterfly
+        plan = t.Plan(t.SWING_1D, v, 1, n, total, t.EXEC_FUSED)
+        assert plan.launches == 1
+        plan.close()
     plan = t.Plan(t.SWING, v, side, 327680, total, t.EXEC_FUSED)
     assert plan.launches == 1
     plan.close()

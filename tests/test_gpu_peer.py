@@ -412,6 +412,12 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
             peer.allreduce(x.data_ptr(), n, s, local, 8, t.SWING, x.data_ptr())
         with pytest.raises(_lib.AllredError):   # a second start without finishing the first
             peer.allreduce_pipelined(x.data_ptr(), None, n, s)
+        y = data[0].clone()
+        with pytest.raises(_lib.AllredError):   # prev is not the pending bucket
+            peer.allreduce_pipelined(None, y.data_ptr(), n, s)
+        if n % (2 * 256) == 0:
+            with pytest.raises(_lib.AllredError):   # the pending bucket with another size
+                peer.allreduce_pipelined(None, x.data_ptr(), n // 2, s)
         peer.allreduce_pipelined(None, x.data_ptr(), n, s)
         with pytest.raises(_lib.AllredError):   # nothing pending
             peer.allreduce_pipelined(None, x.data_ptr(), n, s)
