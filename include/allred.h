@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ALLRED_ABI_VERSION 2
+#define ALLRED_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------- */
 #define ALLRED_OK 0
@@ -267,6 +267,9 @@ typedef struct {
     int32_t device;          /* HIP device ordinal, -1 = current (ALLRED_DEVICE env); the
                                 reference's CreateDevice(0) / IDevice*, allred_BO_2D.cpp:8 */
     int32_t mem_accum;       /* extension (ALLRED_MEM_ACC=bf16): ALLRED_ACC_FP32 / ALLRED_ACC_BF16 */
+    int32_t gpus;            /* extension (argv[10] or ALLRED_GPUS): 0 = every rank a virtual rank on
+                                `device` (the default); G >= 1 = the ranks spread over GPUs
+                                device .. device + G - 1, one host thread and one RCCL rank per GPU */
 } allred_args;
 /* Parses argv exactly like AllredConfig's ctor (std::stoi semantics: leading
  * integer, junk -> ALLRED_ERR_ARG where the reference would throw).          */
@@ -283,6 +286,21 @@ typedef struct {
 } allred_report;
 /* Generate inputs, H2D, run (if run_kernel), D2H of print_core, validate
  * (printing like the reference when verbose), report timing, on args->device.
+ * args->gpus = G >= 1 (ALLRED_GPUS / argv[10]): the same program on G GPUs of
+ * this node in ONE process, one host thread per GPU, one RCCL communicator per
+ * GPU (ncclCommInitAll).  The total_nodes ranks are split into G groups of
+ * L = total / G consecutive ranks, group g on GPU device + g (G a power of two
+ * dividing total, G <= the visible GPUs; else ALLRED_ERR_ARG before any HIP
+ * call).  L == 1: the reference's own (side, total) schedule runs across the
+ * GPUs (allred_dist_allreduce: Swing / RecDub BO or LO, or mem_2D's
+ * one-shot exchange); L > 1: each GPU reduces its L ranks with the (side, L)
+ * sub-grid's tree (or (2,2)/(2,4)/(4,8)/... when the rows do not form one),
+ * the GPUs allreduce the partials on the (2,2)/(2,4)/(4,8) grid, and every
+ * rank gets the result (mem_2D: L == 1 or G == 1 only, else
+ * ALLRED_ERR_UNSUPPORTED).  Every GPU's first rank is validated as well as
+ * print_core (ALLRED_CHECK_ALL: every rank); device_seconds / e2e_seconds are
+ * the slowest GPU's.  The reference is single-chip (allred_BO_2D.cpp:7-29,
+ * allred_helper.cpp:205-220): this is its argv across the GPUs of one node.
  * ALLRED_PROFILE_LOG=<path> also writes every rank's ALL_RED_LOOP zone in the
  * layout of tt-metal's profile_log_device.csv (the reference's
  * TT_METAL_DEVICE_PROFILER=1 run, python/timing_taker.py:60-65).            */
@@ -297,11 +315,18 @@ int allred_run(const allred_args* args, int verbose, allred_report* report);
 typedef struct allred_comm allred_comm;
 int allred_comm_get_unique_id(uint8_t* id /*[128]*/);
 int allred_comm_init(const uint8_t* id, int nranks, int rank, int device, allred_comm** out);
+/* ndev communicators in ONE process (ncclCommInitAll), rank i on devices[i]:
+ * one host thread per communicator afterwards (each thread its own stream).
+ * The reference's CreateDevice(0) (allred_BO_2D.cpp:8) for the GPUs of a node. */
+int allred_comm_init_all(int ndev, const int* devices, allred_comm** out /*[ndev]*/);
 int allred_comm_destroy(allred_comm* comm);
 
 typedef struct {
     int32_t algo;           /* ALLRED_SWING / ALLRED_RECDUB                     */
-    int32_t variant;        /* ALLRED_BO or ALLRED_LO                           */
+    int32_t variant;        /* ALLRED_BO, ALLRED_LO, or ALLRED_MEM (local_ranks == 1: the
+                               mem_2D one-shot exchange, allred_mem_2D.cpp:4-165 — every
+                               rank's copy of block b to rank b, summed there in mem_2D
+                               order, then gathered; all links at once)      */
     int32_t side_length;    /* GPU grid                                         */
     int32_t total_nodes;    /* == nranks                                        */
     uint64_t elems;         /* bf16 elements per GPU bucket (multiple of 8*total for BO) */
@@ -312,6 +337,7 @@ typedef struct {
     int32_t local_algo;
     int32_t channels;       /* link-spreading channels: 0 = auto (all 2^S-1 links for
                                buckets >= 1 MiB on XOR grids), 1 = the plain schedule */
+    int32_t mem_accum;      /* ALLRED_MEM only: ALLRED_ACC_FP32 (default) / ALLRED_ACC_BF16 */
 } allred_dist_desc;
 /* Scratch device bytes the call needs (recv staging + hierarchical partial). */
 size_t allred_dist_workspace_bytes(const allred_dist_desc* desc);

@@ -270,6 +270,20 @@ class Comm:
         self._h = h
         self.nranks, self.rank = nranks, rank
 
+    @classmethod
+    def init_all(cls, devices: Sequence[int]) -> list:
+        """One communicator per device in this process (allred_comm_init_all)."""
+        devs = (C.c_int * len(devices))(*devices)
+        hs = (C.c_void_p * len(devices))()
+        check(lib.allred_comm_init_all(len(devices), devs, hs), "comm_init_all")
+        out = []
+        for i, h in enumerate(hs):
+            c = cls.__new__(cls)
+            c._h = C.c_void_p(h)
+            c.nranks, c.rank = len(devices), i
+            out.append(c)
+        return out
+
     def close(self):
         if self._h:
             lib.allred_comm_destroy(self._h)
@@ -277,8 +291,8 @@ class Comm:
 
 
 def dist_desc(algo: int, variant: int, side: int, total: int, elems: int, local_ranks: int = 1,
-              local_side: int = 1, local_algo: int = SWING, channels: int = 0) -> DistDesc:
-    return DistDesc(algo, variant, side, total, elems, local_ranks, local_side, local_algo, channels)
+              local_side: int = 1, local_algo: int = SWING, channels: int = 0, mem_accum: int = ACC_FP32) -> DistDesc:
+    return DistDesc(algo, variant, side, total, elems, local_ranks, local_side, local_algo, channels, mem_accum)
 
 
 def dist_workspace_bytes(desc: DistDesc) -> int:

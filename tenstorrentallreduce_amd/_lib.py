@@ -37,7 +37,7 @@ RECDUB, SWING, RECDUB_1D, SWING_1D = 0, 1, 2, 3
 BO, LO, MEM = 0, 1, 2
 EXEC_STEPS, EXEC_FUSED = 0, 1
 ACC_FP32, ACC_BF16 = 0, 1
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_NODES, MAX_STEPS = 64, 6
 UNIQUE_ID_BYTES = 128
 
@@ -77,7 +77,7 @@ class PlanDesc(C.Structure):
 class Args(C.Structure):
     _fields_ = [(n, C.c_int32) for n in (
         "variant", "swing", "run_kernel", "side_length", "seed", "tiles", "error", "print_core",
-        "bandwidth_optimal", "total_nodes", "exec", "round_mode", "num_tiles", "device", "mem_accum")]
+        "bandwidth_optimal", "total_nodes", "exec", "round_mode", "num_tiles", "device", "mem_accum", "gpus")]
 
 
 class Report(C.Structure):
@@ -92,7 +92,7 @@ class DistDesc(C.Structure):
     _fields_ = [
         ("algo", C.c_int32), ("variant", C.c_int32), ("side_length", C.c_int32), ("total_nodes", C.c_int32),
         ("elems", C.c_uint64), ("local_ranks", C.c_int32), ("local_side", C.c_int32), ("local_algo", C.c_int32),
-        ("channels", C.c_int32),
+        ("channels", C.c_int32), ("mem_accum", C.c_int32),
     ]
 
 
@@ -146,6 +146,7 @@ SIGNATURES = [
     ("allred_run", C.c_int, [C.POINTER(Args), C.c_int, C.POINTER(Report)]),
     ("allred_comm_get_unique_id", C.c_int, [_P]),
     ("allred_comm_init", C.c_int, [_P, C.c_int, C.c_int, C.c_int, C.POINTER(_P)]),
+    ("allred_comm_init_all", C.c_int, [C.c_int, C.POINTER(C.c_int), C.POINTER(_P)]),
     ("allred_comm_destroy", C.c_int, [_P]),
     ("allred_dist_workspace_bytes", C.c_size_t, [C.POINTER(DistDesc)]),
     ("allred_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),

@@ -803,6 +803,11 @@ int allred_args_parse(int argc, const char* const* argv, int variant, allred_arg
     const char* env_dev = std::getenv("ALLRED_DEVICE");
     if (env_dev && stoi_like(env_dev, &a->device)) return ALLRED_ERR_ARG;
     a->mem_accum = env_is("ALLRED_MEM_ACC", "bf16") ? ALLRED_ACC_BF16 : ALLRED_ACC_FP32;
+    // extension: the ranks over G GPUs of this node (argv[10] or ALLRED_GPUS), 0 = one device
+    const char* env_gpus = std::getenv("ALLRED_GPUS");
+    if (argc >= 11) { if (stoi_like(argv[10], &a->gpus)) return ALLRED_ERR_ARG; }
+    else if (env_gpus && stoi_like(env_gpus, &a->gpus)) return ALLRED_ERR_ARG;
+    if (a->gpus < 0) a->gpus = 0;
     const bool large = variant == ALLRED_MEM || (variant == ALLRED_BO && a->bandwidth_optimal);
     a->num_tiles = allred_normalize_tiles(a->tiles, a->total_nodes, large ? 1 : 0);
     return ALLRED_OK;
@@ -822,7 +827,7 @@ int allred_args_parse(int argc, const char* const* argv, int variant, allred_arg
         if (st != ALLRED_OK) goto done;            \
     } while (0)
 
-namespace {
+}  // extern "C"
 
 // tt-metal's profile_log_device.csv layout, as python/profiler_results_analyzer*.py
 // read it (metadata line, column header, one row per zone event): every rank's
@@ -830,7 +835,7 @@ namespace {
 // dataflow_kernel.cpp:147).  Ranks sit on the Wormhole worker cores the
 // reference's grid ran on (physical x / y of python/timing_taker.py:17-18);
 // times in s_memrealtime ticks (100 MHz "cycles").
-int write_profile_log(const char* path, int N, int side, const uint64_t* start, const uint64_t* end) {
+int tsa::write_profile_log(const char* path, int N, int side, const uint64_t* start, const uint64_t* end) {
     static const int phys_x[8] = {1, 2, 3, 4, 6, 7, 8, 9}, phys_y[8] = {1, 2, 3, 4, 5, 7, 8, 9};
     FILE* f = std::fopen(path, "w");
     if (!f) return ALLRED_ERR_ARG;
@@ -848,7 +853,7 @@ int write_profile_log(const char* path, int N, int side, const uint64_t* start, 
     return ALLRED_OK;
 }
 
-}  // namespace
+extern "C" {
 
 int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     if (!a) return ALLRED_ERR_ARG;
@@ -865,6 +870,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     if (print_core < 0 || print_core >= N) return ALLRED_ERR_ARG;
     R->bytes_per_rank = bytes;
     R->total_nodes = N;
+    if (a->gpus > 0) return run_multi_gpu(a, verbose, R);   // dist.cpp: one host thread per GPU
     DeviceGuard guard(a->device);
     if (!guard.ok) return ALLRED_ERR_HIP;
 

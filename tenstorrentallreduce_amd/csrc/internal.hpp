@@ -80,6 +80,14 @@ int launch_copy_ranks(const uint16_t* src, uint64_t src_stride, uint16_t* dst, u
 int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int total, uint16_t* dst, bool acc16,
                       void* stream);
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, bool acc16, void* stream);
+// dst = rows[0] + rows[1] + ... + rows[nrows-1] in that order (fp32 rounded once, or
+// bf16 per add): mem_2D's owner-first sum once the owner's copy is row 0
+int launch_rows_sum(const uint16_t* rows, uint64_t stride, size_t n, int nrows, uint16_t* dst, bool acc16,
+                    void* stream);
+// allred_run with args->gpus > 0 (dist.cpp): the program over G GPUs, one host thread each
+int run_multi_gpu(const allred_args* a, int verbose, allred_report* report);
+// the mem_2D validation of one rank's result and the per-rank profile zones (engine.cpp)
+int write_profile_log(const char* path, int N, int side, const uint64_t* start, const uint64_t* end);
 // the schedule form as one persistent launch (k_bo_steps / k_lo_steps).  BO: d_tab = per block
 // the phase table of engine.cpp bo_steps_table; LO: d_pairs = per step N/2 (r, p) pairs.
 // stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)

@@ -1700,6 +1700,24 @@ int launch_mem_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tota
                  : mem_reduce_impl<false>(r, stride, n / 8, total, dst, (hipStream_t)stream);
 }
 
+int launch_rows_sum(const uint16_t* rows, uint64_t stride, size_t n, int nrows, uint16_t* dst, bool acc16,
+                    void* stream) {
+    if (n % 8 || stride % 8 || nrows < 1 || !aligned16(rows) || !aligned16(dst)) return ALLRED_ERR_ARG;
+    const uint64_t nv = n / 8;
+    if (!nv) return ALLRED_OK;
+    uint64_t g = (nv + kBlock - 1) / kBlock;
+    if (g > (uint64_t)kMaxGrid) g = kMaxGrid;
+    uint16_t* r = const_cast<uint16_t*>(rows);
+    // k_mem with one block (block_vec = n_vec): owner row 0 first, then rows 1 .. nrows-1 in order
+    if (acc16)
+        hipLaunchKernelGGL((k_mem<false, 16, true>), dim3((unsigned)g), dim3(kBlock), 0, (hipStream_t)stream, r, stride,
+                           nrows, nv, nv, dst);
+    else
+        hipLaunchKernelGGL((k_mem<false, 16, false>), dim3((unsigned)g), dim3(kBlock), 0, (hipStream_t)stream, r,
+                           stride, nrows, nv, nv, dst);
+    return last_error();
+}
+
 int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, bool acc16, void* stream) {
     if (n % (8 * (size_t)total) || stride % 8 || !aligned16(ranks)) return ALLRED_ERR_ARG;
     return acc16 ? mem_fused_impl<true>(ranks, stride, n / 8, total, (hipStream_t)stream)

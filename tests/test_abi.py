@@ -6,6 +6,8 @@ import re
 import subprocess
 import sys
 
+import ctypes as C
+
 import numpy as np
 import pytest
 
@@ -45,7 +47,7 @@ def test_header_constants_match_python_bindings():
 
 
 def test_status_strings():
-    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 2
+    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 3
     for st in range(0, -8, -1):
         assert _lib.lib.allred_status_string(st)
 
@@ -219,3 +221,26 @@ int main() {
     p, dirs, b0, b1, hp = out[1].split()
     assert (int(p), int(dirs), int(hp)) == (1, 1, 4)
     assert int(b0) | (int(b1) << 32) == t.get_swing_block_comm_indexes(1, 1, 0, False, 8, 64)
+
+
+def test_gpus_extension_parse_and_validation_without_gpu(monkeypatch):
+    """ALLRED_GPUS / argv[10] (the reference's argv across a node's GPUs): parsed
+    like the other extensions, and a rank split that cannot work (G not a power
+    of two, G not dividing the rank count, mem_2D with several ranks on several
+    GPUs) is refused with ALLRED_ERR_ARG / _UNSUPPORTED before any HIP call."""
+    a = t.parse_args(["allred_BO_2D", "0", "1", "4", "13", "40", "32", "0", "1", "8", "4"], t.BO)
+    assert (a.total_nodes, a.gpus) == (8, 4)
+    monkeypatch.setenv("ALLRED_GPUS", "2")
+    a = t.parse_args(["allred_BO_2D", "0", "1", "4", "13", "40", "32", "0", "1"], t.BO)
+    assert a.gpus == 2
+    monkeypatch.delenv("ALLRED_GPUS")
+    assert t.parse_args(["allred_BO_2D", "0", "1", "4"], t.BO).gpus == 0
+    with pytest.raises(t.AllredError):
+        t.parse_args(["allred_BO_2D", "0", "1", "4", "13", "40", "32", "0", "1", "8", "x"], t.BO)
+    for argv, variant, want in (
+            (["allred_BO_2D", "0", "1", "4", "13", "40", "32", "0", "1", "8", "3"], t.BO, _lib.ERR_ARG),
+            (["allred_BO_2D", "0", "1", "2", "13", "40", "32", "0", "1", "4", "8"], t.BO, _lib.ERR_ARG),
+            (["allred_mem_2D", "1", "1", "4", "13", "40", "32", "0", "0", "8", "2"], t.MEM, _lib.ERR_UNSUPPORTED)):
+        a = t.parse_args(argv, variant)
+        r = _lib.Report()
+        assert _lib.lib.allred_run(C.byref(a), 0, C.byref(r)) == want, argv

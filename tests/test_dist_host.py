@@ -116,6 +116,60 @@ def expected(variant, algo, world, local, data, C):
     return [[p.copy() for _ in range(local)] for p in partials]
 
 
+def mem_worker(rank, world, port, q):
+    """mem_2D over the RCCL program (local_ranks == 1): the pairwise all-to-all
+    rounds, the owner's ordered sum (own copy first, then ranks in order; fp32
+    rounded once, or the reference's bf16 accumulation), the all-gather — the
+    host twin over gloo bit-exact against the oracle's allred_mem_2D restatement."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    import tenstorrentallreduce_amd as t
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    side, total = GRIDS[world]
+    n = 8 * total * 24
+    fails = []
+    for acc in (t.ACC_FP32, t.ACC_BF16):
+        data = inputs(world, 1, n, seed=900 + 10 * world + acc)
+        buf = data[rank][0].copy()
+        scratch = np.zeros(2 * n, dtype=np.uint16)
+        desc = t.dist_desc(t.SWING, t.MEM, side, total, n, mem_accum=acc)
+        t.dist_allreduce_host(desc, rank, buf, scratch, gloo_exchange)
+        want = [d[0].copy() for d in data]
+        oracle.allreduce("mem", 1, side, want, total, acc16=acc == t.ACC_BF16)
+        if not np.array_equal(buf, want[rank]):
+            fails.append((acc, int((buf != want[rank]).sum())))
+    st = t.dist_program_stats(t.dist_desc(t.SWING, t.MEM, side, total, n), rank)
+    if st != {"steps": 2, "add_launches": 1, "segments": 4 * (world - 1)}:
+        fails.append(("stats", st))
+    try:   # hierarchical mem_2D is not an RCCL program
+        t.dist_allreduce_host(t.dist_desc(t.SWING, t.MEM, side, total, n, local_ranks=4, local_side=2), rank,
+                              np.zeros(4 * n, np.uint16), np.zeros(2 * n, np.uint16), gloo_exchange)
+        fails.append("hierarchical mem accepted")
+    except t.AllredError:
+        pass
+    dist.barrier()
+    dist.destroy_process_group()
+    q.put((rank, fails))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_mem_program_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=mem_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, fails in results:
+        assert fails == [], (rank, fails)
+
+
 def worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)

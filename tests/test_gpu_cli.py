@@ -143,3 +143,57 @@ def test_profile_log_per_rank_zones(argv, bo, tmp_path):
     assert min(starts) == 0 and max(starts) < min(ends)
     # zones lie inside the event-timed device interval (100 MHz ticks), with slack for clock skew
     assert max(ends) <= rep["device_s"] * 1e8 * 1.2 + 200
+
+
+@pytest.mark.parametrize("binary,argv", [
+    ("allred_BO_2D", ["0", "1", "4", "13", "40", "32", "0", "1"]),   # BASELINE config 3's invocation (4x2 RecDub BO)
+    ("allred_BO_2D", ["1", "1", "4", "13", "40", "32", "0", "1"]),   # Swing BO, the config-4 program at 640 kB
+    ("allred_BO_2D", ["1", "1", "4", "13", "16", "32", "0", "0"]),   # config 5's Swing LO (32 kB)
+    ("allred_BO_2D", ["1", "1", "8", "13", "5", "32", "0", "1"]),    # config 2's 64 ranks
+    ("allred_mem_2D", ["1", "1", "4", "13", "40", "32"]),            # mem_2D, all ranks on the one GPU
+    ("allred_LO_2D", ["0", "1", "4", "13", "4", "32"]),
+])
+@pytest.mark.parametrize("via", ["env", "argv"])
+def test_gpus_extension_one_gpu(binary, argv, via):
+    """The multi-GPU mode of the reference executables (ALLRED_GPUS or argv[10]:
+    one host thread and one RCCL rank per GPU, ncclCommInitAll) at G = 1: the
+    rank grid's ranks all on GPU 0 (the local tree of the reference's own
+    (side, total) grid, a 1-rank RCCL program, the broadcast), every rank checked
+    with the reference's validate_result_vector; exact (error 0) under the RNE
+    ctor, where the result is RNE(a+b) * N/2 for every tree."""
+    nodes = "8" if argv[2] == "4" else "64"
+    env = {"ALLRED_NODES": nodes, "ALLRED_BF16_ROUND": "rne"}
+    args = list(argv)
+    args[5] = "0"   # error 0
+    if via == "env":
+        env["ALLRED_GPUS"] = "1"
+    else:
+        args = args + ["0"] * (8 - len(args)) + [nodes, "1"]
+    out, rep = run(binary, args, **env)
+    assert "All values match!" in out, out
+    assert rep["mismatches"] == 0 and rep["max_error"] == 0 and rep["ranks"] == int(nodes)
+    assert rep["launches"] == -1 and rep["device_s"] > 0
+
+
+def test_gpus_extension_rejects_more_gpus_than_visible():
+    import torch
+    p = t.run_cli("allred_BO_2D", ["0", "1", "4", "13", "40", "32", "0", "1"],
+                  env={"ALLRED_NODES": "8", "ALLRED_GPUS": str(2 * max(1, torch.cuda.device_count()))})
+    assert p.returncode == 1 and "argument" in p.stderr.lower()
+
+
+def test_comm_init_all_mem_one_rank():
+    """allred_comm_init_all on one device and the mem_2D variant of the RCCL
+    program (local_ranks == 1) on a 1-rank grid: the bucket comes back unchanged."""
+    import numpy as np
+    import torch
+    comms = t.Comm.init_all([0])
+    n = 8 * 1024
+    x = torch.randint(0x3F80, 0x42C8, (n,), dtype=torch.int32).to(torch.int16).to("cuda:0")
+    want = x.clone()
+    desc = t.dist_desc(t.SWING, t.MEM, 1, 1, n)
+    ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device="cuda:0")
+    t.dist_allreduce(comms[0], desc, x.data_ptr(), ws.data_ptr(), torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    assert torch.equal(x, want)
+    comms[0].close()
