@@ -126,7 +126,7 @@ def pmc_traffic(kernel: str):
         return None
 
 
-def tilesum(stream, steps: int, reps: int) -> dict:
+def tilesum(stream, steps: int, reps: int, sizes=(256 << 20, 1 << 30)) -> dict:
     """The local tile-sum (north_star: >= 70 % of per-GPU HBM peak): dst += src
     in bf16 through allred_bf16_add (k_add, the per-step add of
     allred_BO_2D/kernels/compute_kernel.cpp:53-60 over a whole bucket) at 256 MiB
@@ -134,7 +134,7 @@ def tilesum(stream, steps: int, reps: int) -> dict:
     (fp32 add, RNE to bf16), then timed: R repetitions of K back-to-back adds,
     median; algorithmic bytes 3 * n * 2 (two reads, one write) per launch."""
     out = {}
-    for nbytes in (256 << 20, 1 << 30):
+    for nbytes in sizes:
         n = nbytes // 2
         g = torch.Generator(device="cuda:0").manual_seed(nbytes & 0xFFFF)
         dst = (torch.rand(n, generator=g, device="cuda:0") * 100).to(torch.bfloat16)
@@ -1226,6 +1226,9 @@ def main():
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the extras may take before the headline line is printed without them")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
+    ap.add_argument("--tilesum-only", type=int, nargs="*", default=None, metavar="MIB",
+                    help="only the tile-sum part of the N = 1 line, at these sizes in MiB (default 256 1024; "
+                         "for rocprofv3 runs)")
     ap.add_argument("--force-dist", action="store_true", help="run the N>1 code path on one GPU (1-rank RCCL)")
     ap.add_argument("--share-gpu", action="store_true",
                     help="rehearsal: every rank on cuda:0, peer transports only (no RCCL); not a measurement")
@@ -1253,6 +1256,9 @@ def main():
             sys.stderr.flush()
             os._exit(0)
         dist.destroy_process_group()
+    elif args.tilesum_only is not None:
+        sizes = [m << 20 for m in (args.tilesum_only or [256, 1024])]
+        out = {"tilesum": tilesum(torch.cuda.Stream(device="cuda:0"), args.steps, max(1, args.reps), sizes)}
     else:
         out = bench_single(args)
         if args.cpu and not args.main_only:

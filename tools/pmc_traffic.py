@@ -3,7 +3,8 @@
   python tools/pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> \
       <kernel-substring> <key> <algorithmic_bytes_per_launch> [out.json]
 
-<key> is the kernel template the bench launches (bench.py FUSED_KERNEL, e.g.
+<kernel-substring> "=k_hier_x" matches that short kernel name exactly (not
+k_hier_x2<...>).  <key> is the kernel template the bench launches (bench.py FUSED_KERNEL, e.g.
 k_tree_lds_lag<64>); it is stored as "template" with the full Kernel_Name the
 counters were taken on and the git sha of the build (env PMC_GIT_SHA: the GPU
 box has no .git), so bench.py only reports traffic measured on its kernel.
@@ -20,10 +21,33 @@ import sys
 from collections import defaultdict
 
 
+def short_name(kernel_name):
+    """'void tsa::(anonymous namespace)::k_hier_x2<false>(unsigned short*, ...)' -> 'k_hier_x2<false>'"""
+    s = kernel_name[5:] if kernel_name.startswith("void ") else kernel_name
+    depth, cut = 0, len(s)
+    for i, ch in enumerate(s):   # the argument list: the first '(' outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0 and not s[i:].startswith("(anonymous"):
+            cut = i
+            break
+    s = s[:cut]
+    return s.replace("tsa::", "").replace("(anonymous namespace)::", "")
+
+
+def matches(kernel_name, kernel_sub):
+    """kernel_sub '=name': the kernel's short name exactly (k_hier_x is not k_hier_x2<...>); else a substring"""
+    if kernel_sub.startswith("="):
+        return short_name(kernel_name) == kernel_sub[1:]
+    return kernel_sub in kernel_name
+
+
 def per_dispatch(path, counter, kernel_sub, names=None):
     vals = defaultdict(float)
     for r in csv.DictReader(open(path)):
-        if kernel_sub not in r.get("Kernel_Name", ""):
+        if not matches(r.get("Kernel_Name", ""), kernel_sub):
             continue
         if r.get("Counter_Name") != counter:
             continue
