@@ -817,6 +817,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     torch.cuda.synchronize()
     ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)
     partial = torch.empty(ELEMS, dtype=torch.int16, device=dev)
+    partial2 = torch.zeros(ELEMS, dtype=torch.int16, device=dev)
+    ws2 = torch.empty(2 * t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)   # rccl_x: two parities
     vbuf = torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev)   # verification bucket
     t_start = time.perf_counter()
 
@@ -845,21 +847,32 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         per = [m / args.steps for m in ms.tolist()]
         return statistics.median(per), per
 
-    def local_phases_ms():   # tree reduce of the 64 ranks + broadcast: the HBM kernels alone
+    def local_phases_ms(fused=False):
+        """the HBM kernels of the launch transports alone, ms per step: the tree
+        reduce of the 64 ranks + the broadcast of the same bucket (rccl,
+        peer_swing), or (fused) bucket i+1's tree and bucket i's broadcast in one
+        pass (k_tree_bcast_x, rccl_x)"""
         torch.cuda.synchronize()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for i in range(args.steps):
             b = bufs[i % len(bufs)]
-            t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, partial.data_ptr(), stream)
-            t.broadcast(b.data_ptr(), ELEMS, ELEMS, RANKS, partial.data_ptr(), stream)
+            if fused:
+                nb = bufs[(i + 1) % len(bufs)]
+                t.tree_broadcast_pipelined(nb.data_ptr(), b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS,
+                                           partial.data_ptr(), partial2.data_ptr(), stream)
+            else:
+                t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, partial.data_ptr(), stream)
+                t.broadcast(b.data_ptr(), ELEMS, ELEMS, RANKS, partial.data_ptr(), stream)
         e1.record(stream)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / args.steps
 
     # Inter-GPU transport: the candidates for the hierarchical step
     #   rccl        tree -> 2D Swing BO over RCCL -> broadcast (3 launches + RCCL groups)
+    #   rccl_x      the same, consecutive buckets pipelined: bucket i's broadcast and bucket
+    #               i+1's tree in ONE pass (k_tree_bcast_x), then bucket i+1's RCCL program
     #   peer_launches  tree -> mem_2D across GPUs over peer windows (launches) -> broadcast
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
@@ -880,6 +893,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
     pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
+    pend3 = [False]   # rccl_x: a bucket is started and not finished (flush())
     tail = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
@@ -890,6 +904,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
 
     def flush():
         peer = peer_box[0]
+        if pend3[0]:
+            t.dist_allreduce_pipelined(comm, desc, None, ws2.data_ptr(), stream)
+            pend3[0] = False
         if pend[0] is not None:
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
@@ -902,21 +919,26 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         peer = peer_box[0]
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
+        if kind == "rccl_x":   # buckets pipelined: this call writes the previous one's rows
+            if pend[0] is not None or pend2[0]:
+                flush()
+            t.dist_allreduce_pipelined(comm, desc, b.data_ptr(), ws2.data_ptr(), stream)
+            pend3[0] = True
+            return
         if kind == "peer_hier_x":   # buckets pipelined: this call finishes the previous one
-            if pend2[0]:
+            if pend2[0] or pend3[0]:
                 flush()
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
             pend[0] = b.data_ptr()
             return
         if kind in ("peer_hier_x2", "peer_hier_x2t"):   # two deep: this call writes the bucket started two calls ago
-            if pend[0] is not None or (pend2[0] and pend2[0] != kind):
+            if pend[0] is not None or pend3[0] or (pend2[0] and pend2[0] != kind):
                 flush()
             x2_tail(kind == "peer_hier_x2t")
             peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
             pend2[0] = kind
             return
-        if peer is not None:
-            flush()
+        flush()
         if kind == "rccl":
             t.dist_allreduce(comm, desc, b.data_ptr(), ws.data_ptr(), stream)
         elif kind == "peer_swing":
@@ -936,12 +958,12 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
 
         def once(b):
             run(kind, b, fresh=True)
-            if peer is not None:
-                flush()
+            flush()
 
         status = (lambda: peer.status() & t.PEER_TIMEOUT) if kind != "rccl" else None
         v = verify_transport(once, vbuf, world, rank, RANKS, SIDE, side, seed, status=status)
-        same_as = {"peer_swing": "rccl"}.get(kind, None if kind in ("rccl", "peer_launches") else "peer_launches")
+        same_as = {"peer_swing": "rccl", "rccl_x": "rccl"}.get(kind, None if kind in ("rccl", "peer_launches")
+                                                                     else "peer_launches")
         if same_as == "rccl" and not verify.get("rccl", {}).get("verified"):
             same_as = None   # --share-gpu: no RCCL to compare with (the Swing trees differ from mem_2D's)
         if v["verified"] and same_as:   # random real data: bit-identical to the form of the same semantics
@@ -950,8 +972,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 a, b2 = buf.clone(), buf.clone()
                 run(same_as, a, fresh=True)
                 run(kind, b2)
-                if peer is not None:
-                    flush()
+                flush()
                 torch.cuda.synchronize()
                 ok = torch.equal(a, b2) and not (status and status())
                 del a, b2
@@ -966,6 +987,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     # RCCL first, verified before any number of it is measured: the watchdog's
     # fallback line below is only ever an RCCL number that passed both checks
     rccl_ok = comm is not None and check("rccl", 9000)
+    rccl_x_ok = rccl_ok and check("rccl_x", 9050)
     peer_guard = None
     if rccl_ok:
         note(rank, "fallback headline over RCCL")
@@ -997,7 +1019,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     if peer is None and not rccl_ok:
         raise RuntimeError("no verified transport: RCCL " + (comm_err or ("unverified" if comm else "absent")) +
                            f", peer windows: {peer_err}")
-    candidates = ["rccl"] if rccl_ok else []
+    candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
     if peer is not None:
         for i, kind in enumerate(("peer_launches", "peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe",
                                   "peer_hier_x", "peer_hier_x2", "peer_hier_x2t")):
@@ -1013,7 +1035,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         note(rank, f"quick timing: {kind}")
         it = iter(range(1 << 30))
         quick[kind] = round(statistics.median(
-            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush if peer else None)
+            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
             for _ in range(3)), 4)
     transport = choose_transport(quick, verify)
 
@@ -1029,11 +1051,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         step(i)
     for i in range(args.warmup):
         step(i)
-    if peer is not None:
-        flush()
+    flush()
     t0 = time.perf_counter()
-    # peer_hier_x / _x2: the finishing launch is part of each repetition's K steps
-    ms_per_step, rep_ms = timed_steps(step, after=flush if peer is not None else None)
+    # rccl_x / peer_hier_x / _x2: the finishing launch is part of each repetition's K steps
+    ms_per_step, rep_ms = timed_steps(step, after=flush)
     wall = time.perf_counter() - t0
     peer_timeout = False
     if transport != "rccl" and peer is not None:
@@ -1045,21 +1066,24 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             if not rccl_ok:
                 raise RuntimeError(f"peer transport {transport} timed out during the timed steps: no valid number")
             note(rank, f"{transport} timed out in the timed loop: timing the RCCL transport instead")
-            transport = "rccl"
+            transport = "rccl_x" if rccl_x_ok and quick.get("rccl_x", 1e9) < quick.get("rccl", 1e9) else "rccl"
             for i in range(args.warmup):
                 step(i)
-            ms_per_step, rep_ms = timed_steps(step)
+            ms_per_step, rep_ms = timed_steps(step, after=flush)
     if peer is not None:   # defaults again for the extras below
         peer.set_oneshot_max(4 << 20)
         peer.set_hier_ll(0)
         mode[0] = None
-    local_ms = local_phases_ms()
+    local_ms = local_phases_ms(fused=transport == "rccl_x")
+    local_split_ms = local_phases_ms() if transport == "rccl_x" else local_ms
     if peer_guard is not None:   # the headline is measured: the extras have their own watchdog
         peer_guard.cancel()
     HEADLINE_DONE.set()
 
     extras = {"headline_transport": transport, "transport_verified": verify, "transport_quick_ms": quick,
               "peer_timeout_in_timed_loop": peer_timeout,
+              "local_phases_ms": {"tree_then_broadcast": round(local_split_ms, 6),
+                                  **({"tree_broadcast_fused": round(local_ms, 6)} if transport == "rccl_x" else {})},
               "timing": {"repetitions": len(rep_ms), "ms_per_step_per_repetition": [round(x, 6) for x in rep_ms],
                          "ms_per_step": "median repetition (each: the K steps, max over ranks)"}}
     if peer_err:
@@ -1108,7 +1132,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         peer.close()
     if comm is not None:
         comm.close()
-    del bufs, vbuf, ws
+    del bufs, vbuf, ws, ws2
     torch.cuda.synchronize()
     # rank 0 alone (the others wait at the barrier): the reference's program surface
     # across this node's GPUs (config 3), then the CPU baseline of configs 3-5
@@ -1152,6 +1176,10 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
         kern = ONE_LAUNCH[transport]
         roof = {"kernel": f"{kern} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9, "traffic": pmc_traffic(kern)}
+    elif transport == "rccl_x":   # the local HBM pass: bucket i's broadcast + bucket i+1's tree in one kernel
+        roof = {"kernel": "k_tree_bcast_x (local phases of consecutive buckets, one pass)",
+                "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9,
+                "traffic": pmc_traffic("k_tree_bcast_x")}
     else:
         tr, bc = pmc_traffic("k_tree_lds_pipe<64, false>"), pmc_traffic("k_broadcast")
         roof = {"kernel": "k_tree_lds_pipe<64, false> + k_broadcast (local phases)",
@@ -1159,6 +1187,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                 "traffic": tr + bc if tr and bc else None}
     achieved = roof["achieved"]
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
+           "rccl_x": "consecutive buckets pipelined (K buckets in K + 1 calls, all inside the timed region): "
+                     "bucket i's broadcast and bucket i+1's on-GPU tree reduce in one HBM pass, then bucket i+1's "
+                     "2D Swing BO over RCCL/xGMI",
            "peer_launches": "on-GPU tree reduce, mem_2D across GPUs over peer-mapped windows (launches), broadcast",
            "peer_swing": "on-GPU tree reduce, 2D Swing BO over peer-mapped xGMI windows (one kernel), broadcast",
            "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "

@@ -344,6 +344,27 @@ size_t allred_dist_workspace_bytes(const allred_dist_desc* desc);
 int allred_dist_allreduce(allred_comm* comm, const allred_dist_desc* desc, uint16_t* buf,
                           void* workspace, void* stream);
 
+/* The hierarchical step (local_ranks > 1, BO / LO) PIPELINED across consecutive
+ * buckets: the call with `cur` reduces cur's local ranks to its partial (the
+ * local tree), FUSED with writing the previous call's bucket's rows from its
+ * allreduced partial (one HBM pass, k_tree_bcast_x, reads and writes of the two
+ * buckets overlapping), then runs the RCCL program on cur's partial; cur ==
+ * NULL (flush) writes the last pending bucket's rows.  K buckets = K + 1 calls:
+ * b0, b1, ..., b_{K-1}, NULL.  A bucket's rows are final, in stream order,
+ * after the next call (or the flush): keep it alive until then.  workspace:
+ * 2 * allred_dist_workspace_bytes(desc) bytes (two parities), the same on every
+ * call of a sequence; every call of a sequence has the same elems and
+ * local_ranks (else ALLRED_ERR_ARG).  Same result bits as allred_dist_allreduce
+ * per bucket.  The reference runs one vector per program: no counterpart. */
+int allred_dist_allreduce_pipelined(allred_comm* comm, const allred_dist_desc* desc, uint16_t* cur, void* workspace,
+                                    void* stream);
+/* The two local phases of the pipelined step as one call: cur's tree (local
+ * rank 0's, as allred_tree_reduce) into cur_out, and prev_src to every one of
+ * prev's `total` rank rows (as allred_broadcast). */
+int allred_tree_broadcast_pipelined(uint16_t* cur, uint16_t* prev, uint64_t rank_stride, size_t n, int algo,
+                                    int side_length, int total_nodes, uint16_t* cur_out, const uint16_t* prev_src,
+                                    void* stream);
+
 /* The per-rank program allred_dist_allreduce (and its host twin) runs for
  * `desc`: steps = exchange steps (one RCCL group each), add_launches = add
  * kernels it enqueues over all steps (one per reduce-scatter / LO step,

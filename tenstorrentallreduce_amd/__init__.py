@@ -27,7 +27,7 @@ __all__ = [
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
     "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
-    "dist_allreduce_host", "dist_workspace_bytes", "dist_program_stats", "Peer", "tune", "tuned", "ACC_FP32",
+    "dist_allreduce_host", "dist_allreduce_pipelined", "tree_broadcast_pipelined", "dist_workspace_bytes", "dist_program_stats", "Peer", "tune", "tuned", "ACC_FP32",
     "ACC_BF16",
 ]
 
@@ -309,6 +309,19 @@ def dist_program_stats(desc: DistDesc, rank: int) -> dict:
 def dist_allreduce(comm: Comm, desc: DistDesc, buf_ptr: int, workspace_ptr: int, stream=None) -> None:
     check(lib.allred_dist_allreduce(comm._h, C.byref(desc), buf_ptr, workspace_ptr, _stream_ptr(stream)),
           "dist_allreduce")
+
+
+def dist_allreduce_pipelined(comm: Comm, desc: DistDesc, cur_ptr: int | None, workspace_ptr: int, stream=None) -> None:
+    """The hierarchical step pipelined across buckets (allred_dist_allreduce_pipelined):
+    K buckets = K + 1 calls b0, b1, ..., None; workspace = 2 * dist_workspace_bytes(desc)."""
+    check(lib.allred_dist_allreduce_pipelined(comm._h, C.byref(desc), cur_ptr or None, workspace_ptr,
+                                              _stream_ptr(stream)), "dist_allreduce_pipelined")
+
+
+def tree_broadcast_pipelined(cur_ptr: int, prev_ptr: int, stride: int, n: int, algo: int, side: int, total: int,
+                             cur_out_ptr: int, prev_src_ptr: int, stream=None) -> None:
+    check(lib.allred_tree_broadcast_pipelined(cur_ptr, prev_ptr, stride, n, algo, side, total, cur_out_ptr,
+                                              prev_src_ptr, _stream_ptr(stream)), "tree_broadcast_pipelined")
 
 
 def dist_allreduce_host(desc: DistDesc, rank: int, buf: np.ndarray, scratch: np.ndarray,

@@ -150,6 +150,9 @@ SIGNATURES = [
     ("allred_comm_destroy", C.c_int, [_P]),
     ("allred_dist_workspace_bytes", C.c_size_t, [C.POINTER(DistDesc)]),
     ("allred_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
+    ("allred_dist_allreduce_pipelined", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
+    ("allred_tree_broadcast_pipelined", C.c_int,
+     [_u16p, _u16p, C.c_uint64, C.c_size_t, C.c_int, C.c_int, C.c_int, _u16p, _u16p, _P]),
     ("allred_dist_program_stats", C.c_int,
      [C.POINTER(DistDesc), C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("allred_dist_allreduce_host", C.c_int, [C.POINTER(DistDesc), C.c_int, _u16p, _u16p, EXCHANGE_FN, _P]),

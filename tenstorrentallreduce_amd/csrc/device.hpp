@@ -223,6 +223,16 @@ __device__ __forceinline__ void lds_dma16(const void* src, uint32_t lds_base) {
 }
 #pragma clang diagnostic pop
 
+// the 64-byte tree order, one byte per lane of wave 0, loaded by inline asm: the
+// compiler would follow its own load with vmcnt(0) before staging it, so the
+// tiles' LDS-DMA loads (invisible to it) would wait behind the order's round
+// trip; here they go out right behind it and only the byte is waited for
+__device__ __forceinline__ uint32_t order_byte_load(const uint8_t* order, int lane) {
+    uint32_t b;
+    asm volatile("global_load_ubyte %0, %1, off" : "=v"(b) : "v"(order + lane) : "memory");
+    return b;
+}
+
 // workgroup barrier without the release fence of __syncthreads (which waits
 // vmcnt(0)); LDS traffic is ordered by the lgkmcnt wait
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }

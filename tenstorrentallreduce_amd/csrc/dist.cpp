@@ -36,6 +36,12 @@ using namespace tsa;
 struct allred_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    // allred_dist_allreduce_pipelined: the bucket started by the last call (its rows are
+    // written by the next call or the flush) and its allreduced partial in the workspace
+    uint16_t* pend = nullptr;
+    uint16_t* pend_partial = nullptr;
+    int pend_parity = 0, pend_local = 0;
+    size_t pend_elems = 0;
 };
 
 namespace {
@@ -364,6 +370,9 @@ void host_rows_sum(const uint16_t* rows, size_t stride, size_t n, int nrows, boo
     }
 }
 
+int run_program(allred_comm* c, const allred_dist_desc* d, const allred_schedule& s, uint16_t* bucket,
+                uint16_t* staging, void* stream);
+
 }  // namespace
 
 namespace tsa {
@@ -525,6 +534,64 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
         st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
+    st = run_program(c, d, s, bucket, staging, stream);
+    if (st == ALLRED_OK && d->local_ranks > 1) st = launch_broadcast(buf, n, n, d->local_ranks, bucket, stream);
+    return st;
+}
+
+int allred_dist_allreduce_pipelined(allred_comm* c, const allred_dist_desc* d, uint16_t* cur, void* workspace,
+                                    void* stream) {
+    if (!c || !d || !workspace) return ALLRED_ERR_ARG;
+    if (!cur) {   // flush: the pending bucket's rows from its allreduced partial
+        if (!c->pend) return ALLRED_ERR_ARG;
+        const int st = launch_broadcast(c->pend, c->pend_elems, c->pend_elems, c->pend_local, c->pend_partial, stream);
+        c->pend = nullptr;
+        return st;
+    }
+    allred_schedule s;
+    int st = check_desc(d, &s);
+    if (st != ALLRED_OK) return st;
+    if (d->total_nodes != c->nranks || d->local_ranks < 2 || d->variant == ALLRED_MEM) return ALLRED_ERR_ARG;
+    if (((uintptr_t)cur | (uintptr_t)workspace) % 16) return ALLRED_ERR_ARG;
+    const size_t n = (size_t)d->elems;
+    if (c->pend && (n != c->pend_elems || d->local_ranks != c->pend_local)) return ALLRED_ERR_ARG;
+    // two parities of [staging n | partial n]: the pending bucket's partial survives this call
+    const int parity = c->pend ? c->pend_parity ^ 1 : 0;
+    uint16_t* staging = static_cast<uint16_t*>(workspace) + (size_t)parity * 2 * n;
+    uint16_t* partial = staging + n;
+    const uint8_t* order = nullptr;
+    if ((st = local_tree_order(d->local_algo, d->local_side, d->local_ranks, &order)) != ALLRED_OK) return st;
+    st = c->pend ? launch_tree_bcast_x(cur, c->pend, n, n, d->local_ranks, order, partial, c->pend_partial, stream)
+                 : launch_tree_reduce(cur, n, n, d->local_ranks, order, partial, stream);
+    if (st != ALLRED_OK) return st;
+    c->pend = cur;   // from here on the bucket is started: its rows are written by the next call or the flush
+    c->pend_partial = partial;
+    c->pend_parity = parity;
+    c->pend_elems = n;
+    c->pend_local = d->local_ranks;
+    return run_program(c, d, s, partial, staging, stream);
+}
+
+int allred_tree_broadcast_pipelined(uint16_t* cur, uint16_t* prev, uint64_t stride, size_t n, int algo, int side,
+                                    int total, uint16_t* cur_out, const uint16_t* prev_src, void* stream) {
+    if (!cur || !prev || !cur_out || !prev_src || stride < n) return ALLRED_ERR_ARG;
+    const uint8_t* order = nullptr;
+    int st = device_order(algo, side, total, &order);
+    if (st != ALLRED_OK) return st;
+    return launch_tree_bcast_x(cur, prev, stride, n, total, order, cur_out, prev_src, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+// the exchange steps of the rank's program on `bucket` (reduce-scatter adds staged in
+// `staging`), after the local tree; the caller broadcasts
+int run_program(allred_comm* c, const allred_dist_desc* d, const allred_schedule& s, uint16_t* bucket,
+                uint16_t* staging, void* stream) {
+    hipStream_t hs = (hipStream_t)stream;
+    const size_t n = (size_t)d->elems;
+    int st = ALLRED_OK;
     const int C = channels_for(s, d->channels, n);
     const auto prog = cached_program(d, s, c->rank, C);
     const bool check = tune(Tune::check) != 0;
@@ -554,9 +621,12 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
             if (st != ALLRED_OK) return st;
         }
     }
-    if (d->local_ranks > 1) st = launch_broadcast(buf, n, n, d->local_ranks, bucket, stream);
-    return st;
+    return ALLRED_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int allred_dist_program_stats(const allred_dist_desc* d, int rank, int* steps, int* launches, int* segments) {
     allred_schedule s;

@@ -86,6 +86,10 @@ int launch_rows_sum(const uint16_t* rows, uint64_t stride, size_t n, int nrows, 
                     void* stream);
 // allred_run with args->gpus > 0 (dist.cpp): the program over G GPUs, one host thread each
 int run_multi_gpu(const allred_args* a, int verbose, allred_report* report);
+// bucket i+1's tree (-> cur_partial) and bucket i's broadcast (prev_result -> prev's rows) in one
+// pass (k_tree_bcast_x; 64 ranks, whole tiles) or the two launches (same bits)
+int launch_tree_bcast_x(uint16_t* cur, uint16_t* prev, uint64_t stride, size_t n, int total, const uint8_t* order,
+                        uint16_t* cur_partial, const uint16_t* prev_result, void* stream);
 // the mem_2D validation of one rank's result and the per-rank profile zones (engine.cpp)
 int write_profile_log(const char* path, int N, int side, const uint64_t* start, const uint64_t* end);
 // the schedule form as one persistent launch (k_bo_steps / k_lo_steps).  BO: d_tab = per block

@@ -337,6 +337,108 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// k_tree_bcast_x: the two HBM phases of the hierarchical step of CONSECUTIVE
+// buckets in one pass (allred_dist_allreduce_pipelined: tree -> RCCL program ->
+// broadcast per bucket, the broadcast of bucket i and the tree of bucket i+1
+// fused).  Tile j: bucket i+1's 64 rank rows are reduced with the tree of rank 0
+// of the local grid into its partial (one row out, same tree and bits as
+// k_tree_lds_pipe<64, false>), and bucket i's allreduced partial tile is
+// written to bucket i's 64 rank rows (k_broadcast's data movement).  Reads and
+// writes of the two buckets overlap as in the fused one-bucket pass, where one
+// bucket's tree then broadcast run as a read-only launch, then a write-only one.
+// Schedule (k_tree_lds_lag's, stores not lagged: their data does not depend on
+// the tree): iteration j waits for tile j's loads (bucket i+1's rows by LDS-DMA,
+// and — wave 0 — bucket i's result tile by LDS-DMA into a small slot), reduces
+// tile j, writes its partial (wave 0), then issues tile j+2's loads interleaved
+// op by op with the 64 row stores of bucket i's tile j.  Per-wave exact vmcnt:
+// wave 0 issues the result loads and the partial stores, the others do not.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
+                                                         uint64_t stride, const uint8_t* __restrict__ order,
+                                                         uint16_t* __restrict__ cur_partial,
+                                                         const uint16_t* __restrict__ prev_result, uint64_t t0,
+                                                         uint64_t ntiles) {
+    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    static_assert(2 * OPS + 3 <= 63, "vmcnt is 6 bits");
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
+    __shared__ __attribute__((aligned(16))) uint4 res_lds[2][64];   // bucket i's result tile (1 KiB: two copies)
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const bool w0 = w == 0;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    const uint32_t rbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&res_lds[0][0]);
+    auto crow = [&](int k) { return cur + (uint64_t)(RPW * w + RPI * k + q) * stride; };
+    auto prow = [&](int k) { return prev + (uint64_t)(RPW * w + RPI * k + q) * stride; };
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return t0 + blockIdx.x + (uint64_t)j * G; };
+    auto issue_loads = [&](int j) {   // tile j of bucket i+1 into buf[j & 1]; wave 0: bucket i's result tile j
+        const uint64_t t = tile_of(j);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(crow(k)) + t * TV + c,
+                      wbase + (uint32_t)((j & 1) * P * TV * 16 + RPI * k * TV * 16));
+        if (w0) lds_dma16(reinterpret_cast<const uint4*>(prev_result) + t * TV + c, rbase + (uint32_t)((j & 1) * 1024));
+    };
+    const int own = w0 ? 1 : 0;   // wave 0's extra ops per tile: the result load (and the partial store)
+    // the 64-byte tree order of local rank 0 (one byte per lane of wave 0), ahead of the first tiles' loads
+    uint32_t ob = 0;
+    if (w0) ob = order_byte_load(order, lane);
+    if (mine > 0) issue_loads(0);
+    if (mine > 1) issue_loads(1);
+    if (w0) {
+        wait_any((mine > 0 ? OPS + 1 : 0) + (mine > 1 ? OPS + 1 : 0));
+        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
+        ord_lds[lane] = (uint8_t)ob;
+    }
+    lds_barrier();
+    for (int j = 0; j < mine; ++j) {
+        // ops issued after tile j's last load: j = 0 -> tile 1's loads; j = 1 -> iteration 0;
+        // j >= 2 -> the last store of iteration j-2 (behind the last DMA; wave 0's result load
+        // comes after it) and iteration j-1: partial (wave 0), tile j+1's loads, 64 row stores
+        const int next = j + 1 < mine ? OPS + own : 0;
+        if (j == 0) wait_any(next);
+        else wait_any((j >= 2 && !w0 ? 1 : 0) + own + next + OPS);
+        lds_barrier();   // every wave's rows of tile j and wave 0's result tile are in LDS
+        const uint4* tile = buf[j & 1];
+        const uint64_t t = tile_of(j), v0 = t * TV;
+        const uint4 pres = res_lds[j & 1][c];   // bucket i's result, read before the slot is reloaded
+        const uint8_t* ord = ord_lds + RPW * w + LPL * q;
+        uint4 x[LPL];
+#pragma unroll
+        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+        for (int s = 1; s < LPL; s *= 2)
+#pragma unroll
+            for (int i = 0; i < LPL; i += 2 * s) x[i] = add8(x[i], x[i + s]);
+        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));   // tree level across the two lane halves
+        if (q == 0) part[j & 1][w * TV + c] = pw;
+        lds_barrier();   // tile j and result slot j & 1 are read by every wave; the partials are in
+        if (w0) {
+            const uint4* pp = part[j & 1];
+            const uint4 r = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
+            if (q == 0) st_nt(reinterpret_cast<uint4*>(cur_partial) + v0 + c, r);
+        }
+        {   // tile j+2's loads and bucket i's tile j row stores, interleaved op by op
+            const uint64_t tl = tile_of(j + 2);
+            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                if (j + 2 < mine)
+                    lds_dma16(reinterpret_cast<const uint4*>(crow(k)) + tl * TV + c, bl + (uint32_t)(RPI * k * TV * 16));
+                st_nt(reinterpret_cast<uint4*>(prow(k)) + v0 + c, pres);
+            }
+            if (w0 && j + 2 < mine)
+                lds_dma16(reinterpret_cast<const uint4*>(prev_result) + tl * TV + c, rbase + (uint32_t)((j & 1) * 1024));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // LO allreduce of P ranks in one pass: the butterfly itself.  Rank x keeps
 // its own tree (for Swing the P results differ in bf16 rounding, exactly as
 // the reference's per-core LO results do).  Lane (q, x) = q * P + x holds
@@ -1533,6 +1635,24 @@ int launch_tree_reduce(const uint16_t* ranks, uint64_t stride, size_t n, int tot
     if (n % 8 || stride % 8 || !aligned16(ranks) || !aligned16(out)) return ALLRED_ERR_ARG;
     return tree_dispatch<false>(const_cast<uint16_t*>(ranks), stride, n / 8, total, order, 0, out,
                                 (hipStream_t)stream);
+}
+
+int launch_tree_bcast_x(uint16_t* cur, uint16_t* prev, uint64_t stride, size_t n, int total, const uint8_t* order,
+                        uint16_t* cur_partial, const uint16_t* prev_result, void* stream) {
+    if (n % 8 || stride % 8 || stride < n || !aligned16(cur) || !aligned16(prev) || !aligned16(cur_partial) ||
+        !aligned16(prev_result))
+        return ALLRED_ERR_ARG;
+    // 64 ranks in whole 256-element tiles: one fused pass; else the two launches (same bits)
+    if (total == 64 && n % 256 == 0) {
+        hipStream_t st = (hipStream_t)stream;
+        for_each_chunk(n / 256, [&](uint64_t a, uint64_t b) {
+            hipLaunchKernelGGL(k_tree_bcast_x, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, cur, prev, stride,
+                               order, cur_partial, prev_result, a, b - a);
+        });
+        return last_error();
+    }
+    int st = launch_broadcast(prev, stride, n, total, prev_result, stream);
+    return st != ALLRED_OK ? st : launch_tree_reduce(cur, stride, n, total, order, cur_partial, stream);
 }
 
 int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, const uint16_t* src, void* stream) {

@@ -570,16 +570,6 @@ __device__ __forceinline__ uint4 ll_data(const uint64_t (&wd)[4]) {
     return make_uint4((uint32_t)wd[0], (uint32_t)wd[1], (uint32_t)wd[2], (uint32_t)wd[3]);
 }
 
-// the 64-byte tree order, one byte per lane of wave 0, loaded by inline asm: the
-// compiler would follow its own load with vmcnt(0) before staging it, so the
-// tiles' LDS-DMA loads (invisible to it) would wait behind the order's round
-// trip; here they go out right behind it and only the byte is waited for
-__device__ __forceinline__ uint32_t order_byte_load(const uint8_t* order, int lane) {
-    uint32_t b;
-    asm volatile("global_load_ubyte %0, %1, off" : "=v"(b) : "v"(order + lane) : "memory");
-    return b;
-}
-
 // the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
 // first then ascending, one rounding (allred_mem_2D semantics, k_peer_oneshot's bits)
 __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, int me) {

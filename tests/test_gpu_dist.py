@@ -61,3 +61,68 @@ def test_single_rank_rccl_comm(local):
     with pytest.raises(t.AllredError):
         t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr() + 8, torch.cuda.current_stream())
     comm.close()
+
+
+@pytest.mark.parametrize("n,total,side", [(327680, 64, 8), (64 * 8 * 5, 64, 8), (1061 * 256, 64, 8),
+                                          (8 * 8 * 40, 8, 4)])
+def test_tree_broadcast_pipelined_matches_the_two_launches(n, total, side):
+    """k_tree_bcast_x (bucket i+1's tree and bucket i's broadcast in one pass) is
+    bit-identical to tree_reduce(cur) + broadcast(prev); 8 ranks take the two
+    launches themselves."""
+    rng = np.random.default_rng(n + total)
+    cur = torch.from_numpy(rng.integers(0x3F80, 0x42C8, (total, n)).astype(np.uint16).view(np.int16)).to(DEV)
+    prev = torch.from_numpy(rng.integers(0x3F80, 0x42C8, (total, n)).astype(np.uint16).view(np.int16)).to(DEV)
+    src = torch.from_numpy(rng.integers(0x3F80, 0x42C8, n).astype(np.uint16).view(np.int16)).to(DEV)
+    for algo in (t.SWING, t.RECDUB):
+        out = torch.empty(n, dtype=torch.int16, device=DEV)
+        p2 = prev.clone()
+        t.tree_broadcast_pipelined(cur.data_ptr(), p2.data_ptr(), n, n, algo, side, total, out.data_ptr(),
+                                   src.data_ptr())
+        want = torch.empty_like(out)
+        p3 = prev.clone()
+        t.tree_reduce(cur.data_ptr(), n, n, algo, side, total, want.data_ptr())
+        t.broadcast(p3.data_ptr(), n, n, total, src.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(out, want) and torch.equal(p2, p3)
+        assert (p2 == src[None, :]).all()
+
+
+@pytest.mark.parametrize("buckets", [1, 2, 5])
+def test_dist_allreduce_pipelined_one_rank(buckets):
+    """allred_dist_allreduce_pipelined over a 1-rank communicator: K buckets in
+    K + 1 calls, each bucket bit-identical to allred_dist_allreduce of it; the
+    sequence twice (both workspace parities); protocol errors refused."""
+    comm = t.Comm(t.Comm.unique_id(), 1, 0, 0)
+    n = 327680
+    desc = t.dist_desc(t.SWING, t.BO, 1, 1, n, local_ranks=64, local_side=8, local_algo=t.SWING)
+    wsb = t.dist_workspace_bytes(desc)
+    ws = torch.empty(2 * wsb, dtype=torch.uint8, device=DEV)
+    ws1 = torch.empty(wsb, dtype=torch.uint8, device=DEV)
+    s = torch.cuda.current_stream()
+    rng = np.random.default_rng(buckets)
+    data = [torch.from_numpy(rng.integers(0x3F80, 0x42C8, (64, n)).astype(np.uint16).view(np.int16)).to(DEV)
+            for _ in range(buckets)]
+    want = []
+    for d in data:
+        x = d.clone()
+        t.dist_allreduce(comm, desc, x.data_ptr(), ws1.data_ptr(), s)
+        want.append(x)
+    for _ in range(2):
+        got = [d.clone() for d in data]
+        for g in got:
+            t.dist_allreduce_pipelined(comm, desc, g.data_ptr(), ws.data_ptr(), s)
+        t.dist_allreduce_pipelined(comm, desc, None, ws.data_ptr(), s)
+        torch.cuda.synchronize()
+        for i, (g, w) in enumerate(zip(got, want)):
+            assert torch.equal(g, w), i
+    with pytest.raises(t.AllredError):   # nothing pending
+        t.dist_allreduce_pipelined(comm, desc, None, ws.data_ptr(), s)
+    x = data[0].clone()
+    t.dist_allreduce_pipelined(comm, desc, x.data_ptr(), ws.data_ptr(), s)
+    other = t.dist_desc(t.SWING, t.BO, 1, 1, n // 2, local_ranks=64, local_side=8, local_algo=t.SWING)
+    with pytest.raises(t.AllredError):   # another bucket size mid-sequence
+        t.dist_allreduce_pipelined(comm, other, x.data_ptr(), ws.data_ptr(), s)
+    t.dist_allreduce_pipelined(comm, desc, None, ws.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(x, want[0])
+    comm.close()
