@@ -960,7 +960,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             run(kind, b, fresh=True)
             flush()
 
-        status = (lambda: peer.status() & t.PEER_TIMEOUT) if kind != "rccl" else None
+        status = (lambda: peer.status() & t.PEER_TIMEOUT) if kind.startswith("peer") else None
         v = verify_transport(once, vbuf, world, rank, RANKS, SIDE, side, seed, status=status)
         same_as = {"peer_swing": "rccl", "rccl_x": "rccl"}.get(kind, None if kind in ("rccl", "peer_launches")
                                                                      else "peer_launches")

@@ -353,6 +353,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
 // op by op with the 64 row stores of bucket i's tile j.  Per-wave exact vmcnt:
 // wave 0 issues the result loads and the partial stores, the others do not.
 // ---------------------------------------------------------------------------
+template <int LAG>   // LAG 0: bucket i's tile j rows stored in iteration j; 1: in iteration j + 1
 __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                          uint64_t stride, const uint8_t* __restrict__ order,
                                                          uint16_t* __restrict__ cur_partial,
@@ -360,6 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
                                                          uint64_t ntiles) {
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     static_assert(2 * OPS + 3 <= 63, "vmcnt is 6 bits");
+    static_assert(LAG == 0 || LAG == 1, "lag of the row stores: 0 or 1 iteration");
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
     __shared__ __attribute__((aligned(16))) uint4 res_lds[2][64];   // bucket i's result tile (1 KiB: two copies)
@@ -396,17 +398,19 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
         ord_lds[lane] = (uint8_t)ob;
     }
     lds_barrier();
+    uint4 pres = make_uint4(0, 0, 0, 0);   // LAG 1: bucket i's result of the previous tile
     for (int j = 0; j < mine; ++j) {
-        // ops issued after tile j's last load: j = 0 -> tile 1's loads; j = 1 -> iteration 0;
-        // j >= 2 -> the last store of iteration j-2 (behind the last DMA; wave 0's result load
-        // comes after it) and iteration j-1: partial (wave 0), tile j+1's loads, 64 row stores
+        // ops issued after tile j's last load (its DMAs, then wave 0's result load): j = 0 ->
+        // tile 1's loads; j = 1 -> iteration 0; j >= 2 -> the last row store interleaved behind
+        // tile j's last DMA (a store of tile j-2-LAG: non-zero waves only, wave 0's result load
+        // comes after it) and iteration j-1: partial (wave 0), tile j+1's loads, row stores
         const int next = j + 1 < mine ? OPS + own : 0;
         if (j == 0) wait_any(next);
-        else wait_any((j >= 2 && !w0 ? 1 : 0) + own + next + OPS);
+        else wait_any((j >= 2 + LAG && !w0 ? 1 : 0) + own + next + (j - 1 >= LAG ? OPS : 0));
         lds_barrier();   // every wave's rows of tile j and wave 0's result tile are in LDS
         const uint4* tile = buf[j & 1];
         const uint64_t t = tile_of(j), v0 = t * TV;
-        const uint4 pres = res_lds[j & 1][c];   // bucket i's result, read before the slot is reloaded
+        const uint4 pnew = res_lds[j & 1][c];   // bucket i's result, read before the slot is reloaded
         const uint8_t* ord = ord_lds + RPW * w + LPL * q;
         uint4 x[LPL];
 #pragma unroll
@@ -423,18 +427,24 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
             const uint4 r = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
             if (q == 0) st_nt(reinterpret_cast<uint4*>(cur_partial) + v0 + c, r);
         }
-        {   // tile j+2's loads and bucket i's tile j row stores, interleaved op by op
-            const uint64_t tl = tile_of(j + 2);
+        {   // tile j+2's loads and bucket i's row stores (tile j - LAG), interleaved op by op
+            const uint64_t tl = tile_of(j + 2), ts = tile_of(j - LAG);
+            const uint4 sv = LAG ? pres : pnew;
             const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
 #pragma unroll
             for (int k = 0; k < OPS; ++k) {
                 if (j + 2 < mine)
                     lds_dma16(reinterpret_cast<const uint4*>(crow(k)) + tl * TV + c, bl + (uint32_t)(RPI * k * TV * 16));
-                st_nt(reinterpret_cast<uint4*>(prow(k)) + v0 + c, pres);
+                if (j >= LAG) st_nt(reinterpret_cast<uint4*>(prow(k)) + ts * TV + c, sv);
             }
             if (w0 && j + 2 < mine)
                 lds_dma16(reinterpret_cast<const uint4*>(prev_result) + tl * TV + c, rbase + (uint32_t)((j & 1) * 1024));
         }
+        pres = pnew;
+    }
+    if (LAG && mine > 0) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) st_nt(reinterpret_cast<uint4*>(prow(k)) + tile_of(mine - 1) * TV + c, pres);
     }
 }
 
@@ -1646,8 +1656,12 @@ int launch_tree_bcast_x(uint16_t* cur, uint16_t* prev, uint64_t stride, size_t n
     if (total == 64 && n % 256 == 0) {
         hipStream_t st = (hipStream_t)stream;
         for_each_chunk(n / 256, [&](uint64_t a, uint64_t b) {
-            hipLaunchKernelGGL(k_tree_bcast_x, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, cur, prev, stride,
-                               order, cur_partial, prev_result, a, b - a);
+            if (tune(Tune::tree_bcast_lag))
+                hipLaunchKernelGGL(k_tree_bcast_x<1>, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, cur,
+                                   prev, stride, order, cur_partial, prev_result, a, b - a);
+            else
+                hipLaunchKernelGGL(k_tree_bcast_x<0>, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, cur,
+                                   prev, stride, order, cur_partial, prev_result, a, b - a);
         });
         return last_error();
     }
