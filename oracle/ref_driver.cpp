@@ -20,15 +20,9 @@
 #include <cmath>
 #include <vector>
 
-// prototypes exactly as allred_helper.hpp:24-30 and allred_BO_2D.cpp:4-5
-int highest_power_of_two(int);
-uint32_t get_step_directions(int, int);
-int get_comm_partner_swing_2D(int, int, bool, int, int);
-int get_comm_partner_recdub_2D(int, int, bool, int, uint32_t&, int);
-void get_swing_block_comm_indexes(int, int, uint32_t*, bool, int, int);
-void get_recdub_block_comm_indexes(int, int, uint32_t*, bool, int, int, int, uint32_t&);
-
-#include "ref_sched_src.cpp"  // generated into oracle/_ref by the Makefile
+// prototypes exactly as allred_helper.hpp:24-30 and allred_BO_2D.cpp:4-5; the
+// definitions are the reference's own, compiled by the Makefile into _ref/ref_sched.o
+#include "ref_protos.h"
 
 static void emit(bool swing, int side, int total, bool last) {
     int steps = (int)std::log2((double)total);
