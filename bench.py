@@ -1179,7 +1179,7 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
     elif transport == "rccl_x":   # the local HBM pass: bucket i's broadcast + bucket i+1's tree in one kernel
         roof = {"kernel": "k_tree_bcast_x (local phases of consecutive buckets, one pass)",
                 "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9,
-                "traffic": pmc_traffic("k_tree_bcast_x")}
+                "traffic": pmc_traffic("k_tree_bcast_x<1>")}
     else:
         tr, bc = pmc_traffic("k_tree_lds_pipe<64, false>"), pmc_traffic("k_broadcast")
         roof = {"kernel": "k_tree_lds_pipe<64, false> + k_broadcast (local phases)",
