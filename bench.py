@@ -875,6 +875,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #               i+1's tree in ONE pass (k_tree_bcast_x), then bucket i+1's RCCL program
     #   peer_launches  tree -> mem_2D across GPUs over peer windows (launches) -> broadcast
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
+    #   peer_mem_x  consecutive buckets pipelined: bucket i's broadcast and bucket i+1's tree in
+    #               one pass (k_tree_bcast_x), then bucket i+1's partial through the one-kernel
+    #               mem_2D exchange over the peer windows (k_peer_oneshot)
     #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
     #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
     #   peer_hier_pipe  the same LL hand-offs on the lagged-store pipeline (k_hier_pipe)
@@ -894,6 +897,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
     pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
     pend3 = [False]   # rccl_x: a bucket is started and not finished (flush())
+    pend4 = [None, 0]   # peer_mem_x: the started bucket and the partial slot it used (flush())
+    mem_parts = [torch.empty(ELEMS, dtype=torch.int16, device=dev) for _ in range(2)]
     tail = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
@@ -907,6 +912,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         if pend3[0]:
             t.dist_allreduce_pipelined(comm, desc, None, ws2.data_ptr(), stream)
             pend3[0] = False
+        if pend4[0] is not None:
+            t.broadcast(pend4[0], ELEMS, ELEMS, RANKS, mem_parts[pend4[1]].data_ptr(), stream)
+            pend4[0] = None
         if pend[0] is not None:
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
@@ -920,19 +928,36 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
         if kind == "rccl_x":   # buckets pipelined: this call writes the previous one's rows
-            if pend[0] is not None or pend2[0]:
+            if pend[0] is not None or pend2[0] or pend4[0] is not None:
                 flush()
             t.dist_allreduce_pipelined(comm, desc, b.data_ptr(), ws2.data_ptr(), stream)
             pend3[0] = True
             return
+        if kind == "peer_mem_x":   # buckets pipelined: this call writes the previous one's rows
+            if pend[0] is not None or pend2[0] or pend3[0]:
+                flush()
+            if mode[0] != kind:
+                peer.set_oneshot_max(4 << 20)
+                peer.set_hier_ll(0)
+                mode[0] = kind
+            slot = pend4[1] ^ 1 if pend4[0] is not None else 0
+            out = mem_parts[slot]
+            if pend4[0] is None:
+                t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, out.data_ptr(), stream)
+            else:
+                t.tree_broadcast_pipelined(b.data_ptr(), pend4[0], ELEMS, ELEMS, t.SWING, SIDE, RANKS, out.data_ptr(),
+                                           mem_parts[pend4[1]].data_ptr(), stream)
+            peer.allreduce(out.data_ptr(), ELEMS, stream)   # the partial: mem_2D across the GPUs
+            pend4[0], pend4[1] = b.data_ptr(), slot
+            return
         if kind == "peer_hier_x":   # buckets pipelined: this call finishes the previous one
-            if pend2[0] or pend3[0]:
+            if pend2[0] or pend3[0] or pend4[0] is not None:
                 flush()
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
             pend[0] = b.data_ptr()
             return
         if kind in ("peer_hier_x2", "peer_hier_x2t"):   # two deep: this call writes the bucket started two calls ago
-            if pend[0] is not None or pend3[0] or (pend2[0] and pend2[0] != kind):
+            if pend[0] is not None or pend3[0] or pend4[0] is not None or (pend2[0] and pend2[0] != kind):
                 flush()
             x2_tail(kind == "peer_hier_x2t")
             peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
@@ -1021,8 +1046,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                            f", peer windows: {peer_err}")
     candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
     if peer is not None:
-        for i, kind in enumerate(("peer_launches", "peer_swing", "peer_hier", "peer_hier_ll", "peer_hier_pipe",
-                                  "peer_hier_x", "peer_hier_x2", "peer_hier_x2t")):
+        for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier", "peer_hier_ll",
+                                  "peer_hier_pipe", "peer_hier_x", "peer_hier_x2", "peer_hier_x2t")):
             if check(kind, 9100 + 10 * i):
                 candidates.append(kind)
     if not candidates:
@@ -1074,8 +1099,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         peer.set_oneshot_max(4 << 20)
         peer.set_hier_ll(0)
         mode[0] = None
-    local_ms = local_phases_ms(fused=transport == "rccl_x")
-    local_split_ms = local_phases_ms() if transport == "rccl_x" else local_ms
+    fused_local = transport in ("rccl_x", "peer_mem_x")
+    local_ms = local_phases_ms(fused=fused_local)
+    local_split_ms = local_phases_ms() if fused_local else local_ms
     if peer_guard is not None:   # the headline is measured: the extras have their own watchdog
         peer_guard.cancel()
     HEADLINE_DONE.set()
@@ -1083,7 +1109,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     extras = {"headline_transport": transport, "transport_verified": verify, "transport_quick_ms": quick,
               "peer_timeout_in_timed_loop": peer_timeout,
               "local_phases_ms": {"tree_then_broadcast": round(local_split_ms, 6),
-                                  **({"tree_broadcast_fused": round(local_ms, 6)} if transport == "rccl_x" else {})},
+                                  **({"tree_broadcast_fused": round(local_ms, 6)} if fused_local else {})},
               "timing": {"repetitions": len(rep_ms), "ms_per_step_per_repetition": [round(x, 6) for x in rep_ms],
                          "ms_per_step": "median repetition (each: the K steps, max over ranks)"}}
     if peer_err:
@@ -1176,7 +1202,7 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
         kern = ONE_LAUNCH[transport]
         roof = {"kernel": f"{kern} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9, "traffic": pmc_traffic(kern)}
-    elif transport == "rccl_x":   # the local HBM pass: bucket i's broadcast + bucket i+1's tree in one kernel
+    elif transport in ("rccl_x", "peer_mem_x"):   # the local HBM pass: bucket i's broadcast + i+1's tree, one kernel
         roof = {"kernel": "k_tree_bcast_x (local phases of consecutive buckets, one pass)",
                 "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9,
                 "traffic": pmc_traffic("k_tree_bcast_x<1>")}
@@ -1187,6 +1213,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                 "traffic": tr + bc if tr and bc else None}
     achieved = roof["achieved"]
     via = {"rccl": "on-GPU tree reduce, 2D Swing BO over RCCL/xGMI, broadcast",
+           "peer_mem_x": "consecutive buckets pipelined (K buckets in K + 1 calls, all inside the timed region): "
+                         "bucket i's broadcast and bucket i+1's on-GPU tree reduce in one HBM pass, then bucket i+1's "
+                         "partial through the one-kernel mem_2D exchange over peer-mapped xGMI windows",
            "rccl_x": "consecutive buckets pipelined (K buckets in K + 1 calls, all inside the timed region): "
                      "bucket i's broadcast and bucket i+1's on-GPU tree reduce in one HBM pass, then bucket i+1's "
                      "2D Swing BO over RCCL/xGMI",

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Why k_broadcast runs longer inside the peer launch form (W = 1 hier step,
+rocprofv3: 13.7 us) than alone (7.8 us): the same 64 x 640 kB buckets (32
+rotating sets) through (A) broadcast alone, (B) tree -> broadcast, (C) tree ->
+peer mem_2D launches (copy, barrier, reduce-scatter, barrier, all-gather) ->
+broadcast, (D) tree -> one peer barrier -> broadcast.  Run under rocprofv3
+--kernel-trace: per-kernel durations by arm (arms run in order, K steps each).
+   python tools/bcast_probe.py [steps]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import tenstorrentallreduce_amd as t  # noqa: E402
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+P, n, NS = 64, 327680, 32
+sets = [torch.randint(0x3F80, 0x42C8, (P, n), dtype=torch.int16, device="cuda") for _ in range(NS)]
+ws = torch.empty(n, dtype=torch.int16, device="cuda")
+peer = t.Peer(1, 0, 0, 2 * n)
+peer.connect([peer.handle()])
+peer.set_oneshot_max(0)   # the multi-launch mem_2D form
+s = torch.cuda.Stream()
+for arm in ("A", "B", "C", "D"):
+    for i in range(steps):
+        b = sets[i % NS]
+        if arm in "BCD":
+            t.tree_reduce(b.data_ptr(), n, n, t.SWING, 8, P, ws.data_ptr(), s)
+        if arm == "C":
+            peer.allreduce(ws.data_ptr(), n, s)   # the partial through the peer launches (W = 1)
+        if arm == "D":
+            peer.allreduce(ws[:64].data_ptr(), 64, s)   # a tiny peer call: its barriers, no bytes
+        t.broadcast(b.data_ptr(), n, n, P, ws.data_ptr(), s)
+    torch.cuda.synchronize()
+print("peer_status", peer.status())
+peer.close()
