@@ -693,7 +693,7 @@ def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo,
         ms = timed_max(lambda: fn(b2), reps, stream)
         out[key] = {**arm_stats(ms, nbytes, world, lo), "channels": chans, **v}
 
-    if variant != t.MEM and comm is not None:
+    if comm is not None and (variant != t.MEM or local == 1):   # mem_2D over RCCL: one rank per GPU
         timed(name, lambda b: t.dist_allreduce(comm, d2, b.data_ptr(), w2.data_ptr(), stream), variant == t.LO)
     if peer is not None:
         def status():
