@@ -240,6 +240,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     pass from this many 256-element tiles per rank, the register butterfly below
  *   tree_bcast_lag    1: k_tree_bcast_x (allred_dist_allreduce_pipelined) stores the previous
  *                     bucket's rows of a tile one iteration after the tile's tree (0: in the same one)
+ *   tree_bcast_bal    0; 1: k_tree_bcast_x spreads the result-tile loads and partial stores over
+ *                     its four waves (8 columns each) instead of wave 0
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

@@ -353,7 +353,10 @@ __global__ __launch_bounds__(kBlock) void k_tree_lds_lag(uint16_t* __restrict__ 
 // op by op with the 64 row stores of bucket i's tile j.  Per-wave exact vmcnt:
 // wave 0 issues the result loads and the partial stores, the others do not.
 // ---------------------------------------------------------------------------
-template <int LAG>   // LAG 0: bucket i's tile j rows stored in iteration j; 1: in iteration j + 1
+// LAG 0: bucket i's tile j rows stored in iteration j; 1: in iteration j + 1.
+// BAL: every wave stages 8 columns of the result tile and stores 8 columns of the
+// partial (equal memory queues); else wave 0 does both for all 32 columns.
+template <int LAG, bool BAL>
 __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                          uint64_t stride, const uint8_t* __restrict__ order,
                                                          uint16_t* __restrict__ cur_partial,
@@ -364,11 +367,12 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
     static_assert(LAG == 0 || LAG == 1, "lag of the row stores: 0 or 1 iteration");
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res_lds[2][64];   // bucket i's result tile (1 KiB: two copies)
+    __shared__ __attribute__((aligned(16))) uint4 res_lds[2][64];   // bucket i's result tile (wave 0: two copies)
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
     const bool w0 = w == 0;
+    const bool hasr = BAL || w0;   // this wave issues result loads and partial stores
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
     const uint32_t rbase = __builtin_amdgcn_readfirstlane(
@@ -378,15 +382,25 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
     auto tile_of = [&](int j) { return t0 + blockIdx.x + (uint64_t)j * G; };
+    const uint32_t rbase_w = __builtin_amdgcn_readfirstlane(rbase + (uint32_t)(w * 128));   // BAL: this wave's 8 columns
+    auto issue_res = [&](uint64_t t, int slot) {   // bucket i's result tile t into res_lds[slot]
+        if (BAL) {
+            if (lane < 8)
+                lds_dma16(reinterpret_cast<const uint4*>(prev_result) + t * TV + 8 * w + lane,
+                          rbase_w + (uint32_t)(slot * 1024));
+        } else if (w0) {
+            lds_dma16(reinterpret_cast<const uint4*>(prev_result) + t * TV + c, rbase + (uint32_t)(slot * 1024));
+        }
+    };
     auto issue_loads = [&](int j) {   // tile j of bucket i+1 into buf[j & 1]; wave 0: bucket i's result tile j
         const uint64_t t = tile_of(j);
 #pragma unroll
         for (int k = 0; k < OPS; ++k)
             lds_dma16(reinterpret_cast<const uint4*>(crow(k)) + t * TV + c,
                       wbase + (uint32_t)((j & 1) * P * TV * 16 + RPI * k * TV * 16));
-        if (w0) lds_dma16(reinterpret_cast<const uint4*>(prev_result) + t * TV + c, rbase + (uint32_t)((j & 1) * 1024));
+        issue_res(t, j & 1);
     };
-    const int own = w0 ? 1 : 0;   // wave 0's extra ops per tile: the result load (and the partial store)
+    const int own = hasr ? 1 : 0;   // the extra ops per tile: the result load (and the partial store)
     // the 64-byte tree order of local rank 0 (one byte per lane of wave 0), ahead of the first tiles' loads
     uint32_t ob = 0;
     if (w0) ob = order_byte_load(order, lane);
@@ -406,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
         // comes after it) and iteration j-1: partial (wave 0), tile j+1's loads, row stores
         const int next = j + 1 < mine ? OPS + own : 0;
         if (j == 0) wait_any(next);
-        else wait_any((j >= 2 + LAG && !w0 ? 1 : 0) + own + next + (j - 1 >= LAG ? OPS : 0));
+        else wait_any((j >= 2 + LAG && !hasr ? 1 : 0) + own + next + (j - 1 >= LAG ? OPS : 0));
         lds_barrier();   // every wave's rows of tile j and wave 0's result tile are in LDS
         const uint4* tile = buf[j & 1];
         const uint64_t t = tile_of(j), v0 = t * TV;
@@ -422,10 +436,10 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));   // tree level across the two lane halves
         if (q == 0) part[j & 1][w * TV + c] = pw;
         lds_barrier();   // tile j and result slot j & 1 are read by every wave; the partials are in
-        if (w0) {
+        if (hasr) {
             const uint4* pp = part[j & 1];
             const uint4 r = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
-            if (q == 0) st_nt(reinterpret_cast<uint4*>(cur_partial) + v0 + c, r);
+            if (q == 0 && (!BAL || (c >> 3) == w)) st_nt(reinterpret_cast<uint4*>(cur_partial) + v0 + c, r);
         }
         {   // tile j+2's loads and bucket i's row stores (tile j - LAG), interleaved op by op
             const uint64_t tl = tile_of(j + 2), ts = tile_of(j - LAG);
@@ -437,8 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_tree_bcast_x(uint16_t* __restrict__ 
                     lds_dma16(reinterpret_cast<const uint4*>(crow(k)) + tl * TV + c, bl + (uint32_t)(RPI * k * TV * 16));
                 if (j >= LAG) st_nt(reinterpret_cast<uint4*>(prow(k)) + ts * TV + c, sv);
             }
-            if (w0 && j + 2 < mine)
-                lds_dma16(reinterpret_cast<const uint4*>(prev_result) + tl * TV + c, rbase + (uint32_t)((j & 1) * 1024));
+            if (j + 2 < mine) issue_res(tl, j & 1);
         }
         pres = pnew;
     }
@@ -1656,12 +1669,16 @@ int launch_tree_bcast_x(uint16_t* cur, uint16_t* prev, uint64_t stride, size_t n
     if (total == 64 && n % 256 == 0) {
         hipStream_t st = (hipStream_t)stream;
         for_each_chunk(n / 256, [&](uint64_t a, uint64_t b) {
-            if (tune(Tune::tree_bcast_lag))
-                hipLaunchKernelGGL(k_tree_bcast_x<1>, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, cur,
-                                   prev, stride, order, cur_partial, prev_result, a, b - a);
-            else
-                hipLaunchKernelGGL(k_tree_bcast_x<0>, dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, cur,
-                                   prev, stride, order, cur_partial, prev_result, a, b - a);
+            const dim3 grid(persistent_grid(b - a, 512));
+            switch (tune(Tune::tree_bcast_lag) * 2 + tune(Tune::tree_bcast_bal)) {
+#define TSA_TBX(L, B) hipLaunchKernelGGL((k_tree_bcast_x<L, B>), grid, dim3(kBlock), 0, st, cur, prev, stride, order, \
+                                         cur_partial, prev_result, a, b - a)
+                case 0: TSA_TBX(0, false); break;
+                case 1: TSA_TBX(0, true); break;
+                case 2: TSA_TBX(1, false); break;
+                default: TSA_TBX(1, true); break;
+#undef TSA_TBX
+            }
         });
         return last_error();
     }

@@ -63,10 +63,10 @@ def test_single_rank_rccl_comm(local):
     comm.close()
 
 
-@pytest.mark.parametrize("lag", [0, 1])
+@pytest.mark.parametrize("lag,bal", [(0, 0), (1, 0), (1, 1), (0, 1)])
 @pytest.mark.parametrize("n,total,side", [(327680, 64, 8), (64 * 8 * 5, 64, 8), (1061 * 256, 64, 8),
                                           (8 * 8 * 40, 8, 4)])
-def test_tree_broadcast_pipelined_matches_the_two_launches(n, total, side, lag):
+def test_tree_broadcast_pipelined_matches_the_two_launches(n, total, side, lag, bal):
     """k_tree_bcast_x (bucket i+1's tree and bucket i's broadcast in one pass) is
     bit-identical to tree_reduce(cur) + broadcast(prev); 8 ranks take the two
     launches themselves."""
@@ -77,7 +77,7 @@ def test_tree_broadcast_pipelined_matches_the_two_launches(n, total, side, lag):
     for algo in (t.SWING, t.RECDUB):
         out = torch.empty(n, dtype=torch.int16, device=DEV)
         p2 = prev.clone()
-        with t.tuned(tree_bcast_lag=lag):   # the row stores in the tile's iteration or one later: same bytes
+        with t.tuned(tree_bcast_lag=lag, tree_bcast_bal=bal):   # store timing / which waves stage: same bytes
             t.tree_broadcast_pipelined(cur.data_ptr(), p2.data_ptr(), n, n, algo, side, total, out.data_ptr(),
                                        src.data_ptr())
         want = torch.empty_like(out)
