@@ -13,3 +13,4 @@ for l in open("gpurun_out/r03f/local.jsonl"):
 PY
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -f csv -d $out/bp -o run -- python3 tools/bcast_probe.py 100 > $out/bp.out 2> $out/bp.err || exit 1
 bash tools/gpu.sh prof r03prof_bench
+timeout -k 10 120 python tools/streams_probe.py 100 5 > $out/streams.json 2> $out/streams.err && cat $out/streams.json
