@@ -3,7 +3,9 @@
 rocprofv3: 13.7 us) than alone (7.8 us): the same 64 x 640 kB buckets (32
 rotating sets) through (A) broadcast alone, (B) tree -> broadcast, (C) tree ->
 peer mem_2D launches (copy, barrier, reduce-scatter, barrier, all-gather) ->
-broadcast, (D) tree -> one peer barrier -> broadcast.  Run under rocprofv3
+broadcast, (D) tree -> a tiny peer call -> broadcast, (E) as B with the
+broadcast's source another buffer, (F) as B writing a bucket the tree did not
+just read, (G) B's launches replayed from a HIP graph.  Run under rocprofv3
 --kernel-trace: per-kernel durations by arm (arms run in order, K steps each).
    python tools/bcast_probe.py [steps]"""
 import os
@@ -21,16 +23,31 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 peer.set_oneshot_max(0)   # the multi-launch mem_2D form
 s = torch.cuda.Stream()
-for arm in ("A", "B", "C", "D"):
-    for i in range(steps):
+ws2 = torch.empty(n, dtype=torch.int16, device="cuda")
+# E: the broadcast's source is NOT the partial the tree just wrote; F: the broadcast writes
+# a bucket set the tree did NOT just read; G: B's launches captured in a HIP graph
+for arm in ("A", "B", "C", "D", "E", "F", "G"):
+    def one(i):
         b = sets[i % NS]
-        if arm in "BCD":
+        if arm in "BCDEFG":
             t.tree_reduce(b.data_ptr(), n, n, t.SWING, 8, P, ws.data_ptr(), s)
         if arm == "C":
             peer.allreduce(ws.data_ptr(), n, s)   # the partial through the peer launches (W = 1)
         if arm == "D":
             peer.allreduce(ws[:64].data_ptr(), 64, s)   # a tiny peer call: its barriers, no bytes
-        t.broadcast(b.data_ptr(), n, n, P, ws.data_ptr(), s)
+        dst = sets[(i + NS // 2) % NS] if arm == "F" else b
+        t.broadcast(dst.data_ptr(), n, n, P, (ws2 if arm == "E" else ws).data_ptr(), s)
+    if arm == "G":
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for i in range(steps):
+                one(i)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            g.replay()
+    else:
+        for i in range(steps):
+            one(i)
     torch.cuda.synchronize()
 print("peer_status", peer.status())
 peer.close()
