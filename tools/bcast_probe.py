@@ -19,14 +19,17 @@ steps = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 P, n, NS = 64, 327680, 32
 sets = [torch.randint(0x3F80, 0x42C8, (P, n), dtype=torch.int16, device="cuda") for _ in range(NS)]
 ws = torch.empty(n, dtype=torch.int16, device="cuda")
-peer = t.Peer(1, 0, 0, 2 * n)
-peer.connect([peer.handle()])
-peer.set_oneshot_max(0)   # the multi-launch mem_2D form
+NO_PEER = os.environ.get("NO_PEER") == "1"   # no peer windows in the process: arms C and D skipped
+peer = None
+if not NO_PEER:
+    peer = t.Peer(1, 0, 0, 2 * n)
+    peer.connect([peer.handle()])
+    peer.set_oneshot_max(0)   # the multi-launch mem_2D form
 s = torch.cuda.Stream()
 ws2 = torch.empty(n, dtype=torch.int16, device="cuda")
 # E: the broadcast's source is NOT the partial the tree just wrote; F: the broadcast writes
 # a bucket set the tree did NOT just read; G: B's launches captured in a HIP graph
-for arm in ("A", "B", "C", "D", "E", "F", "G"):
+for arm in ("A", "B", "E", "F", "G") if NO_PEER else ("A", "B", "C", "D", "E", "F", "G"):
     def one(i):
         b = sets[i % NS]
         if arm in "BCDEFG":
@@ -49,5 +52,6 @@ for arm in ("A", "B", "C", "D", "E", "F", "G"):
         for i in range(steps):
             one(i)
     torch.cuda.synchronize()
-print("peer_status", peer.status())
-peer.close()
+if peer is not None:
+    print("peer_status", peer.status())
+    peer.close()
