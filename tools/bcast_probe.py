@@ -6,7 +6,8 @@ peer mem_2D launches (copy, barrier, reduce-scatter, barrier, all-gather) ->
 broadcast, (D) tree -> a tiny peer call -> broadcast, (E) as B with the
 broadcast's source another buffer, (F) as B writing a bucket the tree did not
 just read, (G) B's launches replayed from a HIP graph, (H) as B with a partial
-buffer per bucket set (tools/hier_local.py's pattern).  Prints event-timed us
+buffer per bucket set (tools/hier_local.py's pattern), (I) / (J) as B with the
+partial alternating over 2 / 4 buffers.  Prints event-timed us
 per step of the eager arms.  Run under rocprofv3
 --kernel-trace: per-kernel durations by arm (arms run in order, K steps each).
    python tools/bcast_probe.py [steps]"""
@@ -33,11 +34,11 @@ outs = [torch.empty(n, dtype=torch.int16, device="cuda") for _ in range(NS)]   #
 ev = {}
 # E: the broadcast's source is NOT the partial the tree just wrote; F: the broadcast writes
 # a bucket set the tree did NOT just read; G: B's launches captured in a HIP graph
-for arm in ("A", "B", "E", "F", "G", "H") if NO_PEER else ("A", "B", "C", "D", "E", "F", "G", "H"):
+for arm in ("A", "B", "E", "F", "G", "H", "I", "J") if NO_PEER else ("A", "B", "C", "D", "E", "F", "G", "H", "I", "J"):
     def one(i):
         b = sets[i % NS]
-        part = outs[i % NS] if arm == "H" else ws
-        if arm in "BCDEFGH":
+        part = {"H": outs[i % NS], "I": outs[i % 2], "J": outs[i % 4]}.get(arm, ws)
+        if arm in "BCDEFGHIJ":
             t.tree_reduce(b.data_ptr(), n, n, t.SWING, 8, P, part.data_ptr(), s)
         if arm == "C":
             peer.allreduce(ws.data_ptr(), n, s)   # the partial through the peer launches (W = 1)
