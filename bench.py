@@ -862,9 +862,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 nb = bufs[(i + 1) % len(bufs)]
                 t.tree_broadcast_pipelined(nb.data_ptr(), b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS,
                                            partial.data_ptr(), partial2.data_ptr(), stream)
-            else:
-                t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, partial.data_ptr(), stream)
-                t.broadcast(b.data_ptr(), ELEMS, ELEMS, RANKS, partial.data_ptr(), stream)
+            else:   # the partial alternates between two buffers, as in allred_dist_allreduce
+                pp = (partial, partial2)[i & 1]
+                t.tree_reduce(b.data_ptr(), ELEMS, ELEMS, t.SWING, SIDE, RANKS, pp.data_ptr(), stream)
+                t.broadcast(b.data_ptr(), ELEMS, ELEMS, RANKS, pp.data_ptr(), stream)
         e1.record(stream)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / args.steps

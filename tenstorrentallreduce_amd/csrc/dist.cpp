@@ -38,6 +38,7 @@ struct allred_comm {
     int nranks = 0, rank = 0, device = 0;
     // allred_dist_allreduce_pipelined: the bucket started by the last call (its rows are
     // written by the next call or the flush) and its allreduced partial in the workspace
+    uint64_t calls = 0;             // allred_dist_allreduce calls (the hierarchical partial alternates halves)
     uint16_t* pend = nullptr;
     uint16_t* pend_partial = nullptr;
     int pend_parity = 0, pend_local = 0;
@@ -530,7 +531,16 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
         return ALLRED_OK;
     }
     if (d->local_ranks > 1) {
-        bucket = staging + n;  // the GPU's partial
+        // the GPU's partial: the two halves of the workspace swap the partial / staging
+        // roles on every call.  A partial rewritten in the same place by consecutive
+        // steps made the following broadcast run 13.6 instead of 8 us (rows just read
+        // by the tree; tools/bcast_probe.py, profiles/r03_bcast_probe.txt)
+        if (c->calls++ & 1) {
+            bucket = staging;
+            staging += n;
+        } else {
+            bucket = staging + n;
+        }
         st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }

@@ -48,6 +48,7 @@ struct allred_peer {
     bool opened[ALLRED_MAX_NODES] = {};
     uint32_t calls = 0;
     uint32_t seq = 0;               // progress-flag base of the scheduled form
+    uint64_t dist_calls = 0;        // allred_peer_dist_allreduce calls (hierarchical partial halves)
     bool last_all_peer = false;     // previous call read every rank's window
     uint64_t oneshot_max = 4ull << 20;  // buckets up to this many bytes use the one-kernel form
     bool connected = false;
@@ -373,7 +374,8 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
     uint16_t* bucket = buf;
     if (d->local_ranks > 1) {
         if (!workspace) return ALLRED_ERR_ARG;
-        bucket = static_cast<uint16_t*>(workspace) + n;
+        // the partial alternates between the workspace's halves (as allred_dist_allreduce)
+        bucket = static_cast<uint16_t*>(workspace) + ((p->dist_calls++ & 1) ? 0 : n);
         st = allred_tree_reduce(buf, n, n, d->local_algo, d->local_side, d->local_ranks, bucket, stream);
         if (st != ALLRED_OK) return st;
     }
