@@ -502,6 +502,7 @@ def verify_transport(run, buf: torch.Tensor, world: int, rank: int, local: int, 
     n = buf.shape[1]
     rows = world * local
     res = {}
+    err = None
     for check in ("exact_sum", "closed_form"):
         ok = True
         try:
@@ -527,9 +528,12 @@ def verify_transport(run, buf: torch.Tensor, world: int, rank: int, local: int, 
             del want
         except Exception as e:  # reported, never silently dropped: the check fails
             print(f"[bench r{rank}] verify {check}: {e!r}", file=sys.stderr)
+            err = err or repr(e)
             ok = False
         res[check] = agreed(ok)
     res["verified"] = res["exact_sum"] and res["closed_form"]
+    if err:   # e.g. a form the shape does not support (ALLRED_ERR_UNSUPPORTED): not a wrong result
+        res["error"] = err[:200]
     return res
 
 

@@ -1212,16 +1212,19 @@ constexpr int kBoPipeTab = kBoPipeTabBytes;
 template <int P>
 constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 
-template <int P, bool BO>
-__global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
+// NW waves per workgroup (4 or 8): wave w owns TV / NW columns of every row.
+template <int P, bool BO, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void k_steps_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
                                                        const uint8_t* __restrict__ tab, uint64_t bv, uint64_t slices,
                                                        uint64_t units, uint64_t* __restrict__ stamps) {
-    constexpr int NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, H = P / 2, S = log2_of<P>();
-    constexpr int IPW = (H * 8 + 63) / 64;   // items (row pair, one of the wave's 8 columns) per lane, H pairs
+    constexpr int TV = 32, CPW = TV / NW, RPI = 2, RPW = P / NW, OPS = RPW / RPI, H = P / 2, S = log2_of<P>();
+    constexpr int IPW = (H * CPW + 63) / 64;   // items (row pair, one of the wave's CPW columns) per lane, H pairs
+    constexpr int TPW = kBoPipeTab / NW;        // BO table bytes staged per wave
     constexpr int TOPS = BO ? 1 : 0;          // the BO unit's table comes with its rows
     constexpr int NPH = BO ? 2 * S - 2 : S - 1;   // phases after step 0
     constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
     static_assert(OPS >= 1 && 2 * (OPS + TOPS) + OPS <= 63, "vmcnt is 6 bits");
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint8_t tl[BO ? 2 : 1][BO ? kBoPipeTab : 16];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1229,15 +1232,15 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
     const uint32_t wbase = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
     const uint32_t tbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&tl[0][0] + (uint32_t)(w * 64));
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&tl[0][0] + (uint32_t)(w * TPW));
     auto row = [&](int k) { return ranks + (uint64_t)(RPW * w + RPI * k + q) * stride; };
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < units ? (int)((units - 1 - blockIdx.x) / G + 1) : 0;
     auto unit_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
     auto col0 = [&](uint64_t u) { return BO ? (u / slices) * bv + (u % slices) * TV : u * TV; };
-    auto issue_tab = [&](uint64_t u, int b) {   // BO: 64 bytes of the block's table per wave (lanes 0-3)
+    auto issue_tab = [&](uint64_t u, int b) {   // BO: TPW bytes of the block's table per wave (TPW / 16 lanes)
         if constexpr (BO) {
-            if (lane < 4) lds_dma16(tab + (u / slices) * kBoPipeTab + w * 64 + lane * 16, tbase + (uint32_t)(b * kBoPipeTab));
+            if (lane < TPW / 16) lds_dma16(tab + (u / slices) * kBoPipeTab + w * TPW + lane * 16, tbase + (uint32_t)(b * kBoPipeTab));
         }
     };
     auto issue = [&](uint64_t u, int b) {
@@ -1257,7 +1260,7 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
         for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
         return o;
     };
-    constexpr int MPH = BO ? (P / 4 * 8 + 63) / 64 : IPW;   // most items per lane in one phase
+    constexpr int MPH = BO ? (P / 4 * CPW + 63) / 64 : IPW;   // most items per lane in one phase
     // This lane's table entries (pair = a | b << 8; final row) for the whole unit,
     // fetched in one batch: a phase then waits for its operand rows only.
     uint32_t p0[IPW], pp[NPH > 0 ? NPH : 1][MPH];
@@ -1267,14 +1270,14 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
             const int i = lane + 64 * t;
-            p0[t] = i < H * 8 ? t16[i >> 3] : 0;
+            p0[t] = i < H * CPW ? t16[i / CPW] : 0;
         }
 #pragma unroll
         for (int ph = 1; ph <= NPH; ++ph)
 #pragma unroll
             for (int m = 0; m < MPH; ++m) {
                 const int i = lane + 64 * m;
-                pp[ph - 1][m] = i < cnt_of(ph) * 8 ? t16[off_of(ph) / 2 + (i >> 3)] : 0;
+                pp[ph - 1][m] = i < cnt_of(ph) * CPW ? t16[off_of(ph) / 2 + i / CPW] : 0;
             }
 #pragma unroll
         for (int k = 0; k < OPS; ++k) fin[k] = tb[off_of(NPH + 1) + RPW * w + RPI * k + q];
@@ -1294,19 +1297,19 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
         stamp(stamps, u * STAMPS);
         uint4* tile = buf[j & 1];
         if constexpr (BO) fetch(tl[j & 1]);
-        // The step program runs per column: wave w owns columns 8w .. 8w+7 of
-        // every row, so a step needs no workgroup barrier — LDS operations of
+        // The step program runs per column: wave w owns columns CPW w .. CPW w + CPW - 1
+        // of every row, so a step needs no workgroup barrier — LDS operations of
         // one wave execute in order, and no other wave touches these columns.
-        const int cw = 8 * w + (lane & 7);
-        uint4 val[IPW];   // LO: this lane's rows (x = (lane + 64t) >> 3) after the latest step
+        const int cw = CPW * w + lane % CPW;
+        uint4 val[IPW];   // LO: this lane's rows (x = (lane + 64t) / CPW) after the latest step
         {   // step 0 from the staged rows: pair x = (r, p) -> row x (every read before any write)
 #pragma unroll
             for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * 8)
+                if (lane + 64 * t < H * CPW)
                     val[t] = add8(tile[(p0[t] & 255) * TV + cw], tile[(p0[t] >> 8) * TV + cw]);
 #pragma unroll
             for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * 8) tile[((lane + 64 * t) >> 3) * TV + cw] = val[t];
+                if (lane + 64 * t < H * CPW) tile[((lane + 64 * t) / CPW) * TV + cw] = val[t];
             __builtin_amdgcn_wave_barrier();
             stamp(stamps, u * STAMPS + 1);
         }
@@ -1316,7 +1319,7 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
                 const bool rs = ph < S;
 #pragma unroll
                 for (int m = 0; m < MPH; ++m)
-                    if (lane + 64 * m < cnt_of(ph) * 8) {
+                    if (lane + 64 * m < cnt_of(ph) * CPW) {
                         const int a = (pp[ph - 1][m] & 255) * TV + cw, cc = (pp[ph - 1][m] >> 8) * TV + cw;
                         tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
                     }
@@ -1324,12 +1327,12 @@ __global__ __launch_bounds__(kBlock) void k_steps_pipe(uint16_t* __restrict__ ra
                 uint4 oth[IPW];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * 8) oth[m] = tile[(pp[ph - 1][m] >> 8) * TV + cw];
+                    if (lane + 64 * m < H * CPW) oth[m] = tile[(pp[ph - 1][m] >> 8) * TV + cw];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * 8) {
+                    if (lane + 64 * m < H * CPW) {
                         val[m] = add8(val[m], oth[m]);
-                        tile[((lane + 64 * m) >> 3) * TV + cw] = val[m];
+                        tile[((lane + 64 * m) / CPW) * TV + cw] = val[m];
                     }
             }
             __builtin_amdgcn_wave_barrier();
@@ -1703,13 +1706,17 @@ int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
         const dim3 grid(persistent_grid(units, 512));
+        const bool w8 = tune(Tune::steps_waves) == 8 && total >= 16;
+#define TSA_SP(PP, NWV) hipLaunchKernelGGL((k_steps_pipe<PP, true, NWV>), grid, dim3(NWV * 64), 0, st, ranks, stride, \
+                                           d_pipe_tab, bv, slices, units, stamps)
         switch (total) {
-            case 8: hipLaunchKernelGGL((k_steps_pipe<8, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
-            case 16: hipLaunchKernelGGL((k_steps_pipe<16, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
-            case 32: hipLaunchKernelGGL((k_steps_pipe<32, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
-            case 64: hipLaunchKernelGGL((k_steps_pipe<64, true>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, bv, slices, units, stamps); return last_error();
+            case 8: TSA_SP(8, 4); return last_error();
+            case 16: if (w8) TSA_SP(16, 8); else TSA_SP(16, 4); return last_error();
+            case 32: if (w8) TSA_SP(32, 8); else TSA_SP(32, 4); return last_error();
+            case 64: if (w8) TSA_SP(64, 8); else TSA_SP(64, 4); return last_error();
             default: break;
         }
+#undef TSA_SP
     }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
     hipLaunchKernelGGL(k_bo_steps, dim3(grid), dim3(kBlock), 0, st, ranks, stride, d_tab, total, steps,
@@ -1729,13 +1736,17 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     hipStream_t st = (hipStream_t)stream;
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
         const dim3 grid(persistent_grid(units, 512));
+        const bool w8 = tune(Tune::steps_waves) == 8 && total >= 16;
+#define TSA_SP(PP, NWV) hipLaunchKernelGGL((k_steps_pipe<PP, false, NWV>), grid, dim3(NWV * 64), 0, st, ranks, stride, \
+                                           d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps)
         switch (total) {
-            case 8: hipLaunchKernelGGL((k_steps_pipe<8, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
-            case 16: hipLaunchKernelGGL((k_steps_pipe<16, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
-            case 32: hipLaunchKernelGGL((k_steps_pipe<32, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
-            case 64: hipLaunchKernelGGL((k_steps_pipe<64, false>), grid, dim3(kBlock), 0, st, ranks, stride, d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps); return last_error();
+            case 8: TSA_SP(8, 4); return last_error();
+            case 16: if (w8) TSA_SP(16, 8); else TSA_SP(16, 4); return last_error();
+            case 32: if (w8) TSA_SP(32, 8); else TSA_SP(32, 4); return last_error();
+            case 64: if (w8) TSA_SP(64, 8); else TSA_SP(64, 4); return last_error();
             default: break;
         }
+#undef TSA_SP
     }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
     hipLaunchKernelGGL(k_lo_steps, dim3(grid), dim3(kBlock), 0, st, ranks, stride, d_pairs, total,

@@ -108,6 +108,7 @@ def test_verify_transport_accepts_correct_and_refuses_corrupted(world):
                 assert v["verified"] is False, (rank, name, v)   # every rank refuses it (agreed)
             else:
                 assert v == {"exact_sum": True, "closed_form": True, "verified": True}, (rank, name, v)
+        assert "error" not in out["bo_hier_corrupt"]   # a wrong result, not a refused call
         assert out["bo_hier_corrupt"]["exact_sum"] is False and out["bo_hier_corrupt"]["closed_form"] is False
 
 

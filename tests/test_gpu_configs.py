@@ -91,7 +91,7 @@ def test_config5_reference_inputs(n):
 
 
 # ------------------------------------------------------------------ schedule form
-@pytest.mark.parametrize("steps_form", [0, 1, 2])
+@pytest.mark.parametrize("steps_form,waves", [(0, 4), (0, 8), (1, 4), (2, 4)])
 @pytest.mark.parametrize("variant", ["bo", "lo"])
 @pytest.mark.parametrize("algo,grid,n", [(t.SWING, (8, 64), 327680), (t.RECDUB, (8, 64), 327680),
                                          (t.SWING, (8, 64), 64 * 8 * 3), (t.SWING, (4, 8), 8 * 8 * 5),
@@ -99,17 +99,18 @@ def test_config5_reference_inputs(n):
                                          (t.SWING, (1, 1), 64), (t.SWING, (4, 8), 8 * 256 * 3),
                                          (t.SWING, (8, 32), 32 * 256 * 3), (t.RECDUB, (4, 16), 16 * 256 * 5),
                                          (t.SWING_1D, (1, 16), 16 * 256 * 2), (t.SWING, (8, 64), 1 << 20)])
-def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form):
+def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, waves):
     """The schedule form as one pipelined launch (k_steps_pipe, steps_form 0:
     whole 512-byte units of 8..64 ranks staged into LDS two ahead, the step
     program among LDS rows, stores one unit late; other shapes fall back to
     k_bo_steps / k_lo_steps), with every unit resident at once (steps_form 2)
     and as one launch per step (steps_form 1, the round-1 kernels), on slices
     narrower than a unit (3 and 5 vectors per block), odd unit counts and at
-    config-2 size, against the oracle."""
+    config-2 size, against the oracle; k_steps_pipe with 4 and 8 waves per
+    workgroup (steps_waves)."""
     side, total = grid
     ranks = rand_ranks(total, n, seed=7 * total + n % 97 + algo)
-    with t.tuned(steps_form=steps_form):
+    with t.tuned(steps_form=steps_form, steps_waves=waves):
         got = run_plan(algo, {"bo": t.BO, "lo": t.LO}[variant], side, total, ranks, t.EXEC_STEPS,
                        stride=n + 64)
     want = [r.copy() for r in ranks]
