@@ -242,8 +242,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     bucket's rows of a tile one iteration after the tile's tree (0: in the same one)
  *   tree_bcast_bal    0; 1: k_tree_bcast_x spreads the result-tile loads and partial stores over
  *                     its four waves (8 columns each) instead of wave 0
- *   steps_waves       4: waves per workgroup of the pipelined schedule form k_steps_pipe (8: each
- *                     wave owns 4 columns of every row; 16 ranks and more)
+ *   steps_waves       0: waves per workgroup of the pipelined schedule form k_steps_pipe — 0 auto
+ *                     (BO 4, LO 8: the LO steps are LDS-bound), 4, or 8 (each wave owns 4 columns
+ *                     of every row; 16 ranks and more)
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,

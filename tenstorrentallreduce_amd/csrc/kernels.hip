@@ -1706,6 +1706,7 @@ int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
         const dim3 grid(persistent_grid(units, 512));
+        // BO: 4 waves (17.4-17.6 vs 18.9-19.2 us with 8 at config 2, profiles/r03_steps_waves_ab.txt)
         const bool w8 = tune(Tune::steps_waves) == 8 && total >= 16;
 #define TSA_SP(PP, NWV) hipLaunchKernelGGL((k_steps_pipe<PP, true, NWV>), grid, dim3(NWV * 64), 0, st, ranks, stride, \
                                            d_pipe_tab, bv, slices, units, stamps)
@@ -1736,7 +1737,8 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     hipStream_t st = (hipStream_t)stream;
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
         const dim3 grid(persistent_grid(units, 512));
-        const bool w8 = tune(Tune::steps_waves) == 8 && total >= 16;
+        // LO (LDS-bound steps): 8 waves (18.2-18.5 vs 19.0-19.2 us with 4 at 640 kB, same file)
+        const bool w8 = tune(Tune::steps_waves) != 4 && total >= 16;
 #define TSA_SP(PP, NWV) hipLaunchKernelGGL((k_steps_pipe<PP, false, NWV>), grid, dim3(NWV * 64), 0, st, ranks, stride, \
                                            d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps)
         switch (total) {

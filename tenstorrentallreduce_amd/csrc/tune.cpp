@@ -38,7 +38,7 @@ const Key kKeys[] = {
     {"lo_tree_min_tiles", 64, 0, 1ll << 40},   // 64-rank rank-uniform LO: tree pass from this many 256-element tiles
     {"tree_bcast_lag", 1, 0, 1},      // k_tree_bcast_x: the row stores one iteration behind the tree (0: same iteration)
     {"tree_bcast_bal", 0, 0, 1},      // k_tree_bcast_x: every wave stages / stores 8 result columns (0: wave 0 all)
-    {"steps_waves", 4, 4, 8},         // k_steps_pipe: waves per workgroup (4 or 8; 8 needs >= 16 ranks)
+    {"steps_waves", 0, 0, 8},         // k_steps_pipe: waves per workgroup, 0 auto (BO 4, LO 8) | 4 | 8 (>= 16 ranks)
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");
