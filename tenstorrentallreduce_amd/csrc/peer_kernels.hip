@@ -883,6 +883,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
 // satisfied.
 constexpr int kHierXMaxTiles = 8;   // lanes (j, c) of the whole workgroup serve tile j
 
+// LAG (tune hier_x_lag): prev's / old's tile rows stored in the iteration of cur's tile j - LAG
+// (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order)
+template <int LAG>
 __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
@@ -930,8 +933,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     lds_barrier();   // order bytes and results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
-            // after L(j): S(j-2)'s last op, this wave's partial word of tile j-1, L(j+1), S(j-1)
-            wait_any((j >= 2 && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && prev ? OPS : 0) +
+            // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
+            // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
+            wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
                      (j >= 1 ? 1 : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
@@ -954,17 +958,24 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                 ll_put_word(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur, w);
             }
         }
-        // ---- cur's tile j+2 in, prev's tile j out, interleaved op by op
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(j);
+        // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(j - LAG);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-        const uint4 rv = prev ? res[j][c] : make_uint4(0, 0, 0, 0);
+        const bool st = prev && j >= LAG;
+        const uint4 rv = st ? res[j - LAG][c] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             if (cur && j + 2 < mine)
                 lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
                           bl + (uint32_t)(RPI * k * TV * 16));
-            if (prev) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
+            if (st) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
         }
+    }
+    if (LAG && prev && mine > 0) {   // prev's last tile
+        const uint4 rv = res[mine - 1][c];
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(mine - 1) * TV + c, rv);
     }
     // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
     // partial (during this launch's loop): W partials summed (fp32, owner first,
@@ -1015,7 +1026,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // t (launch i+1) before it pushes bucket i's result of t, so LL parity k & 1
 // (inbox and box) is reused only after its previous reader is done.
 // Same bits as k_hier_ll / k_hier_x; at most kHierXMaxTiles tiles per workgroup.
-template <bool TAIL>
+template <bool TAIL, int LAG>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
@@ -1091,9 +1102,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
-            // after L(j): S(j-2)'s last op, this wave's partial word of tile j-1, L(j+1), S(j-1),
-            // this wave's owned-sum pushes (j < 2)
-            wait_any((j >= 2 && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j >= 1 && old ? OPS : 0) +
+            // after L(j): the last row store interleaved behind it (old's tile j-2-LAG), this wave's
+            // partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG), this
+            // wave's owned-sum pushes (j < 2)
+            wait_any((j >= 2 + LAG && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && old ? OPS : 0) +
                      (j >= 1 ? 1 : 0) + (j < 2 ? pushed : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
@@ -1116,18 +1128,20 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                 ll_put_word(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur, w);
             }
         }
-        // ---- cur's tile j+2 in, old's tile j out, interleaved op by op
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(j);
+        // ---- cur's tile j+2 in, old's tile j - LAG out, interleaved op by op
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(j - LAG);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-        const uint4 rv = old ? res[j][c] : make_uint4(0, 0, 0, 0);
+        const bool st = old && j >= LAG;
+        const uint4 rv = st ? res[j - LAG][c] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             if (cur && j + 2 < mine)
                 lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
                           bl + (uint32_t)(RPI * k * TV * 16));
-            if (old) st_nt(reinterpret_cast<uint4*>(old + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
+            if (st) st_nt(reinterpret_cast<uint4*>(old + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
         }
     }
+    if (LAG && old && mine > 0) store_rows(old, mine - 1);   // old's last tile
     if (TAIL && rmid) owned_sums();   // TAIL: mid's partials arrived during the launch i-1
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
         __syncthreads();   // every wave has read old's results out of res
@@ -1402,8 +1416,10 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
         lc.ll[q] = llc ? llc[q] : nullptr;
         lp.ll[q] = llp ? llp[q] : nullptr;
     }
-    hipLaunchKernelGGL(k_hier_x, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, prev, stride, order, lc, lp,
-                       nranks, me, ntiles, ntiles / nranks, box_words, ecur, eprev, status);
+    auto* kern = tune(Tune::hier_x_lag) ? k_hier_x<1> : k_hier_x<0>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
+                       (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
+                       box_words, ecur, eprev, status);
     return peer_last_error();
 }
 
@@ -1426,8 +1442,11 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         lm.ll[q] = llm ? llm[q] : nullptr;
         lo.ll[q] = llo ? llo[q] : nullptr;
     }
-    hipLaunchKernelGGL(tune(Tune::hier_x2_tail) ? k_hier_x2<true> : k_hier_x2<false>, dim3(grid), dim3(kBlock), 0,
-                       (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
+    const int form = (tune(Tune::hier_x2_tail) ? 2 : 0) + (tune(Tune::hier_x_lag) ? 1 : 0);
+    auto* kern = form == 3 ? k_hier_x2<true, 1> : form == 2 ? k_hier_x2<true, 0>
+               : form == 1 ? k_hier_x2<false, 1>
+                           : k_hier_x2<false, 0>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
                        box_words, ecur, emid, eold, llm ? 1 : 0, status);
     return peer_last_error();
 }

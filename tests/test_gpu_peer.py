@@ -394,14 +394,15 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for _ in range(2):   # twice: the second sequence reuses both LL parities
+        for rep in range(4):   # row stores with the tree's tile / one behind; reruns reuse both LL parities
             bufs = [x.clone() for x in data]
             prev = None
-            for b in bufs:
-                peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
-                prev = b.data_ptr()
-            peer.allreduce_pipelined(None, prev, n, s)
-            torch.cuda.synchronize()
+            with t.tuned(hier_x_lag=rep % 2):
+                for b in bufs:
+                    peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
+                    prev = b.data_ptr()
+                peer.allreduce_pipelined(None, prev, n, s)
+                torch.cuda.synchronize()
             for i, (b, w) in enumerate(zip(bufs, want)):
                 bad = int((b.cpu().numpy().view(np.uint16) != w[None, :]).sum())
                 assert bad == 0, (i, bad)
@@ -549,7 +550,7 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             want.append(loc[0])
         s = torch.cuda.current_stream()
         for rep in range(4):   # owned sums at the start (0, 1) / the end (2, 3) of a launch
-            with t.tuned(hier_x2_tail=rep // 2):
+            with t.tuned(hier_x2_tail=rep // 2, hier_x_lag=rep % 2):
                 bufs = [x.clone() for x in data]
                 for b in bufs:
                     peer.allreduce_pipelined2(b.data_ptr(), n, s)
