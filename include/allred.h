@@ -245,8 +245,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   steps_waves       0: waves per workgroup of the pipelined schedule form k_steps_pipe — 0 auto
  *                     (BO 4, LO 8: the LO steps are LDS-bound), 4, or 8 (each wave owns 4 columns
  *                     of every row; 16 ranks and more)
- *   hier_x_lag        1; 0: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
- *                     iteration after the tree of the matching tile of the bucket being read
+ *   hier_x_lag        1: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
+ *                     iteration after the tree of the matching tile of the bucket being read; 0: in
+ *                     the same iteration
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,
