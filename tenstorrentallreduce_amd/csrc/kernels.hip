@@ -1366,6 +1366,187 @@ __global__ __launch_bounds__(NW * 64) void k_steps_pipe(uint16_t* __restrict__ r
     }
 }
 
+// k_steps_wave<P, BO, NW, NB>: the schedule form of k_steps_pipe (same steps,
+// same tables, same bits) with every WAVE its own pipeline.  k_steps_pipe's
+// waves already run the step program on their own 8 columns of the unit, but
+// they share the unit's loads (wave w loads rows 16w..16w+15, all 32 columns)
+// and its stores (every row's 32 columns from all waves' LDS columns), so each
+// unit costs two workgroup barriers and the slowest wave paces the four.  Here
+// a wave's work item is a STRIP — 8 columns (128 bytes) of one unit in all P
+// rank rows, 8 KiB at P = 64 — which it loads itself (8 rows x 128 bytes per
+// LDS-DMA instruction), runs the step program on, and stores itself, one strip
+// late and interleaved with strip j+NB's loads; nothing is shared between
+// waves (each also stages its own copy of the block's step table), so no
+// barrier remains and a wave stalls only on its own loads.  NB strip buffers
+// per wave: while a wave runs a strip's step chain (≈2.4 us at config 2, device
+// stamps: ten dependent LDS read-add-write phases), its other NB - 1 buffers'
+// loads stay in flight — with two buffers per wave the chain leaves the CU's
+// share of HBM idle.  Strip s = quarter s % 4 of unit s / 4; wave gw of the
+// grid takes strips gw, gw + GW, ... (NW = 4: the four waves of a workgroup take
+// the four quarters of the same units, so a row's 512 bytes are read at about
+// the same time; NW = 1: one-wave workgroups, as many per CU as LDS allows).
+template <int P, bool BO, int NW, int NB>
+__global__ __launch_bounds__(NW * 64) void k_steps_wave(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                       const uint8_t* __restrict__ tab, uint64_t bv, uint64_t slices,
+                                                       uint64_t units, uint64_t* __restrict__ stamps) {
+    constexpr int TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
+    constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
+    constexpr int TOPS = BO ? 1 : 0;          // the BO strip's table comes with its rows
+    constexpr int NPH = BO ? 2 * S - 2 : S - 1;
+    constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
+    static_assert(OPS >= 1 && NB >= 2, "one op per 8 rows; two buffers at least");
+    __shared__ __attribute__((aligned(16))) uint4 buf[NW][NB][P * CW];
+    __shared__ __attribute__((aligned(16))) uint8_t tl[NW][BO ? NB : 1][BO ? kBoPipeTab : 16];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cl = lane % CW, rl = lane / CW;   // column in the strip; row within a load / store op
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[w][0][0]);
+    const uint32_t tbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&tl[w][0][0]);
+    auto row = [&](int k) { return ranks + (uint64_t)(RPO * k + rl) * stride; };
+    const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
+    const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
+    auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
+    auto col0 = [&](uint64_t s) {
+        const uint64_t u = s / Q;
+        return (BO ? (u / slices) * bv + (u % slices) * TV : u * TV) + (s % Q) * CW;
+    };
+    auto issue_tab = [&](uint64_t s, int b) {   // BO: the block's whole table, 16 lanes x 16 bytes
+        if constexpr (BO) {
+            if (lane < kBoPipeTab / 16) lds_dma16(tab + (s / Q / slices) * kBoPipeTab + lane * 16, tbase + (uint32_t)(b * kBoPipeTab));
+        }
+    };
+    auto issue = [&](uint64_t s, int b) {   // op k: rows RPO k .. RPO k + 7, 128 bytes each -> LDS rows, 1 KiB
+        issue_tab(s, b);
+        const uint64_t c0 = col0(s);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + c0 + cl, wbase + (uint32_t)(b * P * CW * 16 + k * 1024));
+    };
+    // VMEM ops of iteration i (strip i+NB's loads, strip i-1's stores) and, for
+    // the wait of iteration j, the ops this wave issued after the last of strip j's loads
+    auto ops_it = [&](int i) { return (i + NB < mine ? OPS + TOPS : 0) + (i >= 1 ? OPS : 0); };
+    auto after_load = [&](int j) {
+        int n = 0;
+        if (j >= NB) {   // loaded in iteration j - NB, behind it that iteration's last store
+            n = j - NB >= 1 ? 1 : 0;
+            for (int i = j - NB + 1; i < j; ++i) n += ops_it(i);
+        } else {         // loaded in the prologue
+            for (int x = j + 1; x < NB; ++x) n += x < mine ? OPS + TOPS : 0;
+            for (int i = 0; i < j; ++i) n += ops_it(i);
+        }
+        return n;
+    };
+    auto cnt_of = [](int ph) {
+        if (!BO) return H;
+        const int k = ph < S ? ph : 2 * S - 1 - ph;
+        return P >> (k + 1);
+    };
+    auto off_of = [&](int ph) {
+        int o = 2 * H;
+        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
+        return o;
+    };
+    constexpr int MPH = BO ? (P / 4 * CW + 63) / 64 : IPW;
+    uint32_t p0[IPW], pp[NPH > 0 ? NPH : 1][MPH];
+    int fin[OPS];
+    auto fetch = [&](const uint8_t* tb) {
+        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
+#pragma unroll
+        for (int t = 0; t < IPW; ++t) {
+            const int i = lane + 64 * t;
+            p0[t] = i < H * CW ? t16[i / CW] : 0;
+        }
+#pragma unroll
+        for (int ph = 1; ph <= NPH; ++ph)
+#pragma unroll
+            for (int m = 0; m < MPH; ++m) {
+                const int i = lane + 64 * m;
+                pp[ph - 1][m] = i < cnt_of(ph) * CW ? t16[off_of(ph) / 2 + i / CW] : 0;
+            }
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) fin[k] = tb[off_of(NPH + 1) + RPO * k + rl];
+    };
+    if constexpr (!BO) {   // the LO step program is the same for every strip
+        fetch(tab);
+        wait_vm<0>();
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+        if (b < mine) issue(strip_of(b), b);
+    uint4 prev[OPS];
+    for (int j = 0; j < mine; ++j) {
+        const uint64_t s = strip_of(j);
+        const int b = j % NB;
+        const bool st_on = stamps && s % Q == 0 && lane == 0;   // one stamp set per unit (its first quarter)
+        wait_any(after_load(j));
+        if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
+        uint4* tile = buf[w][b];
+        if constexpr (BO) fetch(tl[w][b]);
+        uint4 val[IPW];
+        {   // step 0 from the staged rows: pair x = (r, p) -> row x (every read before any write)
+#pragma unroll
+            for (int t = 0; t < IPW; ++t)
+                if (lane + 64 * t < H * CW)
+                    val[t] = add8(tile[(p0[t] & 255) * CW + cl], tile[(p0[t] >> 8) * CW + cl]);
+#pragma unroll
+            for (int t = 0; t < IPW; ++t)
+                if (lane + 64 * t < H * CW) tile[((lane + 64 * t) / CW) * CW + cl] = val[t];
+            if (st_on) stamps[(s / Q) * STAMPS + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+#pragma unroll
+        for (int ph = 1; ph <= NPH; ++ph) {
+            if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
+                const bool rs = ph < S;
+#pragma unroll
+                for (int m = 0; m < MPH; ++m)
+                    if (lane + 64 * m < cnt_of(ph) * CW) {
+                        const int a = (pp[ph - 1][m] & 255) * CW + cl, cc = (pp[ph - 1][m] >> 8) * CW + cl;
+                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
+                    }
+            } else {   // exchange step ph: pair x = row x (kept in val) + the row of its other rank
+                uint4 oth[IPW];
+#pragma unroll
+                for (int m = 0; m < IPW; ++m)
+                    if (lane + 64 * m < H * CW) oth[m] = tile[(pp[ph - 1][m] >> 8) * CW + cl];
+#pragma unroll
+                for (int m = 0; m < IPW; ++m)
+                    if (lane + 64 * m < H * CW) {
+                        val[m] = add8(val[m], oth[m]);
+                        tile[((lane + 64 * m) / CW) * CW + cl] = val[m];
+                    }
+            }
+            if (st_on) stamps[(s / Q) * STAMPS + 1 + ph] = __builtin_amdgcn_s_memrealtime();
+        }
+        // the strip's result rows: rank r's value is row fin
+        uint4 cur[OPS];
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) cur[k] = tile[fin[k] * CW + cl];
+        // every LDS read of buffer b (and of its table) has returned before strip
+        // j+NB's LDS-DMA may land there
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        {   // strip j+NB's loads and strip j-1's stores, interleaved op by op
+            const bool ld = j + NB < mine;
+            const uint32_t bl = wbase + (uint32_t)(b * P * CW * 16);
+            const uint64_t cld = ld ? col0(strip_of(j + NB)) : 0, cs = j >= 1 ? col0(strip_of(j - 1)) : 0;
+            if (ld) issue_tab(strip_of(j + NB), b);
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {
+                if (ld) lds_dma16(reinterpret_cast<const uint4*>(row(k)) + cld + cl, bl + (uint32_t)(k * 1024));
+                if (j >= 1) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + cl, prev[k]);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) prev[k] = cur[k];
+        if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
+    }
+    if (mine > 0) {
+        const uint64_t cs = col0(strip_of(mine - 1));
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + cl, prev[k]);
+    }
+}
+
 template <bool ADD, int U>
 __global__ __launch_bounds__(64) void k_step_w(uint16_t* __restrict__ ranks, uint64_t stride,
                                                const int16_t* __restrict__ partner,
@@ -1474,6 +1655,32 @@ unsigned persistent_grid(uint64_t tiles, uint64_t dflt) {
     const int64_t g = tune(Tune::pipe_grid);
     const uint64_t cap = g > 0 ? (uint64_t)g : dflt;
     return (unsigned)(tiles < cap ? tiles : cap);
+}
+
+// the schedule form with wave-local strips (k_steps_wave): 8..64 ranks; false if the shape has no instance.
+// steps_wave 1: 4-wave workgroups, 2 strip buffers per wave, 2 workgroups per CU; 2 / 3 / 4: one-wave
+// workgroups with 2 / 3 / 4 buffers, 8 / 6 / 4 per CU (LDS: 16.5 / 24.75 / 33 KiB per wave at 64 ranks)
+bool launch_steps_wave(bool bo, int form, uint16_t* ranks, uint64_t stride, int total, const uint8_t* tab,
+                       uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps, hipStream_t st) {
+    if (form < 1 || form > 4) return false;
+    const uint64_t strips = units * 4;
+    static const unsigned per_cu[5] = {0, 0, 8, 6, 4};
+    const dim3 grid(form == 1 ? persistent_grid(units, 512) : persistent_grid(strips, 256 * per_cu[form]));
+#define TSA_SW(PP, BOV, NWV, NBV) hipLaunchKernelGGL((k_steps_wave<PP, BOV, NWV, NBV>), grid, dim3(NWV * 64), 0, st, \
+                                                     ranks, stride, tab, bv, slices, units, stamps)
+#define TSA_SWF(PP, BOV) do { switch (form) { case 1: TSA_SW(PP, BOV, 4, 2); break; case 2: TSA_SW(PP, BOV, 1, 2); break; \
+                                              case 3: TSA_SW(PP, BOV, 1, 3); break; default: TSA_SW(PP, BOV, 1, 4); } } while (0)
+#define TSA_SWP(PP) do { if (bo) TSA_SWF(PP, true); else TSA_SWF(PP, false); } while (0)
+    switch (total) {
+        case 8: TSA_SWP(8); return true;
+        case 16: TSA_SWP(16); return true;
+        case 32: TSA_SWP(32); return true;
+        case 64: TSA_SWP(64); return true;
+        default: return false;
+    }
+#undef TSA_SWP
+#undef TSA_SWF
+#undef TSA_SW
 }
 
 }  // namespace
@@ -1704,6 +1911,14 @@ int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
     hipStream_t st = (hipStream_t)stream;
     // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
+    // BO: every wave its own pipeline over 128-byte strips, one-wave workgroups (k_steps_wave, steps_wave 2:
+    // 17.0-17.2 vs 17.2-17.7 us for k_steps_pipe at config 2, profiles/r03_steps_wave_ab.txt)
+    const int64_t swv = tune(Tune::steps_wave);
+    if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total && swv != 0) {
+        if (launch_steps_wave(true, swv < 0 ? 2 : (int)swv, ranks, stride, total, d_pipe_tab, bv, slices, units,
+                              stamps, st))
+            return last_error();
+    }
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
         const dim3 grid(persistent_grid(units, 512));
         // BO: 4 waves (17.4-17.6 vs 18.9-19.2 us with 8 at config 2, profiles/r03_steps_waves_ab.txt)
@@ -1735,6 +1950,12 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
     hipStream_t st = (hipStream_t)stream;
+    // LO: k_steps_pipe below unless steps_wave asks for k_steps_wave (no faster for LO, same file)
+    const int64_t swv = tune(Tune::steps_wave);
+    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total && swv > 0) {
+        if (launch_steps_wave(false, (int)swv, ranks, stride, total, d_pipe_tab, 0, 1, units, stamps, st))
+            return last_error();
+    }
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
         const dim3 grid(persistent_grid(units, 512));
         // LO (LDS-bound steps): 8 waves (18.2-18.5 vs 19.0-19.2 us with 4 at 640 kB, same file)

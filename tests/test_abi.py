@@ -117,6 +117,13 @@ def test_tune_entry_point():
     with pytest.raises(t.AllredError):
         t.tune("fused_form", 9)          # out of range
     assert t.tune("fused_form") == 0
+    # the schedule form's auto default (-1: BO one-wave strips, LO k_steps_pipe) and its range
+    assert t.tune("steps_wave") == -1
+    with t.tuned(steps_wave=4):
+        assert t.tune("steps_wave") == 4
+    with pytest.raises(t.AllredError):
+        t.tune("steps_wave", 5)
+    assert t.tune("steps_wave") == -1
 
 
 def test_tune_env_is_read_at_load():
@@ -125,6 +132,10 @@ def test_tune_env_is_read_at_load():
     env = dict(os.environ, ALLRED_TUNE="steps_form=1,lo_dag_place=0,bogus=3,pipe_grid=99999999")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env).stdout.split()
     assert out == ["1", "0", "0"]   # out-of-range and unknown keys are ignored
+    env = dict(os.environ, ALLRED_TUNE="steps_wave=0")
+    out = subprocess.run([sys.executable, "-c", code.replace("t.tune('steps_form'), ", "t.tune('steps_wave'), ")],
+                         capture_output=True, text=True, env=env).stdout.split()
+    assert out[0] == "0"
 
 
 def test_peer_window_limit_without_gpu():
