@@ -50,6 +50,7 @@ struct allred_plan {
     uint8_t* d_dag = nullptr;               // LO: interned DAG (lo_dag_lanes form), 64 ranks only
     uint8_t* d_steps_tab = nullptr;         // schedule form, one launch: BO per-block phase ranks / LO step pairs
     uint8_t* d_steps_pipe_tab = nullptr;    // the same programs in the pipelined form's layout (k_steps_pipe)
+    bool steps_reg_tab = false;             // BO: k_steps_reg's program appended to d_steps_pipe_tab
     bool steps_persistent = false;          // schedule form as one launch (k_bo_steps / k_lo_steps)
     size_t ws_bytes = 0;
     int launches = 0;
@@ -186,6 +187,40 @@ std::vector<uint8_t> bo_steps_pipe_table(const std::vector<uint8_t>& tab, int N,
             o[body + holders[x]] = (uint8_t)x;
         }
     }
+    return out;
+}
+
+// The BO program for the register-staged schedule form (k_steps_reg), appended
+// to the pipe table: N blocks x 256 bytes, the pipe layout with step 0 recast
+// for loads that cannot depend on the block — the step-0 pairs are the same
+// for every block, only which of the two ranks holds (keeps the sum, adds
+// first) and the holder's row differ.  Pair u = the u-th (r, partner_0(r)) with
+// r < partner in rank order; byte u of a block = its row x | 0x80 when the
+// higher rank holds; bytes H .. 2H-1 zero; phases and result rows as the pipe
+// table.  Then the H pairs' ranks (2 bytes each), shared by every block.
+// Empty if the step-0 pairs are not the pipe table's (never for a valid schedule).
+std::vector<uint8_t> bo_steps_reg_table(const std::vector<uint8_t>& pipe, const allred_schedule& s, int N) {
+    const int H = N / 2;
+    if (pipe.size() != (size_t)kBoPipeTabBytes * N || s.steps < 1) return {};
+    std::vector<uint8_t> pr;
+    for (int r = 0; r < N; ++r)
+        if (r < s.partner[r][0]) pr.push_back((uint8_t)r), pr.push_back((uint8_t)s.partner[r][0]);
+    if ((int)pr.size() != 2 * H) return {};
+    std::vector<uint8_t> out(pipe);
+    for (int b = 0; b < N; ++b) {
+        const uint8_t* t = &pipe[(size_t)b * kBoPipeTabBytes];
+        uint8_t* o = &out[(size_t)b * kBoPipeTabBytes];
+        std::memset(o, 0, 2 * (size_t)H);
+        std::vector<int> seen(H, 0);
+        for (int x = 0; x < H; ++x) {
+            const int r = t[2 * x], q = t[2 * x + 1], lo = r < q ? r : q, hi = r < q ? q : r;
+            int u = 0;
+            while (u < H && !(pr[2 * u] == lo && pr[2 * u + 1] == hi)) ++u;
+            if (u == H || seen[u]++) return {};
+            o[u] = (uint8_t)(x | (r == hi ? 0x80 : 0));
+        }
+    }
+    out.insert(out.end(), pr.begin(), pr.end());
     return out;
 }
 
@@ -555,8 +590,13 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
                 return ALLRED_ERR_SCHEDULE;
             }
         }
-        const std::vector<uint8_t> pipe = desc->variant == ALLRED_BO ? bo_steps_pipe_table(tab, total, steps)
-                                                                     : lo_steps_pipe_table(p->sched, total);
+        std::vector<uint8_t> pipe = desc->variant == ALLRED_BO ? bo_steps_pipe_table(tab, total, steps)
+                                                               : lo_steps_pipe_table(p->sched, total);
+        if (desc->variant == ALLRED_BO && !pipe.empty()) {   // + k_steps_reg's program (bo_steps_reg_table)
+            const std::vector<uint8_t> reg = bo_steps_reg_table(pipe, p->sched, total);
+            pipe.insert(pipe.end(), reg.begin(), reg.end());
+            p->steps_reg_tab = !reg.empty();
+        }
         if ((st = upload(&p->d_steps_tab, tab)) || (st = upload(&p->d_steps_pipe_tab, pipe))) {
             free_plan(p);
             return st;
@@ -703,7 +743,9 @@ int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t strid
     }
     if (p->steps_persistent) {
         if (p->desc.variant == ALLRED_BO)
-            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab, p->block_elems,
+            return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab,
+                                   p->steps_reg_tab ? p->d_steps_pipe_tab + (size_t)kBoPipeTabBytes * N : nullptr,
+                                   p->block_elems,
                                    stamps, stream);
         return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab, p->n, stamps, stream);
     }

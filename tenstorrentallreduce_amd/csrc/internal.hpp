@@ -96,9 +96,11 @@ int write_profile_log(const char* path, int N, int side, const uint64_t* start, 
 // the phase table of engine.cpp bo_steps_table; LO: d_pairs = per step N/2 (r, p) pairs.
 // stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)
 constexpr int kBoPipeTabBytes = 256;   // k_steps_pipe's BO table bytes per block (4N - 4 <= 252)
-// d_pipe_tab: the pipelined form's table (engine.cpp bo_steps_pipe_table / lo_steps_pipe_table), or null
+// d_pipe_tab: the pipelined form's table (engine.cpp bo_steps_pipe_table / lo_steps_pipe_table), or null;
+// d_reg_tab: k_steps_reg's program (bo_steps_reg_table: N x 256 bytes, then the step-0 pairs), or null
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    const uint8_t* d_pipe_tab, size_t block_elems, uint64_t* stamps, void* stream);
+                    const uint8_t* d_pipe_tab, const uint8_t* d_reg_tab, size_t block_elems, uint64_t* stamps,
+                    void* stream);
 uint64_t bo_steps_units(size_t block_elems, int total);
 int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs,
                     const uint8_t* d_pipe_tab, size_t n, uint64_t* stamps, void* stream);

@@ -1547,6 +1547,157 @@ __global__ __launch_bounds__(NW * 64) void k_steps_wave(uint16_t* __restrict__ r
     }
 }
 
+// k_steps_reg<P, BO, MINW>: the schedule form with the strips staged in
+// REGISTERS.  k_steps_wave stages a strip's P rank rows in LDS (8 KiB at P =
+// 64) and then runs the step program in place; two buffers per wave cap a CU
+// at about ten strips in flight, and the step chain (ten dependent LDS phases
+// for BO) is what bounds it.  Here step 0 happens in registers as the rows
+// arrive: lane (pair u, column) loads both ranks of its step-0 pairs straight
+// into VGPRs (global loads, one strip ahead), adds them and writes only the H
+// pair rows to LDS; the later phases then run among those rows exactly as in
+// k_steps_wave, and the result rows are read out and stored.  LDS per wave: H
+// rows x 128 bytes (4 KiB) (+ BO: every block's program, P x 256 bytes, shared
+// by the workgroup's four waves).  Same tables, same adds, same bits as
+// k_steps_pipe.
+//   BO: the step-0 pairs are the same for every block, only which rank holds
+//   (keeps the sum, adds first) and the holder's row differ: tab =
+//   bo_steps_reg_table (engine.cpp), per block 256 bytes — byte u = row of
+//   pair u | 0x80 when its higher rank holds, then the pipe table's phases and
+//   result rows; pairs: H x (lower rank, higher rank).
+//   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
+//   the loads), pairs unused.
+// MINW: waves per SIMD the compiler must allow (BO 64 ranks: 3 -> 141 VGPRs, no
+// spill; 4 -> 128 VGPRs with a spill, slower: profiles/r03_steps_wave_ab.txt).
+template <int P, bool BO, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                         const uint8_t* __restrict__ tab,
+                                                         const uint8_t* __restrict__ pairs, uint64_t bv,
+                                                         uint64_t slices, uint64_t units, uint64_t* __restrict__ stamps) {
+    constexpr int NW = 4, TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
+    constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
+    constexpr int NPH = BO ? 2 * S - 2 : S - 1;
+    constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
+    constexpr int MPH = BO ? (P / 4 * CW + 63) / 64 : IPW;
+    // the program(s) in LDS: BO every block's (P x 256 bytes), LO the one step program (2H S + P <= 448 bytes)
+    constexpr int LOTAB = 2 * H * S + P;
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[BO ? P : 1][BO ? kBoPipeTab : (LOTAB + 15) / 16 * 16];
+    __shared__ __attribute__((aligned(16))) uint4 work[NW][H * CW];   // per wave: the strip's pair rows
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cl = lane % CW, rl = lane / CW;
+    auto cnt_of = [](int ph) {
+        if (!BO) return H;
+        const int k = ph < S ? ph : 2 * S - 1 - ph;
+        return P >> (k + 1);
+    };
+    auto off_of = [&](int ph) {
+        int o = 2 * H;
+        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
+        return o;
+    };
+    uint32_t pra[IPW], prb[IPW];   // this lane's step-0 pairs: first / second rank
+    if constexpr (BO) {
+        for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
+            reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
+#pragma unroll
+        for (int t = 0; t < IPW; ++t) {
+            const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;
+            pra[t] = pairs[2 * u];
+            prb[t] = pairs[2 * u + 1];
+        }
+    } else {
+        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
+        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tab);
+#pragma unroll
+        for (int t = 0; t < IPW; ++t) {
+            const int i = lane + 64 * t;
+            const uint32_t e = i < H * CW ? t16[i / CW] : 0;
+            pra[t] = e & 255;
+            prb[t] = e >> 8;
+        }
+    }
+    __syncthreads();   // the program(s) in LDS (the only barrier)
+    uint4* tile = work[w];
+    const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
+    const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
+    auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
+    auto col0 = [&](uint64_t s) {
+        const uint64_t u = s / Q;
+        return (BO ? (u / slices) * bv + (u % slices) * TV : u * TV) + (s % Q) * CW;
+    };
+    auto grow = [&](uint32_t r) { return reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride); };
+    auto load = [&](int j, uint4 (&A)[IPW], uint4 (&B)[IPW]) {   // both ranks of every pair item of strip j
+        const uint64_t c0 = col0(strip_of(j)) + cl;
+#pragma unroll
+        for (int t = 0; t < IPW; ++t)
+            if (lane + 64 * t < H * CW) {
+                A[t] = ld_nt(grow(pra[t]) + c0);
+                B[t] = ld_nt(grow(prb[t]) + c0);
+            }
+    };
+    // strip j: step 0 from A / B (registers), the later phases among the pair rows, result rows stored
+    auto body = [&](int j, const uint4 (&A)[IPW], const uint4 (&B)[IPW]) {
+        const uint64_t s = strip_of(j);
+        const bool st_on = stamps && s % Q == 0 && lane == 0;
+        if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
+        const uint8_t* tb = tabs[BO ? (s / Q) / slices : 0];
+        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
+        uint4 val[BO ? 1 : IPW];   // LO: this lane's pair rows after the latest step
+#pragma unroll
+        for (int t = 0; t < IPW; ++t)
+            if (lane + 64 * t < H * CW) {
+                if constexpr (BO) {
+                    const uint32_t e = tb[(lane + 64 * t) / CW];   // row | 0x80: the higher rank holds
+                    tile[(e & 127) * CW + cl] = (e & 128) ? add8(B[t], A[t]) : add8(A[t], B[t]);
+                } else {
+                    val[t] = add8(A[t], B[t]);
+                    tile[((lane + 64 * t) / CW) * CW + cl] = val[t];
+                }
+            }
+        if (st_on) stamps[(s / Q) * STAMPS + 1] = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int ph = 1; ph <= NPH; ++ph) {
+            if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
+                const bool rs = ph < S;
+#pragma unroll
+                for (int m = 0; m < MPH; ++m)
+                    if (lane + 64 * m < cnt_of(ph) * CW) {
+                        const uint32_t pr = t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
+                        const int a = (pr & 255) * CW + cl, cc = (pr >> 8) * CW + cl;
+                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
+                    }
+            } else {   // exchange step ph: pair x = row x (kept in val) + the row of its other rank
+                uint4 oth[IPW];
+#pragma unroll
+                for (int m = 0; m < IPW; ++m)
+                    if (lane + 64 * m < H * CW) oth[m] = tile[(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8) * CW + cl];
+#pragma unroll
+                for (int m = 0; m < IPW; ++m)
+                    if (lane + 64 * m < H * CW) {
+                        val[m] = add8(val[m], oth[m]);
+                        tile[((lane + 64 * m) / CW) * CW + cl] = val[m];
+                    }
+            }
+            if (st_on) stamps[(s / Q) * STAMPS + 1 + ph] = __builtin_amdgcn_s_memrealtime();
+        }
+        const uint64_t cs = col0(s) + cl;
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs,
+                  tile[(int)tb[off_of(NPH + 1) + RPO * k + rl] * CW + cl]);
+        }
+        if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
+    };
+    uint4 A0[IPW], B0[IPW], A1[IPW], B1[IPW];
+    if (mine > 0) load(0, A0, B0);
+    for (int j = 0; j < mine; j += 2) {   // two register sets, strip j+1's loads in flight behind strip j's work
+        if (j + 1 < mine) load(j + 1, A1, B1);
+        body(j, A0, B0);
+        if (j + 1 >= mine) break;
+        if (j + 2 < mine) load(j + 2, A0, B0);
+        body(j + 1, A1, B1);
+    }
+}
+
 template <bool ADD, int U>
 __global__ __launch_bounds__(64) void k_step_w(uint16_t* __restrict__ ranks, uint64_t stride,
                                                const int16_t* __restrict__ partner,
@@ -1681,6 +1832,27 @@ bool launch_steps_wave(bool bo, int form, uint16_t* ranks, uint64_t stride, int 
 #undef TSA_SWP
 #undef TSA_SWF
 #undef TSA_SW
+}
+
+// the schedule form with register-staged strips (k_steps_reg): 8..64 ranks; false if the shape has no instance.
+// w4: four 4-wave workgroups per CU (the compiler held to 128 VGPRs), else three
+bool launch_steps_reg(bool bo, bool w4, uint16_t* ranks, uint64_t stride, int total, const uint8_t* tab,
+                      const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
+                      hipStream_t st) {
+    const dim3 grid(persistent_grid(units, w4 ? 1024 : 768));
+#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
+                                               pairs, bv, slices, units, stamps)
+#define TSA_SRP(PP) do { if (bo) { if (w4) TSA_SR(PP, true, 4); else TSA_SR(PP, true, 3); } \
+                         else { if (w4) TSA_SR(PP, false, 4); else TSA_SR(PP, false, 3); } } while (0)
+    switch (total) {
+        case 8: TSA_SRP(8); return true;
+        case 16: TSA_SRP(16); return true;
+        case 32: TSA_SRP(32); return true;
+        case 64: TSA_SRP(64); return true;
+        default: return false;
+    }
+#undef TSA_SRP
+#undef TSA_SR
 }
 
 }  // namespace
@@ -1905,15 +2077,24 @@ int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
 }
 
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    const uint8_t* d_pipe_tab, size_t block_elems, uint64_t* stamps, void* stream) {
+                    const uint8_t* d_pipe_tab, const uint8_t* d_reg_tab, size_t block_elems, uint64_t* stamps,
+                    void* stream) {
     if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
     if (block_elems % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
     hipStream_t st = (hipStream_t)stream;
     // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
+    // register-staged strips (k_steps_reg: steps_wave 5, the auto default (16.3-16.7 vs 17.1-17.5 us for
+    // k_steps_wave and 17.3-17.6 for k_steps_pipe at config 2); 6: 4 groups per CU with a spill, slower)
+    const int64_t swv = tune(Tune::steps_wave);
+    if (d_reg_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total &&
+        (swv >= 5 || swv < 0)) {
+        if (launch_steps_reg(true, swv == 6, ranks, stride, total, d_reg_tab,
+                             d_reg_tab + (size_t)kBoPipeTabBytes * total, bv, slices, units, stamps, st))
+            return last_error();
+    }
     // BO: every wave its own pipeline over 128-byte strips, one-wave workgroups (k_steps_wave, steps_wave 2:
     // 17.0-17.2 vs 17.2-17.7 us for k_steps_pipe at config 2, profiles/r03_steps_wave_ab.txt)
-    const int64_t swv = tune(Tune::steps_wave);
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total && swv != 0) {
         if (launch_steps_wave(true, swv < 0 ? 2 : (int)swv, ranks, stride, total, d_pipe_tab, bv, slices, units,
                               stamps, st))
@@ -1950,8 +2131,14 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
     hipStream_t st = (hipStream_t)stream;
-    // LO: k_steps_pipe below unless steps_wave asks for k_steps_wave (no faster for LO, same file)
+    // LO: k_steps_reg by default (steps_wave -1 / 5: 16.1-16.5 vs 18.2-18.4 us for k_steps_pipe at 640 kB,
+    // profiles/r03_steps_wave_ab.txt); steps_wave 0 k_steps_pipe, 1-4 k_steps_wave (no faster than the pipe)
     const int64_t swv = tune(Tune::steps_wave);
+    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total &&
+        (swv >= 5 || swv < 0)) {
+        if (launch_steps_reg(false, swv == 6, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units, stamps, st))
+            return last_error();
+    }
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total && swv > 0) {
         if (launch_steps_wave(false, (int)swv, ranks, stride, total, d_pipe_tab, 0, 1, units, stamps, st))
             return last_error();

@@ -117,12 +117,12 @@ def test_tune_entry_point():
     with pytest.raises(t.AllredError):
         t.tune("fused_form", 9)          # out of range
     assert t.tune("fused_form") == 0
-    # the schedule form's auto default (-1: BO one-wave strips, LO k_steps_pipe) and its range
+    # the schedule form's auto default (-1: k_steps_reg, register-staged strips) and its range
     assert t.tune("steps_wave") == -1
     with t.tuned(steps_wave=4):
         assert t.tune("steps_wave") == 4
     with pytest.raises(t.AllredError):
-        t.tune("steps_wave", 5)
+        t.tune("steps_wave", 7)
     assert t.tune("steps_wave") == -1
 
 

@@ -1,0 +1,17 @@
+# round-3: k_steps_reg at 3 (steps_wave 5) vs 4 (6, compiler held to 128 VGPRs) workgroups per CU — parity, A/B
+set -o pipefail
+export TMPDIR=/tmp
+out=gpurun_out/r03o
+mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py -x -q -k "schedule_form" \
+    --timeout 200 --timeout-method thread > $out/t.log 2>&1; rc=$?; tail -2 $out/t.log; [ $rc -eq 0 ] || exit $rc
+for r in 1 2 3; do for sw in 2 5 6; do
+  AB_EXEC=steps AB_SETS=32 ALLRED_TUNE=steps_wave=$sw timeout -k 10 120 python tools/ab_fused.py bo 5 200 >> $out/ab.jsonl 2>> $out/ab.err || exit 1
+done; done
+python - <<'PY'
+import json, collections
+by = collections.defaultdict(list)
+for l in open("gpurun_out/r03o/ab.jsonl"):
+    d = json.loads(l); by[(d["variant"], d["env"].get("ALLRED_TUNE"))].append(d["us"])
+for k, v in sorted(by.items()): print(k, v)
+PY

@@ -299,7 +299,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(order, ord.data(), ord.size(), hipMemcpyHostToDevice));
     hipStream_t st;
     CK(hipStreamCreate(&st));
-    constexpr int NF = 11;
+    constexpr int NF = 13;
     auto run = [&](int form, uint16_t* r) {
         if (form == 0)
             hipLaunchKernelGGL((k_tree_lds_pipe_ab<64, 1, 32, true, true>), dim3(grid), dim3(kBlock), 0, st, r, stride,
@@ -323,15 +323,22 @@ int main(int argc, char** argv) {
             hipLaunchKernelGGL((k_tree_lds_lag_ab<64, 32, 7>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
         else if (form == 9)
             hipLaunchKernelGGL((k_tree_lds_lag_ab<64, 32, 8>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
-        else
+        else if (form == 10)
             hipLaunchKernelGGL((k_tree_lds_lag_ab<64, 32, 9>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv, tiles);
+        else if (form == 11)   // 256-byte rows (16 KiB tiles): 2560 tiles, 5 per workgroup (no half-loaded tail)
+            hipLaunchKernelGGL((k_tree_lds_lag_ab<64, 16, 7>), dim3(grid), dim3(kBlock), 0, st, r, stride, order, bv,
+                               tiles * 2);
+        else   // 256-byte rows, 4 workgroups per CU (2.5 tiles each)
+            hipLaunchKernelGGL((k_tree_lds_lag_ab<64, 16, 7>), dim3(2 * grid), dim3(kBlock), 0, st, r, stride, order, bv,
+                               tiles * 2);
     };
     const char* names[NF] = {"k_tree_lds_pipe<64,1,32,true,true>", "k_tree_lds_lag<64,32,0> table first",
                              "k_tree_lds_lag<64,32,1> lds-counter barrier", "k_tree_lds_lag<64,32,2> loads before table",
                              "k_tree_lds_lag<64,32,3> no table (timing only)",
                              "k_tree_lds_lag<64,64,2> 1 KiB rows, grid 256", "k_tree_lds_lag<64,32,2,2> two waves",
                              "k_tree_lds_lag<64,32,2,8> eight waves", "k_tree_lds_lag<64,32,7> interleaved (product)",
-                             "k_tree_lds_lag<64,32,8> interleaved S L", "k_tree_lds_lag<64,32,9> interleaved L L S S"};
+                             "k_tree_lds_lag<64,32,8> interleaved S L", "k_tree_lds_lag<64,32,9> interleaved L L S S",
+                             "k_tree_lds_lag<64,16,7> 256-B rows, grid 512", "k_tree_lds_lag<64,16,7> 256-B rows, grid 1024"};
     // bits: every form on a copy of set 0
     const size_t bytes = (size_t)P * stride * 2;
     std::vector<uint16_t> ref(P * stride), got(P * stride);
