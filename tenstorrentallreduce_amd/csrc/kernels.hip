@@ -1566,8 +1566,10 @@ __global__ __launch_bounds__(NW * 64) void k_steps_wave(uint16_t* __restrict__ r
 //   result rows; pairs: H x (lower rank, higher rank).
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), pairs unused.
-// MINW: waves per SIMD the compiler must allow (BO 64 ranks: 3 -> 141 VGPRs, no
-// spill; 4 -> 128 VGPRs with a spill, slower: profiles/r03_steps_wave_ab.txt).
+// One register set per lane: strip j+1's loads go out right after strip j's
+// step 0 (its registers are free then) and land behind the step chain: 99
+// VGPRs at 64 ranks, four waves per SIMD.  MINW: waves per SIMD the compiler
+// must allow (3, 4, 5: workgroups per CU).
 template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
@@ -1634,8 +1636,10 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 B[t] = ld_nt(grow(prb[t]) + c0);
             }
     };
-    // strip j: step 0 from A / B (registers), the later phases among the pair rows, result rows stored
-    auto body = [&](int j, const uint4 (&A)[IPW], const uint4 (&B)[IPW]) {
+    // strip j: step 0 from A / B (registers), then strip j+1's loads into the same registers (free once
+    // step 0 has written the pair rows), the later phases among the pair rows, result rows stored
+    uint4 A[IPW], B[IPW];
+    auto body = [&](int j) {
         const uint64_t s = strip_of(j);
         const bool st_on = stamps && s % Q == 0 && lane == 0;
         if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
@@ -1654,6 +1658,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 }
             }
         if (st_on) stamps[(s / Q) * STAMPS + 1] = __builtin_amdgcn_s_memrealtime();
+        if (j + 1 < mine) load(j + 1, A, B);   // in flight behind this strip's step chain and stores
 #pragma unroll
         for (int ph = 1; ph <= NPH; ++ph) {
             if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
@@ -1687,15 +1692,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
-    uint4 A0[IPW], B0[IPW], A1[IPW], B1[IPW];
-    if (mine > 0) load(0, A0, B0);
-    for (int j = 0; j < mine; j += 2) {   // two register sets, strip j+1's loads in flight behind strip j's work
-        if (j + 1 < mine) load(j + 1, A1, B1);
-        body(j, A0, B0);
-        if (j + 1 >= mine) break;
-        if (j + 2 < mine) load(j + 2, A0, B0);
-        body(j + 1, A1, B1);
-    }
+    if (mine > 0) load(0, A, B);
+    for (int j = 0; j < mine; ++j) body(j);
 }
 
 template <bool ADD, int U>
@@ -1835,15 +1833,16 @@ bool launch_steps_wave(bool bo, int form, uint16_t* ranks, uint64_t stride, int 
 }
 
 // the schedule form with register-staged strips (k_steps_reg): 8..64 ranks; false if the shape has no instance.
-// w4: four 4-wave workgroups per CU (the compiler held to 128 VGPRs), else three
-bool launch_steps_reg(bool bo, bool w4, uint16_t* ranks, uint64_t stride, int total, const uint8_t* tab,
+// per_cu: four-wave workgroups per CU (3, 4 or 5; 5 x 32 KiB of LDS at 64 ranks fills the CU's 160 KiB)
+bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int total, const uint8_t* tab,
                       const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
                       hipStream_t st) {
-    const dim3 grid(persistent_grid(units, w4 ? 1024 : 768));
+    const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
 #define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
                                                pairs, bv, slices, units, stamps)
-#define TSA_SRP(PP) do { if (bo) { if (w4) TSA_SR(PP, true, 4); else TSA_SR(PP, true, 3); } \
-                         else { if (w4) TSA_SR(PP, false, 4); else TSA_SR(PP, false, 3); } } while (0)
+#define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
+                              else TSA_SR(PP, BOV, 3); } while (0)
+#define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)
     switch (total) {
         case 8: TSA_SRP(8); return true;
         case 16: TSA_SRP(16); return true;
@@ -1852,6 +1851,7 @@ bool launch_steps_reg(bool bo, bool w4, uint16_t* ranks, uint64_t stride, int to
         default: return false;
     }
 #undef TSA_SRP
+#undef TSA_SRB
 #undef TSA_SR
 }
 
@@ -2084,12 +2084,12 @@ int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
     hipStream_t st = (hipStream_t)stream;
     // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
-    // register-staged strips (k_steps_reg: steps_wave 5, the auto default (16.3-16.7 vs 17.1-17.5 us for
-    // k_steps_wave and 17.3-17.6 for k_steps_pipe at config 2); 6: 4 groups per CU with a spill, slower)
+    // register-staged strips (k_steps_reg, the auto default: 3 groups per CU = steps_wave 5, 15.3-15.7 us at
+    // config 2 vs 16.8-17.2 with 4 per CU and 17.3-17.6 for k_steps_pipe, profiles/r03_steps_wave_ab.txt)
     const int64_t swv = tune(Tune::steps_wave);
     if (d_reg_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total &&
         (swv >= 5 || swv < 0)) {
-        if (launch_steps_reg(true, swv == 6, ranks, stride, total, d_reg_tab,
+        if (launch_steps_reg(true, swv < 0 ? 3 : (int)swv - 2, ranks, stride, total, d_reg_tab,
                              d_reg_tab + (size_t)kBoPipeTabBytes * total, bv, slices, units, stamps, st))
             return last_error();
     }
@@ -2131,12 +2131,13 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
     hipStream_t st = (hipStream_t)stream;
-    // LO: k_steps_reg by default (steps_wave -1 / 5: 16.1-16.5 vs 18.2-18.4 us for k_steps_pipe at 640 kB,
-    // profiles/r03_steps_wave_ab.txt); steps_wave 0 k_steps_pipe, 1-4 k_steps_wave (no faster than the pipe)
+    // LO: k_steps_reg by default (4 groups per CU = steps_wave 6: 15.6-15.8 us at 640 kB vs 16.1-16.3 with 3 and
+    // 18.2-18.4 for k_steps_pipe, profiles/r03_steps_wave_ab.txt); 0 k_steps_pipe, 1-4 k_steps_wave (no faster)
     const int64_t swv = tune(Tune::steps_wave);
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total &&
         (swv >= 5 || swv < 0)) {
-        if (launch_steps_reg(false, swv == 6, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units, stamps, st))
+        if (launch_steps_reg(false, swv < 0 ? 4 : (int)swv - 2, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units,
+                             stamps, st))
             return last_error();
     }
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total && swv > 0) {

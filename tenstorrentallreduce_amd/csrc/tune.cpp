@@ -40,8 +40,8 @@ const Key kKeys[] = {
     {"tree_bcast_bal", 0, 0, 1},      // k_tree_bcast_x: every wave stages / stores 8 result columns (0: wave 0 all)
     {"steps_waves", 0, 0, 8},         // k_steps_pipe: waves per workgroup, 0 auto (BO 4, LO 8) | 4 | 8 (>= 16 ranks)
     {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
-    {"steps_wave", -1, -1, 6},        // schedule form: -1 auto (= 5) | 0 k_steps_pipe | k_steps_wave 1: 4-wave
-                                      // workgroups | 2/3/4: one-wave workgroups, 2/3/4 strip buffers | 5/6 k_steps_reg (3/4 groups per CU)
+    {"steps_wave", -1, -1, 7},        // schedule form: -1 auto (BO 5, LO 6) | 0 k_steps_pipe | k_steps_wave 1: 4-wave
+                                      // workgroups | 2/3/4: one-wave workgroups, 2/3/4 strip buffers | 5/6/7 k_steps_reg (3/4/5 groups per CU)
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

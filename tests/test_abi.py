@@ -122,7 +122,7 @@ def test_tune_entry_point():
     with t.tuned(steps_wave=4):
         assert t.tune("steps_wave") == 4
     with pytest.raises(t.AllredError):
-        t.tune("steps_wave", 7)
+        t.tune("steps_wave", 8)
     assert t.tune("steps_wave") == -1
 
 

@@ -93,7 +93,7 @@ def test_config5_reference_inputs(n):
 # ------------------------------------------------------------------ schedule form
 @pytest.mark.parametrize("steps_form,waves,wave_local", [(0, 4, 0), (0, 8, 0), (1, 4, 0), (2, 4, 0), (0, 4, 1),
                                                         (0, 4, 2), (0, 4, 3), (0, 4, 4), (0, 4, 5),
-                                                        (0, 4, 6)])
+                                                        (0, 4, 6), (0, 4, 7)])
 @pytest.mark.parametrize("variant", ["bo", "lo"])
 @pytest.mark.parametrize("algo,grid,n", [(t.SWING, (8, 64), 327680), (t.RECDUB, (8, 64), 327680),
                                          (t.SWING, (8, 64), 64 * 8 * 3), (t.SWING, (4, 8), 8 * 8 * 5),
@@ -122,7 +122,7 @@ def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, waves, wave
     assert np.array_equal(got, np.stack(want))
 
 
-@pytest.mark.parametrize("steps_form,wave_local", [(0, 0), (2, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6)])
+@pytest.mark.parametrize("steps_form,wave_local", [(0, 0), (2, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 7)])
 @pytest.mark.parametrize("variant", [t.BO, t.LO])
 def test_schedule_form_device_stamps(variant, steps_form, wave_local):
     """execute(stamps_ptr=...): every unit's start and per-step stamps
