@@ -2136,8 +2136,11 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     const int64_t swv = tune(Tune::steps_wave);
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total &&
         (swv >= 5 || swv < 0)) {
-        if (launch_steps_reg(false, swv < 0 ? 4 : (int)swv - 2, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units,
-                             stamps, st))
+        // auto: 4 groups per CU, but 3 where 4 would give every wave exactly one strip (768 < units <= 1024:
+        // all loads, then all stores, 17.1 vs 15.4 us at 512 kB; every other size prefers one strip per
+        // group's wave over two: profiles/r03_steps_wave_ab.txt)
+        const int per_cu = swv >= 5 ? (int)swv - 2 : (units > 768 && units <= 1024 ? 3 : 4);
+        if (launch_steps_reg(false, per_cu, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units, stamps, st))
             return last_error();
     }
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total && swv > 0) {
