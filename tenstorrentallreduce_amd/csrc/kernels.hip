@@ -1177,399 +1177,46 @@ __global__ __launch_bounds__(kBlock) void k_lo_steps(uint16_t* __restrict__ rank
     }
 }
 
-// One launch per step (allred_tune_set("steps_form", 1), the round-1 form, A/B):
-// one wave per (rank, block), U vectors' loads in flight per lane.
-//   RS: ranks[r][b] += ranks[p][b] for b in recv_mask_k(r)   (in place: the
-//       pair's recv masks are disjoint, so nobody reads what another writes)
-//   AG: ranks[r][b]  = ranks[p][b] for b in send_mask_k(r) (= recv_mask_k(p))
-// ---------------------------------------------------------------------------
-// k_steps_pipe<P, BO>: the schedule form (every RS / AG step of BO, every
-// exchange step of LO, in order, on the unit's rows) on k_tree_lds_lag's
-// pipeline: a persistent grid of two workgroups per CU, each unit (a 512-byte
-// column slice of all P rank rows, 32 KiB at P = 64) staged into LDS by
-// LDS-DMA two units ahead — the reference's DRAM -> L1 reads — then the step
-// program runs among LDS rows (the Tensix L1 of the reference), and the
-// unit's P result rows are read into registers and stored one iteration late,
-// interleaved with the loads of unit j+2.  Step 0 reads the staged rows of
-// both partners (its sums go to compact rows: the staged rows are the work
-// rows too).  Wave w owns columns 8w .. 8w+7 of every row, so the steps need
-// no workgroup barrier, and each lane fetches all its table entries of the
-// unit in one batch (a step then waits for its operand rows only).  S =
-// log2(P) (every 2D and 1D schedule of P ranks), so the step loop unrolls.
-//   BO tab (bo_steps_pipe_table, 256 bytes per block, staged by LDS-DMA with
-//     the unit): (r, p) x P/2 of RS step 0 -> row i; (row a, row c) pairs of
-//     RS 1..S-1 and AG S-1..1 (RS: a += c, AG: a = c); then P bytes: the row
-//     holding rank r's result after AG step 0 (holders: their own row,
-//     receivers: their step-0 partner's).
-//   LO tab (lo_steps_pipe_table, staged once): per step P/2 (r, p) ranks (step
-//     0) / (row of r, row of p) (steps >= 1) -> row i = pair i; then P bytes:
-//     rank r's pair at the last step.
-// Measured against k_bo_steps / k_lo_steps (all units resident at once, the
-// loads before and the stores after the whole step chain): DESIGN.md §4.
+// The schedule form's programs (engine.cpp), read by k_steps_reg:
+//   BO (bo_steps_pipe_table, 256 bytes per block): (r, p) x P/2 of RS step 0 ->
+//     row i; (row a, row c) pairs of RS 1..S-1 and AG S-1..1 (RS: a += c, AG:
+//     a = c); then P bytes: the row holding rank r's result after AG step 0
+//     (holders: their own row, receivers: their step-0 partner's).
+//   LO (lo_steps_pipe_table): per step P/2 (r, p) ranks (step 0) / (row of r,
+//     row of p) (steps >= 1) -> row i = pair i; then P bytes: rank r's pair at
+//     the last step.
+// S = log2(P) (every 2D and 1D schedule of P ranks), so the step loops unroll.
 // ---------------------------------------------------------------------------
 constexpr int kBoPipeTab = kBoPipeTabBytes;
 
 template <int P>
 constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 
-// NW waves per workgroup (4 or 8): wave w owns TV / NW columns of every row.
-template <int P, bool BO, int NW = 4>
-__global__ __launch_bounds__(NW * 64) void k_steps_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                       const uint8_t* __restrict__ tab, uint64_t bv, uint64_t slices,
-                                                       uint64_t units, uint64_t* __restrict__ stamps) {
-    constexpr int TV = 32, CPW = TV / NW, RPI = 2, RPW = P / NW, OPS = RPW / RPI, H = P / 2, S = log2_of<P>();
-    constexpr int IPW = (H * CPW + 63) / 64;   // items (row pair, one of the wave's CPW columns) per lane, H pairs
-    constexpr int TPW = kBoPipeTab / NW;        // BO table bytes staged per wave
-    constexpr int TOPS = BO ? 1 : 0;          // the BO unit's table comes with its rows
-    constexpr int NPH = BO ? 2 * S - 2 : S - 1;   // phases after step 0
-    constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
-    static_assert(OPS >= 1 && 2 * (OPS + TOPS) + OPS <= 63, "vmcnt is 6 bits");
-    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint8_t tl[BO ? 2 : 1][BO ? kBoPipeTab : 16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane % TV, q = lane / TV;
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
-    const uint32_t tbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&tl[0][0] + (uint32_t)(w * TPW));
-    auto row = [&](int k) { return ranks + (uint64_t)(RPW * w + RPI * k + q) * stride; };
-    const uint64_t G = gridDim.x;
-    const int mine = blockIdx.x < units ? (int)((units - 1 - blockIdx.x) / G + 1) : 0;
-    auto unit_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    auto col0 = [&](uint64_t u) { return BO ? (u / slices) * bv + (u % slices) * TV : u * TV; };
-    auto issue_tab = [&](uint64_t u, int b) {   // BO: TPW bytes of the block's table per wave (TPW / 16 lanes)
-        if constexpr (BO) {
-            if (lane < TPW / 16) lds_dma16(tab + (u / slices) * kBoPipeTab + w * TPW + lane * 16, tbase + (uint32_t)(b * kBoPipeTab));
-        }
-    };
-    auto issue = [&](uint64_t u, int b) {
-        issue_tab(u, b);
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + col0(u) + c, wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
-    };
-    // phase ph (1 .. NPH): its pair count and table offset (bytes), compile-time after unrolling
-    auto cnt_of = [](int ph) {
-        if (!BO) return H;
-        const int k = ph < S ? ph : 2 * S - 1 - ph;
-        return P >> (k + 1);
-    };
-    auto off_of = [&](int ph) {
-        int o = 2 * H;
-        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
-        return o;
-    };
-    constexpr int MPH = BO ? (P / 4 * CPW + 63) / 64 : IPW;   // most items per lane in one phase
-    // This lane's table entries (pair = a | b << 8; final row) for the whole unit,
-    // fetched in one batch: a phase then waits for its operand rows only.
-    uint32_t p0[IPW], pp[NPH > 0 ? NPH : 1][MPH];
-    int fin[OPS];
-    auto fetch = [&](const uint8_t* tb) {   // tb: LDS (BO, per unit) or global (LO, once)
-        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
-#pragma unroll
-        for (int t = 0; t < IPW; ++t) {
-            const int i = lane + 64 * t;
-            p0[t] = i < H * CPW ? t16[i / CPW] : 0;
-        }
-#pragma unroll
-        for (int ph = 1; ph <= NPH; ++ph)
-#pragma unroll
-            for (int m = 0; m < MPH; ++m) {
-                const int i = lane + 64 * m;
-                pp[ph - 1][m] = i < cnt_of(ph) * CPW ? t16[off_of(ph) / 2 + i / CPW] : 0;
-            }
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) fin[k] = tb[off_of(NPH + 1) + RPW * w + RPI * k + q];
-    };
-    if constexpr (!BO) {   // the LO step program is the same for every unit
-        fetch(tab);
-        wait_vm<0>();
-    }
-    if (mine > 0) issue(unit_of(0), 0);
-    if (mine > 1) issue(unit_of(1), 1);
-    uint4 prev[OPS];
-    for (int j = 0; j < mine; ++j) {
-        const uint64_t u = unit_of(j);
-        // after L(j): the last op of S(j-3), L(j+1) (+ its table op), S(j-2)
-        wait_any((j >= 3 ? 1 : 0) + (j + 1 < mine ? OPS + TOPS : 0) + (j >= 2 ? OPS : 0));
-        lds_barrier();   // unit j's rows (and table) are in LDS
-        stamp(stamps, u * STAMPS);
-        uint4* tile = buf[j & 1];
-        if constexpr (BO) fetch(tl[j & 1]);
-        // The step program runs per column: wave w owns columns CPW w .. CPW w + CPW - 1
-        // of every row, so a step needs no workgroup barrier — LDS operations of
-        // one wave execute in order, and no other wave touches these columns.
-        const int cw = CPW * w + lane % CPW;
-        uint4 val[IPW];   // LO: this lane's rows (x = (lane + 64t) / CPW) after the latest step
-        {   // step 0 from the staged rows: pair x = (r, p) -> row x (every read before any write)
-#pragma unroll
-            for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * CPW)
-                    val[t] = add8(tile[(p0[t] & 255) * TV + cw], tile[(p0[t] >> 8) * TV + cw]);
-#pragma unroll
-            for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * CPW) tile[((lane + 64 * t) / CPW) * TV + cw] = val[t];
-            __builtin_amdgcn_wave_barrier();
-            stamp(stamps, u * STAMPS + 1);
-        }
-#pragma unroll
-        for (int ph = 1; ph <= NPH; ++ph) {
-            if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
-                const bool rs = ph < S;
-#pragma unroll
-                for (int m = 0; m < MPH; ++m)
-                    if (lane + 64 * m < cnt_of(ph) * CPW) {
-                        const int a = (pp[ph - 1][m] & 255) * TV + cw, cc = (pp[ph - 1][m] >> 8) * TV + cw;
-                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
-                    }
-            } else {   // exchange step ph: pair x = row x (kept in val) + the row of its other rank
-                uint4 oth[IPW];
-#pragma unroll
-                for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CPW) oth[m] = tile[(pp[ph - 1][m] >> 8) * TV + cw];
-#pragma unroll
-                for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CPW) {
-                        val[m] = add8(val[m], oth[m]);
-                        tile[((lane + 64 * m) / CPW) * TV + cw] = val[m];
-                    }
-            }
-            __builtin_amdgcn_wave_barrier();
-            stamp(stamps, u * STAMPS + 1 + ph);
-        }
-        lds_barrier();   // every column's program is done
-        // the unit's result rows: rank r's value is row fin
-        uint4 cur[OPS];
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) cur[k] = tile[fin[k] * TV + c];
-        lds_barrier();   // every wave has read unit j out of buf[j & 1] (and its table)
-        {   // unit j+2's loads and unit j-1's stores, interleaved op by op
-            const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-            const uint64_t cl = j + 2 < mine ? col0(unit_of(j + 2)) : 0, cs = j >= 1 ? col0(unit_of(j - 1)) : 0;
-            if (j + 2 < mine) issue_tab(unit_of(j + 2), j & 1);
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                if (j + 2 < mine)
-                    lds_dma16(reinterpret_cast<const uint4*>(row(k)) + cl + c, bl + (uint32_t)(RPI * k * TV * 16));
-                if (j >= 1) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + c, prev[k]);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) prev[k] = cur[k];
-        if (BO) stamp(stamps, u * STAMPS + 2 * S);
-    }
-    if (mine > 0) {
-        const uint64_t cs = col0(unit_of(mine - 1));
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + c, prev[k]);
-    }
-}
-
-// k_steps_wave<P, BO, NW, NB>: the schedule form of k_steps_pipe (same steps,
-// same tables, same bits) with every WAVE its own pipeline.  k_steps_pipe's
-// waves already run the step program on their own 8 columns of the unit, but
-// they share the unit's loads (wave w loads rows 16w..16w+15, all 32 columns)
-// and its stores (every row's 32 columns from all waves' LDS columns), so each
-// unit costs two workgroup barriers and the slowest wave paces the four.  Here
-// a wave's work item is a STRIP — 8 columns (128 bytes) of one unit in all P
-// rank rows, 8 KiB at P = 64 — which it loads itself (8 rows x 128 bytes per
-// LDS-DMA instruction), runs the step program on, and stores itself, one strip
-// late and interleaved with strip j+NB's loads; nothing is shared between
-// waves (each also stages its own copy of the block's step table), so no
-// barrier remains and a wave stalls only on its own loads.  NB strip buffers
-// per wave: while a wave runs a strip's step chain (≈2.4 us at config 2, device
-// stamps: ten dependent LDS read-add-write phases), its other NB - 1 buffers'
-// loads stay in flight — with two buffers per wave the chain leaves the CU's
-// share of HBM idle.  Strip s = quarter s % 4 of unit s / 4; wave gw of the
-// grid takes strips gw, gw + GW, ... (NW = 4: the four waves of a workgroup take
-// the four quarters of the same units, so a row's 512 bytes are read at about
-// the same time; NW = 1: one-wave workgroups, as many per CU as LDS allows).
-template <int P, bool BO, int NW, int NB>
-__global__ __launch_bounds__(NW * 64) void k_steps_wave(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                       const uint8_t* __restrict__ tab, uint64_t bv, uint64_t slices,
-                                                       uint64_t units, uint64_t* __restrict__ stamps) {
-    constexpr int TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
-    constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
-    constexpr int TOPS = BO ? 1 : 0;          // the BO strip's table comes with its rows
-    constexpr int NPH = BO ? 2 * S - 2 : S - 1;
-    constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
-    static_assert(OPS >= 1 && NB >= 2, "one op per 8 rows; two buffers at least");
-    __shared__ __attribute__((aligned(16))) uint4 buf[NW][NB][P * CW];
-    __shared__ __attribute__((aligned(16))) uint8_t tl[NW][BO ? NB : 1][BO ? kBoPipeTab : 16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int cl = lane % CW, rl = lane / CW;   // column in the strip; row within a load / store op
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[w][0][0]);
-    const uint32_t tbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&tl[w][0][0]);
-    auto row = [&](int k) { return ranks + (uint64_t)(RPO * k + rl) * stride; };
-    const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
-    const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
-    auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
-    auto col0 = [&](uint64_t s) {
-        const uint64_t u = s / Q;
-        return (BO ? (u / slices) * bv + (u % slices) * TV : u * TV) + (s % Q) * CW;
-    };
-    auto issue_tab = [&](uint64_t s, int b) {   // BO: the block's whole table, 16 lanes x 16 bytes
-        if constexpr (BO) {
-            if (lane < kBoPipeTab / 16) lds_dma16(tab + (s / Q / slices) * kBoPipeTab + lane * 16, tbase + (uint32_t)(b * kBoPipeTab));
-        }
-    };
-    auto issue = [&](uint64_t s, int b) {   // op k: rows RPO k .. RPO k + 7, 128 bytes each -> LDS rows, 1 KiB
-        issue_tab(s, b);
-        const uint64_t c0 = col0(s);
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + c0 + cl, wbase + (uint32_t)(b * P * CW * 16 + k * 1024));
-    };
-    // VMEM ops of iteration i (strip i+NB's loads, strip i-1's stores) and, for
-    // the wait of iteration j, the ops this wave issued after the last of strip j's loads
-    auto ops_it = [&](int i) { return (i + NB < mine ? OPS + TOPS : 0) + (i >= 1 ? OPS : 0); };
-    auto after_load = [&](int j) {
-        int n = 0;
-        if (j >= NB) {   // loaded in iteration j - NB, behind it that iteration's last store
-            n = j - NB >= 1 ? 1 : 0;
-            for (int i = j - NB + 1; i < j; ++i) n += ops_it(i);
-        } else {         // loaded in the prologue
-            for (int x = j + 1; x < NB; ++x) n += x < mine ? OPS + TOPS : 0;
-            for (int i = 0; i < j; ++i) n += ops_it(i);
-        }
-        return n;
-    };
-    auto cnt_of = [](int ph) {
-        if (!BO) return H;
-        const int k = ph < S ? ph : 2 * S - 1 - ph;
-        return P >> (k + 1);
-    };
-    auto off_of = [&](int ph) {
-        int o = 2 * H;
-        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
-        return o;
-    };
-    constexpr int MPH = BO ? (P / 4 * CW + 63) / 64 : IPW;
-    uint32_t p0[IPW], pp[NPH > 0 ? NPH : 1][MPH];
-    int fin[OPS];
-    auto fetch = [&](const uint8_t* tb) {
-        const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
-#pragma unroll
-        for (int t = 0; t < IPW; ++t) {
-            const int i = lane + 64 * t;
-            p0[t] = i < H * CW ? t16[i / CW] : 0;
-        }
-#pragma unroll
-        for (int ph = 1; ph <= NPH; ++ph)
-#pragma unroll
-            for (int m = 0; m < MPH; ++m) {
-                const int i = lane + 64 * m;
-                pp[ph - 1][m] = i < cnt_of(ph) * CW ? t16[off_of(ph) / 2 + i / CW] : 0;
-            }
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) fin[k] = tb[off_of(NPH + 1) + RPO * k + rl];
-    };
-    if constexpr (!BO) {   // the LO step program is the same for every strip
-        fetch(tab);
-        wait_vm<0>();
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-        if (b < mine) issue(strip_of(b), b);
-    uint4 prev[OPS];
-    for (int j = 0; j < mine; ++j) {
-        const uint64_t s = strip_of(j);
-        const int b = j % NB;
-        const bool st_on = stamps && s % Q == 0 && lane == 0;   // one stamp set per unit (its first quarter)
-        wait_any(after_load(j));
-        if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
-        uint4* tile = buf[w][b];
-        if constexpr (BO) fetch(tl[w][b]);
-        uint4 val[IPW];
-        {   // step 0 from the staged rows: pair x = (r, p) -> row x (every read before any write)
-#pragma unroll
-            for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * CW)
-                    val[t] = add8(tile[(p0[t] & 255) * CW + cl], tile[(p0[t] >> 8) * CW + cl]);
-#pragma unroll
-            for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * CW) tile[((lane + 64 * t) / CW) * CW + cl] = val[t];
-            if (st_on) stamps[(s / Q) * STAMPS + 1] = __builtin_amdgcn_s_memrealtime();
-        }
-#pragma unroll
-        for (int ph = 1; ph <= NPH; ++ph) {
-            if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
-                const bool rs = ph < S;
-#pragma unroll
-                for (int m = 0; m < MPH; ++m)
-                    if (lane + 64 * m < cnt_of(ph) * CW) {
-                        const int a = (pp[ph - 1][m] & 255) * CW + cl, cc = (pp[ph - 1][m] >> 8) * CW + cl;
-                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
-                    }
-            } else {   // exchange step ph: pair x = row x (kept in val) + the row of its other rank
-                uint4 oth[IPW];
-#pragma unroll
-                for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CW) oth[m] = tile[(pp[ph - 1][m] >> 8) * CW + cl];
-#pragma unroll
-                for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CW) {
-                        val[m] = add8(val[m], oth[m]);
-                        tile[((lane + 64 * m) / CW) * CW + cl] = val[m];
-                    }
-            }
-            if (st_on) stamps[(s / Q) * STAMPS + 1 + ph] = __builtin_amdgcn_s_memrealtime();
-        }
-        // the strip's result rows: rank r's value is row fin
-        uint4 cur[OPS];
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) cur[k] = tile[fin[k] * CW + cl];
-        // every LDS read of buffer b (and of its table) has returned before strip
-        // j+NB's LDS-DMA may land there
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        {   // strip j+NB's loads and strip j-1's stores, interleaved op by op
-            const bool ld = j + NB < mine;
-            const uint32_t bl = wbase + (uint32_t)(b * P * CW * 16);
-            const uint64_t cld = ld ? col0(strip_of(j + NB)) : 0, cs = j >= 1 ? col0(strip_of(j - 1)) : 0;
-            if (ld) issue_tab(strip_of(j + NB), b);
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                if (ld) lds_dma16(reinterpret_cast<const uint4*>(row(k)) + cld + cl, bl + (uint32_t)(k * 1024));
-                if (j >= 1) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + cl, prev[k]);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) prev[k] = cur[k];
-        if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
-    }
-    if (mine > 0) {
-        const uint64_t cs = col0(strip_of(mine - 1));
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) st_nt(reinterpret_cast<uint4*>(row(k)) + cs + cl, prev[k]);
-    }
-}
-
-// k_steps_reg<P, BO, MINW>: the schedule form with the strips staged in
-// REGISTERS.  k_steps_wave stages a strip's P rank rows in LDS (8 KiB at P =
-// 64) and then runs the step program in place; two buffers per wave cap a CU
-// at about ten strips in flight, and the step chain (ten dependent LDS phases
-// for BO) is what bounds it.  Here step 0 happens in registers as the rows
-// arrive: lane (pair u, column) loads both ranks of its step-0 pairs straight
-// into VGPRs (global loads, one strip ahead), adds them and writes only the H
-// pair rows to LDS; the later phases then run among those rows exactly as in
-// k_steps_wave, and the result rows are read out and stored.  LDS per wave: H
-// rows x 128 bytes (4 KiB) (+ BO: every block's program, P x 256 bytes, shared
-// by the workgroup's four waves).  Same tables, same adds, same bits as
-// k_steps_pipe.
+// k_steps_reg<P, BO, MINW>: the schedule form (every RS / AG step of BO, every
+// exchange step of LO, in order, one persistent launch).  A wave's work item
+// is a STRIP: 8 columns (128 bytes) of one 512-byte unit in all P rank rows.
+// Step 0 happens in registers as the rows arrive: lane (pair u, column) loads
+// both ranks of its step-0 pairs straight into VGPRs and adds them; only the
+// H pair rows go to LDS (4 KiB per wave), where the later phases run as the
+// tables' row moves (RS a += c, AG a = c; LO: pair x = row x, kept in a
+// register, + its other operand); then the result rows are read out and
+// stored.  One register set per lane: strip j+1's loads go out right after
+// strip j's step 0 (its registers are free then) and land behind strip j's
+// step chain (99 VGPRs at 64 ranks, four waves per SIMD).  No barrier after
+// the programs are staged.  The round-2 form (k_steps_pipe) staged a whole
+// unit's rank rows in LDS by LDS-DMA and ran the step program there: the step
+// chain (ten dependent LDS phases for BO, ≈2.4 us per strip) then held the
+// unit's buffer, so a CU had only about ten strips in flight (17.4 / 18.3 us
+// BO / LO at config 2, no better with every wave its own LDS pipeline or
+// deeper LDS prefetch: profiles/r03_steps_wave_ab.txt; both removed).
 //   BO: the step-0 pairs are the same for every block, only which rank holds
 //   (keeps the sum, adds first) and the holder's row differ: tab =
 //   bo_steps_reg_table (engine.cpp), per block 256 bytes — byte u = row of
 //   pair u | 0x80 when its higher rank holds, then the pipe table's phases and
-//   result rows; pairs: H x (lower rank, higher rank).
+//   result rows — in LDS for the workgroup; pairs: H x (lower rank, higher rank).
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
-//   the loads), pairs unused.
-// One register set per lane: strip j+1's loads go out right after strip j's
-// step 0 (its registers are free then) and land behind the step chain: 99
-// VGPRs at 64 ranks, four waves per SIMD.  MINW: waves per SIMD the compiler
-// must allow (3, 4, 5: workgroups per CU).
+//   the loads), in LDS; pairs unused.
+// MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
 template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
@@ -1696,6 +1343,11 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     for (int j = 0; j < mine; ++j) body(j);
 }
 
+// One launch per step (allred_tune_set("steps_form", 1), the round-1 form, A/B):
+// one wave per (rank, block), U vectors' loads in flight per lane.
+//   RS: ranks[r][b] += ranks[p][b] for b in recv_mask_k(r)   (in place: the
+//       pair's recv masks are disjoint, so nobody reads what another writes)
+//   AG: ranks[r][b]  = ranks[p][b] for b in send_mask_k(r) (= recv_mask_k(p))
 template <bool ADD, int U>
 __global__ __launch_bounds__(64) void k_step_w(uint16_t* __restrict__ ranks, uint64_t stride,
                                                const int16_t* __restrict__ partner,
@@ -1804,32 +1456,6 @@ unsigned persistent_grid(uint64_t tiles, uint64_t dflt) {
     const int64_t g = tune(Tune::pipe_grid);
     const uint64_t cap = g > 0 ? (uint64_t)g : dflt;
     return (unsigned)(tiles < cap ? tiles : cap);
-}
-
-// the schedule form with wave-local strips (k_steps_wave): 8..64 ranks; false if the shape has no instance.
-// steps_wave 1: 4-wave workgroups, 2 strip buffers per wave, 2 workgroups per CU; 2 / 3 / 4: one-wave
-// workgroups with 2 / 3 / 4 buffers, 8 / 6 / 4 per CU (LDS: 16.5 / 24.75 / 33 KiB per wave at 64 ranks)
-bool launch_steps_wave(bool bo, int form, uint16_t* ranks, uint64_t stride, int total, const uint8_t* tab,
-                       uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps, hipStream_t st) {
-    if (form < 1 || form > 4) return false;
-    const uint64_t strips = units * 4;
-    static const unsigned per_cu[5] = {0, 0, 8, 6, 4};
-    const dim3 grid(form == 1 ? persistent_grid(units, 512) : persistent_grid(strips, 256 * per_cu[form]));
-#define TSA_SW(PP, BOV, NWV, NBV) hipLaunchKernelGGL((k_steps_wave<PP, BOV, NWV, NBV>), grid, dim3(NWV * 64), 0, st, \
-                                                     ranks, stride, tab, bv, slices, units, stamps)
-#define TSA_SWF(PP, BOV) do { switch (form) { case 1: TSA_SW(PP, BOV, 4, 2); break; case 2: TSA_SW(PP, BOV, 1, 2); break; \
-                                              case 3: TSA_SW(PP, BOV, 1, 3); break; default: TSA_SW(PP, BOV, 1, 4); } } while (0)
-#define TSA_SWP(PP) do { if (bo) TSA_SWF(PP, true); else TSA_SWF(PP, false); } while (0)
-    switch (total) {
-        case 8: TSA_SWP(8); return true;
-        case 16: TSA_SWP(16); return true;
-        case 32: TSA_SWP(32); return true;
-        case 64: TSA_SWP(64); return true;
-        default: return false;
-    }
-#undef TSA_SWP
-#undef TSA_SWF
-#undef TSA_SW
 }
 
 // the schedule form with register-staged strips (k_steps_reg): 8..64 ranks; false if the shape has no instance.
@@ -2083,37 +1709,13 @@ int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (block_elems % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
     hipStream_t st = (hipStream_t)stream;
-    // whole 512-byte slices, 8..64 ranks: the pipelined form (k_steps_pipe)
-    // register-staged strips (k_steps_reg, the auto default: 3 groups per CU = steps_wave 5, 15.3-15.7 us at
-    // config 2 vs 16.8-17.2 with 4 per CU and 17.3-17.6 for k_steps_pipe, profiles/r03_steps_wave_ab.txt)
-    const int64_t swv = tune(Tune::steps_wave);
-    if (d_reg_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total &&
-        (swv >= 5 || swv < 0)) {
-        if (launch_steps_reg(true, swv < 0 ? 3 : (int)swv - 2, ranks, stride, total, d_reg_tab,
-                             d_reg_tab + (size_t)kBoPipeTabBytes * total, bv, slices, units, stamps, st))
+    // whole 512-byte slices, 8..64 ranks: the register-staged form (k_steps_reg), 3 workgroups per CU by
+    // default (15.3-15.7 us at config 2 vs 16.8-17.2 with 4 per CU, profiles/r03_steps_wave_ab.txt)
+    if (d_reg_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
+        const int g = (int)tune(Tune::steps_groups);
+        if (launch_steps_reg(true, g ? g : 3, ranks, stride, total, d_reg_tab, d_reg_tab + (size_t)kBoPipeTabBytes * total,
+                             bv, slices, units, stamps, st))
             return last_error();
-    }
-    // BO: every wave its own pipeline over 128-byte strips, one-wave workgroups (k_steps_wave, steps_wave 2:
-    // 17.0-17.2 vs 17.2-17.7 us for k_steps_pipe at config 2, profiles/r03_steps_wave_ab.txt)
-    if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total && swv != 0) {
-        if (launch_steps_wave(true, swv < 0 ? 2 : (int)swv, ranks, stride, total, d_pipe_tab, bv, slices, units,
-                              stamps, st))
-            return last_error();
-    }
-    if (d_pipe_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
-        const dim3 grid(persistent_grid(units, 512));
-        // BO: 4 waves (17.4-17.6 vs 18.9-19.2 us with 8 at config 2, profiles/r03_steps_waves_ab.txt)
-        const bool w8 = tune(Tune::steps_waves) == 8 && total >= 16;
-#define TSA_SP(PP, NWV) hipLaunchKernelGGL((k_steps_pipe<PP, true, NWV>), grid, dim3(NWV * 64), 0, st, ranks, stride, \
-                                           d_pipe_tab, bv, slices, units, stamps)
-        switch (total) {
-            case 8: TSA_SP(8, 4); return last_error();
-            case 16: if (w8) TSA_SP(16, 8); else TSA_SP(16, 4); return last_error();
-            case 32: if (w8) TSA_SP(32, 8); else TSA_SP(32, 4); return last_error();
-            case 64: if (w8) TSA_SP(64, 8); else TSA_SP(64, 4); return last_error();
-            default: break;
-        }
-#undef TSA_SP
     }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
     hipLaunchKernelGGL(k_bo_steps, dim3(grid), dim3(kBlock), 0, st, ranks, stride, d_tab, total, steps,
@@ -2131,36 +1733,14 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
     hipStream_t st = (hipStream_t)stream;
-    // LO: k_steps_reg by default (4 groups per CU = steps_wave 6: 15.6-15.8 us at 640 kB vs 16.1-16.3 with 3 and
-    // 18.2-18.4 for k_steps_pipe, profiles/r03_steps_wave_ab.txt); 0 k_steps_pipe, 1-4 k_steps_wave (no faster)
-    const int64_t swv = tune(Tune::steps_wave);
-    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total &&
-        (swv >= 5 || swv < 0)) {
-        // auto: 4 groups per CU, but 3 where 4 would give every wave exactly one strip (768 < units <= 1024:
-        // all loads, then all stores, 17.1 vs 15.4 us at 512 kB; every other size prefers one strip per
-        // group's wave over two: profiles/r03_steps_wave_ab.txt)
-        const int per_cu = swv >= 5 ? (int)swv - 2 : (units > 768 && units <= 1024 ? 3 : 4);
+    // whole 512-byte slices, 8..64 ranks: k_steps_reg, 4 workgroups per CU by default (15.6-15.8 us at 640 kB
+    // vs 16.1-16.3 with 3), but 3 where 4 would give every wave exactly one strip (768 < units <= 1024: all
+    // loads, then all stores, 17.1 vs 15.4 us at 512 kB; profiles/r03_steps_wave_ab.txt)
+    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
+        const int g = (int)tune(Tune::steps_groups);
+        const int per_cu = g ? g : (units > 768 && units <= 1024 ? 3 : 4);
         if (launch_steps_reg(false, per_cu, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units, stamps, st))
             return last_error();
-    }
-    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total && swv > 0) {
-        if (launch_steps_wave(false, (int)swv, ranks, stride, total, d_pipe_tab, 0, 1, units, stamps, st))
-            return last_error();
-    }
-    if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
-        const dim3 grid(persistent_grid(units, 512));
-        // LO (LDS-bound steps): 8 waves (18.2-18.5 vs 19.0-19.2 us with 4 at 640 kB, same file)
-        const bool w8 = tune(Tune::steps_waves) != 4 && total >= 16;
-#define TSA_SP(PP, NWV) hipLaunchKernelGGL((k_steps_pipe<PP, false, NWV>), grid, dim3(NWV * 64), 0, st, ranks, stride, \
-                                           d_pipe_tab, (uint64_t)0, (uint64_t)1, units, stamps)
-        switch (total) {
-            case 8: TSA_SP(8, 4); return last_error();
-            case 16: if (w8) TSA_SP(16, 8); else TSA_SP(16, 4); return last_error();
-            case 32: if (w8) TSA_SP(32, 8); else TSA_SP(32, 4); return last_error();
-            case 64: if (w8) TSA_SP(64, 8); else TSA_SP(64, 4); return last_error();
-            default: break;
-        }
-#undef TSA_SP
     }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
     hipLaunchKernelGGL(k_lo_steps, dim3(grid), dim3(kBlock), 0, st, ranks, stride, d_pairs, total,

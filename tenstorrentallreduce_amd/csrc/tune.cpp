@@ -38,10 +38,8 @@ const Key kKeys[] = {
     {"lo_tree_min_tiles", 64, 0, 1ll << 40},   // 64-rank rank-uniform LO: tree pass from this many 256-element tiles
     {"tree_bcast_lag", 1, 0, 1},      // k_tree_bcast_x: the row stores one iteration behind the tree (0: same iteration)
     {"tree_bcast_bal", 0, 0, 1},      // k_tree_bcast_x: every wave stages / stores 8 result columns (0: wave 0 all)
-    {"steps_waves", 0, 0, 8},         // k_steps_pipe: waves per workgroup, 0 auto (BO 4, LO 8) | 4 | 8 (>= 16 ranks)
     {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
-    {"steps_wave", -1, -1, 7},        // schedule form: -1 auto (BO 5, LO 6) | 0 k_steps_pipe | k_steps_wave 1: 4-wave
-                                      // workgroups | 2/3/4: one-wave workgroups, 2/3/4 strip buffers | 5/6/7 k_steps_reg (3/4/5 groups per CU)
+    {"steps_groups", 0, 0, 5},        // k_steps_reg: workgroups per CU, 0 auto (BO 3, LO 4 or 3) | 3 | 4 | 5
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

@@ -117,13 +117,13 @@ def test_tune_entry_point():
     with pytest.raises(t.AllredError):
         t.tune("fused_form", 9)          # out of range
     assert t.tune("fused_form") == 0
-    # the schedule form's auto default (-1: k_steps_reg, register-staged strips) and its range
-    assert t.tune("steps_wave") == -1
-    with t.tuned(steps_wave=4):
-        assert t.tune("steps_wave") == 4
+    # the schedule form's grid: auto by default, at most 5 workgroups per CU
+    assert t.tune("steps_groups") == 0
+    with t.tuned(steps_groups=4):
+        assert t.tune("steps_groups") == 4
     with pytest.raises(t.AllredError):
-        t.tune("steps_wave", 8)
-    assert t.tune("steps_wave") == -1
+        t.tune("steps_groups", 6)
+    assert t.tune("steps_groups") == 0
 
 
 def test_tune_env_is_read_at_load():
@@ -132,10 +132,10 @@ def test_tune_env_is_read_at_load():
     env = dict(os.environ, ALLRED_TUNE="steps_form=1,lo_dag_place=0,bogus=3,pipe_grid=99999999")
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env).stdout.split()
     assert out == ["1", "0", "0"]   # out-of-range and unknown keys are ignored
-    env = dict(os.environ, ALLRED_TUNE="steps_wave=0")
-    out = subprocess.run([sys.executable, "-c", code.replace("t.tune('steps_form'), ", "t.tune('steps_wave'), ")],
+    env = dict(os.environ, ALLRED_TUNE="steps_groups=3")
+    out = subprocess.run([sys.executable, "-c", code.replace("t.tune('steps_form'), ", "t.tune('steps_groups'), ")],
                          capture_output=True, text=True, env=env).stdout.split()
-    assert out[0] == "0"
+    assert out[0] == "3"
 
 
 def test_peer_window_limit_without_gpu():

@@ -91,9 +91,7 @@ def test_config5_reference_inputs(n):
 
 
 # ------------------------------------------------------------------ schedule form
-@pytest.mark.parametrize("steps_form,waves,wave_local", [(0, 4, 0), (0, 8, 0), (1, 4, 0), (2, 4, 0), (0, 4, 1),
-                                                        (0, 4, 2), (0, 4, 3), (0, 4, 4), (0, 4, 5),
-                                                        (0, 4, 6), (0, 4, 7)])
+@pytest.mark.parametrize("steps_form,groups", [(0, 0), (0, 3), (0, 4), (0, 5), (1, 0), (2, 0)])
 @pytest.mark.parametrize("variant", ["bo", "lo"])
 @pytest.mark.parametrize("algo,grid,n", [(t.SWING, (8, 64), 327680), (t.RECDUB, (8, 64), 327680),
                                          (t.SWING, (8, 64), 64 * 8 * 3), (t.SWING, (4, 8), 8 * 8 * 5),
@@ -101,20 +99,18 @@ def test_config5_reference_inputs(n):
                                          (t.SWING, (1, 1), 64), (t.SWING, (4, 8), 8 * 256 * 3),
                                          (t.SWING, (8, 32), 32 * 256 * 3), (t.RECDUB, (4, 16), 16 * 256 * 5),
                                          (t.SWING_1D, (1, 16), 16 * 256 * 2), (t.SWING, (8, 64), 1 << 20)])
-def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, waves, wave_local):
-    """The schedule form as one pipelined launch (k_steps_pipe, steps_form 0:
-    whole 512-byte units of 8..64 ranks staged into LDS two ahead, the step
-    program among LDS rows, stores one unit late; other shapes fall back to
-    k_bo_steps / k_lo_steps), with every unit resident at once (steps_form 2)
-    and as one launch per step (steps_form 1, the round-1 kernels), on slices
+def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, groups):
+    """The schedule form as one persistent launch (k_steps_reg, steps_form 0:
+    128-byte strips of whole 512-byte units of 8..64 ranks, step 0 from
+    registers, the later steps among LDS rows; other shapes fall back to
+    k_bo_steps / k_lo_steps) at the auto grid and at 3 / 4 / 5 workgroups per
+    CU (steps_groups), with every unit resident at once (steps_form 2) and as
+    one launch per step (steps_form 1, the round-1 kernels), on slices
     narrower than a unit (3 and 5 vectors per block), odd unit counts and at
-    config-2 size, against the oracle; k_steps_pipe with 4 and 8 waves per
-    workgroup (steps_waves); k_steps_wave (every wave its own pipeline over
-    128-byte strips, steps_wave 1: 4-wave workgroups, 2 / 3 / 4: one-wave
-    workgroups with 2 / 3 / 4 strip buffers)."""
+    config-2 size, against the oracle."""
     side, total = grid
     ranks = rand_ranks(total, n, seed=7 * total + n % 97 + algo)
-    with t.tuned(steps_form=steps_form, steps_waves=waves, steps_wave=wave_local):
+    with t.tuned(steps_form=steps_form, steps_groups=groups):
         got = run_plan(algo, {"bo": t.BO, "lo": t.LO}[variant], side, total, ranks, t.EXEC_STEPS,
                        stride=n + 64)
     want = [r.copy() for r in ranks]
@@ -122,9 +118,9 @@ def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, waves, wave
     assert np.array_equal(got, np.stack(want))
 
 
-@pytest.mark.parametrize("steps_form,wave_local", [(0, 0), (2, 0), (0, 1), (0, 2), (0, 3), (0, 4), (0, 5), (0, 6), (0, 7)])
+@pytest.mark.parametrize("steps_form,groups", [(0, 0), (2, 0), (0, 4)])
 @pytest.mark.parametrize("variant", [t.BO, t.LO])
-def test_schedule_form_device_stamps(variant, steps_form, wave_local):
+def test_schedule_form_device_stamps(variant, steps_form, groups):
     """execute(stamps_ptr=...): every unit's start and per-step stamps
     (s_memrealtime, 100 MHz) are written and monotonic within a unit; the
     per-rank zones (allred_plan_rank_zones) open before they close, and the
@@ -133,11 +129,11 @@ def test_schedule_form_device_stamps(variant, steps_form, wave_local):
     ranks = rand_ranks(total, n, seed=99)
     host = np.stack(ranks)
     buf = torch.from_numpy(host.view(np.int16)).to(DEV)
-    with t.tuned(steps_form=steps_form, steps_wave=wave_local):
+    with t.tuned(steps_form=steps_form, steps_groups=groups):
         plan = t.Plan(t.SWING, variant, side, n, total, t.EXEC_STEPS)
     assert plan.launches == 1 and plan.stamp_words > 0
     st = torch.zeros(plan.stamp_words, dtype=torch.int64, device=DEV)
-    with t.tuned(steps_form=steps_form, steps_wave=wave_local):
+    with t.tuned(steps_form=steps_form, steps_groups=groups):
         plan.execute(buf.data_ptr(), n, None, torch.cuda.current_stream(), stamps_ptr=st.data_ptr())
     torch.cuda.synchronize()
     stamps = st.cpu().numpy().view(np.uint64)
