@@ -117,11 +117,12 @@ int allred_schedule_build(int algo, int side_length, int total_nodes, allred_sch
  * *read_conflicts = extra LDS bank cycles of its reads per column group and
  * tile (0 once placed; allred_tune_set("lo_dag_place", 0) keeps first-appearance order). */
 int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size_t cap, int* read_conflicts);
-/* The schedule form's step program as k_steps_pipe reads it (kernels.hip):
+/* The schedule form's step program as k_steps_reg reads it (kernels.hip):
  * the per-core RS / AG loops of allred_BO_2D/kernels/dataflow_kernel.cpp:152-267
  * (variant ALLRED_BO: total x 256 bytes, one block per 256) or the LO exchange
  * steps of allred_LOO_2D/kernels/dataflow_kernel.cpp:127-175 (ALLRED_LO:
- * 2 (total/2) S + total bytes), restated on the unit's LDS rows.  Returns the
+ * 2 (total/2) S + total bytes), restated on a strip's pair rows (BO: the
+ * kernel recasts step 0 per block for its register-staged loads).  Returns the
  * bytes written into out[cap], 0 when the schedule has no such program, or a
  * negative status.  For inspection and CPU checks (tests/test_steps_program.py). */
 int allred_steps_program(int algo, int variant, int side_length, int total_nodes, uint8_t* out, size_t cap);
@@ -242,9 +243,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     bucket's rows of a tile one iteration after the tile's tree (0: in the same one)
  *   tree_bcast_bal    0; 1: k_tree_bcast_x spreads the result-tile loads and partial stores over
  *                     its four waves (8 columns each) instead of wave 0
- *   steps_waves       0: waves per workgroup of the pipelined schedule form k_steps_pipe — 0 auto
- *                     (BO 4, LO 8: the LO steps are LDS-bound), 4, or 8 (each wave owns 4 columns
- *                     of every row; 16 ranks and more)
+ *   steps_groups      0: workgroups per CU of the schedule form k_steps_reg — 0 auto (BO 3; LO 4,
+ *                     or 3 where 4 would leave every wave exactly one strip), 3, 4 or 5
  *   hier_x_lag        1: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
  *                     iteration after the tree of the matching tile of the bucket being read; 0: in
  *                     the same iteration

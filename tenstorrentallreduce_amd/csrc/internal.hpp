@@ -95,7 +95,7 @@ int write_profile_log(const char* path, int N, int side, const uint64_t* start, 
 // the schedule form as one persistent launch (k_bo_steps / k_lo_steps).  BO: d_tab = per block
 // the phase table of engine.cpp bo_steps_table; LO: d_pairs = per step N/2 (r, p) pairs.
 // stamps: null, or bo/lo_steps_units() x (2S + 1) / (S + 1) words (s_memrealtime)
-constexpr int kBoPipeTabBytes = 256;   // k_steps_pipe's BO table bytes per block (4N - 4 <= 252)
+constexpr int kBoPipeTabBytes = 256;   // the schedule form's BO program bytes per block (4N - 4 <= 252)
 // d_pipe_tab: the pipelined form's table (engine.cpp bo_steps_pipe_table / lo_steps_pipe_table), or null;
 // d_reg_tab: k_steps_reg's program (bo_steps_reg_table: N x 256 bytes, then the step-0 pairs), or null
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,

@@ -1,5 +1,5 @@
 """The schedule form's step programs (allred_steps_program: the tables
-k_steps_pipe reads) evaluated on the CPU the way the kernel runs them — step
+k_steps_reg reads) evaluated on the CPU the way the kernel runs them — step
 0 sums pairs of staged rank rows into compact rows (every read before any
 write), BO's later phases add / copy among those rows, LO's later steps add
 the row kept in the lane's register to the other operand row — against the
@@ -34,7 +34,7 @@ def bf16_add(a, b):
 
 
 def run_bo(tab, total, block):
-    """k_steps_pipe<P, true> on one block's staged rows ([total, cols])."""
+    """the BO schedule form (k_steps_reg<P, true>) on one block's rank rows ([total, cols])."""
     H, S = total // 2, total.bit_length() - 1
     rows = block.copy()
     p0 = tab[:2 * H].reshape(H, 2)
