@@ -124,7 +124,12 @@ int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size
  * 2 (total/2) S + total bytes), restated on a strip's pair rows (BO: the
  * kernel recasts step 0 per block for its register-staged loads).  Returns the
  * bytes written into out[cap], 0 when the schedule has no such program, or a
- * negative status.  For inspection and CPU checks (tests/test_steps_program.py). */
+ * negative status.  For inspection and CPU checks (tests/test_steps_program.py).
+ * variant ALLRED_BO | ALLRED_STEPS_REG: the program k_steps_reg actually loads
+ * for BO (engine.cpp bo_steps_reg_table): per block 256 bytes with step 0 recast
+ * as byte u = row of step-0 pair u | 0x80 when its higher rank holds, then the
+ * (total/2) pairs' (lower, higher) ranks — total x 256 + total bytes. */
+#define ALLRED_STEPS_REG 0x100
 int allred_steps_program(int algo, int variant, int side_length, int total_nodes, uint8_t* out, size_t cap);
 
 /* ======================================================================

@@ -35,6 +35,7 @@ lib = C.CDLL(LIB_PATH)
 OK, ERR_ARG, ERR_SCHEDULE, ERR_HIP, ERR_RCCL, ERR_NOMEM, ERR_UNSUPPORTED, ERR_TRANSPORT = 0, -1, -2, -3, -4, -5, -6, -7
 RECDUB, SWING, RECDUB_1D, SWING_1D = 0, 1, 2, 3
 BO, LO, MEM = 0, 1, 2
+STEPS_REG = 0x100   # allred_steps_program: | ALLRED_BO -> the register-staged form's program
 EXEC_STEPS, EXEC_FUSED = 0, 1
 ACC_FP32, ACC_BF16 = 0, 1
 ABI_VERSION = 3

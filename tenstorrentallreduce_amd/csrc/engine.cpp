@@ -657,14 +657,15 @@ int allred_lo_dag(int algo, int side_length, int total_nodes, uint8_t* out, size
 
 int allred_steps_program(int algo, int variant, int side_length, int total_nodes, uint8_t* out, size_t cap) {
     if (!out && cap) return ALLRED_ERR_ARG;
-    if (variant != ALLRED_BO && variant != ALLRED_LO) return ALLRED_ERR_ARG;
+    const bool reg = variant == (ALLRED_BO | ALLRED_STEPS_REG);
+    if (variant != ALLRED_BO && variant != ALLRED_LO && !reg) return ALLRED_ERR_ARG;
     const int total = total_nodes > 0 ? total_nodes : side_length * side_length;
     allred_schedule s{};
     int st = build_schedule(algo, side_length, total, &s, nullptr);
     if (st) return st;
-    const std::vector<uint8_t> prog = variant == ALLRED_BO
-                                          ? bo_steps_pipe_table(bo_steps_table(s, total), total, s.steps)
-                                          : lo_steps_pipe_table(s, total);
+    std::vector<uint8_t> prog = variant == ALLRED_LO ? lo_steps_pipe_table(s, total)
+                                                     : bo_steps_pipe_table(bo_steps_table(s, total), total, s.steps);
+    if (reg) prog = bo_steps_reg_table(prog, s, total);
     if (prog.empty()) return 0;
     if (cap < prog.size()) return ALLRED_ERR_ARG;
     std::memcpy(out, prog.data(), prog.size());

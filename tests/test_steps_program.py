@@ -90,6 +90,60 @@ def test_bo_program_matches_oracle(grid, algo):
     assert (got == np.stack(want)).all()
 
 
+def run_bo_reg(tab, pairs, total, block):
+    """k_steps_reg<P, true> on one block's rank rows: step 0 from the block-independent
+    pairs (lower, higher rank) as the loads see them, holder first, into the holder's row;
+    then the same phases and result rows as the pipe table."""
+    H, S = total // 2, total.bit_length() - 1
+    rows = np.zeros_like(block)
+    for u in range(H):
+        x, swap = tab[u] & 127, tab[u] >> 7
+        a, b = block[pairs[2 * u]], block[pairs[2 * u + 1]]
+        rows[x] = bf16_add(b, a) if swap else bf16_add(a, b)
+    e = 2 * H
+    for ph in range(1, 2 * S - 1):
+        rs = ph < S
+        k = ph if rs else 2 * S - 1 - ph
+        for x in range(total >> (k + 1)):
+            a, c = tab[e + 2 * x], tab[e + 2 * x + 1]
+            rows[a] = bf16_add(rows[a], rows[c]) if rs else rows[c].copy()
+        e += 2 * (total >> (k + 1))
+    return np.stack([rows[tab[e + r]] for r in range(total)])
+
+
+@pytest.mark.parametrize("algo", [t.SWING, t.RECDUB])
+@pytest.mark.parametrize("grid", GRIDS)
+def test_bo_register_program_matches_oracle(grid, algo):
+    """The program the register-staged schedule form loads (ALLRED_STEPS_REG): the step-0
+    pairs are the same for every block (each pair once, lower rank first), every block
+    maps each pair to one distinct holder row, and evaluating it bit-matches the oracle."""
+    side, total = grid
+    H = total // 2
+    cap = total * 256 + total
+    buf = (C.c_uint8 * cap)()
+    n = _lib.lib.allred_steps_program(algo, t.BO | _lib.STEPS_REG, side, total, buf, cap)
+    assert n == total * 256 + total, n
+    prog = np.frombuffer(bytes(buf), dtype=np.uint8)[:n].astype(np.int64)
+    pairs = prog[total * 256:]
+    assert sorted(pairs.tolist()) == list(range(total))             # every rank in exactly one pair
+    assert all(pairs[2 * u] < pairs[2 * u + 1] for u in range(H))
+    pipe = program(algo, t.BO, side, total)
+    rng = np.random.default_rng(11 + total + algo)
+    n_el = total * 16
+    ranks = [rng.integers(0x3F80, 0x42C8, n_el).astype(np.uint16) for _ in range(total)]
+    want = [r.copy() for r in ranks]
+    oracle.allreduce("bo", algo, side, want, total)
+    blk = n_el // total
+    got = np.zeros((total, n_el), dtype=np.uint16)
+    stacked = np.stack(ranks)
+    for b in range(total):
+        tab = prog[b * 256:(b + 1) * 256]
+        assert sorted((tab[:H] & 127).tolist()) == list(range(H))    # one holder row per pair
+        assert (tab[2 * H:] == pipe[b * 256 + 2 * H:(b + 1) * 256]).all()   # phases, result rows as the pipe's
+        got[:, b * blk:(b + 1) * blk] = run_bo_reg(tab, pairs, total, stacked[:, b * blk:(b + 1) * blk])
+    assert (got == np.stack(want)).all()
+
+
 @pytest.mark.parametrize("algo,grid", [(a, g) for a in (t.SWING, t.RECDUB) for g in GRIDS] +
                          [(t.SWING_1D, (1, 16)), (t.SWING_1D, (1, 64)), (t.RECDUB_1D, (1, 32))])
 def test_lo_program_matches_oracle(algo, grid):
