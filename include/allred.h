@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ALLRED_ABI_VERSION 3
+#define ALLRED_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------- */
 #define ALLRED_OK 0
@@ -249,10 +249,14 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   tree_bcast_bal    0; 1: k_tree_bcast_x spreads the result-tile loads and partial stores over
  *                     its four waves (8 columns each) instead of wave 0
  *   steps_groups      0: workgroups per CU of the schedule form k_steps_reg — 0 auto (BO 3; LO 4,
- *                     or 3 where 4 would leave every wave exactly one strip), 3, 4 or 5
+ *                     or 3 where 4 would leave every wave exactly one strip), 3, 4 or 5 (1 and 2:
+ *                     ALLRED_ERR_ARG)
  *   hier_x_lag        1: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
  *                     iteration after the tree of the matching tile of the bucket being read; 0: in
  *                     the same iteration
+ *   rccl_fault        0; fault injection of the bounded RCCL waits (tests only), a bit mask: 1 init,
+ *                     2 every group end, 4 every allred_comm_wait stays pending as if a peer never
+ *                     arrived, so the deadline / ncclCommAbort path runs (ALLRED_ERR_TRANSPORT)
  * Plans read the keys when they are created (lo_*, steps_form) or launched.
  * ALLRED_ERR_ARG: unknown key or value out of range.  No reference
  * counterpart (the reference picks its kernel directory by string,
@@ -400,6 +404,84 @@ typedef int (*allred_exchange_fn)(void* ctx, int peer, int nsend, const allred_s
 int allred_dist_allreduce_host(const allred_dist_desc* desc, int rank, uint16_t* buf,
                                uint16_t* scratch, allred_exchange_fn exchange, void* ctx);
 
+/* ---- bounded RCCL (a bad configuration returns an error
+ * instead of hanging; the reference hangs, allred_helper.hpp:84-96) -------
+ * Communicators are created non-blocking (ncclConfig_t.blocking = 0): init
+ * and every ncclGroupEnd are polled (ncclCommGetAsyncError) against a
+ * deadline; allred_comm_wait polls the stream the same way.  Past the
+ * deadline the communicator is aborted (ncclCommAbort: its kernels leave
+ * their waits) and the call returns ALLRED_ERR_TRANSPORT; every later call
+ * on that communicator returns ALLRED_ERR_TRANSPORT too (destroy it).
+ * timeout_ms: 0 = the default, ALLRED_RCCL_TIMEOUT_MS or 4000 ms for
+ * operations (init: at least 60 s — a node's first RCCL init takes seconds). */
+int allred_comm_set_timeout(allred_comm* comm, int timeout_ms);
+/* Waits until `stream` has drained (hipStreamQuery) or the deadline passed
+ * (-> ncclCommAbort, ALLRED_ERR_TRANSPORT); an asynchronous RCCL error ->
+ * ALLRED_ERR_RCCL.  Replaces hipStreamSynchronize after RCCL work. */
+int allred_comm_wait(allred_comm* comm, void* stream);
+/* 1 once the communicator was aborted, else 0. */
+int allred_comm_aborted(const allred_comm* comm);
+
+/* ======================================================================
+ * allred_run across GPUs (args->gpus = G >= 1) in two parts.
+ * (1) The PLAN — pure host computation, no HIP call: how the reference's
+ *     (side, total) ranks (allred_BO_2D.cpp:7-29, allred_helper.cpp:205-220)
+ *     split over G GPUs and which exchange every GPU runs.
+ * (2) An EXCHANGE BACKEND executing it, one host thread per GPU:
+ *   ALLRED_TRANSPORT_RCCL  one RCCL rank per GPU (allred_comm_init_all +
+ *                          allred_dist_allreduce), the default;
+ *   ALLRED_TRANSPORT_PEER  peer windows of the G threads mapped into each other
+ *                          in-process (allred_peer_connect_all) and
+ *                          allred_peer_dist_allreduce; with share_device every
+ *                          group runs on ONE GPU (a rehearsal of the G-GPU
+ *                          orchestration on hardware: threads, barriers, per-GPU
+ *                          H2D / D2H slices, validation);
+ *   ALLRED_TRANSPORT_HOST  the host twin: G threads on host memory running
+ *                          allred_dist_allreduce_host with an in-memory exchange;
+ *                          no HIP call at all (CPU tests of the orchestration;
+ *                          only ever selected explicitly).
+ * allred_run picks them from ALLRED_TRANSPORT=rccl|peer|host and
+ * ALLRED_SHARE_GPU=1.
+ * ==================================================================== */
+#define ALLRED_MULTI_FLAT 0   /* L = 1: the reference's own (side, total) schedule across the GPUs */
+#define ALLRED_MULTI_HIER 1   /* L > 1: each GPU's L ranks -> its sub-grid's tree, the partials
+                                 allreduced on the (2,2)/(2,4)/(4,8)... GPU grid, the result written
+                                 to every rank: a hierarchical COMPOSITION — on arbitrary data its
+                                 bits differ from the flat one-GPU plan of the same argv; on the
+                                 reference's own inputs both are exactly RNE(a+b)*N/2 */
+#define ALLRED_MULTI_LOCAL 2  /* G = 1, mem_2D: the fused mem_2D pass over every rank, no exchange */
+#define ALLRED_TRANSPORT_RCCL 0
+#define ALLRED_TRANSPORT_PEER 1
+#define ALLRED_TRANSPORT_HOST 2
+typedef struct {
+    int32_t gpus;             /* G                                                   */
+    int32_t local_ranks;      /* L = total / G: ranks g*L .. g*L + L - 1 live on GPU g */
+    int32_t total_nodes;
+    int32_t variant;          /* ALLRED_BO / ALLRED_LO / ALLRED_MEM, as executed      */
+    int32_t mode;             /* ALLRED_MULTI_*                                      */
+    int32_t print_core;       /* validated with the reference's printed report        */
+    uint64_t elems;           /* bf16 elements per rank                              */
+    uint64_t validated_mask;  /* bit r: rank r goes through validate_result_vector    */
+    allred_dist_desc desc;    /* the exchange every GPU runs (FLAT / HIER)            */
+} allred_multi_plan;
+/* check_all != 0: every rank validated (ALLRED_CHECK_ALL), else print_core and
+ * every GPU's first rank.  ALLRED_ERR_ARG / _SCHEDULE / _UNSUPPORTED exactly
+ * where allred_run refuses the split (before any HIP call). */
+int allred_multi_plan_build(const allred_args* args, int check_all, allred_multi_plan* out);
+typedef struct {
+    int32_t transport;        /* ALLRED_TRANSPORT_*                                  */
+    int32_t share_device;     /* 1: every group on args->device (PEER / HOST only)     */
+    int32_t timeout_ms;       /* RCCL deadline (0 = default); HOST: exchange deadline */
+    int32_t reserved;
+} allred_multi_opts;
+/* allred_run's multi-GPU form with an explicit backend.  in_all: NULL (the
+ * reference's generated inputs, validated as allred_run does), or total * elems
+ * bf16 rank-major inputs of the caller's own (arbitrary data: validation is
+ * skipped, report->mismatches = -1).  out_all: NULL, or total * elems bf16
+ * receiving every rank's result (rank-major) for checks. */
+int allred_run_multi(const allred_args* args, const allred_multi_opts* opts, int verbose, allred_report* report,
+                     const uint16_t* in_all, uint16_t* out_all);
+
 /* ======================================================================
  * Peer-mapped one-shot allreduce across GPUs: the shared-memory variant
  * (allred_mem_2D.cpp:4-165) with every GPU's window IPC-mapped into every
@@ -426,6 +508,11 @@ typedef struct allred_peer allred_peer;
 int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, allred_peer** out);
 int allred_peer_handle(allred_peer* peer, uint8_t* handle /*[ALLRED_PEER_HANDLE_BYTES]*/);
 int allred_peer_connect(allred_peer* peer, const uint8_t* all_handles /*[nranks * ALLRED_PEER_HANDLE_BYTES]*/);
+/* The peers of ONE process (peers[q] = rank q, one host thread per rank
+ * afterwards): every window mapped into every peer directly, no IPC (peer
+ * access enabled between distinct devices).  Replaces handle + connect when
+ * the ranks are threads (allred_run across GPUs, ALLRED_TRANSPORT_PEER). */
+int allred_peer_connect_all(int nranks, allred_peer* const* peers);
 /* elems % (8 * nranks) == 0, elems <= max_elems.  local_ranks > 1: `buf`
  * holds local_ranks virtual ranks (stride elems) reduced on-GPU first
  * (tree of local rank 0) into `workspace` (elems * 2 bytes), then broadcast. */

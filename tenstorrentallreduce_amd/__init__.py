@@ -17,8 +17,9 @@ from typing import Callable, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (ACC_BF16, ACC_FP32, BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, RECDUB, RECDUB_1D, SWING, SWING_1D,  # noqa: F401
-                   AllredError, Args, DistDesc, PlanDesc, Report, Schedule, Seg, check, lib)
+from ._lib import (ACC_BF16, ACC_FP32, BO, EXEC_FUSED, EXEC_STEPS, LO, MEM, MULTI_FLAT, MULTI_HIER,  # noqa: F401
+                   MULTI_LOCAL, RECDUB, RECDUB_1D, SWING, SWING_1D, TRANSPORT_HOST, TRANSPORT_PEER, TRANSPORT_RCCL,
+                   AllredError, Args, DistDesc, MultiOpts, MultiPlan, PlanDesc, Report, Schedule, Seg, check, lib)
 
 __all__ = [
     "BO", "LO", "MEM", "SWING", "RECDUB", "SWING_1D", "RECDUB_1D", "get_comm_partner_swing_1D",
@@ -28,7 +29,8 @@ __all__ = [
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
     "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
     "dist_allreduce_host", "dist_allreduce_pipelined", "tree_broadcast_pipelined", "dist_workspace_bytes", "dist_program_stats", "Peer", "tune", "tuned", "ACC_FP32",
-    "ACC_BF16",
+    "ACC_BF16", "multi_plan", "run_multi", "TRANSPORT_RCCL", "TRANSPORT_PEER", "TRANSPORT_HOST", "MULTI_FLAT",
+    "MULTI_HIER", "MULTI_LOCAL",
 ]
 
 
@@ -253,6 +255,42 @@ def run_cli(binary: str, args: Sequence[str], env: dict | None = None, timeout: 
                           env=e, timeout=timeout)
 
 
+def multi_plan(argv: Sequence[str], variant: int = BO, gpus: int | None = None, check_all: bool = False) -> MultiPlan:
+    """The plan of allred_run across GPUs (allred_multi_plan_build): pure host
+    computation, no HIP call.  gpus overrides argv[10] / ALLRED_GPUS."""
+    a = parse_args(argv, variant)
+    if gpus is not None:
+        a.gpus = gpus
+    p = MultiPlan()
+    check(lib.allred_multi_plan_build(C.byref(a), int(check_all), C.byref(p)), "multi_plan_build")
+    return p
+
+
+def run_multi(argv: Sequence[str], variant: int = BO, gpus: int | None = None, transport: int = TRANSPORT_RCCL,
+              share_device: bool = False, timeout_ms: int = 0, verbose: bool = False, outputs: bool = True,
+              inputs: np.ndarray | None = None):
+    """allred_run across GPUs with an explicit backend (allred_run_multi).
+    inputs: None (the reference's generated, validated inputs) or a (total,
+    elems) uint16 array of arbitrary rank vectors (validation skipped).
+    Returns (Report, every rank's result as a (total, elems) uint16 array or None)."""
+    a = parse_args(argv, variant)
+    if gpus is not None:
+        a.gpus = gpus
+    n = a.num_tiles * 1024
+    r = Report()
+    out = np.zeros((a.total_nodes, n), dtype=np.uint16) if outputs else None
+    inp = None
+    if inputs is not None:
+        inp = np.ascontiguousarray(inputs, dtype=np.uint16)
+        if inp.shape != (a.total_nodes, n):
+            raise ValueError(f"inputs must be ({a.total_nodes}, {n})")
+    o = MultiOpts(transport, int(share_device), timeout_ms, 0)
+    check(lib.allred_run_multi(C.byref(a), C.byref(o), int(verbose), C.byref(r),
+                               None if inp is None else inp.ctypes.data, None if out is None else out.ctypes.data),
+          "run_multi")
+    return r, out
+
+
 # ---------------------------------------------------------------- multi-GPU
 class Comm:
     """One RCCL communicator per process/GPU (allred_comm_*)."""
@@ -283,6 +321,17 @@ class Comm:
             c.nranks, c.rank = len(devices), i
             out.append(c)
         return out
+
+    def set_timeout(self, ms: int) -> None:
+        check(lib.allred_comm_set_timeout(self._h, ms), "comm_set_timeout")
+
+    def wait(self, stream=None) -> None:
+        """Bounded stream drain (allred_comm_wait): ALLRED_ERR_TRANSPORT past the deadline."""
+        check(lib.allred_comm_wait(self._h, _stream_ptr(stream)), "comm_wait")
+
+    @property
+    def aborted(self) -> bool:
+        return bool(lib.allred_comm_aborted(self._h))
 
     def close(self):
         if self._h:
@@ -373,6 +422,13 @@ class Peer:
         blob = b"".join(handles)
         arr = (C.c_uint8 * len(blob)).from_buffer_copy(blob)
         check(lib.allred_peer_connect(self._h, arr), "peer_connect")
+
+    @staticmethod
+    def connect_all(peers: Sequence["Peer"]) -> None:
+        """The peers of ONE process (peers[q] = rank q), mapped into each other
+        without IPC (allred_peer_connect_all)."""
+        arr = (C.c_void_p * len(peers))(*[p._h.value for p in peers])
+        check(lib.allred_peer_connect_all(len(peers), arr), "peer_connect_all")
 
     def allreduce(self, buf_ptr: int, elems: int, stream=None, local_ranks: int = 1, local_side: int = 1,
                   local_algo: int = SWING, workspace_ptr: int | None = None, check_status: bool = False) -> None:

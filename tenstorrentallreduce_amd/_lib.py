@@ -38,9 +38,11 @@ BO, LO, MEM = 0, 1, 2
 STEPS_REG = 0x100   # allred_steps_program: | ALLRED_BO -> the register-staged form's program
 EXEC_STEPS, EXEC_FUSED = 0, 1
 ACC_FP32, ACC_BF16 = 0, 1
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_NODES, MAX_STEPS = 64, 6
 UNIQUE_ID_BYTES = 128
+MULTI_FLAT, MULTI_HIER, MULTI_LOCAL = 0, 1, 2          # allred_multi_plan.mode
+TRANSPORT_RCCL, TRANSPORT_PEER, TRANSPORT_HOST = 0, 1, 2
 
 
 class AllredError(RuntimeError):
@@ -95,6 +97,19 @@ class DistDesc(C.Structure):
         ("elems", C.c_uint64), ("local_ranks", C.c_int32), ("local_side", C.c_int32), ("local_algo", C.c_int32),
         ("channels", C.c_int32), ("mem_accum", C.c_int32),
     ]
+
+
+class MultiPlan(C.Structure):
+    _fields_ = [
+        ("gpus", C.c_int32), ("local_ranks", C.c_int32), ("total_nodes", C.c_int32), ("variant", C.c_int32),
+        ("mode", C.c_int32), ("print_core", C.c_int32), ("elems", C.c_uint64), ("validated_mask", C.c_uint64),
+        ("desc", DistDesc),
+    ]
+
+
+class MultiOpts(C.Structure):
+    _fields_ = [("transport", C.c_int32), ("share_device", C.c_int32), ("timeout_ms", C.c_int32),
+                ("reserved", C.c_int32)]
 
 
 class Seg(C.Structure):
@@ -157,9 +172,15 @@ SIGNATURES = [
     ("allred_dist_program_stats", C.c_int,
      [C.POINTER(DistDesc), C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     ("allred_dist_allreduce_host", C.c_int, [C.POINTER(DistDesc), C.c_int, _u16p, _u16p, EXCHANGE_FN, _P]),
+    ("allred_comm_set_timeout", C.c_int, [_P, C.c_int]),
+    ("allred_comm_wait", C.c_int, [_P, _P]),
+    ("allred_comm_aborted", C.c_int, [_P]),
+    ("allred_multi_plan_build", C.c_int, [C.POINTER(Args), C.c_int, C.POINTER(MultiPlan)]),
+    ("allred_run_multi", C.c_int, [C.POINTER(Args), C.POINTER(MultiOpts), C.c_int, C.POINTER(Report), _u16p, _u16p]),
     ("allred_peer_create", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_uint64, C.POINTER(_P)]),
     ("allred_peer_handle", C.c_int, [_P, _P]),
     ("allred_peer_connect", C.c_int, [_P, _P]),
+    ("allred_peer_connect_all", C.c_int, [C.c_int, C.POINTER(_P)]),
     ("allred_peer_allreduce", C.c_int, [_P, _u16p, C.c_uint64, C.c_int, C.c_int, C.c_int, _P, _P]),
     ("allred_peer_allreduce_pipelined", C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_peer_allreduce_pipelined2", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, _P]),

@@ -21,6 +21,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <memory>
@@ -36,6 +38,11 @@ using namespace tsa;
 struct allred_comm {
     ncclComm_t comm = nullptr;
     int nranks = 0, rank = 0, device = 0;
+    // bounded RCCL: non-blocking communicator, polled against a deadline; aborted
+    // past it (every later call then returns ALLRED_ERR_TRANSPORT)
+    int timeout_ms = 0;             // 0 = default_timeout_ms()
+    bool aborted = false;
+    const std::atomic<int>* cancel = nullptr;   // run_multi_gpu: another GPU's thread failed
     // allred_dist_allreduce_pipelined: the bucket started by the last call (its rows are
     // written by the next call or the flush) and its allreduced partial in the workspace
     uint64_t calls = 0;             // allred_dist_allreduce calls (the hierarchical partial alternates halves)
@@ -374,11 +381,90 @@ void host_rows_sum(const uint16_t* rows, size_t stride, size_t n, int nrows, boo
 int run_program(allred_comm* c, const allred_dist_desc* d, const allred_schedule& s, uint16_t* bucket,
                 uint16_t* staging, void* stream);
 
+// ---- bounded RCCL ----------------------------------------------------------
+// The reference's host blocks in Finish() forever when a core never signals
+// (allred_helper.hpp:84-96).  Here every RCCL wait has a deadline: the
+// communicator is non-blocking, its pending state is polled, and past the
+// deadline it is aborted (ncclCommAbort makes its kernels leave their waits).
+// Fault injection (tune "rccl_fault", a bit mask) keeps a wait pending as if
+// a peer never arrived, so the abort path is testable on one GPU.
+enum class Fault : int64_t { none = 0, init = 1, group = 2, drain = 4 };
+
+int env_timeout_ms() {
+    static const int v = [] {
+        const char* e = std::getenv("ALLRED_RCCL_TIMEOUT_MS");
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        return x > 0 && x < (1l << 30) ? (int)x : 4000;   // the peer kernels' spin bound
+    }();
+    return v;
+}
+int op_timeout_ms(const allred_comm* c) { return c->timeout_ms > 0 ? c->timeout_ms : env_timeout_ms(); }
+// a node's first RCCL init (topology discovery, connection setup) takes seconds:
+// ALLRED_RCCL_INIT_TIMEOUT_MS, default 60 s (never below the operation deadline)
+int init_timeout_ms(const allred_comm* c) {
+    static const int init = [] {
+        const char* e = std::getenv("ALLRED_RCCL_INIT_TIMEOUT_MS");
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        return x > 0 && x < (1l << 30) ? (int)x : 60000;
+    }();
+    const int t = op_timeout_ms(c);
+    return (tune(Tune::rccl_fault) & (int64_t)Fault::init) ? t : std::max(t, init);
+}
+
+void abort_comm(allred_comm* c, hipStream_t hs) {
+    if (c->aborted) return;
+    if (c->comm) (void)ncclCommAbort(c->comm);
+    c->aborted = true;
+    c->comm = nullptr;
+    if (hs) {   // the aborted kernels drain; bounded, the caller returns an error either way
+        const auto t0 = std::chrono::steady_clock::now();
+        while (hipStreamQuery(hs) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(op_timeout_ms(c)))
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
+// poll the communicator out of ncclInProgress (non-blocking init / group end / finalize)
+int settle(allred_comm* c, int timeout_ms, Fault f) {
+    const bool fault = f != Fault::none && (tune(Tune::rccl_fault) & (int64_t)f) != 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        ncclResult_t a = ncclInProgress;
+        if (ncclCommGetAsyncError(c->comm, &a) != ncclSuccess) a = ncclInternalError;
+        if (fault) a = ncclInProgress;
+        if (a == ncclSuccess) return ALLRED_OK;
+        if (a != ncclInProgress) {
+            abort_comm(c, nullptr);
+            return ALLRED_ERR_RCCL;
+        }
+        if ((c->cancel && c->cancel->load()) ||
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms)) {
+            abort_comm(c, nullptr);
+            return ALLRED_ERR_TRANSPORT;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+// after ncclGroupEnd on a non-blocking communicator
+int group_end(allred_comm* c, bool ok) {
+    const ncclResult_t r = ncclGroupEnd();
+    if (!ok || (r != ncclSuccess && r != ncclInProgress)) return ALLRED_ERR_RCCL;
+    if (r == ncclSuccess && !(tune(Tune::rccl_fault) & (int64_t)Fault::group)) return ALLRED_OK;
+    return settle(c, op_timeout_ms(c), Fault::group);
+}
+
 }  // namespace
 
 namespace tsa {
 
 int local_tree_order(int algo, int side, int total, const uint8_t** out) { return device_order(algo, side, total, out); }
+
+int dist_check_desc(const allred_dist_desc* d, allred_schedule* s) { return check_desc(d, s); }
+
+void comm_set_cancel(allred_comm* c, const std::atomic<int>* cancel) {
+    if (c) c->cancel = cancel;
+}
 
 // The RCCL program's exchanges, as tables for the peer-mapped kernel
 // (k_peer_sched): per channel, the step partner and this rank's block masks
@@ -454,9 +540,14 @@ int allred_comm_init(const uint8_t* id, int nranks, int rank, int device, allred
     (void)hipGetDevice(&c->device);
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof(u));
-    if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, u, rank, &cfg);
+    int st = (r == ncclSuccess || r == ncclInProgress) ? settle(c, init_timeout_ms(c), Fault::init) : ALLRED_ERR_RCCL;
+    if (st != ALLRED_OK) {   // a rank that never joins: aborted past the deadline, no hang
+        if (c->comm && !c->aborted) (void)ncclCommAbort(c->comm);
         delete c;
-        return ALLRED_ERR_RCCL;
+        return st;
     }
     *out = c;
     return ALLRED_OK;
@@ -465,26 +556,86 @@ int allred_comm_init(const uint8_t* id, int nranks, int rank, int device, allred
 int allred_comm_init_all(int ndev, const int* devices, allred_comm** out) {
     if (!devices || !out || ndev < 1 || ndev > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     for (int i = 0; i < ndev; ++i) out[i] = nullptr;
-    std::vector<ncclComm_t> comms((size_t)ndev);
-    std::vector<int> devs(devices, devices + ndev);
-    if (ncclCommInitAll(comms.data(), ndev, devs.data()) != ncclSuccess) return ALLRED_ERR_RCCL;
+    // ncclCommInitAll's work as one group of non-blocking ncclCommInitRankConfig
+    // calls (one unique id, rank i on devices[i]), so init is bounded too
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return ALLRED_ERR_RCCL;
+    std::vector<allred_comm*> cs((size_t)ndev, nullptr);
     for (int i = 0; i < ndev; ++i) {
-        auto* c = new allred_comm();
-        c->comm = comms[(size_t)i];
-        c->nranks = ndev;
-        c->rank = i;
-        c->device = devs[(size_t)i];
-        out[i] = c;
+        cs[(size_t)i] = new allred_comm();
+        cs[(size_t)i]->nranks = ndev;
+        cs[(size_t)i]->rank = i;
+        cs[(size_t)i]->device = devices[i];
     }
+    int st = ALLRED_OK;
+    if (ncclGroupStart() != ncclSuccess) st = ALLRED_ERR_RCCL;
+    for (int i = 0; i < ndev && st == ALLRED_OK; ++i) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        if (hipSetDevice(devices[i]) != hipSuccess) { st = ALLRED_ERR_HIP; break; }
+        const ncclResult_t r = ncclCommInitRankConfig(&cs[(size_t)i]->comm, ndev, u, i, &cfg);
+        if (r != ncclSuccess && r != ncclInProgress) st = ALLRED_ERR_RCCL;
+    }
+    const ncclResult_t ge = ncclGroupEnd();
+    if (st == ALLRED_OK && ge != ncclSuccess && ge != ncclInProgress) st = ALLRED_ERR_RCCL;
+    for (int i = 0; i < ndev && st == ALLRED_OK; ++i) st = settle(cs[(size_t)i], init_timeout_ms(cs[(size_t)i]), Fault::init);
+    if (st != ALLRED_OK) {
+        for (allred_comm* c : cs) {
+            if (c->comm && !c->aborted) (void)ncclCommAbort(c->comm);
+            delete c;
+        }
+        return st;
+    }
+    for (int i = 0; i < ndev; ++i) out[i] = cs[(size_t)i];
     return ALLRED_OK;
 }
 
 int allred_comm_destroy(allred_comm* c) {
     if (!c) return ALLRED_OK;
-    if (c->comm) ncclCommDestroy(c->comm);
+    if (c->comm && !c->aborted) {
+        // non-blocking teardown: finalize (polled against the deadline), then destroy;
+        // a finalize that never settles is aborted instead
+        const ncclResult_t f = ncclCommFinalize(c->comm);
+        const int st = (f == ncclSuccess || f == ncclInProgress) ? settle(c, op_timeout_ms(c), Fault::none) : ALLRED_ERR_RCCL;
+        if (st == ALLRED_OK) (void)ncclCommDestroy(c->comm);
+        else if (!c->aborted) (void)ncclCommAbort(c->comm);
+    }
     delete c;
     return ALLRED_OK;
 }
+
+int allred_comm_set_timeout(allred_comm* c, int timeout_ms) {
+    if (!c || timeout_ms < 0) return ALLRED_ERR_ARG;
+    c->timeout_ms = timeout_ms;
+    return ALLRED_OK;
+}
+
+int allred_comm_wait(allred_comm* c, void* stream) {
+    if (!c) return ALLRED_ERR_ARG;
+    if (c->aborted) return ALLRED_ERR_TRANSPORT;
+    hipStream_t hs = (hipStream_t)stream;
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = std::chrono::milliseconds(op_timeout_ms(c));
+    const bool fault = (tune(Tune::rccl_fault) & (int64_t)Fault::drain) != 0;
+    for (;;) {
+        const hipError_t q = hipStreamQuery(hs);
+        if (q == hipSuccess && !fault) break;
+        if (q != hipSuccess && q != hipErrorNotReady) return ALLRED_ERR_HIP;
+        ncclResult_t a = ncclSuccess;
+        if (c->comm && ncclCommGetAsyncError(c->comm, &a) == ncclSuccess && a != ncclSuccess && a != ncclInProgress) {
+            abort_comm(c, hs);
+            return ALLRED_ERR_RCCL;
+        }
+        if ((c->cancel && c->cancel->load()) || std::chrono::steady_clock::now() - t0 > limit) {
+            abort_comm(c, hs);   // its kernels leave their waits; the stream drains (bounded)
+            return ALLRED_ERR_TRANSPORT;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    return ALLRED_OK;
+}
+
+int allred_comm_aborted(const allred_comm* c) { return c && c->aborted ? 1 : 0; }
 
 size_t allred_dist_workspace_bytes(const allred_dist_desc* d) {
     if (!d) return 0;
@@ -494,6 +645,10 @@ size_t allred_dist_workspace_bytes(const allred_dist_desc* d) {
 int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* buf, void* workspace,
                           void* stream) {
     if (!c || !buf || !workspace) return ALLRED_ERR_ARG;
+    if (c->aborted) return ALLRED_ERR_TRANSPORT;
+    // a pipelined bucket is pending: its partial lives in [ws, ws + 2n) that this
+    // call would overwrite (flush the sequence first, as the peer path demands)
+    if (c->pend) return ALLRED_ERR_ARG;
     allred_schedule s;
     int st = check_desc(d, &s);
     if (st != ALLRED_OK) return st;
@@ -522,7 +677,7 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
                 ok = ok && ncclSend(snd, blk * 2, ncclUint8, q, c->comm, hs) == ncclSuccess;
                 ok = ok && ncclRecv(rcv, blk * 2, ncclUint8, q, c->comm, hs) == ncclSuccess;
             }
-            if (ncclGroupEnd() != ncclSuccess || !ok) return ALLRED_ERR_RCCL;
+            if ((st = group_end(c, ok)) != ALLRED_OK) return st;
             if (phase == 0) {
                 st = launch_rows_sum(staging, blk, blk, N, own, d->mem_accum == ALLRED_ACC_BF16, stream);
                 if (st != ALLRED_OK) return st;
@@ -552,6 +707,7 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
 int allred_dist_allreduce_pipelined(allred_comm* c, const allred_dist_desc* d, uint16_t* cur, void* workspace,
                                     void* stream) {
     if (!c || !d || !workspace) return ALLRED_ERR_ARG;
+    if (c->aborted) return ALLRED_ERR_TRANSPORT;
     if (!cur) {   // flush: the pending bucket's rows from its allreduced partial
         if (!c->pend) return ALLRED_ERR_ARG;
         const int st = launch_broadcast(c->pend, c->pend_elems, c->pend_elems, c->pend_local, c->pend_partial, stream);
@@ -565,6 +721,12 @@ int allred_dist_allreduce_pipelined(allred_comm* c, const allred_dist_desc* d, u
     if (((uintptr_t)cur | (uintptr_t)workspace) % 16) return ALLRED_ERR_ARG;
     const size_t n = (size_t)d->elems;
     if (c->pend && (n != c->pend_elems || d->local_ranks != c->pend_local)) return ALLRED_ERR_ARG;
+    // cur's rows are read while the pending bucket's are written (k_tree_bcast_x, __restrict__):
+    // the two buckets must not overlap
+    if (c->pend) {
+        const size_t span = (size_t)d->local_ranks * n;
+        if (cur < c->pend + span && c->pend < cur + span) return ALLRED_ERR_ARG;
+    }
     // two parities of [staging n | partial n]: the pending bucket's partial survives this call
     const int parity = c->pend ? c->pend_parity ^ 1 : 0;
     uint16_t* staging = static_cast<uint16_t*>(workspace) + (size_t)parity * 2 * n;
@@ -623,8 +785,9 @@ int run_program(allred_comm* c, const allred_dist_desc* d, const allred_schedule
                                     c->comm, hs) == ncclSuccess;
         }
         // the group is always closed, also after a failed send / recv, so the
-        // next call does not start inside a dangling group
-        if (ncclGroupEnd() != ncclSuccess || !ok) return ALLRED_ERR_RCCL;
+        // next call does not start inside a dangling group; a group that never
+        // completes (a partner that never arrives) is aborted at the deadline
+        if ((st = group_end(c, ok)) != ALLRED_OK) return st;
         for (size_t i = 0; i < step.add_off.size(); i += kMaxAddSegs) {   // one launch per step (<= 64 segments)
             const int ns = (int)std::min<size_t>(kMaxAddSegs, step.add_off.size() - i);
             st = launch_bf16_add_segs(bucket, staging, step.add_off.data() + i, step.add_len.data() + i, ns, stream);
@@ -646,7 +809,7 @@ int allred_dist_program_stats(const allred_dist_desc* d, int rank, int* steps, i
     if (d->variant == ALLRED_MEM) {   // one all-to-all group, one ordered sum, one all-gather group
         const int N = d->total_nodes;
         if (steps) *steps = N > 1 ? 2 : 0;
-        if (launches) *launches = 1;
+        if (launches) *launches = N > 1 ? 1 : 0;   // one rank: no exchange, no sum kernel
         if (segments) *segments = 4 * (N - 1);
         return ALLRED_OK;
     }
@@ -724,211 +887,3 @@ int allred_dist_allreduce_host(const allred_dist_desc* d, int rank, uint16_t* bu
 }
 
 }  // extern "C"
-
-// ---------------------------------------------------------------------------
-// allred_run across the GPUs of one node (args->gpus = G): the reference's
-// argv (allred_BO_2D.cpp:7-29, allred_helper.cpp:205-220) with its ranks spread
-// over G GPUs, one host thread and one RCCL rank (ncclCommInitAll) per GPU.
-// ---------------------------------------------------------------------------
-namespace {
-
-// (side, total) grids the reference's 2D functions accept for `c` ranks: SURVEY §8(e)
-// (2,2), (2,4), (4,8) and the squares / rectangles above
-int grid_side(int c) {
-    switch (c) {
-        case 1: return 1;
-        case 2: case 4: return 2;
-        case 8: case 16: return 4;
-        default: return 8;
-    }
-}
-
-struct HostBarrier {   // the G device threads meet before the timed region
-    std::mutex mu;
-    std::condition_variable cv;
-    int n, waiting = 0, gen = 0;
-    explicit HostBarrier(int count) : n(count) {}
-    void wait() {
-        std::unique_lock<std::mutex> l(mu);
-        const int g = gen;
-        if (++waiting == n) {
-            waiting = 0;
-            ++gen;
-            cv.notify_all();
-        } else {
-            cv.wait(l, [&] { return gen != g; });
-        }
-    }
-};
-
-}  // namespace
-
-int tsa::run_multi_gpu(const allred_args* a, int verbose, allred_report* R) {
-    const int G = a->gpus, N = a->total_nodes;
-    // everything checkable without a GPU first (ALLRED_ERR_ARG, no HIP call)
-    if (G < 1 || G > ALLRED_MAX_NODES || (G & (G - 1)) || N % G) return ALLRED_ERR_ARG;
-    const int L = N / G;
-    const size_t n = (size_t)a->num_tiles * 1024, bytes = n * 2;
-    const int variant = a->variant == ALLRED_MEM ? ALLRED_MEM
-                        : (a->variant == ALLRED_BO && a->bandwidth_optimal) ? ALLRED_BO : ALLRED_LO;
-    const int algo = a->swing ? ALLRED_SWING : ALLRED_RECDUB;
-    if (variant == ALLRED_MEM && L > 1 && G > 1) return ALLRED_ERR_UNSUPPORTED;
-    allred_dist_desc d{};
-    d.algo = algo;
-    d.variant = variant;
-    d.elems = n;
-    d.channels = 0;
-    d.mem_accum = a->mem_accum;
-    if (L == 1) {   // one rank per GPU: the reference's own grid across the GPUs
-        d.side_length = a->side_length;
-        d.total_nodes = N;
-        d.local_ranks = 1;
-        d.local_side = 1;
-    } else {        // L ranks per GPU: their sub-grid (rows of the reference's grid if they form one)
-        d.side_length = grid_side(G);
-        d.total_nodes = G;
-        d.local_ranks = L;
-        allred_schedule ls;
-        d.local_side = (L % a->side_length == 0 && build_schedule(algo, a->side_length, L, &ls, nullptr) == ALLRED_OK)
-                           ? a->side_length : grid_side(L);
-        d.local_algo = algo;
-    }
-    if (variant == ALLRED_MEM && G == 1) {   // every rank on one GPU: the fused mem_2D pass, no exchange
-        if (n % (8 * (size_t)N)) return ALLRED_ERR_ARG;
-    } else {
-        allred_schedule s;
-        int st = check_desc(&d, &s);
-        if (st != ALLRED_OK) return st;
-        if (L > 1 && (st = build_schedule(algo, d.local_side, L, &s, nullptr)) != ALLRED_OK) return st;
-        if (L > 1 && n % 8) return ALLRED_ERR_ARG;
-    }
-    int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess) return ALLRED_ERR_HIP;
-    const int dev0 = a->device > 0 ? a->device : 0;
-    if (dev0 + G > ndev) return ALLRED_ERR_ARG;
-
-    std::vector<uint32_t> src0(bytes / 4), src1(bytes / 4);
-    if (a->seed < 0) {
-        allred_constant_bf16_vector(bytes, 1.0f, src0.data());
-        src1 = src0;
-    } else {
-        allred_random_bf16_vector(bytes, 100, a->seed, a->round_mode, src0.data());
-        allred_random_bf16_vector(bytes, 100, a->seed + 1, a->round_mode, src1.data());
-    }
-    const size_t all_bytes = (size_t)N * bytes;
-    uint16_t *h_in = nullptr, *h_out = nullptr;
-    if (hipHostMalloc((void**)&h_in, all_bytes, hipHostMallocPortable) != hipSuccess) return ALLRED_ERR_NOMEM;
-    if (hipHostMalloc((void**)&h_out, all_bytes, hipHostMallocPortable) != hipSuccess) {
-        (void)hipHostFree(h_in);
-        return ALLRED_ERR_NOMEM;
-    }
-    // even x loads src_1, odd x loads src_0 (allred_BO_2D.cpp:79-85)
-    for (int r = 0; r < N; ++r)
-        std::memcpy(h_in + (size_t)r * n, ((r % a->side_length) % 2 == 0) ? src1.data() : src0.data(), bytes);
-
-    std::vector<int> devs((size_t)G);
-    for (int g = 0; g < G; ++g) devs[(size_t)g] = dev0 + g;
-    std::vector<allred_comm*> comms((size_t)G, nullptr);
-    int st = allred_comm_init_all(G, devs.data(), comms.data());
-    std::vector<int> status((size_t)G, ALLRED_OK);
-    std::vector<float> dev_ms((size_t)G, 0.f), e2e_ms((size_t)G, 0.f);
-    if (st == ALLRED_OK) {
-        HostBarrier bar(G);
-        std::vector<int> ready((size_t)G, 0);
-        std::vector<std::thread> th;
-        for (int g = 0; g < G; ++g) {
-            th.emplace_back([&, g] {
-                int& s = status[(size_t)g];
-                uint16_t *d_buf = nullptr, *d_tmp = nullptr;
-                void* d_ws = nullptr;
-                hipStream_t hs = nullptr;
-                hipEvent_t e[4] = {};
-                const size_t mine = (size_t)L * bytes;
-                const bool mem_local = variant == ALLRED_MEM && G == 1;   // all ranks here: the fused mem_2D pass
-                auto hip = [&](hipError_t x) { if (x != hipSuccess && s == ALLRED_OK) s = ALLRED_ERR_HIP; };
-                auto reduce = [&](uint16_t* b) {
-                    if (s != ALLRED_OK || !a->run_kernel) return;
-                    s = mem_local ? launch_mem_fused(b, n, n, L, a->mem_accum == ALLRED_ACC_BF16, hs)
-                                  : allred_dist_allreduce(comms[(size_t)g], &d, b, d_ws, hs);
-                };
-                hip(hipSetDevice(devs[(size_t)g]));
-                hip(hipStreamCreateWithFlags(&hs, hipStreamNonBlocking));
-                hip(hipMalloc((void**)&d_buf, mine));
-                hip(hipMalloc((void**)&d_tmp, mine));
-                hip(hipMalloc(&d_ws, allred_dist_workspace_bytes(&d) + 16));
-                for (auto& ev : e) hip(hipEventCreate(&ev));
-                // warm-up on a scratch copy (RCCL connection setup and code-object loads stay untimed)
-                hip(hipMemcpyAsync(d_tmp, h_in + (size_t)g * L * n, mine, hipMemcpyHostToDevice, hs));
-                // every thread agrees before any collective: one failed allocation ends all
-                ready[(size_t)g] = s == ALLRED_OK;
-                bar.wait();
-                bool all = true;
-                for (int q = 0; q < G; ++q) all = all && ready[(size_t)q];
-                if (all) {
-                    reduce(d_tmp);
-                    hip(hipStreamSynchronize(hs));
-                    bar.wait();
-                    // timed: H2D | allreduce | D2H (the reference's EnqueueWriteBuffer,
-                    // EnqueueProgram + Finish, EnqueueReadBuffer; allred_helper.hpp:84-96)
-                    hip(hipEventRecord(e[0], hs));
-                    hip(hipMemcpyAsync(d_buf, h_in + (size_t)g * L * n, mine, hipMemcpyHostToDevice, hs));
-                    hip(hipEventRecord(e[1], hs));
-                    reduce(d_buf);
-                    hip(hipEventRecord(e[2], hs));
-                    hip(hipMemcpyAsync(h_out + (size_t)g * L * n, d_buf, mine, hipMemcpyDeviceToHost, hs));
-                    hip(hipEventRecord(e[3], hs));
-                    hip(hipStreamSynchronize(hs));
-                    hip(hipEventElapsedTime(&dev_ms[(size_t)g], e[1], e[2]));
-                    hip(hipEventElapsedTime(&e2e_ms[(size_t)g], e[0], e[3]));
-                } else if (s == ALLRED_OK) {
-                    s = ALLRED_ERR_HIP;   // another GPU failed to set up
-                }
-                for (auto& ev : e)
-                    if (ev) (void)hipEventDestroy(ev);
-                if (d_ws) (void)hipFree(d_ws);
-                if (d_tmp) (void)hipFree(d_tmp);
-                if (d_buf) (void)hipFree(d_buf);
-                if (hs) (void)hipStreamDestroy(hs);
-            });
-        }
-        for (auto& x : th) x.join();
-        for (int g = 0; g < G && st == ALLRED_OK; ++g) st = status[(size_t)g];
-    }
-    for (allred_comm* c : comms) allred_comm_destroy(c);
-    if (st == ALLRED_OK) {
-        float dmax = 0, emax = 0;
-        for (int g = 0; g < G; ++g) {
-            dmax = std::max(dmax, dev_ms[(size_t)g]);
-            emax = std::max(emax, e2e_ms[(size_t)g]);
-        }
-        R->device_seconds = dmax * 1e-3;
-        R->e2e_seconds = emax * 1e-3;
-        R->launches = -1;   // RCCL groups and add kernels per GPU: allred_dist_program_stats
-        if (const char* log = std::getenv("ALLRED_PROFILE_LOG")) {   // one zone per rank: its GPU's interval
-            std::vector<uint64_t> zs((size_t)N, 0), ze((size_t)N, 0);
-            for (int r = 0; r < N; ++r) ze[(size_t)r] = (uint64_t)(dev_ms[(size_t)(r / L)] * 1e5);
-            st = write_profile_log(log, N, a->side_length, zs.data(), ze.data());
-        }
-    }
-    if (st == ALLRED_OK) {
-        // print_core exactly as the reference (verbose report), then every GPU's first
-        // rank (every rank with ALLRED_CHECK_ALL) silently into the count
-        float maxe = 0;
-        R->mismatches = allred_validate_result_vector(
-            reinterpret_cast<const uint32_t*>(h_out + (size_t)a->print_core * n), src0.data(), src1.data(),
-            bytes / 4, (float)a->error, (uint32_t)N, verbose, &maxe);
-        R->max_error = maxe;
-        const bool all = std::getenv("ALLRED_CHECK_ALL") != nullptr;
-        for (int r = 0; r < N; ++r) {
-            if (r == a->print_core || (!all && r % L != 0)) continue;
-            float m = 0;
-            R->mismatches += allred_validate_result_vector(reinterpret_cast<const uint32_t*>(h_out + (size_t)r * n),
-                                                           src0.data(), src1.data(), bytes / 4, (float)a->error,
-                                                           (uint32_t)N, 0, &m);
-            R->max_error = std::max(R->max_error, m);
-        }
-    }
-    (void)hipHostFree(h_in);
-    (void)hipHostFree(h_out);
-    return st;
-}

@@ -1,6 +1,7 @@
 // internal.hpp — shared declarations inside liballred.so (not installed).
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <cstring>
@@ -40,6 +41,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
+    rccl_fault,
     count
 };
 int64_t tune(Tune key);
@@ -84,8 +86,13 @@ int launch_mem_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, bool
 // bf16 per add): mem_2D's owner-first sum once the owner's copy is row 0
 int launch_rows_sum(const uint16_t* rows, uint64_t stride, size_t n, int nrows, uint16_t* dst, bool acc16,
                     void* stream);
-// allred_run with args->gpus > 0 (dist.cpp): the program over G GPUs, one host thread each
+// allred_run with args->gpus > 0 (multi.cpp): the plan over G GPUs, one host thread each,
+// on the backend ALLRED_TRANSPORT / ALLRED_SHARE_GPU select
 int run_multi_gpu(const allred_args* a, int verbose, allred_report* report);
+// run_multi_gpu: a flag every RCCL wait of `c` polls (another GPU's thread failed -> abort)
+void comm_set_cancel(allred_comm* c, const std::atomic<int>* cancel);
+// the checks allred_dist_allreduce applies to a desc (and its schedule)
+int dist_check_desc(const allred_dist_desc* d, allred_schedule* s);
 // bucket i+1's tree (-> cur_partial) and bucket i's broadcast (prev_result -> prev's rows) in one
 // pass (k_tree_bcast_x; 64 ranks, whole tiles) or the two launches (same bits)
 int launch_tree_bcast_x(uint16_t* cur, uint16_t* prev, uint64_t stride, size_t n, int total, const uint8_t* order,

@@ -187,6 +187,33 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
     return ALLRED_OK;
 }
 
+int allred_peer_connect_all(int nranks, allred_peer* const* peers) {
+    if (!peers || nranks < 1 || nranks > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
+    for (int q = 0; q < nranks; ++q)
+        if (!peers[q] || peers[q]->connected || peers[q]->nranks != nranks || peers[q]->rank != q) return ALLRED_ERR_ARG;
+    for (int me = 0; me < nranks; ++me) {
+        allred_peer* p = peers[me];
+        DeviceGuard guard(p->device);
+        if (!guard.ok) return ALLRED_ERR_HIP;
+        for (int q = 0; q < nranks; ++q) {
+            const allred_peer* o = peers[q];
+            if (o->device != p->device) {   // another GPU of this process: map it (xGMI)
+                const hipError_t e = hipDeviceEnablePeerAccess(o->device, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return ALLRED_ERR_HIP;
+                (void)hipGetLastError();
+            }
+            p->peer_win[q][0] = o->win[0];
+            p->peer_win[q][1] = o->win[1];
+            p->peer_flags[q] = o->flags;
+            uint8_t* f = reinterpret_cast<uint8_t*>(o->flags);
+            p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + o->hfl_off);
+            p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + o->ll_off);
+        }
+    }
+    for (int q = 0; q < nranks; ++q) peers[q]->connected = true;   // opened[] stays false: nothing to close
+    return ALLRED_OK;
+}
+
 namespace {
 
 // windows of this call's parity, as mapped in this process

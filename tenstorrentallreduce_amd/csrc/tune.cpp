@@ -40,6 +40,7 @@ const Key kKeys[] = {
     {"tree_bcast_bal", 0, 0, 1},      // k_tree_bcast_x: every wave stages / stores 8 result columns (0: wave 0 all)
     {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
     {"steps_groups", 0, 0, 5},        // k_steps_reg: workgroups per CU, 0 auto (BO 3, LO 4 or 3) | 3 | 4 | 5
+    {"rccl_fault", 0, 0, 7},          // fault injection (tests): 1 init, 2 group end, 4 stream drain never settle
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");
@@ -55,6 +56,7 @@ int find(const char* key) {
 
 bool set(int i, int64_t v) {
     if (v < kKeys[i].lo || v > kKeys[i].hi) return false;
+    if (i == (int)Tune::steps_groups && (v == 1 || v == 2)) return false;   // 0 auto, 3, 4, 5 only
     g_val[i].store(v, std::memory_order_relaxed);
     return true;
 }

@@ -128,3 +128,96 @@ def test_dist_allreduce_pipelined_one_rank(buckets):
     torch.cuda.synchronize()
     assert torch.equal(x, want[0])
     comm.close()
+
+
+def test_plain_call_refused_while_a_pipelined_bucket_is_pending():
+    """A plain allred_dist_allreduce would overwrite the pending bucket's partial
+    in the shared workspace: refused (ALLRED_ERR_ARG) until the flush; so is a
+    next bucket overlapping the pending one (k_tree_bcast_x reads cur while it
+    writes the pending rows)."""
+    comm = t.Comm(t.Comm.unique_id(), 1, 0, 0)
+    n = 64 * 8 * 5
+    desc = t.dist_desc(t.SWING, t.BO, 1, 1, n, local_ranks=64, local_side=8, local_algo=t.SWING)
+    ws = torch.empty(2 * t.dist_workspace_bytes(desc), dtype=torch.uint8, device=DEV)
+    s = torch.cuda.current_stream()
+    rng = np.random.default_rng(3)
+    a = torch.from_numpy(rng.integers(0x3F80, 0x42C8, (64, n)).astype(np.uint16).view(np.int16)).to(DEV)
+    b = torch.from_numpy(rng.integers(0x3F80, 0x42C8, (64, n)).astype(np.uint16).view(np.int16)).to(DEV)
+    want = a.clone()
+    t.dist_allreduce(comm, desc, want.data_ptr(), ws.data_ptr(), s)
+    t.dist_allreduce_pipelined(comm, desc, a.data_ptr(), ws.data_ptr(), s)
+    for bad in (lambda: t.dist_allreduce(comm, desc, b.data_ptr(), ws.data_ptr(), s),
+                lambda: t.dist_allreduce_pipelined(comm, desc, a.data_ptr(), ws.data_ptr(), s),
+                lambda: t.dist_allreduce_pipelined(comm, desc, a.data_ptr() + 2 * n, ws.data_ptr(), s)):
+        with pytest.raises(t.AllredError) as e:
+            bad()
+        assert e.value.status == t._lib.ERR_ARG
+    t.dist_allreduce_pipelined(comm, desc, None, ws.data_ptr(), s)
+    torch.cuda.synchronize()
+    assert torch.equal(a, want)   # the refused calls touched nothing
+    comm.close()
+
+
+def test_rccl_wait_is_bounded_and_aborts():
+    """Bounded RCCL: a wait that never completes — injected with
+    tune rccl_fault = 4, as if a partner never arrived — returns
+    ALLRED_ERR_TRANSPORT at the deadline, the communicator is aborted
+    (ncclCommAbort), and every later call on it refuses (ERR_TRANSPORT)."""
+    import time
+    comm = t.Comm.init_all([0])[0]
+    comm.set_timeout(300)
+    n = 8 * 64 * 4
+    desc = t.dist_desc(t.SWING, t.BO, 1, 1, n)
+    buf = torch.zeros(n, dtype=torch.int16, device=DEV)
+    ws = torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=DEV)
+    s = torch.cuda.current_stream()
+    t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr(), s)
+    comm.wait(s)                           # a real drain: fine
+    with t.tuned(rccl_fault=4):
+        t0 = time.monotonic()
+        with pytest.raises(t.AllredError) as e:
+            comm.wait(s)
+        dt = time.monotonic() - t0
+    assert e.value.status == t._lib.ERR_TRANSPORT and 0.25 < dt < 10, dt
+    assert comm.aborted
+    with pytest.raises(t.AllredError) as e:
+        t.dist_allreduce(comm, desc, buf.data_ptr(), ws.data_ptr(), s)
+    assert e.value.status == t._lib.ERR_TRANSPORT
+    comm.close()
+
+
+def test_rccl_init_fault_is_bounded():
+    """An init that never settles (tune rccl_fault = 1) fails at the operation
+    deadline with ALLRED_ERR_TRANSPORT instead of blocking."""
+    import time
+    with t.tuned(rccl_fault=1):
+        t0 = time.monotonic()
+        with pytest.raises(t.AllredError) as e:
+            t.Comm.init_all([0])
+        dt = time.monotonic() - t0
+    assert e.value.status == t._lib.ERR_TRANSPORT and dt < 30, dt
+
+
+def test_rccl_init_with_a_missing_rank_returns_instead_of_hanging():
+    """A real missing peer: rank 0 of a 2-rank communicator whose rank 1 never
+    joins.  The reference would hang (allred_helper.hpp:84-96); here the
+    non-blocking init is aborted at ALLRED_RCCL_INIT_TIMEOUT_MS.  Own process:
+    the abort of a half-initialised communicator stays out of the test runner."""
+    import os
+    import subprocess
+    import sys
+    import time
+    code = ("import tenstorrentallreduce_amd as t\n"
+            "try:\n"
+            "    t.Comm(t.Comm.unique_id(), 2, 0, 0)\n"
+            "    print('joined')\n"
+            "except t.AllredError as e:\n"
+            "    print('status', e.status)\n")
+    env = dict(os.environ, ALLRED_RCCL_INIT_TIMEOUT_MS="3000", ALLRED_RCCL_TIMEOUT_MS="3000",
+               PYTHONPATH=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=90)
+    dt = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().endswith(f"status {t._lib.ERR_TRANSPORT}"), (r.stdout, r.stderr[-2000:])
+    assert dt < 60, dt
