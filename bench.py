@@ -248,7 +248,7 @@ def bench_single(args) -> dict:
         steps_plan.close()
         return {"ms_per_step": ms_per_step, "value": bytes_all / (ms_per_step * 1e-3) / 1e9}
 
-    # schedule-faithful form (12 launches: 6 RS + 6 AG steps), same buckets, eager
+    # schedule form (k_steps_reg: every RS / AG step of every rank in ONE persistent launch), same buckets, eager
     with torch.cuda.stream(stream):
         for i in range(3):
             step(i, steps_plan)
@@ -564,19 +564,28 @@ def open_peer(rank, world, local_rank, max_elems):
     return peer, None
 
 
-def arm_stats(ms, nbytes, world, lo=False) -> dict:
+def bounded_frac(x, crossed: bool):
+    """A roofline fraction as printed: null unless the bytes really crossed
+    xGMI (not a --share-gpu rehearsal, where "remote" memory is local and the
+    ratio means nothing) and 0 < x <= 1."""
+    if not crossed or x is None or not (0 < x <= 1):
+        return None
+    return round(x, 4)
+
+
+def arm_stats(ms, nbytes, world, lo=False, crossed=True) -> dict:
     """busbw = 2(p-1)/p * n / t (nccl-tests); xgmi_frac = busbw over this GPU's
     egress to its p-1 peers (one xGMI link each on the full mesh) at the spec
-    per-direction link rate."""
+    per-direction link rate — bounded (bounded_frac)."""
     sec = ms * 1e-3
     busbw = 2 * (world - 1) / world * nbytes / sec / 1e9   # nccl-tests convention
     if lo:
         busbw = nbytes / sec / 1e9   # LO moves the whole bucket every step: report algbw
     return {"ms": round(ms, 4), "algbw_GBps": round(nbytes / sec / 1e9, 3), "busbw_GBps": round(busbw, 3),
-            "xgmi_frac_spec": round(busbw / (max(1, world - 1) * XGMI_LINK_DIR_GBPS), 4)}
+            "xgmi_frac_spec": bounded_frac(busbw / (max(1, world - 1) * XGMI_LINK_DIR_GBPS), crossed)}
 
 
-def roofline_xgmi(extras: dict, world: int) -> dict | None:
+def roofline_xgmi(extras: dict, world: int, crossed: bool = True) -> dict | None:
     """The N > 1 xGMI roofline (north_star's >= 80 % target): the
     BASELINE config-4 arm (8-rank-grid Swing BO, 1 GiB of real bf16 per GPU, all
     links), the faster of its RCCL and peer-window transports among the arms
@@ -605,7 +614,7 @@ def roofline_xgmi(extras: dict, world: int) -> dict | None:
             "peak_source": "measured link_probe (RCCL sendrecv, both directions at once)" if link
                            else "not measured (no RCCL link probe: --share-gpu); frac null",
             "frac_unbounded": round(frac, 4) if frac is not None and not sane else None,
-            "peak_spec": peak_spec, "frac_spec": round(bus / peak_spec, 4),
+            "peak_spec": peak_spec, "frac_spec": bounded_frac(bus / peak_spec, crossed),
             "achieved_def": "busbw = 2(p-1)/p * bytes_per_gpu / t"}
 
 
@@ -643,7 +652,7 @@ def link_probe(rank, world, dev) -> dict:
             "spec_GBps_per_direction": XGMI_LINK_DIR_GBPS, "pairs": "2i<->2i+1, both directions at once"}
 
 
-def xgmi_arms(comm, peer, world, rank, dev, stream, side, total) -> dict:
+def xgmi_arms(comm, peer, world, rank, dev, stream, side, total, crossed=True) -> dict:
     """Flat / hierarchical inter-GPU allreduces (BASELINE configs 3-5 regimes),
     each through RCCL (allred_dist_allreduce) and through the peer windows
     (allred_peer_dist_allreduce: same program, same bits, one kernel), each
@@ -668,7 +677,7 @@ def xgmi_arms(comm, peer, world, rank, dev, stream, side, total) -> dict:
         # record it, agree, and go on with the next arm instead of losing the line
         err = None
         try:
-            xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, *arm)
+            xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, *arm, crossed=crossed)
         except Exception as e:  # reported, never silently dropped
             err = repr(e)
         if not agreed(err is None):
@@ -678,7 +687,7 @@ def xgmi_arms(comm, peer, world, rank, dev, stream, side, total) -> dict:
 
 
 def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo, variant, nbytes, reps, chans,
-             local):
+             local, crossed=True):
     """One arm of xgmi_arms: each transport verified (exact sums and the closed
     form, verify_transport), then timed on real data (uniform [0,100) bf16 per
     rank) into out[...] with its verdict beside the numbers."""
@@ -695,7 +704,7 @@ def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo,
         for r in range(local):   # real data for the timing
             b2[r].copy_((torch.rand(n, generator=g, device=dev) * 100).to(torch.bfloat16).view(torch.int16))
         ms = timed_max(lambda: fn(b2), reps, stream)
-        out[key] = {**arm_stats(ms, nbytes, world, lo), "channels": chans, **v}
+        out[key] = {**arm_stats(ms, nbytes, world, lo, crossed), "channels": chans, **v}
 
     if comm is not None and (variant != t.MEM or local == 1):   # mem_2D over RCCL: one rank per GPU
         timed(name, lambda b: t.dist_allreduce(comm, d2, b.data_ptr(), w2.data_ptr(), stream), variant == t.LO)
@@ -1144,14 +1153,15 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         guard.daemon = True
         guard.start()
         extras.update(xgmi_arms(comm, peer if verify.get("peer_swing", {}).get("verified") else None, world, rank,
-                                dev, stream, side, total))
+                                dev, stream, side, total, crossed=not args.share_gpu))
         if world > 1 and comm is not None:
             try:
                 extras["link_probe"] = link_probe(rank, world, dev)
                 mb = extras["link_probe"]["GBps_per_direction"]
                 for v in extras.values():  # the fraction again against the MEASURED link rate
                     if isinstance(v, dict) and "busbw_GBps" in v:
-                        v["xgmi_frac_measured_link"] = round(v["busbw_GBps"] / ((world - 1) * mb), 4)
+                        v["xgmi_frac_measured_link"] = bounded_frac(v["busbw_GBps"] / ((world - 1) * mb),
+                                                                    not args.share_gpu)
             except Exception as e:  # reported, never silently dropped
                 extras["link_probe"] = {"error": repr(e)}
         guard.cancel()
@@ -1264,7 +1274,7 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": roof["traffic"], "kernel": roof["kernel"],
                      "algorithmic_bytes_per_launch": roof["algorithmic_bytes_per_launch"],
                      "local_phases_ms": round(local_ms, 6)},
-        "roofline_xgmi": roofline_xgmi(extras, world),
+        "roofline_xgmi": roofline_xgmi(extras, world, crossed=not args.share_gpu),
         "xgmi": extras,
         "host_wall_s": round(wall, 6),
     }

@@ -528,7 +528,9 @@ int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int 
  * While a bucket is pending, the other peer allreduce calls return
  * ALLRED_ERR_ARG; so does a prev that is not the pending bucket.
  * ALLRED_ERR_UNSUPPORTED: local_ranks != 64, more than 8 GPUs, flags not
- * uncached, or more than 8 tiles of 256 elements per workgroup (n > 2^20).
+ * uncached, or a bucket beyond the LL boxes (elems > min(max_elems, 4 Mi)).
+ * Any grid cap (allred_peer_set_max_groups) works: a workgroup runs any number
+ * of tiles, its results staged in LDS 8 tiles at a time.
  * No reference counterpart (the reference runs one vector per program). */
 int allred_peer_allreduce_pipelined(allred_peer* peer, uint16_t* cur, uint16_t* prev, uint64_t elems,
                                     int local_ranks, int local_side, int local_algo, void* stream);

@@ -239,17 +239,25 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// bounded waits of the peer kernels: 2^22 polls of an uncached word (~1 us
-// each) ~ 4 s, far above any legitimate skew between ranks.  On timeout bit 0
-// of *status is set; every later wait of the launch sees that bit (checked
-// every 1024 polls) and gives up at once, so a dead or slow peer ends the
-// launch within seconds instead of paying the bound once per wait.
-constexpr uint64_t kPeerSpinLimit = 1ull << 22;
+// bounded waits of the peer kernels: a wait gives up after kPeerWaitTicks of
+// the 100 MHz s_memrealtime clock (4 s, far above any legitimate skew between
+// ranks; a poll count is no clock — polls of uncached memory took ~50-200 ns,
+// so round 3's 2^22-poll bound expired in well under a second when several
+// ranks' grids time-sliced one GPU).  The clock is read every 64 polls.  On
+// timeout bit 0 of *status is set; every later wait of the launch sees that
+// bit (checked with the clock) and gives up at once, so a dead or slow peer
+// ends the launch within seconds instead of paying the bound once per wait.
+constexpr uint64_t kPeerWaitTicks = 400000000ull;
 
-__device__ __forceinline__ bool peer_give_up(uint64_t spin, uint32_t* status) {
-    if (spin > kPeerSpinLimit ||
-        ((spin & 1023u) == 1023u &&
-         (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ALLRED_PEER_TIMEOUT))) {
+__device__ __forceinline__ bool peer_give_up(uint64_t spin, uint64_t& t0, uint32_t* status) {
+    if (spin & 63u) return false;
+    const uint64_t now = __builtin_amdgcn_s_memrealtime();
+    if (spin == 0) {
+        t0 = now;
+        return false;
+    }
+    if (now - t0 > kPeerWaitTicks ||
+        (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ALLRED_PEER_TIMEOUT)) {
         atomicOr(status, ALLRED_PEER_TIMEOUT);
         return true;
     }

@@ -32,9 +32,10 @@ __global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, 
         __hip_atomic_store(pp.flags[t] + me, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     if (t < nranks) {
         uint32_t* mine = pp.flags[me] + t;
+        uint64_t t0 = 0;
         for (uint64_t spin = 0;; ++spin) {
             if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
-            if (peer_give_up(spin, status)) break;   // ~ seconds: a peer never arrived
+            if (peer_give_up(spin, t0, status)) break;   // ~ seconds: a peer never arrived
             __builtin_amdgcn_s_sleep(2);
         }
     }
@@ -122,9 +123,10 @@ __device__ inline void peer_signal_wait(const PeerPtrs& pp, int nranks, int me, 
         __hip_atomic_store(pp.flags[t] + slot_base + me, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (t < nranks) {
         uint32_t* mine = pp.flags[me] + slot_base + t;
+        uint64_t t0 = 0;
         for (uint64_t spin = 0;; ++spin) {
             if (__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) break;
-            if (peer_give_up(spin, status)) break;
+            if (peer_give_up(spin, t0, status)) break;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -214,9 +216,10 @@ __device__ inline void sched_wait(const PeerPtrs& pp, int me, uint32_t slot, int
     const int q = t == 0 ? q0 : (t == 1 ? q1 : -1);
     if (q >= 0) {
         uint32_t* f = pp.flags[me] + slot + q;
+        uint64_t t0 = 0;
         for (uint64_t spin = 0;; ++spin) {
             if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= value) break;
-            if (peer_give_up(spin, status)) break;
+            if (peer_give_up(spin, t0, status)) break;
             __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -343,9 +346,10 @@ struct HierPtrs {
 };
 
 __device__ inline void hier_wait(const uint32_t* f, uint32_t epoch, uint32_t* status) {
+    uint64_t t0 = 0;
     for (uint64_t spin = 0;; ++spin) {
         if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) return;
-        if (peer_give_up(spin, status)) return;
+        if (peer_give_up(spin, t0, status)) return;
         __builtin_amdgcn_s_sleep(1);
     }
 }
@@ -543,6 +547,7 @@ __device__ __forceinline__ void ll_put_word(uint64_t* dst, uint4 v, uint32_t e, 
 // poll 4 LL words until all carry epoch e (bounded: status bit 0 on timeout)
 __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_t* status) {
     uint64_t w0, w1, w2, w3;
+    uint64_t t0 = 0;
     for (uint64_t spin = 0;; ++spin) {
         w0 = __hip_atomic_load(src + 0 * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         w1 = __hip_atomic_load(src + 1 * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -551,7 +556,7 @@ __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_
         if ((uint32_t)(w0 >> 32) == e && (uint32_t)(w1 >> 32) == e && (uint32_t)(w2 >> 32) == e &&
             (uint32_t)(w3 >> 32) == e)
             break;
-        if (peer_give_up(spin, status)) break;
+        if (peer_give_up(spin, t0, status)) break;
         __builtin_amdgcn_s_sleep(1);
     }
     return make_uint4((uint32_t)w0, (uint32_t)w1, (uint32_t)w2, (uint32_t)w3);
@@ -876,12 +881,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
 //   R(cur)   the tiles of cur this GPU owns: the W partials (pushed during
 //            this launch's loops) polled, summed (fp32, owner first, one
 //            rounding), the result pushed to every GPU's box
-// Up to kHierXMaxTiles tiles per workgroup (results staged in LDS).  Every poll
-// waits for work that waits on nothing of the poller (the results: the owners'
-// previous launches; R(cur): every GPU's loop of this launch, which polls only
-// results of the previous launch), and the grid is resident, so every wait is
-// satisfied.
-constexpr int kHierXMaxTiles = 8;   // lanes (j, c) of the whole workgroup serve tile j
+// Any number of tiles per workgroup: prev's results are staged in LDS chunks of
+// kHierXChunk tiles (lanes (j, c) of the whole workgroup serve tile j of a
+// chunk), two chunks resident — chunk k + 1 is polled when the row stores of
+// chunk k begin, into the slot chunk k - 1 left — and R(cur) runs chunk by
+// chunk.  Every poll waits for work that waits on nothing of the poller (the
+// results: the owners' previous launches; R(cur): every GPU's loop of this
+// launch, which polls only results of the previous launch), and the grid is
+// resident, so every wait is satisfied.
+constexpr int kHierXChunk = 8;
 
 // LAG (tune hier_x_lag): prev's / old's tile rows stored in the iteration of cur's tile j - LAG
 // (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order)
@@ -894,7 +902,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res[kHierXMaxTiles][TV];
+    __shared__ __attribute__((aligned(16))) uint4 res[2][kHierXChunk][TV];   // two chunks of prev's results
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
@@ -920,15 +928,22 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
         ord_lds[lane] = (uint8_t)ob;
     }
-    // ---- prev's results of this workgroup's tiles -> LDS: lane (j, c) (32 j + c)
-    // serves tile j, column c.  The owners pushed them at the end of the previous
-    // launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep HBM busy.
+    // ---- prev's results of this workgroup's tiles -> LDS: lane (jr, c) (32 jr + c)
+    // serves tile jr of a chunk, column c.  The owners pushed them at the end of the
+    // previous launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep
+    // HBM busy.  Chunks 0 and 1 now, chunk k + 1 when chunk k's row stores begin.
     const int jr = threadIdx.x / TV;
-    if (prev && jr < kHierXMaxTiles && jr < mine) {
-        const uint64_t* at = lpv.ll[me] + box_words + tile_of(jr) * 128 + c;
+    auto poll_prev = [&](int ch) {
+        const int j = ch * kHierXChunk + jr;
+        if (j >= mine) return;
+        const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
-        res[jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+        res[ch & 1][jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+    };
+    if (prev) {
+        poll_prev(0);
+        if (mine > kHierXChunk) poll_prev(1);
     }
     lds_barrier();   // order bytes and results in LDS
     for (int j = 0; j < mine; ++j) {
@@ -959,10 +974,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             }
         }
         // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(j - LAG);
+        const int sj = j - LAG;   // the tile whose rows this iteration stores
+        if (prev && sj >= kHierXChunk && sj % kHierXChunk == 0) {
+            // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
+            // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1
+            if (!cur) lds_barrier();
+            poll_prev(sj / kHierXChunk + 1);
+        }
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-        const bool st = prev && j >= LAG;
-        const uint4 rv = st ? res[j - LAG][c] : make_uint4(0, 0, 0, 0);
+        const bool st = prev && sj >= 0;
+        const uint4 rv = st ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             if (cur && j + 2 < mine)
@@ -972,16 +994,19 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         }
     }
     if (LAG && prev && mine > 0) {   // prev's last tile
-        const uint4 rv = res[mine - 1][c];
+        if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
+        const int sj = mine - 1;
+        const uint4 rv = res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c];
 #pragma unroll
         for (int k = 0; k < OPS; ++k)
-            st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(mine - 1) * TV + c, rv);
+            st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
     }
     // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
     // partial (during this launch's loop): W partials summed (fp32, owner first,
     // one rounding), the result pushed to every GPU's box for the next launch.
-    if (cur && jr < kHierXMaxTiles && jr < mine) {
-        const uint64_t t = tile_of(jr);
+    for (int j0 = 0; cur && j0 < mine; j0 += kHierXChunk) {
+        if (j0 + jr >= mine) break;
+        const uint64_t t = tile_of(j0 + jr);
         if (owner_of(t) == me) {
             const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
             uint64_t wr[kLLMaxGpus][4];
@@ -1025,7 +1050,11 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // it pushes bucket i's partial of t, and the owner reads bucket i's partials of
 // t (launch i+1) before it pushes bucket i's result of t, so LL parity k & 1
 // (inbox and box) is reused only after its previous reader is done.
-// Same bits as k_hier_ll / k_hier_x; at most kHierXMaxTiles tiles per workgroup.
+// Any number of tiles per workgroup, in chunks of kHierXChunk as in k_hier_x:
+// mid's owned sums chunk by chunk, old's results two chunks resident (chunk k
+// + 1 polled when chunk k's row stores begin — before cur's partial of any of
+// its tiles is pushed, so the order above holds per tile).
+// Same bits as k_hier_ll / k_hier_x.
 template <bool TAIL, int LAG>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
@@ -1036,7 +1065,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res[kHierXMaxTiles][TV];
+    __shared__ __attribute__((aligned(16))) uint4 res[2][kHierXChunk][TV];   // two chunks of results
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
@@ -1045,6 +1074,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    const int nch = (mine + kHierXChunk - 1) / kHierXChunk;
     auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
     auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
     auto issue = [&](uint64_t t, int b) {
@@ -1053,9 +1083,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
                       wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
     };
-    // rows of tile j of bucket `dst` from res[j] (lanes of wave w, half q: rows RPW w + q + RPI k)
+    // rows of tile j of bucket `dst` from its chunk's slot (lanes of wave w, half q: rows RPW w + q + RPI k)
     auto store_rows = [&](uint16_t* dst, int j) {
-        const uint4 rv = res[j][c];
+        const uint4 rv = res[(j / kHierXChunk) & 1][j % kHierXChunk][c];
 #pragma unroll
         for (int k = 0; k < OPS; ++k)
             st_nt(reinterpret_cast<uint4*>(dst + row_off + (uint64_t)(RPI * k) * stride) + tile_of(j) * TV + c, rv);
@@ -1069,14 +1099,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
         ord_lds[lane] = (uint8_t)ob;
     }
-    // ---- lane (jr, c) (32 jr + c) serves tile jr of this workgroup, column c
+    // ---- lane (jr, c) (32 jr + c) serves tile jr of a chunk of this workgroup, column c
     const int jr = threadIdx.x / TV;
-    const bool act = jr < kHierXMaxTiles && jr < mine;
-    const uint64_t tr = tile_of(jr);
-    const bool rmid = has_mid && act && owner_of(tr) == me;
-    const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
-    // mid's owned sums: polls of its W partials, owner sum, pushed to every GPU's box
-    auto owned_sums = [&]() {
+    auto act_in = [&](int ch) { return ch * kHierXChunk + jr < mine; };
+    auto rmid_in = [&](int ch) { return has_mid && act_in(ch) && owner_of(tile_of(ch * kHierXChunk + jr)) == me; };
+    // mid's owned sums of chunk ch: polls of its W partials, owner sum, pushed to every GPU's box
+    auto owned_sums = [&](int ch) {
+        if (!rmid_in(ch)) return;
+        const uint64_t tr = tile_of(ch * kHierXChunk + jr);
+        const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
         uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
         for (int src = 0; src < kLLMaxGpus; ++src)
@@ -1092,13 +1123,26 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
             if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
     };
+    // old's results of chunk ch -> its slot
+    auto poll_old = [&](int ch) {
+        if (!act_in(ch)) return;
+        const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c;
+        uint64_t wd[4];
+        ll_load(at, wd);
+        res[ch & 1][jr][c] = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
+    };
     uint64_t wo[4];
-    if (old && act) ll_load(lo.ll[me] + box_words + tr * 128 + c, wo);
-    if (!TAIL && rmid) owned_sums();
-    if (old && act) res[jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tr * 128 + c, eold, status);
+    if (old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
+    if (!TAIL)
+        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
+    if (old && act_in(0))
+        res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
+    if (old && nch > 1) poll_old(1);
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
-    // (the polls before them have returned, and with them both tiles' loads)
-    const int pushed = !TAIL && __ballot(rmid) != 0 ? 4 * W : 0;
+    // (the polls before them have returned, and with them both tiles' loads).  With
+    // several chunks an earlier chunk's pushes may be in flight too: counting none
+    // only waits longer (the loads of tile j are never waited for too little)
+    const int pushed = !TAIL && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
@@ -1129,10 +1173,18 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             }
         }
         // ---- cur's tile j+2 in, old's tile j - LAG out, interleaved op by op
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(j - LAG);
+        const int sj = j - LAG;   // the tile whose rows this iteration stores
+        if (old && sj >= kHierXChunk && sj % kHierXChunk == 0) {
+            // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
+            // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1.
+            // Its tiles' partials of cur are pushed in later iterations (sj + 8 > j)
+            if (!cur) lds_barrier();
+            poll_old(sj / kHierXChunk + 1);
+        }
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-        const bool st = old && j >= LAG;
-        const uint4 rv = st ? res[j - LAG][c] : make_uint4(0, 0, 0, 0);
+        const bool st = old && sj >= 0;
+        const uint4 rv = st ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             if (cur && j + 2 < mine)
@@ -1141,13 +1193,20 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             if (st) st_nt(reinterpret_cast<uint4*>(old + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
         }
     }
-    if (LAG && old && mine > 0) store_rows(old, mine - 1);   // old's last tile
-    if (TAIL && rmid) owned_sums();   // TAIL: mid's partials arrived during the launch i-1
+    if (LAG && old && mine > 0) {   // old's last tile
+        if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
+        store_rows(old, mine - 1);
+    }
+    if (TAIL)   // TAIL: mid's partials arrived during the launch i-1
+        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
-        __syncthreads();   // every wave has read old's results out of res
-        if (act) res[jr][c] = ll_get(lm.ll[me] + box_words + tr * 128 + c, emid, status);
-        lds_barrier();
-        for (int j = 0; j < mine; ++j) store_rows(fin, j);
+        for (int ch = 0; ch < nch; ++ch) {
+            __syncthreads();   // every wave has read the slot's previous results
+            if (act_in(ch))
+                res[ch & 1][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
+            lds_barrier();
+            for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
+        }
     }
 }
 
@@ -1184,6 +1243,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
     }
     for (uint64_t u = gt; u < bv; u += GT) {   // R: my block
         uint4 y[kLLMaxGpus];
+        uint64_t t0 = 0;
         for (uint64_t spin = 0;; ++spin) {
             uint64_t wv[kLLMaxGpus][4];
 #pragma unroll
@@ -1202,7 +1262,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
                 y[q] = make_uint4((uint32_t)wv[q][0], (uint32_t)wv[q][1], (uint32_t)wv[q][2], (uint32_t)wv[q][3]);
             }
             if (bad == 0) break;
-            if (peer_give_up(spin, status)) break;
+            if (peer_give_up(spin, t0, status)) break;
             __builtin_amdgcn_s_sleep(1);
         }
         float a[8];
@@ -1410,7 +1470,6 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    if ((ntiles + grid - 1) / grid > (uint64_t)kHierXMaxTiles) return ALLRED_ERR_UNSUPPORTED;
     LLPtrs lc{}, lp{};
     for (int q = 0; q < nranks; ++q) {
         lc.ll[q] = llc ? llc[q] : nullptr;
@@ -1435,7 +1494,6 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
     // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    if ((ntiles + grid - 1) / grid > (uint64_t)kHierXMaxTiles) return ALLRED_ERR_UNSUPPORTED;
     LLPtrs lc{}, lm{}, lo{};
     for (int q = 0; q < nranks; ++q) {
         lc.ll[q] = llc ? llc[q] : nullptr;

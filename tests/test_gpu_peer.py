@@ -112,8 +112,12 @@ def worker(rank, world, port, q):
                                                      ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
-                                                     ("hier_x2_tail", 0, 0, 0))):
-            if cap < 0:   # k_hier_x / k_hier_x2 take at most 8 tiles per workgroup
+                                                     ("hier_x2_tail", 0, 0, 0),
+                                                     # one workgroup: 3 * world tiles, results staged 8 at a time
+                                                     # (two chunks resident, the third reusing the first's slot)
+                                                     ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
+                                                     ("hier_x2_tail_one_group", 0, 0, 1))):
+            if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
@@ -125,7 +129,7 @@ def worker(rank, world, port, q):
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
-                    with t.tuned(hier_x2_tail=int(mode == "hier_x2_tail")):
+                    with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail"))):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
                     peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
@@ -134,7 +138,7 @@ def worker(rank, world, port, q):
                     peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
-                with t.tuned(hier_x2_tail=int(mode == "hier_x2_tail")):
+                with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail"))):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
                 peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())

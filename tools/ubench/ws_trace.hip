@@ -11,6 +11,9 @@
 #include "../../tenstorrentallreduce_amd/csrc/kernels.hip"
 #include "../../tenstorrentallreduce_amd/csrc/peer_kernels.hip"
 
+// this probe still bounds its own waits by poll count (the product waits by the clock)
+constexpr uint64_t kPeerSpinLimit = 1ull << 22;
+
 // k_hier_ws: the round-1 pipelined specialised-wave form of the hierarchical
 // step (removed from the product library: 27-38 us vs 18 for k_hier_ll at W = 1,
 // DESIGN.md §5); kept here with its launcher for this study.
@@ -325,7 +328,7 @@ __global__ __launch_bounds__(kWsBlock) void k_hier_ws(uint16_t* __restrict__ ran
                     y[k] = make_uint4((uint32_t)v[k][0], (uint32_t)v[k][1], (uint32_t)v[k][2], (uint32_t)v[k][3]);
                 }
                 if (bad == 0) break;
-                if (peer_give_up(spin, status)) break;
+                if (spin > kPeerSpinLimit) { atomicOr(status, ALLRED_PEER_TIMEOUT); break; }
                 ws_nap();
             }
             if (j == 0) WS_MARK(14);
