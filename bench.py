@@ -683,7 +683,28 @@ def xgmi_arms(comm, peer, world, rank, dev, stream, side, total, crossed=True) -
         if not agreed(err is None):
             out[arm[0] + "_error"] = err or "failed on another rank"
             torch.cuda.synchronize()
+    out["best_per_config"] = best_arms(out)
     return out
+
+
+def best_arms(out: dict) -> dict:
+    """The fastest VERIFIED arm of each configuration over every transport and
+    swept shape (RCCL, peer windows, grid sizes, LL / one-shot thresholds):
+    what a tuned 8-GPU node would run for that bucket."""
+    best = {}
+    for key, v in out.items():
+        if not isinstance(v, dict) or v.get("verified") is not True or "ms" not in v or v.get("peer_timeout"):
+            continue
+        cfg = key
+        for pre in ("peer_sched_", "peer_oneshot_", "peer_"):
+            if cfg.startswith(pre):
+                cfg = cfg[len(pre):]
+                break
+        if cfg.startswith("g") and "_" in cfg and cfg.split("_", 1)[0][1:].isdigit():
+            cfg = cfg.split("_", 1)[1]
+        if cfg not in best or v["ms"] < best[cfg]["ms"]:
+            best[cfg] = {"arm": key, "ms": v["ms"], "busbw_GBps": v.get("busbw_GBps")}
+    return best
 
 
 def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo, variant, nbytes, reps, chans,
@@ -720,6 +741,17 @@ def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo,
         if status():   # sticky: this arm (or an earlier one) timed out, the numbers are void
             out["peer_" + name]["peer_timeout"] = True
             out["peer_" + name]["verified"] = False
+        if variant != t.MEM and local == 1 and name.startswith(("config3", "config4")):
+            # the scheduled form's grid is a guess (256 workgroups, 7 channels sharing
+            # them): the same program at a quarter and a half of it, each a verified arm
+            cap = 256 if crossed else 512 // world
+            for groups in (cap // 4, cap // 2):
+                peer.set_max_groups(groups)
+                try:
+                    timed(f"peer_g{groups}_" + name, peer_fn, variant == t.LO, status)
+                    out[f"peer_g{groups}_" + name]["sched_groups"] = groups
+                finally:
+                    peer.set_max_groups(0 if crossed else cap)
         if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
             peer.set_lo_ll_max(0)
             try:

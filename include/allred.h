@@ -592,7 +592,8 @@ int allred_peer_set_mem_ll_max(allred_peer* peer, uint64_t bytes);
  * RCCL replaced by direct reads of the partners' IPC-mapped windows: one
  * kernel, each step waits only for its partner (allred_BO_2D
  * dataflow_kernel.cpp:152-267 semaphore handshakes, over xGMI).
- * desc->variant ALLRED_MEM runs allred_peer_allreduce.  desc->total_nodes
+ * desc->variant ALLRED_MEM runs allred_peer_allreduce (fp32 accumulation only: mem_accum
+ * ALLRED_ACC_BF16 -> ALLRED_ERR_UNSUPPORTED; RCCL runs it).  desc->total_nodes
  * must equal nranks; elems <= max_elems (BO) or max_elems / 2 (LO);
  * workspace: allred_dist_workspace_bytes(desc) bytes when local_ranks > 1. */
 int allred_peer_dist_allreduce(allred_peer* peer, const allred_dist_desc* desc, uint16_t* buf, void* workspace,

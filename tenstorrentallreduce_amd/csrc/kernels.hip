@@ -1217,7 +1217,11 @@ constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), in LDS; pairs unused.
 // MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
-template <int P, bool BO, int MINW>
+// PF (tune steps_prefetch): the strip's program words (every later phase's
+// row pairs, the result rows) are read out of LDS into registers before step
+// 0, so a phase's dependent chain is its row reads, add and row write only —
+// without PF every phase first waits for its own table read.
+template <int P, bool BO, int MINW, bool PF>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
@@ -1292,6 +1296,22 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
         const uint8_t* tb = tabs[BO ? (s / Q) / slices : 0];
         const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
+        // PF: phase ph's operand words (BO: MPH <= 2 pairs of row bytes; LO: IPW <= 4 other-row
+        // bytes) and the result rows (OPS bytes), packed; every read stays inside the block's
+        // table (BO: < 220 of 256 bytes; LO: < 384 of 448), unused lanes' words are ignored
+        uint32_t pw[PF ? NPH : 1] = {}, fw[PF ? (OPS + 3) / 4 : 1] = {};
+        if constexpr (PF) {
+#pragma unroll
+            for (int ph = 1; ph <= NPH; ++ph) {
+#pragma unroll
+                for (int m = 0; m < (BO ? MPH : IPW); ++m) {
+                    const uint32_t e = t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
+                    pw[ph - 1] |= BO ? e << (16 * m) : (e >> 8) << (8 * m);
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) fw[k / 4] |= (uint32_t)tb[off_of(NPH + 1) + RPO * k + rl] << (8 * (k % 4));
+        }
         uint4 val[BO ? 1 : IPW];   // LO: this lane's pair rows after the latest step
 #pragma unroll
         for (int t = 0; t < IPW; ++t)
@@ -1313,7 +1333,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
 #pragma unroll
                 for (int m = 0; m < MPH; ++m)
                     if (lane + 64 * m < cnt_of(ph) * CW) {
-                        const uint32_t pr = t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
+                        const uint32_t pr = PF ? (pw[ph - 1] >> (16 * m)) & 0xffffu : t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
                         const int a = (pr & 255) * CW + cl, cc = (pr >> 8) * CW + cl;
                         tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
                     }
@@ -1321,7 +1341,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 uint4 oth[IPW];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CW) oth[m] = tile[(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8) * CW + cl];
+                    if (lane + 64 * m < H * CW)
+                        oth[m] = tile[(PF ? (pw[ph - 1] >> (8 * m)) & 255u : (uint32_t)(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8)) * CW + cl];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
                     if (lane + 64 * m < H * CW) {
@@ -1334,8 +1355,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         const uint64_t cs = col0(s) + cl;
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
-            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs,
-                  tile[(int)tb[off_of(NPH + 1) + RPO * k + rl] * CW + cl]);
+            const uint32_t fin = PF ? (fw[k / 4] >> (8 * (k % 4))) & 255u : (uint32_t)tb[off_of(NPH + 1) + RPO * k + rl];
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs, tile[fin * CW + cl]);
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
@@ -1464,8 +1485,11 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
-#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
-                                               pairs, bv, slices, units, stamps)
+    const bool pf = tune(Tune::steps_prefetch) != 0;
+#define TSA_SR(PP, BOV, MW) do { if (pf) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, true>), grid, dim3(256), 0, st, \
+                                     ranks, stride, tab, pairs, bv, slices, units, stamps); \
+                                 else hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, false>), grid, dim3(256), 0, st, \
+                                     ranks, stride, tab, pairs, bv, slices, units, stamps); } while (0)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)

@@ -391,6 +391,9 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
     if (d->total_nodes != p->nranks || p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;
     const size_t n = (size_t)d->elems;
     if (d->variant == ALLRED_MEM) {
+        // the peer mem_2D kernels sum in fp32 with one rounding; the reference's bf16
+        // dest-register accumulation runs over RCCL (launch_rows_sum) only
+        if (d->mem_accum == ALLRED_ACC_BF16) return ALLRED_ERR_UNSUPPORTED;
         uint16_t* ws = workspace ? static_cast<uint16_t*>(workspace) + n : nullptr;  // dist workspace layout
         return allred_peer_allreduce(p, buf, n, d->local_ranks, d->local_side, d->local_algo, ws, stream);
     }

@@ -41,6 +41,7 @@ const Key kKeys[] = {
     {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
     {"steps_groups", 0, 0, 5},        // k_steps_reg: workgroups per CU, 0 auto (BO 3, LO 4 or 3) | 3 | 4 | 5
     {"rccl_fault", 0, 0, 7},          // fault injection (tests): 1 init, 2 group end, 4 stream drain never settle
+    {"steps_prefetch", 1, 0, 1},      // k_steps_reg: a strip's program words in registers before step 0
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");
