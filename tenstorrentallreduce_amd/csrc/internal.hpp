@@ -41,7 +41,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
-    rccl_fault, steps_prefetch,
+    rccl_fault, steps_prefetch, hier_handoff,
     count
 };
 int64_t tune(Tune key);
@@ -170,10 +170,14 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
 // the previous launch started (llm non-null: its parity's LL areas), writes `old` (started two
 // launches ago; llo: its parity); the flush launch (cur null) also writes that middle bucket
 // `fin` from its results
+// xfl: null = LL hand-offs; else every GPU's hand-off flag block (kXFlagBytes, the FLG form: data
+// in the LL slots without epochs, one flag per workgroup and peer; parities = the LL parities of
+// cur / mid / old in bits 0 / 1 / 2)
+constexpr size_t kXFlagBytes = 4 * 2 * 2 * 8 * 512;
 int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
                    uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
-                   unsigned max_grid, void* stream);
+                   unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream);
 // allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * (n / 8 rounded up to 32)
 int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
                        uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream);

@@ -57,6 +57,8 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
+    size_t xfl_off = 0;             // k_hier_x2's hand-off flags (FLG form) behind the LL boxes
+    uint32_t* peer_xfl[ALLRED_MAX_NODES] = {};
     int hier_ll = 0;                // 0 off, 1 k_hier_ll (LL push hand-offs), 2 k_hier_pipe (the same, pipelined)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
@@ -72,6 +74,7 @@ struct allred_peer {
     uint16_t* x2_buf[2] = {};
     uint32_t x2_k[2] = {};          // their call numbers
     uint64_t x2_elems = 0;          // the sequence's bucket size
+    bool x2_flg = false;            // the sequence's hand-off form (tune hier_handoff at its first call)
 };
 
 extern "C" {
@@ -101,7 +104,8 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     const uint64_t ll_elems = p->max_elems < (4ull << 20) ? p->max_elems : (4ull << 20);
     p->ll_off = (p->hfl_off + p->hfl_bytes + 255) / 256 * 256;
     p->ll_box_words = (ll_elems / 256) * 128;
-    const size_t flag_bytes = p->ll_off + 2 * 2 * p->ll_box_words * 8;
+    p->xfl_off = (p->ll_off + 2 * 2 * p->ll_box_words * 8 + 255) / 256 * 256;
+    const size_t flag_bytes = p->xfl_off + kXFlagBytes;
     const size_t win_bytes = p->max_elems * 2;
     auto release = [p]() {
         for (uint16_t* w : p->win) (void)hipFree(w);
@@ -182,6 +186,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
         uint8_t* f = reinterpret_cast<uint8_t*>(p->peer_flags[q]);
         p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + p->hfl_off);
         p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + p->ll_off);
+        p->peer_xfl[q] = reinterpret_cast<uint32_t*>(f + p->xfl_off);
     }
     p->connected = true;
     return ALLRED_OK;
@@ -208,6 +213,7 @@ int allred_peer_connect_all(int nranks, allred_peer* const* peers) {
             uint8_t* f = reinterpret_cast<uint8_t*>(o->flags);
             p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + o->hfl_off);
             p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + o->ll_off);
+            p->peer_xfl[q] = reinterpret_cast<uint32_t*>(f + o->xfl_off);
         }
     }
     for (int q = 0; q < nranks; ++q) peers[q]->connected = true;   // opened[] stays false: nothing to close
@@ -290,9 +296,11 @@ int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t ele
     area(ko, llo);
     uint16_t* old = has_old ? p->x2_buf[0] : nullptr;
     uint16_t* fin = !cur ? p->x2_buf[p->x2_n - 1] : nullptr;
+    if (p->x2_n == 0) p->x2_flg = tune(Tune::hier_handoff) != 0;   // a sequence keeps its hand-off form
+    const uint32_t parities = (kc & 1u) | ((km & 1u) << 1) | ((ko & 1u) << 2);
     st = launch_hier_x2(cur, old, fin, n, order, cur ? llc : nullptr, p->x2_n > 0 ? llm : nullptr,
                         has_old ? llo : nullptr, p->nranks, p->rank, n, p->ll_box_words, kc + 1u, km + 1u, ko + 1u,
-                        p->status, p->max_groups, stream);
+                        p->status, p->max_groups, p->x2_flg ? p->peer_xfl : nullptr, parities, stream);
     if (st != ALLRED_OK) return st;
     if (!cur) {   // flushed: nothing pending
         p->x2_n = 0;

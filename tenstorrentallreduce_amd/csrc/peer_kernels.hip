@@ -1027,6 +1027,58 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     }
 }
 
+// ---- hand-off flags (FLG forms of k_hier_x2, tune hier_handoff = 1) ----------
+// LL words carry 4 data bytes + a 4-byte epoch each: every hand-off moves twice
+// its data.  In the FLG form the data go as plain system-coherent 16-byte
+// stores (sc0 sc1, the LL stores' policy) into the first 512 bytes of the same
+// LL slot, and each workgroup raises ONE flag per peer GPU when every wave's
+// hand-off stores of the launch have completed (s_waitcnt vmcnt(0): the one
+// in-order counter — the ordering k_peer_oneshot's barriers already rely on).
+// The consumer is the same workgroup index on the peer (tile t is served by
+// workgroup t mod G on every GPU) one launch later: it polls its W flags, then
+// reads the data.  Flags: [parity][0 partials | 1 results][GPU][workgroup] in
+// each GPU's flag allocation; values = the bucket's epoch (monotonic).
+constexpr int kXFlagGroups = 512;
+constexpr size_t kXFlagWords = 2 * 2 * kLLMaxGpus * kXFlagGroups;
+static_assert(kXFlagWords * 4 == kXFlagBytes, "internal.hpp kXFlagBytes: the flag block the host allocates");
+struct XFPtrs {
+    uint32_t* f[kLLMaxGpus];   // GPU q's hand-off flag block
+};
+__device__ __forceinline__ uint32_t* xflag(uint32_t* base, uint32_t parity, int kind, int q) {
+    return base + (((parity * 2 + kind) * kLLMaxGpus + q) * kXFlagGroups + blockIdx.x);
+}
+__device__ __forceinline__ void st_sys16(uint4* p, uint4 v) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ uint4 ld_sys16(const uint4* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+// every wave's stores so far have completed; then lane q raises the flag in GPU q's block
+__device__ __forceinline__ void xflag_raise(const XFPtrs& xf, uint32_t parity, int kind, int me, int W, uint32_t e) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if ((int)threadIdx.x < W)
+        __hip_atomic_store(xflag(xf.f[threadIdx.x], parity, kind, me), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// lane q waits for GPU q's flag in this GPU's block, then the workgroup goes on (bounded)
+__device__ __forceinline__ void xflag_wait(uint32_t* mine, uint32_t parity, int kind, int W, uint32_t e,
+                                           uint32_t* status) {
+    if ((int)threadIdx.x < W) {
+        const uint32_t* f = xflag(mine, parity, kind, threadIdx.x);
+        uint64_t t0 = 0;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) break;
+            if (peer_give_up(spin, t0, status)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    lds_barrier();
+}
+
 // ---- hierarchical step, two-deep bucket pipeline ----------------------------
 // k_hier_x2: launch i starts bucket i (cur: tree -> partial pushed to the
 // tile's owner), sums the owned tiles of bucket i-1 (mid: its W partials were
@@ -1055,13 +1107,14 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // + 1 polled when chunk k's row stores begin — before cur's partial of any of
 // its tiles is pushed, so the order above holds per tile).
 // Same bits as k_hier_ll / k_hier_x.
-template <bool TAIL, int LAG>
+template <bool TAIL, int LAG, bool FLG>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
-                                                    int has_mid, uint32_t* status) {
+                                                    int has_mid, uint32_t* status, XFPtrs xf, uint32_t par) {
+    // FLG: par = the LL parities of cur / mid / old in bits 0 / 1 / 2
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
@@ -1104,45 +1157,81 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     auto act_in = [&](int ch) { return ch * kHierXChunk + jr < mine; };
     auto rmid_in = [&](int ch) { return has_mid && act_in(ch) && owner_of(tile_of(ch * kHierXChunk + jr)) == me; };
     // mid's owned sums of chunk ch: polls of its W partials, owner sum, pushed to every GPU's box
+    const uint32_t pc = par & 1u, pm = (par >> 1) & 1u, po = (par >> 2) & 1u;
+    // a hand-off slot's data in the FLG form: the first 512 bytes of its 1 KiB LL slot
+    auto dslot = [&](uint64_t* base, uint64_t slot) { return reinterpret_cast<uint4*>(base + slot * 128) + c; };
     auto owned_sums = [&](int ch) {
         if (!rmid_in(ch)) return;
         const uint64_t tr = tile_of(ch * kHierXChunk + jr);
         const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
-        uint64_t wr[kLLMaxGpus][4];
-#pragma unroll
-        for (int src = 0; src < kLLMaxGpus; ++src)
-            if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
         uint4 y[kLLMaxGpus];
+        if constexpr (FLG) {   // the W flags were waited for: plain loads
 #pragma unroll
-        for (int src = 0; src < kLLMaxGpus; ++src)
-            if (src < W)
-                y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
-                                                 : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W) y[src] = ld_sys16(dslot(lm.ll[me], lr * W + src));
+        } else {
+            uint64_t wr[kLLMaxGpus][4];
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
+#pragma unroll
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W)
+                    y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
+                                                     : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
+        }
         const uint4 o = owner_sum(y, W, me);
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
-            if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
+            if (dst < W) {
+                if constexpr (FLG) st_sys16(dslot(lm.ll[dst] + box_words, tr), o);
+                else ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
+            }
+    };
+    // FLG: mid's partials have arrived from every GPU (their previous launch raised its
+    // flag after its loop); the owned sums; every GPU told that this workgroup's sums are out
+    auto all_owned_sums = [&]() {
+        if constexpr (FLG) {
+            if (!has_mid) return;
+            xflag_wait(xf.f[me], pm, 0, W, emid, status);
+        }
+        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
+        if constexpr (FLG) xflag_raise(xf, pm, 1, me, W, emid);
     };
     // old's results of chunk ch -> its slot
     auto poll_old = [&](int ch) {
         if (!act_in(ch)) return;
+        if constexpr (FLG) {
+            res[ch & 1][jr][c] = ld_sys16(dslot(lo.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
+            return;
+        }
         const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
         res[ch & 1][jr][c] = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
     };
-    uint64_t wo[4];
-    if (old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
-    if (!TAIL)
-        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
-    if (old && act_in(0))
-        res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
-    if (old && nch > 1) poll_old(1);
+    if constexpr (FLG) {
+        if (!TAIL) all_owned_sums();
+        if (old) {   // every owner's results of old are out (raised one launch ago)
+            xflag_wait(xf.f[me], po, 1, W, eold, status);
+            poll_old(0);
+            if (nch > 1) poll_old(1);
+        }
+    } else {
+        uint64_t wo[4];
+        if (old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
+        if (!TAIL)
+            for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
+        if (old && act_in(0))
+            res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
+        if (old && nch > 1) poll_old(1);
+    }
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
     // (the polls before them have returned, and with them both tiles' loads).  With
     // several chunks an earlier chunk's pushes may be in flight too: counting none
-    // only waits longer (the loads of tile j are never waited for too little)
-    const int pushed = !TAIL && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
+    // only waits longer (the loads of tile j are never waited for too little).  FLG:
+    // the flag raise has drained them
+    const int pushed = !FLG && !TAIL && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
@@ -1164,12 +1253,16 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            if (q == 0) {   // the partial -> its owner's inbox, wave w writing word w
+            // the partial -> its owner's inbox: LL, wave w writing word w of every column;
+            // FLG, wave w writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
+            if (q == 0 && (!FLG || (c >> 3) == w)) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
-                ll_put_word(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur, w);
+                const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
+                if constexpr (FLG) st_sys16(dslot(lc.ll[o], slot), pr);
+                else ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
             }
         }
         // ---- cur's tile j+2 in, old's tile j - LAG out, interleaved op by op
@@ -1197,13 +1290,23 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
         store_rows(old, mine - 1);
     }
-    if (TAIL)   // TAIL: mid's partials arrived during the launch i-1
-        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
+    if constexpr (FLG)   // cur's partials of this workgroup are out: every owner told
+        if (cur) xflag_raise(xf, pc, 0, me, W, ecur);
+    if (TAIL) {   // TAIL: mid's partials arrived during the launch i-1
+        if constexpr (FLG) all_owned_sums();
+        else
+            for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
+    }
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
+        if constexpr (FLG) xflag_wait(xf.f[me], pm, 1, W, emid, status);
         for (int ch = 0; ch < nch; ++ch) {
             __syncthreads();   // every wave has read the slot's previous results
-            if (act_in(ch))
-                res[ch & 1][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
+            if (act_in(ch)) {
+                if constexpr (FLG)
+                    res[ch & 1][jr][c] = ld_sys16(dslot(lm.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
+                else
+                    res[ch & 1][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
+            }
             lds_barrier();
             for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
         }
@@ -1485,7 +1588,7 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
 int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
                    uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
-                   unsigned max_grid, void* stream) {
+                   unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
         (!cur && !old && !fin) || (cur && !llc) || (old && !llo) || (fin && (cur || !llm)) ||
@@ -1500,12 +1603,23 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         lm.ll[q] = llm ? llm[q] : nullptr;
         lo.ll[q] = llo ? llo[q] : nullptr;
     }
-    const int form = (tune(Tune::hier_x2_tail) ? 2 : 0) + (tune(Tune::hier_x_lag) ? 1 : 0);
-    auto* kern = form == 3 ? k_hier_x2<true, 1> : form == 2 ? k_hier_x2<true, 0>
-               : form == 1 ? k_hier_x2<false, 1>
-                           : k_hier_x2<false, 0>;
+    XFPtrs xf{};
+    for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
+    const int form = (tune(Tune::hier_x2_tail) ? 2 : 0) + (tune(Tune::hier_x_lag) ? 1 : 0) + (xfl ? 4 : 0);
+    if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
+    decltype(&k_hier_x2<false, 0, false>) kern;
+    switch (form) {
+        case 7: kern = k_hier_x2<true, 1, true>; break;
+        case 6: kern = k_hier_x2<true, 0, true>; break;
+        case 5: kern = k_hier_x2<false, 1, true>; break;
+        case 4: kern = k_hier_x2<false, 0, true>; break;
+        case 3: kern = k_hier_x2<true, 1, false>; break;
+        case 2: kern = k_hier_x2<true, 0, false>; break;
+        case 1: kern = k_hier_x2<false, 1, false>; break;
+        default: kern = k_hier_x2<false, 0, false>; break;
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, emid, eold, llm ? 1 : 0, status);
+                       box_words, ecur, emid, eold, llm ? 1 : 0, status, xf, parities);
     return peer_last_error();
 }
 

@@ -221,3 +221,48 @@ def test_rccl_init_with_a_missing_rank_returns_instead_of_hanging():
     assert r.returncode == 0, r.stderr[-2000:]
     assert r.stdout.strip().endswith(f"status {t._lib.ERR_TRANSPORT}"), (r.stdout, r.stderr[-2000:])
     assert dt < 60, dt
+
+
+@pytest.mark.parametrize("acc", [t.ACC_FP32, t.ACC_BF16])
+def test_mem_2d_over_rccl_across_visible_gpus(acc):
+    """mem_2D as an RCCL program across every visible GPU (one thread's worth of
+    calls per communicator, ncclCommInitAll-style init): the pairwise rounds,
+    the owner-first ordered sum and the gather, bit-exact vs the oracle for fp32
+    and the reference's bf16 accumulation.  Needs >= 2 GPUs (skipped on a
+    1-GPU box; RCCL refuses two ranks on one device)."""
+    import threading
+    ng = torch.cuda.device_count()
+    if ng < 2:
+        pytest.skip("needs >= 2 GPUs")
+    ng = 1 << (ng.bit_length() - 1)   # a power of two
+    side = {2: 2, 4: 2, 8: 4}[ng]
+    n = 8 * ng * 640
+    rng = np.random.default_rng(acc + 11)
+    data = [rng.integers(0x3F80, 0x42C8, n).astype(np.uint16) for _ in range(ng)]
+    comms = t.Comm.init_all(list(range(ng)))
+    desc = t.dist_desc(t.SWING, t.MEM, side, ng, n, mem_accum=acc)
+    bufs = [torch.from_numpy(d.view(np.int16)).to(f"cuda:{g}") for g, d in enumerate(data)]
+    wss = [torch.empty(t.dist_workspace_bytes(desc), dtype=torch.uint8, device=f"cuda:{g}") for g in range(ng)]
+    errs = []
+
+    def one(g):
+        try:
+            torch.cuda.set_device(g)
+            s = torch.cuda.current_stream(g)
+            t.dist_allreduce(comms[g], desc, bufs[g].data_ptr(), wss[g].data_ptr(), s)
+            comms[g].wait(s)
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=one, args=(g,)) for g in range(ng)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=60)
+    assert not errs, errs
+    want = [d.copy() for d in data]
+    oracle.allreduce("mem", t.SWING, side, want, ng, acc == t.ACC_BF16)
+    for g in range(ng):
+        assert np.array_equal(bufs[g].cpu().numpy().view(np.uint16), want[g]), g
+    for c in comms:
+        c.close()

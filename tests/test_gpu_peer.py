@@ -116,7 +116,10 @@ def worker(rank, world, port, q):
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
                                                      ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
-                                                     ("hier_x2_tail_one_group", 0, 0, 1))):
+                                                     ("hier_x2_tail_one_group", 0, 0, 1),
+                                                     # the flag hand-offs (tune hier_handoff 1)
+                                                     ("hier_x2_flg", 0, 0, 0), ("hier_x2_tail_flg", 0, 0, 0),
+                                                     ("hier_x2_flg_one_group", 0, 0, 1))):
             if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
@@ -129,7 +132,7 @@ def worker(rank, world, port, q):
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
-                    with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail"))):
+                    with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
                     peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
@@ -138,7 +141,7 @@ def worker(rank, world, port, q):
                     peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
-                with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail"))):
+                with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
                 peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
@@ -525,14 +528,15 @@ def test_config3_config5_eight_processes():
 
 
 @pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 5), (327680, 0, 1), (256 * 5, 0, 2), (256 * 40, 5, 3),
-                                           (327680, 160, 4)])
+                                           (327680, 160, 4), (256 * 40, 1, 3), (327680, 64, 3)])
 def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
     """One GPU (W = 1), 64 local ranks: a sequence of buckets through the
     two-deep pipelined hierarchical step (k_hier_x2: launch i starts bucket i,
     sums bucket i-1's owned tiles and writes bucket i-2), buckets + 1 calls
     (1 bucket: the flush sums and writes it; 2: the flush writes both), every
-    bucket bit-exact vs the oracle; full and capped grids (up to 8 tiles per
-    workgroup), the sequence twice (both LL parities reused).  Protocol errors:
+    bucket bit-exact vs the oracle; full and capped grids (one workgroup with
+    40 tiles: five chunks of staged results), LL and flag hand-offs (tune
+    hier_handoff), the sequence repeated (both LL parities reused).  Protocol errors:
     another peer call or the one-deep pipeline while buckets are pending, a
     different bucket size mid-sequence, a flush with nothing pending."""
     sys.path.insert(0, ROOT)
@@ -553,8 +557,8 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(4):   # owned sums at the start (0, 1) / the end (2, 3) of a launch
-            with t.tuned(hier_x2_tail=rep // 2, hier_x_lag=rep % 2):
+        for rep in range(8):   # owned sums at the start / the end of a launch; LL / flag hand-offs
+            with t.tuned(hier_x2_tail=(rep // 2) % 2, hier_x_lag=rep % 2, hier_handoff=rep // 4):
                 bufs = [x.clone() for x in data]
                 for b in bufs:
                     peer.allreduce_pipelined2(b.data_ptr(), n, s)

@@ -2,7 +2,8 @@
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
 x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_oneshot,
 k_hier_ll, k_hier_pipe, k_hier_x and k_hier_x2 (buckets pipelined one / two
-deep, k_hier_x2 with its owned sums at the start or the end of a launch: K buckets in K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
+deep, k_hier_x2 with its owned sums at the start or the end of a launch, LL or
+flag hand-offs: K buckets in K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
 hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
 kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
 arms interleaved.   python tools/hier_step.py [steps] [rounds]   (HIER_CAP: grid cap)"""
@@ -27,7 +28,7 @@ peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
-res = {k: [] for k in list(arms) + ["hier_x", "hier_x2", "hier_x2_tail"]}
+res = {k: [] for k in list(arms) + ["hier_x", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]}
 host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
 SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -49,8 +50,10 @@ def pipelined(k, deep):   # k buckets in k + 1 calls: k_hier_x (each call finish
 
 
 for _ in range(rounds):
-    for name, deep in (("hier_x", False), ("hier_x2", True), ("hier_x2_tail", True)):
-        t.tune("hier_x2_tail", int(name == "hier_x2_tail"))
+    for name, deep in (("hier_x", False), ("hier_x2", True), ("hier_x2_tail", True), ("hier_x2_flg", True),
+                       ("hier_x2_tail_flg", True)):
+        t.tune("hier_x2_tail", int(name.startswith("hier_x2_tail")))
+        t.tune("hier_handoff", int(name.endswith("_flg")))   # k_hier_x2 hand-offs: LL words / data + flags
         pipelined(20, deep)
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
