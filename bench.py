@@ -941,17 +941,28 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     peer_box = [None]
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
+    pend_kind = [None]   # its transport (peer_hier_x / peer_hier_xf)
     pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
     pend3 = [False]   # rccl_x: a bucket is started and not finished (flush())
     pend4 = [None, 0]   # peer_mem_x: the started bucket and the partial slot it used (flush())
     mem_parts = [torch.empty(ELEMS, dtype=torch.int16, device=dev) for _ in range(2)]
     tail = [None]
+    handoff = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
     def x2_tail(on):   # the host-side switch between the two k_hier_x2 forms, read at launch
         if tail[0] != on:
             t.tune("hier_x2_tail", int(on))
             tail[0] = on
+
+    def set_handoff(flg):   # LL words / data + flags (k_hier_x, k_hier_x2; latched per sequence)
+        if handoff[0] != flg:
+            t.tune("hier_handoff", flg)
+            handoff[0] = flg
+
+    def x2_kind(kind):   # tail / hand-off form of a k_hier_x2 transport
+        x2_tail(kind in ("peer_hier_x2t", "peer_hier_x2tf"))
+        set_handoff(int(kind in ("peer_hier_x2f", "peer_hier_x2tf")))
 
     def flush():
         peer = peer_box[0]
@@ -962,10 +973,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             t.broadcast(pend4[0], ELEMS, ELEMS, RANKS, mem_parts[pend4[1]].data_ptr(), stream)
             pend4[0] = None
         if pend[0] is not None:
+            set_handoff(int(pend_kind[0] == "peer_hier_xf"))
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
         if pend2[0]:
-            x2_tail(pend2[0] == "peer_hier_x2t")
+            x2_kind(pend2[0])
             peer.allreduce_pipelined2(None, ELEMS, stream)
             pend2[0] = False
 
@@ -996,16 +1008,17 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce(out.data_ptr(), ELEMS, stream)   # the partial: mem_2D across the GPUs
             pend4[0], pend4[1] = b.data_ptr(), slot
             return
-        if kind == "peer_hier_x":   # buckets pipelined: this call finishes the previous one
-            if pend2[0] or pend3[0] or pend4[0] is not None:
+        if kind in ("peer_hier_x", "peer_hier_xf"):   # buckets pipelined: this call finishes the previous one
+            if pend2[0] or pend3[0] or pend4[0] is not None or (pend[0] is not None and pend_kind[0] != kind):
                 flush()
+            set_handoff(int(kind == "peer_hier_xf"))
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
-            pend[0] = b.data_ptr()
+            pend[0], pend_kind[0] = b.data_ptr(), kind
             return
-        if kind in ("peer_hier_x2", "peer_hier_x2t"):   # two deep: this call writes the bucket started two calls ago
+        if kind in X2_KINDS:   # two deep: this call writes the bucket started two calls ago
             if pend[0] is not None or pend3[0] or pend4[0] is not None or (pend2[0] and pend2[0] != kind):
                 flush()
-            x2_tail(kind == "peer_hier_x2t")
+            x2_kind(kind)
             peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
             pend2[0] = kind
             return
@@ -1093,7 +1106,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
     if peer is not None:
         for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier", "peer_hier_ll",
-                                  "peer_hier_pipe", "peer_hier_x", "peer_hier_x2", "peer_hier_x2t")):
+                                  "peer_hier_pipe", "peer_hier_x", "peer_hier_xf", *X2_KINDS)):
             if check(kind, 9100 + 10 * i):
                 candidates.append(kind)
     if not candidates:
@@ -1238,7 +1251,10 @@ FALLBACK_DONE = threading.Event()
 
 # the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
 ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
-              "peer_hier_x": "k_hier_x", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>"}
+              "peer_hier_x": "k_hier_x", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
+              "peer_hier_x2f": "k_hier_x2<false, flags>", "peer_hier_x2tf": "k_hier_x2<true, flags>"}
+# the k_hier_x2 transports: owned sums at the start / the end (t) of a launch, LL / flag (f) hand-offs
+X2_KINDS = ("peer_hier_x2", "peer_hier_x2t", "peer_hier_x2f", "peer_hier_x2tf")
 
 
 def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> dict:
@@ -1282,6 +1298,12 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                             "timed region): launch i reads bucket i, writes bucket i-2's rows and at its end sums "
                             "bucket i-1's owned tiles, mem_2D one-shot across GPUs with LL pushes into peer-mapped "
                             "xGMI windows",
+           "peer_hier_xf": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with flag "
+                           "hand-offs: plain data pushes into peer-mapped xGMI windows, one flag per workgroup and peer",
+           "peer_hier_x2f": "ONE kernel per bucket, two buckets deep (as peer_hier_x2) with flag hand-offs: plain "
+                            "data pushes into peer-mapped xGMI windows, one flag per workgroup and peer",
+           "peer_hier_x2tf": "ONE kernel per bucket, two buckets deep, owned sums at the end of a launch (as "
+                             "peer_hier_x2t) with flag hand-offs: plain data pushes, one flag per workgroup and peer",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     v = extras.get("transport_verified", {}).get(transport, {})

@@ -160,12 +160,14 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
 int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                      size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                      void* stream);
+// k_hier_x / k_hier_x2 hand-off flag block per GPU: [2 parities][2 kinds][8 GPUs][512 workgroups] u32
+constexpr size_t kXFlagBytes = 4 * 2 * 2 * 8 * 512;
 // the hierarchical step across consecutive buckets (k_hier_x): finishes `prev` (may be null)
 // and starts `cur` (may be null) in one launch; llc / llp: every GPU's LL area of cur's /
 // prev's parity; ALLRED_ERR_UNSUPPORTED beyond kHierXMaxTiles tiles per workgroup
 int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
                   uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                  uint32_t* status, unsigned max_grid, void* stream);
+                  uint32_t* status, unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream);
 // the same step two buckets deep (k_hier_x2): starts `cur`, sums the owned tiles of the bucket
 // the previous launch started (llm non-null: its parity's LL areas), writes `old` (started two
 // launches ago; llo: its parity); the flush launch (cur null) also writes that middle bucket
@@ -173,7 +175,6 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
 // xfl: null = LL hand-offs; else every GPU's hand-off flag block (kXFlagBytes, the FLG form: data
 // in the LL slots without epochs, one flag per workgroup and peer; parities = the LL parities of
 // cur / mid / old in bits 0 / 1 / 2)
-constexpr size_t kXFlagBytes = 4 * 2 * 2 * 8 * 512;
 int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
                    uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,

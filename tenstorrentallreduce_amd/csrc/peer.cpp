@@ -68,6 +68,7 @@ struct allred_peer {
     uint32_t pipe_k = 0;            // that bucket's call number (epoch pipe_k + 1, LL parity pipe_k & 1)
     uint16_t* pipe_buf = nullptr;   // that bucket, and its size: the next call must finish exactly it
     uint64_t pipe_elems = 0;
+    bool pipe_flg = false;          // the sequence's hand-off form (tune hier_handoff at its first call)
     // allred_peer_allreduce_pipelined2: up to two started, unfinished buckets, older
     // first; with two, the older one's owned tiles are summed already
     int x2_n = 0;
@@ -253,8 +254,11 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
         llc[q] = p->peer_ll[q] + (kc & 1u) * 2 * p->ll_box_words;
         llp[q] = p->peer_ll[q] + (kp & 1u) * 2 * p->ll_box_words;
     }
+    if (!prev) p->pipe_flg = tune(Tune::hier_handoff) != 0;   // a sequence keeps its hand-off form
+    const uint32_t parities = (kc & 1u) | ((kp & 1u) << 1);
     st = launch_hier_x(cur, prev, n, order, cur ? llc : nullptr, prev ? llp : nullptr, p->nranks, p->rank, n,
-                       p->ll_box_words, kc + 1u, kp + 1u, p->status, p->max_groups, stream);
+                       p->ll_box_words, kc + 1u, kp + 1u, p->status, p->max_groups,
+                       p->pipe_flg ? p->peer_xfl : nullptr, parities, stream);
     if (st != ALLRED_OK) return st;
     if (cur) {
         p->pipe_k = kc;

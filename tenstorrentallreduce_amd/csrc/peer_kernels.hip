@@ -863,171 +863,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
     }
 }
 
-// ---- hierarchical step across consecutive buckets ----------------------------
-// k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
-// hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
-// (cur 0, -), (cur 1, prev 0), ..., (-, prev K-1)).  Within one bucket the
-// read phase (tree -> partial) must finish on every GPU before its write phase
-// (result -> 64 rank rows) can start, so k_hier_ll reads only, then writes only
-// (17.6 us at W = 1 vs 14.1 for the fused one-GPU pass).  Across buckets there
-// is no such dependency: this launch streams cur's tiles in (LDS-DMA, two
-// tiles ahead, tree, partial pushed to the tile's owner) while writing prev's
-// tiles out, interleaved op by op as in k_tree_lds_lag.  Order in a launch:
-//   L(cur 0), L(cur 1) issued (HBM busy from the start), then prev's results
-//            of this workgroup's tiles polled into LDS (the owners pushed them
-//            at the end of the previous launch)
-//   loop j:  A(cur j) [tree, partial -> owner] | S(prev j) stores interleaved
-//            with L(cur j+2)
-//   R(cur)   the tiles of cur this GPU owns: the W partials (pushed during
-//            this launch's loops) polled, summed (fp32, owner first, one
-//            rounding), the result pushed to every GPU's box
-// Any number of tiles per workgroup: prev's results are staged in LDS chunks of
-// kHierXChunk tiles (lanes (j, c) of the whole workgroup serve tile j of a
-// chunk), two chunks resident — chunk k + 1 is polled when the row stores of
-// chunk k begin, into the slot chunk k - 1 left — and R(cur) runs chunk by
-// chunk.  Every poll waits for work that waits on nothing of the poller (the
-// results: the owners' previous launches; R(cur): every GPU's loop of this
-// launch, which polls only results of the previous launch), and the grid is
-// resident, so every wait is satisfied.
-constexpr int kHierXChunk = 8;
-
-// LAG (tune hier_x_lag): prev's / old's tile rows stored in the iteration of cur's tile j - LAG
-// (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order)
-template <int LAG>
-__global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
-                                                   uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
-                                                   LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
-                                                   uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                                                   uint32_t* status) {
-    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res[2][kHierXChunk][TV];   // two chunks of prev's results
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane % TV, q = lane / TV;
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
-    const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
-    const uint64_t G = gridDim.x;
-    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
-    auto issue = [&](uint64_t t, int b) {
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
-                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
-    };
-    uint32_t ob = 0;
-    if (w == 0) ob = order_byte_load(order, lane);
-    if (cur && mine > 0) issue(tile_of(0), 0);
-    if (cur && mine > 1) issue(tile_of(1), 1);
-    if (w == 0) {   // the order byte only (the tiles' loads stay in flight)
-        wait_any((cur && mine > 0 ? OPS : 0) + (cur && mine > 1 ? OPS : 0));
-        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
-        ord_lds[lane] = (uint8_t)ob;
-    }
-    // ---- prev's results of this workgroup's tiles -> LDS: lane (jr, c) (32 jr + c)
-    // serves tile jr of a chunk, column c.  The owners pushed them at the end of the
-    // previous launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep
-    // HBM busy.  Chunks 0 and 1 now, chunk k + 1 when chunk k's row stores begin.
-    const int jr = threadIdx.x / TV;
-    auto poll_prev = [&](int ch) {
-        const int j = ch * kHierXChunk + jr;
-        if (j >= mine) return;
-        const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * 128 + c;
-        uint64_t wd[4];
-        ll_load(at, wd);
-        res[ch & 1][jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
-    };
-    if (prev) {
-        poll_prev(0);
-        if (mine > kHierXChunk) poll_prev(1);
-    }
-    lds_barrier();   // order bytes and results in LDS
-    for (int j = 0; j < mine; ++j) {
-        if (cur) {   // ---- A(cur j)
-            // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
-            // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
-            wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
-                     (j >= 1 ? 1 : 0));
-            lds_barrier();   // tile j is in LDS
-            const uint4* tile = buf[j & 1];
-            const uint8_t* ord = ord_lds + RPW * w + LPL * q;
-            uint4 x[LPL];
-#pragma unroll
-            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
-#pragma unroll
-            for (int s2 = 1; s2 < LPL; s2 *= 2)
-#pragma unroll
-                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
-            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
-            if (q == 0) part[j & 1][w * TV + c] = pw;
-            lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            if (q == 0) {   // the partial -> its owner's inbox, wave w writing word w
-                const uint64_t t = tile_of(j);
-                const int o = owner_of(t);
-                const uint4* pp = part[j & 1];
-                const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
-                ll_put_word(lc.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, ecur, w);
-            }
-        }
-        // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
-        const int sj = j - LAG;   // the tile whose rows this iteration stores
-        if (prev && sj >= kHierXChunk && sj % kHierXChunk == 0) {
-            // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
-            // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1
-            if (!cur) lds_barrier();
-            poll_prev(sj / kHierXChunk + 1);
-        }
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
-        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-        const bool st = prev && sj >= 0;
-        const uint4 rv = st ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) {
-            if (cur && j + 2 < mine)
-                lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
-                          bl + (uint32_t)(RPI * k * TV * 16));
-            if (st) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
-        }
-    }
-    if (LAG && prev && mine > 0) {   // prev's last tile
-        if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
-        const int sj = mine - 1;
-        const uint4 rv = res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c];
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
-    }
-    // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
-    // partial (during this launch's loop): W partials summed (fp32, owner first,
-    // one rounding), the result pushed to every GPU's box for the next launch.
-    for (int j0 = 0; cur && j0 < mine; j0 += kHierXChunk) {
-        if (j0 + jr >= mine) break;
-        const uint64_t t = tile_of(j0 + jr);
-        if (owner_of(t) == me) {
-            const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
-            uint64_t wr[kLLMaxGpus][4];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
-            uint4 y[kLLMaxGpus];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W)
-                    y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
-                                                     : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
-            const uint4 o = owner_sum(y, W, me);
-#pragma unroll
-            for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
-        }
-    }
-}
-
-// ---- hand-off flags (FLG forms of k_hier_x2, tune hier_handoff = 1) ----------
+// ---- hand-off flags (FLG forms of k_hier_x / k_hier_x2, tune hier_handoff = 1)
 // LL words carry 4 data bytes + a 4-byte epoch each: every hand-off moves twice
 // its data.  In the FLG form the data go as plain system-coherent 16-byte
 // stores (sc0 sc1, the LL stores' policy) into the first 512 bytes of the same
@@ -1077,6 +913,201 @@ __device__ __forceinline__ void xflag_wait(uint32_t* mine, uint32_t parity, int 
         }
     }
     lds_barrier();
+}
+
+// ---- hierarchical step across consecutive buckets ----------------------------
+// k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
+// hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
+// (cur 0, -), (cur 1, prev 0), ..., (-, prev K-1)).  Within one bucket the
+// read phase (tree -> partial) must finish on every GPU before its write phase
+// (result -> 64 rank rows) can start, so k_hier_ll reads only, then writes only
+// (17.6 us at W = 1 vs 14.1 for the fused one-GPU pass).  Across buckets there
+// is no such dependency: this launch streams cur's tiles in (LDS-DMA, two
+// tiles ahead, tree, partial pushed to the tile's owner) while writing prev's
+// tiles out, interleaved op by op as in k_tree_lds_lag.  Order in a launch:
+//   L(cur 0), L(cur 1) issued (HBM busy from the start), then prev's results
+//            of this workgroup's tiles polled into LDS (the owners pushed them
+//            at the end of the previous launch)
+//   loop j:  A(cur j) [tree, partial -> owner] | S(prev j) stores interleaved
+//            with L(cur j+2)
+//   R(cur)   the tiles of cur this GPU owns: the W partials (pushed during
+//            this launch's loops) polled, summed (fp32, owner first, one
+//            rounding), the result pushed to every GPU's box
+// Any number of tiles per workgroup: prev's results are staged in LDS chunks of
+// kHierXChunk tiles (lanes (j, c) of the whole workgroup serve tile j of a
+// chunk), two chunks resident — chunk k + 1 is polled when the row stores of
+// chunk k begin, into the slot chunk k - 1 left — and R(cur) runs chunk by
+// chunk.  Every poll waits for work that waits on nothing of the poller (the
+// results: the owners' previous launches; R(cur): every GPU's loop of this
+// launch, which polls only results of the previous launch), and the grid is
+// resident, so every wait is satisfied.
+constexpr int kHierXChunk = 8;
+
+// LAG (tune hier_x_lag): prev's / old's tile rows stored in the iteration of cur's tile j - LAG
+// (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order)
+template <int LAG, bool FLG>
+__global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
+                                                   uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
+                                                   LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
+                                                   uint64_t box_words, uint32_t ecur, uint32_t eprev,
+                                                   uint32_t* status, XFPtrs xf, uint32_t par) {
+    // FLG: par = the LL parities of cur / prev in bits 0 / 1
+    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
+    __shared__ __attribute__((aligned(16))) uint4 res[2][kHierXChunk][TV];   // two chunks of prev's results
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane % TV, q = lane / TV;
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
+    const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
+    const uint64_t G = gridDim.x;
+    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
+    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
+    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
+    auto issue = [&](uint64_t t, int b) {
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
+                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
+    };
+    uint32_t ob = 0;
+    if (w == 0) ob = order_byte_load(order, lane);
+    if (cur && mine > 0) issue(tile_of(0), 0);
+    if (cur && mine > 1) issue(tile_of(1), 1);
+    if (w == 0) {   // the order byte only (the tiles' loads stay in flight)
+        wait_any((cur && mine > 0 ? OPS : 0) + (cur && mine > 1 ? OPS : 0));
+        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
+        ord_lds[lane] = (uint8_t)ob;
+    }
+    // ---- prev's results of this workgroup's tiles -> LDS: lane (jr, c) (32 jr + c)
+    // serves tile jr of a chunk, column c.  The owners pushed them at the end of the
+    // previous launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep
+    // HBM busy.  Chunks 0 and 1 now, chunk k + 1 when chunk k's row stores begin.
+    const int jr = threadIdx.x / TV;
+    const uint32_t pc = par & 1u, pp = (par >> 1) & 1u;
+    // a hand-off slot's data in the FLG form: the first 512 bytes of its 1 KiB LL slot
+    auto dslot = [&](uint64_t* base, uint64_t slot) { return reinterpret_cast<uint4*>(base + slot * 128) + c; };
+    auto poll_prev = [&](int ch) {
+        const int j = ch * kHierXChunk + jr;
+        if (j >= mine) return;
+        if constexpr (FLG) {   // every owner's flag was waited for
+            res[ch & 1][jr][c] = ld_sys16(dslot(lpv.ll[me] + box_words, tile_of(j)));
+            return;
+        }
+        const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * 128 + c;
+        uint64_t wd[4];
+        ll_load(at, wd);
+        res[ch & 1][jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+    };
+    if (prev) {
+        if constexpr (FLG) xflag_wait(xf.f[me], pp, 1, W, eprev, status);   // raised at the end of the last launch
+        poll_prev(0);
+        if (mine > kHierXChunk) poll_prev(1);
+    }
+    lds_barrier();   // order bytes and results in LDS
+    for (int j = 0; j < mine; ++j) {
+        if (cur) {   // ---- A(cur j)
+            // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
+            // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
+            wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
+                     (j >= 1 ? 1 : 0));
+            lds_barrier();   // tile j is in LDS
+            const uint4* tile = buf[j & 1];
+            const uint8_t* ord = ord_lds + RPW * w + LPL * q;
+            uint4 x[LPL];
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
+#pragma unroll
+            for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
+            if (q == 0) part[j & 1][w * TV + c] = pw;
+            lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
+            // the partial -> its owner's inbox: LL, wave w writing word w of every column;
+            // FLG, wave w writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
+            if (q == 0 && (!FLG || (c >> 3) == w)) {
+                const uint64_t t = tile_of(j);
+                const int o = owner_of(t);
+                const uint4* pt = part[j & 1];
+                const uint4 pr = add8(add8(pt[0 * TV + c], pt[1 * TV + c]), add8(pt[2 * TV + c], pt[3 * TV + c]));
+                const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
+                if constexpr (FLG) st_sys16(dslot(lc.ll[o], slot), pr);
+                else ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
+            }
+        }
+        // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
+        const int sj = j - LAG;   // the tile whose rows this iteration stores
+        if (prev && sj >= kHierXChunk && sj % kHierXChunk == 0) {
+            // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
+            // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1
+            if (!cur) lds_barrier();
+            poll_prev(sj / kHierXChunk + 1);
+        }
+        const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
+        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
+        const bool st = prev && sj >= 0;
+        const uint4 rv = st ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < OPS; ++k) {
+            if (cur && j + 2 < mine)
+                lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
+                          bl + (uint32_t)(RPI * k * TV * 16));
+            if (st) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
+        }
+    }
+    if (LAG && prev && mine > 0) {   // prev's last tile
+        if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
+        const int sj = mine - 1;
+        const uint4 rv = res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c];
+#pragma unroll
+        for (int k = 0; k < OPS; ++k)
+            st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
+    }
+    // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
+    // partial (during this launch's loop): W partials summed (fp32, owner first,
+    // one rounding), the result pushed to every GPU's box for the next launch.
+    // FLG: this workgroup's partials are out (flag to every owner), then every
+    // GPU's partials of this workgroup's tiles are in (W flags)
+    if constexpr (FLG)
+        if (cur) {
+            xflag_raise(xf, pc, 0, me, W, ecur);
+            xflag_wait(xf.f[me], pc, 0, W, ecur, status);
+        }
+    for (int j0 = 0; cur && j0 < mine; j0 += kHierXChunk) {
+        if (j0 + jr >= mine) break;
+        const uint64_t t = tile_of(j0 + jr);
+        if (owner_of(t) == me) {
+            const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
+            uint4 y[kLLMaxGpus];
+            if constexpr (FLG) {
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) y[src] = ld_sys16(dslot(lc.ll[me], lr * W + src));
+            } else {
+                uint64_t wr[kLLMaxGpus][4];
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W)
+                        y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
+                                                         : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
+            }
+            const uint4 o = owner_sum(y, W, me);
+#pragma unroll
+            for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                if (dst < W) {
+                    if constexpr (FLG) st_sys16(dslot(lc.ll[dst] + box_words, t), o);
+                    else ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
+                }
+        }
+    }
+    if constexpr (FLG)   // this workgroup's results are out: every GPU told (read by its next launch)
+        if (cur) xflag_raise(xf, pc, 1, me, W, ecur);
 }
 
 // ---- hierarchical step, two-deep bucket pipeline ----------------------------
@@ -1565,7 +1596,7 @@ int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uin
 
 int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
                   uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                  uint32_t* status, unsigned max_grid, void* stream) {
+                  uint32_t* status, unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
         (!cur && !prev) || (cur && !aligned16(cur)) || (prev && !aligned16(prev)))
@@ -1578,10 +1609,14 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
         lc.ll[q] = llc ? llc[q] : nullptr;
         lp.ll[q] = llp ? llp[q] : nullptr;
     }
-    auto* kern = tune(Tune::hier_x_lag) ? k_hier_x<1> : k_hier_x<0>;
+    XFPtrs xf{};
+    for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
+    if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
+    const bool lag = tune(Tune::hier_x_lag) != 0;
+    auto* kern = xfl ? (lag ? k_hier_x<1, true> : k_hier_x<0, true>) : (lag ? k_hier_x<1, false> : k_hier_x<0, false>);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, eprev, status);
+                       box_words, ecur, eprev, status, xf, parities);
     return peer_last_error();
 }
 

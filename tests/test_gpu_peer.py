@@ -119,7 +119,8 @@ def worker(rank, world, port, q):
                                                      ("hier_x2_tail_one_group", 0, 0, 1),
                                                      # the flag hand-offs (tune hier_handoff 1)
                                                      ("hier_x2_flg", 0, 0, 0), ("hier_x2_tail_flg", 0, 0, 0),
-                                                     ("hier_x2_flg_one_group", 0, 0, 1))):
+                                                     ("hier_x2_flg_one_group", 0, 0, 1), ("hier_x_flg", 0, 0, 0),
+                                                     ("hier_x_flg_one_group", 0, 0, 1))):
             if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
@@ -135,8 +136,9 @@ def worker(rank, world, port, q):
                     with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
-                    peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
-                                             torch.cuda.current_stream())
+                    with t.tuned(hier_handoff=int("flg" in mode)):
+                        peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
+                                                 torch.cuda.current_stream())
                 else:
                     peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
@@ -144,7 +146,8 @@ def worker(rank, world, port, q):
                 with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
-                peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
+                with t.tuned(hier_handoff=int("flg" in mode)):
+                    peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
             torch.cuda.synchronize()
             for rep, (data, buf, _) in enumerate(runs):
                 partials = []
@@ -374,13 +377,15 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
         peer.close()
 
 
-@pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 4), (256 * 5, 0, 3), (256 * 40, 5, 2), (327680, 160, 1)])
+@pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 4), (256 * 5, 0, 3), (256 * 40, 5, 2), (327680, 160, 1),
+                                           (256 * 40, 1, 3), (327680, 64, 2)])
 def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
     """One GPU (W = 1), 64 local ranks: a sequence of buckets through the
     pipelined hierarchical step (k_hier_x: each launch finishes the previous
     bucket while it reads the next), buckets + 1 calls, every bucket bit-exact
     vs the oracle (tree of local rank 0, the mem_2D sum of one partial, rows
-    overwritten with it); full and capped grids (up to 8 tiles per workgroup).
+    overwritten with it); full and capped grids (one workgroup with 40 tiles:
+    five chunks of staged results); LL and flag hand-offs (tune hier_handoff).
     Protocol errors: a prev that is not the pending bucket, another peer call
     while a bucket is pending, finishing with nothing pending."""
     sys.path.insert(0, ROOT)
@@ -401,10 +406,10 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(4):   # row stores with the tree's tile / one behind; reruns reuse both LL parities
+        for rep in range(8):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL parities
             bufs = [x.clone() for x in data]
             prev = None
-            with t.tuned(hier_x_lag=rep % 2):
+            with t.tuned(hier_x_lag=rep % 2, hier_handoff=rep // 4):
                 for b in bufs:
                     peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
                     prev = b.data_ptr()

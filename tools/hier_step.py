@@ -28,7 +28,7 @@ peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
-res = {k: [] for k in list(arms) + ["hier_x", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]}
+res = {k: [] for k in list(arms) + ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]}
 host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
 SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,8 +50,8 @@ def pipelined(k, deep):   # k buckets in k + 1 calls: k_hier_x (each call finish
 
 
 for _ in range(rounds):
-    for name, deep in (("hier_x", False), ("hier_x2", True), ("hier_x2_tail", True), ("hier_x2_flg", True),
-                       ("hier_x2_tail_flg", True)):
+    for name, deep in (("hier_x", False), ("hier_x_flg", False), ("hier_x2", True), ("hier_x2_tail", True),
+                       ("hier_x2_flg", True), ("hier_x2_tail_flg", True)):
         t.tune("hier_x2_tail", int(name.startswith("hier_x2_tail")))
         t.tune("hier_handoff", int(name.endswith("_flg")))   # k_hier_x2 hand-offs: LL words / data + flags
         pipelined(20, deep)
