@@ -807,14 +807,19 @@ def choose_transport(quick: dict, verify: dict):
     return min(ok, key=lambda k: quick[k]) if ok else None
 
 
-def cli_config3(world: int) -> dict:
+def cli_config3(world: int, share: bool = False) -> dict:
     """BASELINE config 3 through the reference's own program surface on every GPU
     of this node: bin/allred_BO_2D 0 1 4 13 40 32 0 1 with ALLRED_NODES=8 (the 4x2
     grid) and ALLRED_GPUS = the GPUs this process sees (one device thread per GPU,
-    RCCL between them), every GPU's ranks checked with validate_result_vector."""
-    gpus = min(world, torch.cuda.device_count())
+    RCCL between them), every GPU's ranks checked with validate_result_vector.
+    share (--share-gpu rehearsal): ALLRED_GPUS = world groups on the one GPU over
+    the in-process peer windows (ALLRED_TRANSPORT=peer, ALLRED_SHARE_GPU=1), the
+    same G-thread orchestration with the exchange the hardware allows."""
+    gpus = world if share else min(world, torch.cuda.device_count())
     env = {"ALLRED_NODES": "8", "ALLRED_GPUS": str(gpus), "ALLRED_REPORT": "1", "ALLRED_CHECK_ALL": "1",
            "ALLRED_STRICT": "1"}
+    if share:
+        env.update({"ALLRED_TRANSPORT": "peer", "ALLRED_SHARE_GPU": "1", "GPU_MAX_HW_QUEUES": "16"})
     argv = [0, 1, 4, 13, 40, 32, 0, 1]
     p = t.run_cli("allred_BO_2D", argv, env=env, timeout=180)
     rep = {}
@@ -1224,7 +1229,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     # across this node's GPUs (config 3), then the CPU baseline of configs 3-5
     if rank == 0 and args.extras:
         try:
-            extras["cli_config3"] = cli_config3(world)
+            extras["cli_config3"] = cli_config3(world, share=args.share_gpu)
         except Exception as e:  # reported, never silently dropped
             extras["cli_config3"] = {"error": repr(e), "verified": False}
     cpu = None
