@@ -1364,6 +1364,116 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     for (int j = 0; j < mine; ++j) body(j);
 }
 
+// k_steps_reg2<P, MINW>: the BO schedule form of k_steps_reg<P, true, MINW, true>
+// with TWO strips per wave body (tune steps_ilp 2): strips j and j+1 of the
+// wave go through step 0, the step chain and the stores together, their LDS
+// phases interleaved op by op, so the chain of one (ten dependent LDS
+// read-add-write phases, ~2.4 us) hides the other's latency instead of adding
+// to it; the next pair's loads go out right after the pair's step 0.  Same
+// program, same bits; 8 KiB of pair rows per wave (three workgroups per CU at
+// 64 ranks).  No device stamps (the profiled form is k_steps_reg).
+template <int P, int MINW>
+__global__ __launch_bounds__(256, MINW) void k_steps_reg2(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                          const uint8_t* __restrict__ tab,
+                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
+                                                          uint64_t slices, uint64_t units) {
+    constexpr int NW = 4, TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
+    constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
+    constexpr int NPH = 2 * S - 2;
+    constexpr int MPH = (P / 4 * CW + 63) / 64;
+    __shared__ __attribute__((aligned(16))) uint8_t tabs[P][kBoPipeTab];
+    __shared__ __attribute__((aligned(16))) uint4 work[NW][2][H * CW];   // per wave: two strips' pair rows
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cl = lane % CW, rl = lane / CW;
+    auto cnt_of = [](int ph) {
+        const int k = ph < S ? ph : 2 * S - 1 - ph;
+        return P >> (k + 1);
+    };
+    auto off_of = [&](int ph) {
+        int o = 2 * H;
+        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
+        return o;
+    };
+    uint32_t pra[IPW], prb[IPW];
+    for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
+        reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
+#pragma unroll
+    for (int t = 0; t < IPW; ++t) {
+        const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;
+        pra[t] = pairs[2 * u];
+        prb[t] = pairs[2 * u + 1];
+    }
+    __syncthreads();   // the programs in LDS (the only barrier)
+    const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
+    const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
+    auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
+    auto col0 = [&](uint64_t s) {
+        const uint64_t u = s / Q;
+        return (u / slices) * bv + (u % slices) * TV + (s % Q) * CW;
+    };
+    auto grow = [&](uint32_t r) { return reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride); };
+    uint4 A[2][IPW], B[2][IPW];
+    auto load = [&](int j, int il) {
+        const uint64_t c0 = col0(strip_of(j)) + cl;
+#pragma unroll
+        for (int t = 0; t < IPW; ++t)
+            if (lane + 64 * t < H * CW) {
+                A[il][t] = ld_nt(grow(pra[t]) + c0);
+                B[il][t] = ld_nt(grow(prb[t]) + c0);
+            }
+    };
+    if (mine > 0) load(0, 0);
+    if (mine > 1) load(1, 1);
+    for (int j = 0; j < mine; j += 2) {
+        const int n2 = mine - j >= 2 ? 2 : 1;   // wave-uniform
+        // the two strips' programs (their blocks' tables); with two chains interleaved a
+        // phase's table read no longer stalls its chain alone, so it is read in the phase
+        const uint8_t* tb[2];
+#pragma unroll
+        for (int il = 0; il < 2; ++il) tb[il] = tabs[(strip_of(j + (il < n2 ? il : 0)) / Q) / slices];
+#pragma unroll
+        for (int il = 0; il < 2; ++il) {   // step 0 from registers into the pair rows
+            if (il >= n2) break;
+            uint4* tile = work[w][il];
+#pragma unroll
+            for (int t = 0; t < IPW; ++t)
+                if (lane + 64 * t < H * CW) {
+                    const uint32_t e = tb[il][(lane + 64 * t) / CW];   // row | 0x80: the higher rank holds
+                    tile[(e & 127) * CW + cl] = (e & 128) ? add8(B[il][t], A[il][t]) : add8(A[il][t], B[il][t]);
+                }
+        }
+        if (j + 2 < mine) load(j + 2, 0);   // the next pair's loads, behind this pair's chains and stores
+        if (j + 3 < mine) load(j + 3, 1);
+#pragma unroll
+        for (int ph = 1; ph <= NPH; ++ph) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c), the two strips interleaved
+            const bool rs = ph < S;
+#pragma unroll
+            for (int m = 0; m < MPH; ++m)
+#pragma unroll
+                for (int il = 0; il < 2; ++il) {
+                    if (il >= n2) break;
+                    if (lane + 64 * m < cnt_of(ph) * CW) {
+                        uint4* tile = work[w][il];
+                        const uint32_t pr = reinterpret_cast<const uint16_t*>(tb[il])[off_of(ph) / 2 + (lane + 64 * m) / CW];
+                        const int a = (pr & 255) * CW + cl, cc = (pr >> 8) * CW + cl;
+                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
+                    }
+                }
+        }
+#pragma unroll
+        for (int il = 0; il < 2; ++il) {
+            if (il >= n2) break;
+            const uint64_t cs = col0(strip_of(j + il)) + cl;
+            const uint4* tile = work[w][il];
+#pragma unroll
+            for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
+                const uint32_t fin = tb[il][off_of(NPH + 1) + RPO * k + rl];
+                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs, tile[fin * CW + cl]);
+            }
+        }
+    }
+}
+
 // One launch per step (allred_tune_set("steps_form", 1), the round-1 form, A/B):
 // one wave per (rank, block), U vectors' loads in flight per lane.
 //   RS: ranks[r][b] += ranks[p][b] for b in recv_mask_k(r)   (in place: the
@@ -1486,6 +1596,18 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
     const bool pf = tune(Tune::steps_prefetch) != 0;
+    if (bo && !stamps && tune(Tune::steps_ilp) == 2 && per_cu <= 3) {   // two strips per wave body (k_steps_reg2)
+#define TSA_SR2(PP) hipLaunchKernelGGL((k_steps_reg2<PP, 3>), grid, dim3(256), 0, st, ranks, stride, tab, pairs, bv, \
+                                       slices, units)
+        switch (total) {
+            case 8: TSA_SR2(8); return true;
+            case 16: TSA_SR2(16); return true;
+            case 32: TSA_SR2(32); return true;
+            case 64: TSA_SR2(64); return true;
+            default: return false;
+        }
+#undef TSA_SR2
+    }
 #define TSA_SR(PP, BOV, MW) do { if (pf) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, true>), grid, dim3(256), 0, st, \
                                      ranks, stride, tab, pairs, bv, slices, units, stamps); \
                                  else hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, false>), grid, dim3(256), 0, st, \
