@@ -534,6 +534,9 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 step(be->mark(gr, 0));
                 step(be->put(gr, gr.buf, in, mine));
                 step(be->mark(gr, 1));
+                // fault injection (tests): GPU multi_fault - 1 fails its timed allreduce before any
+                // exchange, while its peers are inside theirs: every thread must still return
+                if (a->run_kernel && tune(Tune::multi_fault) == g + 1) step(ALLRED_ERR_TRANSPORT);
                 if (a->run_kernel) step(be->reduce(gr, gr.buf));
                 step(be->mark(gr, 2));
                 step(be->get(gr, h_out + (size_t)g * L * n, gr.buf, mine));

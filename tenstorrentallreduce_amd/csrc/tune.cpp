@@ -44,6 +44,7 @@ const Key kKeys[] = {
     {"steps_prefetch", 1, 0, 1},      // k_steps_reg: a strip's program words in registers before step 0
     {"hier_handoff", 0, 0, 1},        // k_hier_x / k_hier_x2 hand-offs: 0 LL words (data + epoch) | 1 data + one flag per workgroup
     {"steps_ilp", 1, 1, 2},           // BO schedule form: strips per wave body (2: k_steps_reg2, chains interleaved)
+    {"multi_fault", 0, 0, 64},        // fault injection (tests): GPU value - 1 of allred_run_multi fails its timed allreduce
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

@@ -80,3 +80,21 @@ def test_across_gpus_bit_exact_vs_oracle_composition(tmp_path, g, name, variant,
     want = expected(plan, data)
     bad = int((got != want).sum())
     assert bad == 0, f"{name} G={g}: {bad} elements differ"
+
+
+@pytest.mark.parametrize("g,bad", [(2, 2), (4, 1)])
+def test_failed_gpu_ends_every_thread_on_the_gpu(g, bad):
+    """One group fails its timed allreduce (tune multi_fault) while the other
+    groups' peer kernels wait for it: their waits are bounded (4 s of
+    s_memrealtime), every thread returns and the executable exits 1 with the
+    transport error instead of hanging."""
+    import time
+    env = _env(g, 8)
+    env["ALLRED_TUNE"] = f"multi_fault={bad}"
+    t0 = time.monotonic()
+    r = subprocess.run([os.path.join(t._lib.BIN_DIR, "allred_BO_2D"), "0", "1", "4", "13", "40", "32", "0", "1"],
+                       capture_output=True, text=True, env=env, timeout=120)
+    dt = time.monotonic() - t0
+    assert r.returncode == 1, (r.stdout, r.stderr)
+    assert "exchange callback failed" in r.stderr, r.stderr
+    assert dt < 60, dt

@@ -149,3 +149,23 @@ def test_host_twin_report_and_profile_log(monkeypatch, tmp_path):
     lines = log.read_text().splitlines()
     assert len(lines) == 2 + 2 * 8 and "ALL_RED_LOOP" in lines[2]
     assert np.array_equal(out[0], out[7])
+
+
+@pytest.mark.parametrize("g,bad", [(2, 1), (4, 3), (8, 8)])
+def test_host_twin_failed_gpu_ends_every_thread(monkeypatch, g, bad):
+    """One GPU's thread fails its timed allreduce (tune multi_fault) while the
+    others are inside their exchanges: they are cancelled (no waiting for the
+    exchange deadline) and the call returns that thread's error — the
+    orchestration never hangs on a dead peer."""
+    import time
+    _env(monkeypatch, None)
+    argv = ["x", "1", "1", "8", "13", "5", "32", "0", "1"]
+    with t.tuned(multi_fault=bad):
+        t0 = time.monotonic()
+        with pytest.raises(t.AllredError) as e:
+            t.run_multi(argv, t.BO, gpus=g, transport=t.TRANSPORT_HOST, timeout_ms=60000, outputs=False)
+        dt = time.monotonic() - t0
+    assert e.value.status == t._lib.ERR_TRANSPORT
+    assert dt < 20, dt   # cancelled, not the 60 s exchange deadline
+    rep, out = t.run_multi(argv, t.BO, gpus=g, transport=t.TRANSPORT_HOST)   # and the next run is fine
+    assert rep.mismatches == 0
