@@ -123,7 +123,24 @@ def test_tune_entry_point():
         assert t.tune("steps_groups") == 4
     with pytest.raises(t.AllredError):
         t.tune("steps_groups", 6)
+    for v in (1, 2):   # documented values are 0 (auto), 3, 4, 5 only
+        with pytest.raises(t.AllredError):
+            t.tune("steps_groups", v)
     assert t.tune("steps_groups") == 0
+    # round-4 keys: defaults are the product forms / no fault injection
+    assert (t.tune("steps_prefetch"), t.tune("steps_ilp"), t.tune("hier_handoff")) == (1, 1, 0)
+    assert (t.tune("rccl_fault"), t.tune("multi_fault")) == (0, 0)
+    for key, bad in (("steps_ilp", 3), ("hier_handoff", 2), ("rccl_fault", 8)):
+        with pytest.raises(t.AllredError):
+            t.tune(key, bad)
+
+
+def test_mem_program_stats_one_rank_has_no_launch():
+    """mem_2D over RCCL on a 1-rank grid: no exchange, so no sum kernel either."""
+    st = t.dist_program_stats(t.dist_desc(t.SWING, t.MEM, 1, 1, 64), 0)
+    assert (st["steps"], st["add_launches"]) == (0, 0)
+    st = t.dist_program_stats(t.dist_desc(t.SWING, t.MEM, 4, 8, 8 * 8 * 4), 3)
+    assert (st["steps"], st["add_launches"]) == (2, 1)
 
 
 def test_tune_env_is_read_at_load():
