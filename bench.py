@@ -696,7 +696,7 @@ def best_arms(out: dict) -> dict:
         if not isinstance(v, dict) or v.get("verified") is not True or "ms" not in v or v.get("peer_timeout"):
             continue
         cfg = key
-        for pre in ("peer_sched_", "peer_oneshot_", "peer_"):
+        for pre in ("peer_sched_", "peer_oneshot_", "peer_push_", "peer_"):
             if cfg.startswith(pre):
                 cfg = cfg[len(pre):]
                 break
@@ -752,6 +752,12 @@ def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo,
                     out[f"peer_g{groups}_" + name]["sched_groups"] = groups
                 finally:
                     peer.set_max_groups(0 if crossed else cap)
+            # the same program with every exchange pushed by the sender (k_peer_sched_push)
+            peer.set_sched_push(1)
+            try:
+                timed("peer_push_" + name, peer_fn, variant == t.LO, status)
+            finally:
+                peer.set_sched_push(0)
         if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
             peer.set_lo_ll_max(0)
             try:

@@ -496,7 +496,7 @@ int allred_run_multi(const allred_args* args, const allred_multi_opts* opts, int
  * (allred_mem_2D.cpp:4-165) with every GPU's window IPC-mapped into every
  * peer (one process per GPU).  Result semantics = allred_mem_2D: block b is
  * owner b's copy + every other rank's copy in rank order, fp32, one rounding.
- *   create -> handle (192 bytes, exchange with every rank) -> connect(all
+ *   create -> handle (256 bytes, exchange with every rank) -> connect(all
  *   handles in rank order) -> allreduce ... -> destroy.
  * Barriers spin with a bound; allred_peer_status() reports bit 0 = timeout,
  * and the WIN/FLAGS_CACHED bits when uncached (fine-grained) device memory
@@ -505,7 +505,7 @@ int allred_run_multi(const allred_args* args, const allred_multi_opts* opts, int
  * (allred_peer_status after the stream, or allred_peer_check) before using
  * results; the first timeout makes every later wait of that launch give up.
  * ==================================================================== */
-#define ALLRED_PEER_HANDLE_BYTES 192
+#define ALLRED_PEER_HANDLE_BYTES 256
 /* largest IPC-exported window: a peer's hipIpcOpenMemHandle of a ~2 GiB
  * allocation never returned on the MI355X boxes (profiles/r01_peer_open_probe_2gib_hang.txt),
  * so allred_peer_create rejects max_elems * 2 > 1 GiB (ALLRED_ERR_ARG) */
@@ -596,6 +596,15 @@ int allred_peer_set_lo_ll_max(allred_peer* peer, uint64_t bytes);
  * remote reads), larger ones as before.  Same result bits.  Every rank must
  * use the same setting. */
 int allred_peer_set_mem_ll_max(allred_peer* peer, uint64_t bytes);
+/* allred_peer_dist_allreduce runs BO buckets of at least `min_bytes` (default
+ * 0 = never) in the PUSH form (k_peer_sched_push): each exchange is written by
+ * the sender into the receiver's staging window (reduce-scatter) or main window
+ * (all-gather) and announced with a flag, instead of read by the receiver
+ * over xGMI — posted writes, no read round trips.  Same program, same adds,
+ * same result bits.  Every rank must use the same setting.  Replaces the NoC
+ * writes of allred_BO_2D/kernels/dataflow_kernel.cpp:152-267 (the reference's
+ * sender also writes into the receiver's L1). */
+int allred_peer_set_sched_push(allred_peer* peer, uint64_t min_bytes);
 /* The allred_dist_allreduce program (same desc, same result bits: Swing /
  * RecDub BO or LO, link-spreading channels, hierarchical local ranks) with
  * RCCL replaced by direct reads of the partners' IPC-mapped windows: one

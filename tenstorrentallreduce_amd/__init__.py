@@ -487,6 +487,10 @@ class Peer:
         """mem_2D buckets up to nbytes take the LL-push form (same bits; 0 = never)."""
         check(lib.allred_peer_set_mem_ll_max(self._h, nbytes), "peer_set_mem_ll_max")
 
+    def set_sched_push(self, min_bytes: int) -> None:
+        """BO buckets of >= min_bytes in the push form of the scheduled program (0 = never)."""
+        check(lib.allred_peer_set_sched_push(self._h, min_bytes), "peer_set_sched_push")
+
     def set_max_groups(self, groups: int) -> None:
         """Grid cap of the hierarchical one-kernel forms (0 = one full grid per GPU);
         processes sharing a GPU need groups <= 512 / processes."""

@@ -189,12 +189,13 @@ SIGNATURES = [
     ("allred_peer_set_max_groups", C.c_int, [_P, C.c_uint32]),
     ("allred_peer_set_lo_ll_max", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_set_mem_ll_max", C.c_int, [_P, C.c_uint64]),
+    ("allred_peer_set_sched_push", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("allred_peer_check", C.c_int, [_P, _P]),
     ("allred_peer_destroy", C.c_int, [_P]),
 ]
-PEER_HANDLE_BYTES = 192
+PEER_HANDLE_BYTES = 256
 PEER_MAX_WINDOW_BYTES = 1 << 30   # allred_peer_create rejects larger windows (allred.h)
 PEER_TIMEOUT, PEER_WIN_CACHED, PEER_FLAGS_CACHED = 0x1, 0x100, 0x200   # allred_peer_status bits
 

@@ -120,7 +120,9 @@ constexpr uint32_t kPeerFusedFlagOff = 64;
 constexpr uint32_t kPeerFusedMaxGroups = 128;
 constexpr uint32_t kPeerSchedFlagOff = kPeerFusedFlagOff + 2 * kPeerFusedMaxGroups * 64;
 constexpr uint32_t kPeerSchedMaxGroups = 256;
-constexpr size_t kPeerFlagBytes = 4 * ((size_t)kPeerSchedFlagOff + kPeerSchedMaxGroups * 64);
+// the push form's data-arrived slots [kPeerSchedMaxGroups][64 ranks] behind the progress slots
+constexpr uint32_t kPeerSchedPushOff = kPeerSchedFlagOff + kPeerSchedMaxGroups * 64;
+constexpr size_t kPeerFlagBytes = 4 * ((size_t)kPeerSchedPushOff + kPeerSchedMaxGroups * 64);
 
 // One rank's BO / LO program over peer-mapped windows (dist.cpp builds it from
 // the same schedule + link-spreading channels as the RCCL program).
@@ -145,6 +147,12 @@ int launch_peer_barrier(uint32_t* const* flags, int nranks, int me, uint32_t epo
 int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uint16_t* bucket, const PeerProg& prog,
                       uint64_t half_vec, uint32_t base_epoch, uint32_t* status, unsigned max_groups,
                       void* stream);
+// the same BO program with every exchange a PUSH (k_peer_sched_push): the sender writes its blocks
+// into the receiver's staging window (reduce-scatter) or main window (all-gather); stages[q] = GPU
+// q's staging window (max_elems), same offsets as the windows
+int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint32_t* const* flags, int me,
+                           uint16_t* bucket, const PeerProg& prog, uint32_t base_epoch, uint32_t* status,
+                           unsigned max_groups, void* stream);
 // hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast.
 // wins[q] = GPU q's window for this parity ([partial n][result n]); hflags[q]: [tiles][nranks + 1]
 int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,

@@ -37,6 +37,7 @@ struct allred_peer {
     // allocation stays <= 1 GiB + 256 B, since opening a ~2 GiB one in a peer
     // process hung on the MI355X boxes (tools/peer_open_probe.py)
     uint16_t* win[2] = {};
+    uint16_t* stage = nullptr;      // staging window of the push form (k_peer_sched_push), max_elems
     uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp, then hfl and LL
     uint32_t* status = nullptr;     // device status word
     bool flags_uncached = false, win_uncached = false;
@@ -44,6 +45,8 @@ struct allred_peer {
     size_t hfl_bytes = 0;
     uint32_t* peer_hfl[ALLRED_MAX_NODES] = {};
     uint16_t* peer_win[ALLRED_MAX_NODES][2] = {};
+    uint16_t* peer_stage[ALLRED_MAX_NODES] = {};
+    uint64_t sched_push_min = 0;    // BO buckets of at least this many bytes take the push form (0: never)
     uint32_t* peer_flags[ALLRED_MAX_NODES] = {};
     bool opened[ALLRED_MAX_NODES] = {};
     uint32_t calls = 0;
@@ -110,6 +113,7 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     const size_t win_bytes = p->max_elems * 2;
     auto release = [p]() {
         for (uint16_t* w : p->win) (void)hipFree(w);
+        (void)hipFree(p->stage);
         (void)hipFree(p->flags);
         (void)hipFree(p->status);
         delete p;
@@ -121,6 +125,10 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
             p->win_uncached = false;
         }
     }
+    if (p->win_uncached && hipExtMallocWithFlags((void**)&p->stage, win_bytes, hipDeviceMallocUncached) != hipSuccess) {
+        p->stage = nullptr;
+        p->win_uncached = false;
+    }
     if (!p->win_uncached) {   // all cached or all uncached
         for (uint16_t*& w : p->win) {
             (void)hipFree(w);
@@ -129,6 +137,12 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
                 release();
                 return ALLRED_ERR_NOMEM;
             }
+        }
+        (void)hipFree(p->stage);
+        if (hipMalloc((void**)&p->stage, win_bytes) != hipSuccess) {
+            p->stage = nullptr;
+            release();
+            return ALLRED_ERR_NOMEM;
         }
     }
     if (hipExtMallocWithFlags((void**)&p->flags, flag_bytes, hipDeviceMallocUncached) == hipSuccess) {
@@ -149,14 +163,15 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
 
 int allred_peer_handle(allred_peer* p, uint8_t* out) {
     if (!p || !out) return ALLRED_ERR_ARG;
-    // [window parity 0][window parity 1][flags], 64 bytes each
-    static_assert(sizeof(hipIpcMemHandle_t) * 3 <= ALLRED_PEER_HANDLE_BYTES, "handle size");
-    hipIpcMemHandle_t h[3];
+    // [window parity 0][window parity 1][flags][staging window], 64 bytes each
+    static_assert(sizeof(hipIpcMemHandle_t) * 4 <= ALLRED_PEER_HANDLE_BYTES, "handle size");
+    hipIpcMemHandle_t h[4];
     if (hipIpcGetMemHandle(&h[0], p->win[0]) != hipSuccess) return ALLRED_ERR_HIP;
     if (hipIpcGetMemHandle(&h[1], p->win[1]) != hipSuccess) return ALLRED_ERR_HIP;
     if (hipIpcGetMemHandle(&h[2], p->flags) != hipSuccess) return ALLRED_ERR_HIP;
+    if (hipIpcGetMemHandle(&h[3], p->stage) != hipSuccess) return ALLRED_ERR_HIP;
     std::memset(out, 0, ALLRED_PEER_HANDLE_BYTES);
-    for (int i = 0; i < 3; ++i) std::memcpy(out + i * sizeof(hipIpcMemHandle_t), &h[i], sizeof(h[i]));
+    for (int i = 0; i < 4; ++i) std::memcpy(out + i * sizeof(hipIpcMemHandle_t), &h[i], sizeof(h[i]));
     return ALLRED_OK;
 }
 
@@ -169,9 +184,10 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
             p->peer_win[q][0] = p->win[0];
             p->peer_win[q][1] = p->win[1];
             p->peer_flags[q] = p->flags;
+            p->peer_stage[q] = p->stage;
         } else {
-            void* m[3] = {};
-            for (int i = 0; i < 3; ++i) {
+            void* m[4] = {};
+            for (int i = 0; i < 4; ++i) {
                 hipIpcMemHandle_t h;
                 std::memcpy(&h, all + (size_t)q * ALLRED_PEER_HANDLE_BYTES + i * sizeof(h), sizeof(h));
                 if (hipIpcOpenMemHandle(&m[i], h, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
@@ -182,6 +198,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
             p->peer_win[q][0] = static_cast<uint16_t*>(m[0]);
             p->peer_win[q][1] = static_cast<uint16_t*>(m[1]);
             p->peer_flags[q] = static_cast<uint32_t*>(m[2]);
+            p->peer_stage[q] = static_cast<uint16_t*>(m[3]);
             p->opened[q] = true;
         }
         uint8_t* f = reinterpret_cast<uint8_t*>(p->peer_flags[q]);
@@ -211,6 +228,7 @@ int allred_peer_connect_all(int nranks, allred_peer* const* peers) {
             p->peer_win[q][0] = o->win[0];
             p->peer_win[q][1] = o->win[1];
             p->peer_flags[q] = o->flags;
+            p->peer_stage[q] = o->stage;
             uint8_t* f = reinterpret_cast<uint8_t*>(o->flags);
             p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + o->hfl_off);
             p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + o->ll_off);
@@ -440,8 +458,12 @@ int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16
             st = launch_peer_barrier(p->peer_flags, p->nranks, p->rank, 2u * p->calls + 1u, p->status, stream);
             if (st != ALLRED_OK) return st;
         }
-        st = launch_peer_sched(wins, p->peer_flags, p->rank, bucket, prog, p->max_elems / 2 / 8, p->seq, p->status,
-                               p->max_groups, stream);
+        if (!prog.lo && p->sched_push_min && n * 2 >= p->sched_push_min)   // the push form: same program, same bits
+            st = launch_peer_sched_push(wins, p->peer_stage, p->peer_flags, p->rank, bucket, prog, p->seq, p->status,
+                                        p->max_groups, stream);
+        else
+            st = launch_peer_sched(wins, p->peer_flags, p->rank, bucket, prog, p->max_elems / 2 / 8, p->seq, p->status,
+                                   p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         p->seq += 2u * (uint32_t)prog.S + 2u;
         ++p->calls;
@@ -461,6 +483,12 @@ int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
     if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
+    return ALLRED_OK;
+}
+
+int allred_peer_set_sched_push(allred_peer* p, uint64_t min_bytes) {
+    if (!p) return ALLRED_ERR_ARG;
+    p->sched_push_min = min_bytes;
     return ALLRED_OK;
 }
 
@@ -506,8 +534,10 @@ int allred_peer_destroy(allred_peer* p) {
         (void)hipIpcCloseMemHandle(p->peer_win[q][0]);
         (void)hipIpcCloseMemHandle(p->peer_win[q][1]);
         (void)hipIpcCloseMemHandle(p->peer_flags[q]);
+        (void)hipIpcCloseMemHandle(p->peer_stage[q]);
     }
     for (uint16_t* w : p->win) (void)hipFree(w);
+    (void)hipFree(p->stage);
     (void)hipFree(p->flags);
     (void)hipFree(p->status);
     delete p;

@@ -324,6 +324,105 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
     }
 }
 
+// ---- scheduled form, push variant (BO) --------------------------------------
+// k_peer_sched's program with the data moved by the SENDER: remote writes are
+// posted (no read round trip over xGMI), so large buckets may stream faster.
+//   RS step k: wait until partner p finished step k-1 (its staging window free,
+//     progress slot as in the pull form); write my blocks send[k] into p's
+//     staging window; raise p's data slot; wait for p's data slot in mine; add
+//     my staging blocks recv[k] into my window (and, at the last step, bucket);
+//     progress k+1.
+//   AG step i: wait for p's progress; write my owned blocks recv[i] into p's
+//     MAIN window (p's blocks send_p[i] = my recv[i]: its stale partials there
+//     are read by nobody after its RS step i); raise p's data slot; wait for
+//     mine; copy my window's blocks send[i] into the bucket.
+// Same adds in the same order as the pull form: the same bits.
+struct PeerStage {
+    uint16_t* st[ALLRED_MAX_NODES];   // GPU q's staging window, as mapped here
+};
+
+__device__ inline void push_signal(const PeerPtrs& pp, int p, int me, uint32_t slot, uint32_t value) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's pushes have completed
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(pp.flags[p] + kPeerSchedPushOff + slot + me, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kBlock) void k_peer_sched_push(PeerPtrs pp, PeerStage ps, PeerProg pr, int me,
+                                                            uint16_t* __restrict__ bucket, uint32_t base,
+                                                            uint32_t* status) {
+    const int C = pr.C, S = pr.S, N = pr.N;
+    const int g = blockIdx.x, c = g % C, Gc = gridDim.x / C, j = g / C;
+    const uint32_t gs = (uint32_t)g * 64u;                 // this workgroup's slots (progress / pushed data)
+    const uint32_t slot = kPeerSchedFlagOff + gs;
+    uint4* bk = reinterpret_cast<uint4*>(bucket);
+    uint4* mine = reinterpret_cast<uint4*>(pp.win[me]);
+    const uint4* stage = reinterpret_cast<const uint4*>(ps.st[me]);
+    const uint64_t cb = pr.base[c];
+    const int tid = threadIdx.x;
+    const uint64_t blk = pr.len[c] / N;
+    const uint64_t chunk = (blk + Gc - 1) / Gc;
+    const uint64_t lo = (uint64_t)j * chunk, hi = lo + chunk < blk ? lo + chunk : blk;
+    // my sub-slice of every block in `mask`: src -> dst (kSchedU vectors in flight per thread)
+    auto move = [&](uint64_t mask, const uint4* src, uint4* dst) {
+        for (uint64_t m = mask; m; m &= m - 1) {
+            const int b = __builtin_ctzll(m);
+            const uint64_t end = cb + b * blk + hi;
+            for (uint64_t v = cb + b * blk + lo + tid; v < end; v += kSchedU * kBlock) {
+                uint4 y[kSchedU];
+#pragma unroll
+                for (int u = 0; u < kSchedU; ++u)
+                    if (v + u * kBlock < end) y[u] = ld_nt(src + v + u * kBlock);
+#pragma unroll
+                for (int u = 0; u < kSchedU; ++u)
+                    if (v + u * kBlock < end) st_nt(dst + v + u * kBlock, y[u]);
+            }
+        }
+    };
+    for (int b = 0; b < N; ++b)
+        for (uint64_t v = cb + b * blk + lo + tid; v < cb + b * blk + hi; v += kBlock) st_nt(mine + v, ld_nt(bk + v));
+    sched_signal(pp, pr, c, me, slot, base + 1);
+    for (int k = 0; k < S; ++k) {  // reduce-scatter
+        const int p = pr.peer[c][k];
+        sched_wait(pp, me, slot, p, -1, base + 1 + k, status);                 // p's staging is free
+        move(pr.send[c][k], mine, reinterpret_cast<uint4*>(ps.st[p]));         // my blocks -> p's staging
+        push_signal(pp, p, me, gs, base + 1 + k);
+        sched_wait(pp, me, kPeerSchedPushOff + gs, p, -1, base + 1 + k, status);   // p's blocks are in mine
+        const bool last = k == S - 1;
+        for (uint64_t m = pr.recv[c][k]; m; m &= m - 1) {
+            const int b = __builtin_ctzll(m);
+            const uint64_t end = cb + b * blk + hi;
+            for (uint64_t v = cb + b * blk + lo + tid; v < end; v += kSchedU * kBlock) {
+                uint4 x[kSchedU], y[kSchedU];
+#pragma unroll
+                for (int u = 0; u < kSchedU; ++u)
+                    if (v + u * kBlock < end) {
+                        x[u] = ld_nt(mine + v + u * kBlock);
+                        y[u] = ld_nt(stage + v + u * kBlock);
+                    }
+#pragma unroll
+                for (int u = 0; u < kSchedU; ++u)
+                    if (v + u * kBlock < end) {
+                        const uint4 o = add8(x[u], y[u]);
+                        st_nt(mine + v + u * kBlock, o);
+                        if (last) st_nt(bk + v + u * kBlock, o);
+                    }
+            }
+        }
+        sched_signal(pp, pr, c, me, slot, base + 2 + k);
+    }
+    for (int t = 0; t < S; ++t) {  // all-gather, steps in reverse
+        const int i = S - 1 - t, pos = S + t;
+        const int p = pr.peer[c][i];
+        sched_wait(pp, me, slot, p, -1, base + 1 + pos, status);               // p is past its RS step i
+        move(pr.recv[c][i], mine, reinterpret_cast<uint4*>(pp.win[p]));        // my owned blocks -> p's window
+        push_signal(pp, p, me, gs, base + 1 + pos);
+        sched_wait(pp, me, kPeerSchedPushOff + gs, p, -1, base + 1 + pos, status);
+        move(pr.send[c][i], mine, bk);                                          // p's blocks, now in mine -> bucket
+        if (t < S - 1) sched_signal(pp, pr, c, me, slot, base + 2 + pos);
+    }
+}
+
 // ---- hierarchical one-kernel form: 64 local ranks per GPU -------------------
 // The whole hierarchical step (local tree of the 64 virtual ranks -> mem_2D
 // across the W GPUs -> broadcast back to the 64 ranks) as ONE persistent
@@ -1510,6 +1609,31 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
     if (gc < 1) gc = 1;
     hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
                        bucket, half_vec, base_epoch, status);
+    return peer_last_error();
+}
+
+int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint32_t* const* flags, int me,
+                           uint16_t* bucket, const PeerProg& prog, uint32_t base_epoch, uint32_t* status,
+                           unsigned max_groups, void* stream) {
+    if (!aligned16(bucket) || prog.lo || prog.N > ALLRED_MAX_NODES || prog.C < 1 || prog.C > kPeerMaxChannels ||
+        prog.S > kPeerMaxSteps)
+        return ALLRED_ERR_ARG;
+    PeerPtrs pp{};
+    PeerStage ps{};
+    for (int q = 0; q < prog.N; ++q) {
+        pp.win[q] = wins[q];
+        pp.flags[q] = flags[q];
+        ps.st[q] = stages[q];
+    }
+    uint64_t per = 0;
+    for (int c = 0; c < prog.C; ++c) per = prog.len[c] / prog.N > per ? prog.len[c] / prog.N : per;
+    uint64_t gc = (per + kBlock - 1) / kBlock;
+    const uint64_t cap = max_groups && max_groups < kPeerSchedMaxGroups ? max_groups : kPeerSchedMaxGroups;
+    const uint64_t gmax = cap / prog.C > 0 ? cap / prog.C : 1;
+    if (gc > gmax) gc = gmax;
+    if (gc < 1) gc = 1;
+    hipLaunchKernelGGL(k_peer_sched_push, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, ps,
+                       prog, me, bucket, base_epoch, status);
     return peer_last_error();
 }
 

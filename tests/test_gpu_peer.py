@@ -199,8 +199,10 @@ def test_peer_one_shot_multi_process_one_gpu(world):
 def dist_worker(rank, world, port, q):
     """allred_peer_dist_allreduce: every case of the gloo-tested RCCL program
     (tests/test_dist_host.py: Swing / RecDub / 1D schedules, BO and LO, flat and
-    hierarchical, link-spreading channels) over the peer windows, bit-exact with
-    the oracle; each case twice back to back, a mem_2D call in between."""
+    hierarchical, link-spreading channels) over the peer windows — read by the
+    receiver (k_peer_sched), pushed by the sender (k_peer_sched_push, BO), LL
+    (k_peer_lo_ll, small LO) — bit-exact with the oracle; each case twice back
+    to back, a mem_2D call in between."""
     try:
         import torch.distributed as dist
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -217,10 +219,13 @@ def dist_worker(rank, world, port, q):
         peer.connect(handles)
         fails = []
         # LO buckets this small take the LL-push program by default (k_peer_lo_ll);
-        # the second pass forces the scheduled form (k_peer_sched) for every case
-        for ci, (variant, algo, local, chans, ll_max) in enumerate(
-                [c + (256 << 10,) for c in tdh.cases(world)] + [c + (0,) for c in tdh.cases(world)]):
+        # the second pass forces the scheduled form (k_peer_sched) for every case, the
+        # third its push form (k_peer_sched_push) for every BO case
+        for ci, (variant, algo, local, chans, ll_max, push) in enumerate(
+                [c + (256 << 10, 0) for c in tdh.cases(world)] + [c + (0, 0) for c in tdh.cases(world)] +
+                [c + (0, 1) for c in tdh.cases(world) if c[0] == "bo"]):
             peer.set_lo_ll_max(ll_max)
+            peer.set_sched_push(push)
             desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
                                local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
             ws = torch.empty(max(t.dist_workspace_bytes(desc), 16), dtype=torch.uint8, device="cuda:0")
@@ -235,7 +240,7 @@ def dist_worker(rank, world, port, q):
                 want = np.concatenate(tdh.expected(variant, algo, world, local, data, chans)[rank])
                 got = buf.cpu().numpy().view(np.uint16)
                 if not np.array_equal(got, want):
-                    fails.append((variant, algo, local, chans, ll_max, rep, int((got != want).sum())))
+                    fails.append((variant, algo, local, chans, ll_max, push, rep, int((got != want).sum())))
             # a mem_2D call (reads every window) between scheduled calls
             m = torch.zeros(n, dtype=torch.int16, device="cuda:0")
             peer.allreduce(m.data_ptr(), n, torch.cuda.current_stream())
