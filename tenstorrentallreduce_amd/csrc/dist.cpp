@@ -42,6 +42,7 @@ struct allred_comm {
     // past it (every later call then returns ALLRED_ERR_TRANSPORT)
     int timeout_ms = 0;             // 0 = default_timeout_ms()
     bool aborted = false;
+    uint64_t connected = 0;         // peers this communicator has exchanged with (RCCL set their connections up)
     const std::atomic<int>* cancel = nullptr;   // run_multi_gpu: another GPU's thread failed
     // allred_dist_allreduce_pipelined: the bucket started by the last call (its rows are
     // written by the next call or the flush) and its allreduced partial in the workspace
@@ -446,12 +447,17 @@ int settle(allred_comm* c, int timeout_ms, Fault f) {
     }
 }
 
-// after ncclGroupEnd on a non-blocking communicator
-int group_end(allred_comm* c, bool ok) {
+// after ncclGroupEnd on a non-blocking communicator.  peers: the group's partners
+// (bit mask): a group with a partner this communicator never exchanged with
+// sets the connection up (seconds on a busy node) and gets the init deadline
+int group_end(allred_comm* c, bool ok, uint64_t peers) {
     const ncclResult_t r = ncclGroupEnd();
     if (!ok || (r != ncclSuccess && r != ncclInProgress)) return ALLRED_ERR_RCCL;
-    if (r == ncclSuccess && !(tune(Tune::rccl_fault) & (int64_t)Fault::group)) return ALLRED_OK;
-    return settle(c, op_timeout_ms(c), Fault::group);
+    int st = ALLRED_OK;
+    if (r != ncclSuccess || (tune(Tune::rccl_fault) & (int64_t)Fault::group))
+        st = settle(c, (peers & ~c->connected) ? init_timeout_ms(c) : op_timeout_ms(c), Fault::group);
+    if (st == ALLRED_OK) c->connected |= peers;
+    return st;
 }
 
 }  // namespace
@@ -677,7 +683,9 @@ int allred_dist_allreduce(allred_comm* c, const allred_dist_desc* d, uint16_t* b
                 ok = ok && ncclSend(snd, blk * 2, ncclUint8, q, c->comm, hs) == ncclSuccess;
                 ok = ok && ncclRecv(rcv, blk * 2, ncclUint8, q, c->comm, hs) == ncclSuccess;
             }
-            if ((st = group_end(c, ok)) != ALLRED_OK) return st;
+            uint64_t peers = 0;
+            for (int k = 1; k < N; ++k) peers |= 1ull << (me ^ k);
+            if ((st = group_end(c, ok, peers)) != ALLRED_OK) return st;
             if (phase == 0) {
                 st = launch_rows_sum(staging, blk, blk, N, own, d->mem_accum == ALLRED_ACC_BF16, stream);
                 if (st != ALLRED_OK) return st;
@@ -787,7 +795,9 @@ int run_program(allred_comm* c, const allred_dist_desc* d, const allred_schedule
         // the group is always closed, also after a failed send / recv, so the
         // next call does not start inside a dangling group; a group that never
         // completes (a partner that never arrives) is aborted at the deadline
-        if ((st = group_end(c, ok)) != ALLRED_OK) return st;
+        uint64_t peers = 0;
+        for (const Exch& e : step.ex) peers |= 1ull << e.peer;
+        if ((st = group_end(c, ok, peers)) != ALLRED_OK) return st;
         for (size_t i = 0; i < step.add_off.size(); i += kMaxAddSegs) {   // one launch per step (<= 64 segments)
             const int ns = (int)std::min<size_t>(kMaxAddSegs, step.add_off.size() - i);
             st = launch_bf16_add_segs(bucket, staging, step.add_off.data() + i, step.add_len.data() + i, ns, stream);
