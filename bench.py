@@ -1041,8 +1041,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         else:
             if mode[0] != kind:
                 peer.set_oneshot_max(0 if kind == "peer_launches" else (4 << 20))
-                peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_pipe": 2}.get(kind, 0))
+                peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_llf": 1, "peer_hier_pipe": 2}.get(kind, 0))
                 mode[0] = kind
+            set_handoff(int(kind == "peer_hier_llf"))   # read at launch (the x / x2 kinds set it too)
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
     verify = {}
@@ -1117,7 +1118,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
     if peer is not None:
         for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier", "peer_hier_ll",
-                                  "peer_hier_pipe", "peer_hier_x", "peer_hier_xf", *X2_KINDS)):
+                                  "peer_hier_llf", "peer_hier_pipe", "peer_hier_x", "peer_hier_xf", *X2_KINDS)):
             if check(kind, 9100 + 10 * i):
                 candidates.append(kind)
     if not candidates:
@@ -1261,7 +1262,8 @@ HEADLINE_DONE = threading.Event()
 FALLBACK_DONE = threading.Event()
 
 # the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
-ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_pipe": "k_hier_pipe",
+ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_llf": "k_hier_ll<flags>",
+              "peer_hier_pipe": "k_hier_pipe",
               "peer_hier_x": "k_hier_x", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
               "peer_hier_x2f": "k_hier_x2<false, flags>", "peer_hier_x2tf": "k_hier_x2<true, flags>"}
 # the k_hier_x2 transports: owned sums at the start / the end (t) of a launch, LL / flag (f) hand-offs
@@ -1316,7 +1318,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
            "peer_hier_x2tf": "ONE kernel per bucket, two buckets deep, owned sums at the end of a launch (as "
                              "peer_hier_x2t) with flag hand-offs: plain data pushes, one flag per workgroup and peer",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
-                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
+                           "(data+epoch words) into peer-mapped xGMI windows, broadcast",
+           "peer_hier_llf": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with plain data pushes "
+                            "into peer-mapped xGMI windows and one flag per workgroup and peer, broadcast"}[transport]
     v = extras.get("transport_verified", {}).get(transport, {})
     return {
         "metric": METRIC,

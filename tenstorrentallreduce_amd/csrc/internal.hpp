@@ -160,9 +160,10 @@ int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, 
                         unsigned max_grid, void* stream);
 // the same step with LL (push) hand-offs: ll[q] = GPU q's LL area for this parity,
 // [inbox box_words words][result box box_words words]; nranks <= 8; epoch grows by 1 per call
+// xfl: null = LL hand-offs, else every GPU's hand-off flag block (kXFlagBytes; parity = this call's LL parity)
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   void* stream);
+                   uint32_t* const* xfl, uint32_t parity, void* stream);
 // the same step on the lagged-store pipeline (k_hier_pipe): tree / owner sum / row stores of
 // tiles j, j-1, j-2 in one iteration; same arguments and bits as launch_hier_ll
 int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,

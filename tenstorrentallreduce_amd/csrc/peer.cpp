@@ -358,9 +358,12 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
-        st = (p->hier_ll == 2 ? launch_hier_pipe : launch_hier_ll)(buf, n, order, ll, p->nranks, p->rank, n,
-                                                                   p->ll_box_words, p->calls + 1u, p->status,
-                                                                   p->max_groups, stream);
+        if (p->hier_ll == 2)
+            st = launch_hier_pipe(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
+                                  p->max_groups, stream);
+        else   // tune hier_handoff 1: plain data + one flag per workgroup and peer (same bits)
+            st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
+                                p->max_groups, tune(Tune::hier_handoff) ? p->peer_xfl : nullptr, p->calls & 1u, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;

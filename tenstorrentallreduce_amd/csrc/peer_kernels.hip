@@ -693,10 +693,65 @@ __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, 
     return make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
 }
 
+// ---- hand-off flags (FLG forms of k_hier_ll / k_hier_x / k_hier_x2, tune hier_handoff = 1)
+// LL words carry 4 data bytes + a 4-byte epoch each: every hand-off moves twice
+// its data.  In the FLG form the data go as plain system-coherent 16-byte
+// stores (sc0 sc1, the LL stores' policy) into the first 512 bytes of the same
+// LL slot, and each workgroup raises ONE flag per peer GPU when every wave's
+// hand-off stores of the launch have completed (s_waitcnt vmcnt(0): the one
+// in-order counter — the ordering k_peer_oneshot's barriers already rely on).
+// The consumer is the same workgroup index on the peer (tile t is served by
+// workgroup t mod G on every GPU) one launch later: it polls its W flags, then
+// reads the data.  Flags: [parity][0 partials | 1 results][GPU][workgroup] in
+// each GPU's flag allocation; values = the bucket's epoch (monotonic).
+constexpr int kXFlagGroups = 512;
+constexpr size_t kXFlagWords = 2 * 2 * kLLMaxGpus * kXFlagGroups;
+static_assert(kXFlagWords * 4 == kXFlagBytes, "internal.hpp kXFlagBytes: the flag block the host allocates");
+struct XFPtrs {
+    uint32_t* f[kLLMaxGpus];   // GPU q's hand-off flag block
+};
+__device__ __forceinline__ uint32_t* xflag(uint32_t* base, uint32_t parity, int kind, int q) {
+    return base + (((parity * 2 + kind) * kLLMaxGpus + q) * kXFlagGroups + blockIdx.x);
+}
+__device__ __forceinline__ void st_sys16(uint4* p, uint4 v) {
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ uint4 ld_sys16(const uint4* p) {
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
+    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+}
+// every wave's stores so far have completed; then lane q raises the flag in GPU q's block
+__device__ __forceinline__ void xflag_raise(const XFPtrs& xf, uint32_t parity, int kind, int me, int W, uint32_t e) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    if ((int)threadIdx.x < W)
+        __hip_atomic_store(xflag(xf.f[threadIdx.x], parity, kind, me), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// lane q waits for GPU q's flag in this GPU's block, then the workgroup goes on (bounded)
+__device__ __forceinline__ void xflag_wait(uint32_t* mine, uint32_t parity, int kind, int W, uint32_t e,
+                                           uint32_t* status) {
+    if ((int)threadIdx.x < W) {
+        const uint32_t* f = xflag(mine, parity, kind, threadIdx.x);
+        uint64_t t0 = 0;
+        for (uint64_t spin = 0;; ++spin) {
+            if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) break;
+            if (peer_give_up(spin, t0, status)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    lds_barrier();
+}
+
+template <bool FLG>
 __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status) {
+                                                    uint32_t epoch, uint32_t* status, XFPtrs xf, uint32_t par) {
+    // FLG: par = this call's LL parity; partials / results move as plain data, one flag per workgroup and peer
+    auto dslot = [&](uint64_t* base, uint64_t slot, int col) { return reinterpret_cast<uint4*>(base + slot * 128) + col; };
     constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
@@ -765,14 +820,71 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
         if (h == 0) part[w * TV + c] = pw;
         lds_barrier();
-        if (h == 0) {   // the partial -> its owner's inbox, wave w writing word w
+        // the partial -> its owner's inbox: LL, wave w writing word w of every column; FLG, wave w
+        // writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
+        if (h == 0 && (!FLG || (c >> 3) == w)) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-            ll_put_word(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, res, epoch, w);
+            const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
+            if constexpr (FLG) st_sys16(dslot(lp.ll[o], slot, c), res);
+            else ll_put_word(lp.ll[o] + slot * 128 + c, res, epoch, w);
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
     uint4* xs = buf[0];   // [8][32] results of a batch
+    if constexpr (FLG) {
+        // R: this workgroup's partials are out (flag to every owner), every GPU's partials of
+        // its tiles are in (W flags); owned tiles summed batch by batch, results pushed to the
+        // other GPUs' boxes, their rows stored.  B: every owner's results are in; the other
+        // tiles' rows.  (The LL form interleaves R and B per batch; here each waits once.)
+        constexpr int BB = 8;
+        xflag_raise(xf, par, 0, me, W, epoch);
+        xflag_wait(xf.f[me], par, 0, W, epoch, status);
+        const int b = threadIdx.x >> 5, cc = threadIdx.x & 31;
+        auto rows = [&](int j0, int nb, bool owned) {
+#pragma unroll
+            for (int bb = 0; bb < BB; ++bb) {
+                if (bb >= nb) break;
+                if ((owner_of(tile_of(j0 + bb)) == me) != owned) continue;
+                const uint4 rv = xs[bb * 32 + c];
+                const uint64_t v0 = tile_of(j0 + bb) * TV;
+#pragma unroll
+                for (int k = 0; k < OPS; ++k)
+                    st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPW * w + 2 * k + h) * stride) + v0 + c, rv);
+            }
+        };
+        for (int j0 = 0; j0 < mine; j0 += BB) {
+            const int nb = mine - j0 < BB ? mine - j0 : BB;
+            const uint64_t t = tile_of(j0 + b);
+            if (b < nb && owner_of(t) == me) {
+                const uint64_t li = t - (uint64_t)me * tiles_per_owner;
+                uint4 y[kLLMaxGpus];
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) y[src] = ld_sys16(dslot(lp.ll[me], li * W + src, cc));
+                const uint4 val = owner_sum(y, W, me);
+#pragma unroll
+                for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                    if (dst < W && dst != me) st_sys16(dslot(lp.ll[dst] + box_words, t, cc), val);
+                xs[b * 32 + cc] = val;
+            }
+            __syncthreads();
+            rows(j0, nb, true);
+            __syncthreads();   // xs is reused by the next batch
+        }
+        if (W == 1) return;
+        xflag_raise(xf, par, 1, me, W, epoch);
+        xflag_wait(xf.f[me], par, 1, W, epoch, status);
+        for (int j0 = 0; j0 < mine; j0 += BB) {
+            const int nb = mine - j0 < BB ? mine - j0 : BB;
+            const uint64_t t = tile_of(j0 + b);
+            if (b < nb && owner_of(t) != me) xs[b * 32 + cc] = ld_sys16(dslot(lp.ll[me] + box_words, t, cc));
+            __syncthreads();
+            rows(j0, nb, false);
+            __syncthreads();
+        }
+        return;
+    }
     // ---- R + B, 8 tiles at a time; lane (jr, c) serves tile jr of the batch, column c.
     // R: for a tile I own, the W partials of its column are polled from my inbox
     // (all in flight at once), summed and pushed to every OTHER GPU's box; the
@@ -960,58 +1072,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
             if (do_b) st_nt(reinterpret_cast<uint4*>(row(k)) + ts * TV + c, res);
         }
     }
-}
-
-// ---- hand-off flags (FLG forms of k_hier_x / k_hier_x2, tune hier_handoff = 1)
-// LL words carry 4 data bytes + a 4-byte epoch each: every hand-off moves twice
-// its data.  In the FLG form the data go as plain system-coherent 16-byte
-// stores (sc0 sc1, the LL stores' policy) into the first 512 bytes of the same
-// LL slot, and each workgroup raises ONE flag per peer GPU when every wave's
-// hand-off stores of the launch have completed (s_waitcnt vmcnt(0): the one
-// in-order counter — the ordering k_peer_oneshot's barriers already rely on).
-// The consumer is the same workgroup index on the peer (tile t is served by
-// workgroup t mod G on every GPU) one launch later: it polls its W flags, then
-// reads the data.  Flags: [parity][0 partials | 1 results][GPU][workgroup] in
-// each GPU's flag allocation; values = the bucket's epoch (monotonic).
-constexpr int kXFlagGroups = 512;
-constexpr size_t kXFlagWords = 2 * 2 * kLLMaxGpus * kXFlagGroups;
-static_assert(kXFlagWords * 4 == kXFlagBytes, "internal.hpp kXFlagBytes: the flag block the host allocates");
-struct XFPtrs {
-    uint32_t* f[kLLMaxGpus];   // GPU q's hand-off flag block
-};
-__device__ __forceinline__ uint32_t* xflag(uint32_t* base, uint32_t parity, int kind, int q) {
-    return base + (((parity * 2 + kind) * kLLMaxGpus + q) * kXFlagGroups + blockIdx.x);
-}
-__device__ __forceinline__ void st_sys16(uint4* p, uint4 v) {
-    const u32x4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
-}
-__device__ __forceinline__ uint4 ld_sys16(const uint4* p) {
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-}
-// every wave's stores so far have completed; then lane q raises the flag in GPU q's block
-__device__ __forceinline__ void xflag_raise(const XFPtrs& xf, uint32_t parity, int kind, int me, int W, uint32_t e) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    if ((int)threadIdx.x < W)
-        __hip_atomic_store(xflag(xf.f[threadIdx.x], parity, kind, me), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// lane q waits for GPU q's flag in this GPU's block, then the workgroup goes on (bounded)
-__device__ __forceinline__ void xflag_wait(uint32_t* mine, uint32_t parity, int kind, int W, uint32_t e,
-                                           uint32_t* status) {
-    if ((int)threadIdx.x < W) {
-        const uint32_t* f = xflag(mine, parity, kind, threadIdx.x);
-        uint64_t t0 = 0;
-        for (uint64_t spin = 0;; ++spin) {
-            if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) break;
-            if (peer_give_up(spin, t0, status)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    lds_barrier();
 }
 
 // ---- hierarchical step across consecutive buckets ----------------------------
@@ -1686,7 +1746,7 @@ int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, 
 
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   void* stream) {
+                   uint32_t* const* xfl, uint32_t parity, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
         ntiles * 128 > box_words)
@@ -1696,8 +1756,10 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
-                       me, ntiles, ntiles / nranks, box_words, epoch, status);
+    XFPtrs xf{};
+    for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
+    hipLaunchKernelGGL(xfl ? k_hier_ll<true> : k_hier_ll<false>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks,
+                       stride, order, lp, nranks, me, ntiles, ntiles / nranks, box_words, epoch, status, xf, parity);
     return peer_last_error();
 }
 

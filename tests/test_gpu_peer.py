@@ -120,7 +120,8 @@ def worker(rank, world, port, q):
                                                      # the flag hand-offs (tune hier_handoff 1)
                                                      ("hier_x2_flg", 0, 0, 0), ("hier_x2_tail_flg", 0, 0, 0),
                                                      ("hier_x2_flg_one_group", 0, 0, 1), ("hier_x_flg", 0, 0, 0),
-                                                     ("hier_x_flg_one_group", 0, 0, 1))):
+                                                     ("hier_x_flg_one_group", 0, 0, 1), ("hier_ll_flg", 0, 1, 0),
+                                                     ("hier_ll_flg_capped", 0, 1, 2))):
             if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
@@ -140,7 +141,9 @@ def worker(rank, world, port, q):
                         peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
                                                  torch.cuda.current_stream())
                 else:
-                    peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+                    with t.tuned(hier_handoff=int("flg" in mode)):
+                        peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING,
+                                       ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
                 with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
@@ -365,17 +368,19 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (2, 0), (1, 0), (2, 0)):
+        for ll, limit, flg in ((1, 0, 0), (0, 1 << 40, 0), (0, 0, 0), (2, 0, 0), (1, 0, 0), (2, 0, 0), (1, 0, 1),
+                               (1, 0, 0), (1, 0, 1)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
             torch.cuda.synchronize()
-            for b in bufs:   # back to back: both LL parities / epochs
-                peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+            with t.tuned(hier_handoff=flg):   # k_hier_ll: LL words / plain data + flags
+                for b in bufs:   # back to back: both LL parities / epochs
+                    peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
             torch.cuda.synchronize()
             for rep, (b, (_, want)) in enumerate(zip(bufs, cases)):
                 bad = int((b.cpu().numpy().view(np.uint16) != want[None, :]).sum())
-                assert bad == 0, (ll, limit, rep, bad)
+                assert bad == 0, (ll, limit, flg, rep, bad)
         assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.set_hier_ll(0)

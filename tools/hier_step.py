@@ -27,7 +27,7 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
-arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_pipe": (0, 2)}
+arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_ll_flg": (0, 1), "hier_pipe": (0, 2)}
 res = {k: [] for k in list(arms) + ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]}
 host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
 SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
@@ -68,6 +68,7 @@ for _ in range(rounds):
     for name, (limit, ll) in arms.items():
         peer.set_oneshot_max(limit)
         peer.set_hier_ll(ll)
+        t.tune("hier_handoff", int(name.endswith("_flg")))   # k_hier_ll: LL words / data + flags
         for i in range(20):
             peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
         torch.cuda.synchronize()
