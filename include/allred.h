@@ -254,10 +254,6 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   hier_x_lag        1: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
  *                     iteration after the tree of the matching tile of the bucket being read; 0: in
  *                     the same iteration
- *   steps_prefetch    1: k_steps_reg reads a strip's program words into registers before step 0 (0: in
- *                     each phase)
- *   steps_ilp         1; 2: the BO schedule form runs two strips per wave body, their step chains
- *                     interleaved (k_steps_reg2)
  *   hier_handoff      0: k_hier_x / k_hier_x2 hand-offs as LL words (4 data bytes + epoch per 8 bytes);
  *                     1: plain data + one flag per workgroup and peer (read one launch later, or after
  *                     the R phase's flag wait); a sequence keeps the form of its first call

@@ -1217,11 +1217,7 @@ constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), in LDS; pairs unused.
 // MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
-// PF (tune steps_prefetch): the strip's program words (every later phase's
-// row pairs, the result rows) are read out of LDS into registers before step
-// 0, so a phase's dependent chain is its row reads, add and row write only —
-// without PF every phase first waits for its own table read.
-template <int P, bool BO, int MINW, bool PF>
+template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
@@ -1296,22 +1292,6 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
         const uint8_t* tb = tabs[BO ? (s / Q) / slices : 0];
         const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tb);
-        // PF: phase ph's operand words (BO: MPH <= 2 pairs of row bytes; LO: IPW <= 4 other-row
-        // bytes) and the result rows (OPS bytes), packed; every read stays inside the block's
-        // table (BO: < 220 of 256 bytes; LO: < 384 of 448), unused lanes' words are ignored
-        uint32_t pw[PF ? NPH : 1] = {}, fw[PF ? (OPS + 3) / 4 : 1] = {};
-        if constexpr (PF) {
-#pragma unroll
-            for (int ph = 1; ph <= NPH; ++ph) {
-#pragma unroll
-                for (int m = 0; m < (BO ? MPH : IPW); ++m) {
-                    const uint32_t e = t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
-                    pw[ph - 1] |= BO ? e << (16 * m) : (e >> 8) << (8 * m);
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) fw[k / 4] |= (uint32_t)tb[off_of(NPH + 1) + RPO * k + rl] << (8 * (k % 4));
-        }
         uint4 val[BO ? 1 : IPW];   // LO: this lane's pair rows after the latest step
 #pragma unroll
         for (int t = 0; t < IPW; ++t)
@@ -1333,7 +1313,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
 #pragma unroll
                 for (int m = 0; m < MPH; ++m)
                     if (lane + 64 * m < cnt_of(ph) * CW) {
-                        const uint32_t pr = PF ? (pw[ph - 1] >> (16 * m)) & 0xffffu : t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
+                        const uint32_t pr = t16[off_of(ph) / 2 + (lane + 64 * m) / CW];
                         const int a = (pr & 255) * CW + cl, cc = (pr >> 8) * CW + cl;
                         tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
                     }
@@ -1341,8 +1321,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 uint4 oth[IPW];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CW)
-                        oth[m] = tile[(PF ? (pw[ph - 1] >> (8 * m)) & 255u : (uint32_t)(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8)) * CW + cl];
+                    if (lane + 64 * m < H * CW) oth[m] = tile[(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8) * CW + cl];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
                     if (lane + 64 * m < H * CW) {
@@ -1355,123 +1334,13 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         const uint64_t cs = col0(s) + cl;
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
-            const uint32_t fin = PF ? (fw[k / 4] >> (8 * (k % 4))) & 255u : (uint32_t)tb[off_of(NPH + 1) + RPO * k + rl];
-            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs, tile[fin * CW + cl]);
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs,
+                  tile[(int)tb[off_of(NPH + 1) + RPO * k + rl] * CW + cl]);
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
     if (mine > 0) load(0, A, B);
     for (int j = 0; j < mine; ++j) body(j);
-}
-
-// k_steps_reg2<P, MINW>: the BO schedule form of k_steps_reg<P, true, MINW, true>
-// with TWO strips per wave body (tune steps_ilp 2): strips j and j+1 of the
-// wave go through step 0, the step chain and the stores together, their LDS
-// phases interleaved op by op, so the chain of one (ten dependent LDS
-// read-add-write phases, ~2.4 us) hides the other's latency instead of adding
-// to it; the next pair's loads go out right after the pair's step 0.  Same
-// program, same bits; 8 KiB of pair rows per wave (three workgroups per CU at
-// 64 ranks).  No device stamps (the profiled form is k_steps_reg).
-template <int P, int MINW>
-__global__ __launch_bounds__(256, MINW) void k_steps_reg2(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                          const uint8_t* __restrict__ tab,
-                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
-                                                          uint64_t slices, uint64_t units) {
-    constexpr int NW = 4, TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
-    constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
-    constexpr int NPH = 2 * S - 2;
-    constexpr int MPH = (P / 4 * CW + 63) / 64;
-    __shared__ __attribute__((aligned(16))) uint8_t tabs[P][kBoPipeTab];
-    __shared__ __attribute__((aligned(16))) uint4 work[NW][2][H * CW];   // per wave: two strips' pair rows
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int cl = lane % CW, rl = lane / CW;
-    auto cnt_of = [](int ph) {
-        const int k = ph < S ? ph : 2 * S - 1 - ph;
-        return P >> (k + 1);
-    };
-    auto off_of = [&](int ph) {
-        int o = 2 * H;
-        for (int x = 1; x < ph; ++x) o += 2 * cnt_of(x);
-        return o;
-    };
-    uint32_t pra[IPW], prb[IPW];
-    for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
-        reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
-#pragma unroll
-    for (int t = 0; t < IPW; ++t) {
-        const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;
-        pra[t] = pairs[2 * u];
-        prb[t] = pairs[2 * u + 1];
-    }
-    __syncthreads();   // the programs in LDS (the only barrier)
-    const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
-    const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
-    auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
-    auto col0 = [&](uint64_t s) {
-        const uint64_t u = s / Q;
-        return (u / slices) * bv + (u % slices) * TV + (s % Q) * CW;
-    };
-    auto grow = [&](uint32_t r) { return reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride); };
-    uint4 A[2][IPW], B[2][IPW];
-    auto load = [&](int j, int il) {
-        const uint64_t c0 = col0(strip_of(j)) + cl;
-#pragma unroll
-        for (int t = 0; t < IPW; ++t)
-            if (lane + 64 * t < H * CW) {
-                A[il][t] = ld_nt(grow(pra[t]) + c0);
-                B[il][t] = ld_nt(grow(prb[t]) + c0);
-            }
-    };
-    if (mine > 0) load(0, 0);
-    if (mine > 1) load(1, 1);
-    for (int j = 0; j < mine; j += 2) {
-        const int n2 = mine - j >= 2 ? 2 : 1;   // wave-uniform
-        // the two strips' programs (their blocks' tables); with two chains interleaved a
-        // phase's table read no longer stalls its chain alone, so it is read in the phase
-        const uint8_t* tb[2];
-#pragma unroll
-        for (int il = 0; il < 2; ++il) tb[il] = tabs[(strip_of(j + (il < n2 ? il : 0)) / Q) / slices];
-#pragma unroll
-        for (int il = 0; il < 2; ++il) {   // step 0 from registers into the pair rows
-            if (il >= n2) break;
-            uint4* tile = work[w][il];
-#pragma unroll
-            for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * CW) {
-                    const uint32_t e = tb[il][(lane + 64 * t) / CW];   // row | 0x80: the higher rank holds
-                    tile[(e & 127) * CW + cl] = (e & 128) ? add8(B[il][t], A[il][t]) : add8(A[il][t], B[il][t]);
-                }
-        }
-        if (j + 2 < mine) load(j + 2, 0);   // the next pair's loads, behind this pair's chains and stores
-        if (j + 3 < mine) load(j + 3, 1);
-#pragma unroll
-        for (int ph = 1; ph <= NPH; ++ph) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c), the two strips interleaved
-            const bool rs = ph < S;
-#pragma unroll
-            for (int m = 0; m < MPH; ++m)
-#pragma unroll
-                for (int il = 0; il < 2; ++il) {
-                    if (il >= n2) break;
-                    if (lane + 64 * m < cnt_of(ph) * CW) {
-                        uint4* tile = work[w][il];
-                        const uint32_t pr = reinterpret_cast<const uint16_t*>(tb[il])[off_of(ph) / 2 + (lane + 64 * m) / CW];
-                        const int a = (pr & 255) * CW + cl, cc = (pr >> 8) * CW + cl;
-                        tile[a] = rs ? add8(tile[a], tile[cc]) : tile[cc];
-                    }
-                }
-        }
-#pragma unroll
-        for (int il = 0; il < 2; ++il) {
-            if (il >= n2) break;
-            const uint64_t cs = col0(strip_of(j + il)) + cl;
-            const uint4* tile = work[w][il];
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
-                const uint32_t fin = tb[il][off_of(NPH + 1) + RPO * k + rl];
-                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs, tile[fin * CW + cl]);
-            }
-        }
-    }
 }
 
 // One launch per step (allred_tune_set("steps_form", 1), the round-1 form, A/B):
@@ -1595,23 +1464,8 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
-    const bool pf = tune(Tune::steps_prefetch) != 0;
-    if (bo && !stamps && tune(Tune::steps_ilp) == 2 && per_cu <= 3) {   // two strips per wave body (k_steps_reg2)
-#define TSA_SR2(PP) hipLaunchKernelGGL((k_steps_reg2<PP, 3>), grid, dim3(256), 0, st, ranks, stride, tab, pairs, bv, \
-                                       slices, units)
-        switch (total) {
-            case 8: TSA_SR2(8); return true;
-            case 16: TSA_SR2(16); return true;
-            case 32: TSA_SR2(32); return true;
-            case 64: TSA_SR2(64); return true;
-            default: return false;
-        }
-#undef TSA_SR2
-    }
-#define TSA_SR(PP, BOV, MW) do { if (pf) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, true>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps); \
-                                 else hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, false>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps); } while (0)
+#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
+                                               pairs, bv, slices, units, stamps)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)

@@ -713,9 +713,14 @@ struct XFPtrs {
 __device__ __forceinline__ uint32_t* xflag(uint32_t* base, uint32_t parity, int kind, int q) {
     return base + (((parity * 2 + kind) * kLLMaxGpus + q) * kXFlagGroups + blockIdx.x);
 }
+// two system-scope 8-byte stores (global_store_dwordx2 sc0 sc1, the LL stores' policy): compiler-issued,
+// so the compiler also keeps the data VGPRs alive until the stores have read them (an inline-asm
+// dwordx4 store hid that from it and corrupted data); FLG push accounting counts 2 ops per store
+constexpr int kSys16Ops = 2;
 __device__ __forceinline__ void st_sys16(uint4* p, uint4 v) {
-    const u32x4 w = {v.x, v.y, v.z, v.w};
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 __device__ __forceinline__ uint4 ld_sys16(const uint4* p) {
     const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
@@ -804,7 +809,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
     for (int j = 0; j < mine; ++j) {
         // in flight after tile j's loads: this wave's LL store of tile j-1
-        if (j > 0) wait_vm<1>(); else wait_vm<0>();
+        if (j > 0) { if constexpr (FLG) wait_vm<kSys16Ops>(); else wait_vm<1>(); } else wait_vm<0>();
         lds_barrier();
         if (j + 1 < mine) issue(tile_a(j + 1), (j + 1) & 1);
         const uint4* tile = buf[j & 1];
@@ -1171,7 +1176,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
             // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
             wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
-                     (j >= 1 ? 1 : 0));
+                     (j >= 1 ? (FLG ? kSys16Ops : 1) : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -1429,7 +1434,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             // partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG), this
             // wave's owned-sum pushes (j < 2)
             wait_any((j >= 2 + LAG && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && old ? OPS : 0) +
-                     (j >= 1 ? 1 : 0) + (j < 2 ? pushed : 0));
+                     (j >= 1 ? (FLG ? kSys16Ops : 1) : 0) + (j < 2 ? pushed : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;

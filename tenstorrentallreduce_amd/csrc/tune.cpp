@@ -41,9 +41,7 @@ const Key kKeys[] = {
     {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
     {"steps_groups", 0, 0, 5},        // k_steps_reg: workgroups per CU, 0 auto (BO 3, LO 4 or 3) | 3 | 4 | 5
     {"rccl_fault", 0, 0, 7},          // fault injection (tests): 1 init, 2 group end, 4 stream drain never settle
-    {"steps_prefetch", 1, 0, 1},      // k_steps_reg: a strip's program words in registers before step 0
     {"hier_handoff", 0, 0, 1},        // k_hier_x / k_hier_x2 hand-offs: 0 LL words (data + epoch) | 1 data + one flag per workgroup
-    {"steps_ilp", 1, 1, 2},           // BO schedule form: strips per wave body (2: k_steps_reg2, chains interleaved)
     {"multi_fault", 0, 0, 64},        // fault injection (tests): GPU value - 1 of allred_run_multi fails its timed allreduce
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));

@@ -128,9 +128,9 @@ def test_tune_entry_point():
             t.tune("steps_groups", v)
     assert t.tune("steps_groups") == 0
     # round-4 keys: defaults are the product forms / no fault injection
-    assert (t.tune("steps_prefetch"), t.tune("steps_ilp"), t.tune("hier_handoff")) == (1, 1, 0)
+    assert t.tune("hier_handoff") == 0
     assert (t.tune("rccl_fault"), t.tune("multi_fault")) == (0, 0)
-    for key, bad in (("steps_ilp", 3), ("hier_handoff", 2), ("rccl_fault", 8)):
+    for key, bad in (("hier_handoff", 2), ("rccl_fault", 8)):
         with pytest.raises(t.AllredError):
             t.tune(key, bad)
 
