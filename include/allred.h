@@ -257,6 +257,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   hier_handoff      0: k_hier_x / k_hier_x2 hand-offs as LL words (4 data bytes + epoch per 8 bytes);
  *                     1: plain data + one flag per workgroup and peer (read one launch later, or after
  *                     the R phase's flag wait); a sequence keeps the form of its first call
+ *   hier_x_chunked    0: k_hier_x / k_hier_x2 stage results in chunks of 8 tiles only when a workgroup
+ *                     has more than 8 tiles; 1: always (A/B timing of the chunk bookkeeping)
  *   multi_fault       0; fault injection (tests only): GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return)
  *   rccl_fault        0; fault injection of the bounded RCCL waits (tests only), a bit mask: 1 init,

@@ -46,6 +46,14 @@ int grid_side(int c) {
     }
 }
 
+// workgroup slots the groups sharing one GPU divide among their grids (default 256
+// of the 512 the chip holds at two per CU); ALLRED_SHARE_SLOTS overrides (probes)
+unsigned share_slots() {
+    const char* s = std::getenv("ALLRED_SHARE_SLOTS");
+    const int v = s && *s ? std::atoi(s) : 256;
+    return (unsigned)std::min(512, std::max(8, v));
+}
+
 struct HostBarrier {   // the G threads meet before the warm-up and before the timed region
     std::mutex mu;
     std::condition_variable cv;
@@ -194,8 +202,11 @@ class PeerBackend : public DeviceBackend {
             int st = allred_peer_create(G, g, devs[(size_t)g], max_elems, &peers[(size_t)g]);
             if (st != ALLRED_OK) return st;
             // groups sharing one GPU wait for each other inside their kernels: every
-            // group's grid must be resident at once (allred_peer_set_max_groups)
-            if (opts.share_device && G > 1) allred_peer_set_max_groups(peers[(size_t)g], 512u / (unsigned)G);
+            // group's grid must be resident at once (allred_peer_set_max_groups).  The
+            // groups share half the chip's 512 two-per-CU slots (ALLRED_SHARE_SLOTS):
+            // the other groups' copy kernels and next launches find room without
+            // taking the last slot a waiting grid needs
+            if (opts.share_device && G > 1) allred_peer_set_max_groups(peers[(size_t)g], share_slots() / (unsigned)G);
         }
         return allred_peer_connect_all(G, peers.data());
     }

@@ -1108,8 +1108,11 @@ __global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ran
 constexpr int kHierXChunk = 8;
 
 // LAG (tune hier_x_lag): prev's / old's tile rows stored in the iteration of cur's tile j - LAG
-// (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order)
-template <int LAG, bool FLG>
+// (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order).
+// CH: the chunked form (a workgroup with more than kHierXChunk tiles); !CH holds one chunk's
+// results and none of the chunk bookkeeping (the launcher picks it when every workgroup has
+// at most kHierXChunk tiles: the staging costs ~0.3 us a launch at W = 1, profiles/r04_hier_x_chunk_ab.txt)
+template <int LAG, bool FLG, bool CH>
 __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
@@ -1119,7 +1122,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res[2][kHierXChunk][TV];   // two chunks of prev's results
+    __shared__ __attribute__((aligned(16))) uint4 res[CH ? 2 : 1][kHierXChunk][TV];   // two chunks of prev's results
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
@@ -1150,25 +1153,28 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     // previous launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep
     // HBM busy.  Chunks 0 and 1 now, chunk k + 1 when chunk k's row stores begin.
     const int jr = threadIdx.x / TV;
+    // tile j's results in LDS, column c
+    auto rslot = [&](int j) { return CH ? res[(j / kHierXChunk) & 1][j % kHierXChunk][c] : res[0][j][c]; };
     const uint32_t pc = par & 1u, pp = (par >> 1) & 1u;
     // a hand-off slot's data in the FLG form: the first 512 bytes of its 1 KiB LL slot
     auto dslot = [&](uint64_t* base, uint64_t slot) { return reinterpret_cast<uint4*>(base + slot * 128) + c; };
     auto poll_prev = [&](int ch) {
         const int j = ch * kHierXChunk + jr;
         if (j >= mine) return;
+        uint4& slot = res[CH ? ch & 1 : 0][jr][c];
         if constexpr (FLG) {   // every owner's flag was waited for
-            res[ch & 1][jr][c] = ld_sys16(dslot(lpv.ll[me] + box_words, tile_of(j)));
+            slot = ld_sys16(dslot(lpv.ll[me] + box_words, tile_of(j)));
             return;
         }
         const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
-        res[ch & 1][jr][c] = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+        slot = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
     };
     if (prev) {
         if constexpr (FLG) xflag_wait(xf.f[me], pp, 1, W, eprev, status);   // raised at the end of the last launch
         poll_prev(0);
-        if (mine > kHierXChunk) poll_prev(1);
+        if (CH && mine > kHierXChunk) poll_prev(1);
     }
     lds_barrier();   // order bytes and results in LDS
     for (int j = 0; j < mine; ++j) {
@@ -1204,7 +1210,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         }
         // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
         const int sj = j - LAG;   // the tile whose rows this iteration stores
-        if (prev && sj >= kHierXChunk && sj % kHierXChunk == 0) {
+        if (CH && prev && sj >= kHierXChunk && sj % kHierXChunk == 0) {
             // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
             // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1
             if (!cur) lds_barrier();
@@ -1213,7 +1219,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
         const bool st = prev && sj >= 0;
-        const uint4 rv = st ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : make_uint4(0, 0, 0, 0);
+        const uint4 rv = st ? rslot(sj) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             if (cur && j + 2 < mine)
@@ -1224,8 +1230,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     }
     if (LAG && prev && mine > 0) {   // prev's last tile
         if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
+        const uint4 rv = rslot(mine - 1);
         const int sj = mine - 1;
-        const uint4 rv = res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c];
 #pragma unroll
         for (int k = 0; k < OPS; ++k)
             st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
@@ -1240,7 +1246,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             xflag_raise(xf, pc, 0, me, W, ecur);
             xflag_wait(xf.f[me], pc, 0, W, ecur, status);
         }
-    for (int j0 = 0; cur && j0 < mine; j0 += kHierXChunk) {
+    for (int j0 = 0; cur && j0 < mine && (CH || j0 == 0); j0 += kHierXChunk) {
         if (j0 + jr >= mine) break;
         const uint64_t t = tile_of(j0 + jr);
         if (owner_of(t) == me) {
@@ -1302,7 +1308,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // + 1 polled when chunk k's row stores begin — before cur's partial of any of
 // its tiles is pushed, so the order above holds per tile).
 // Same bits as k_hier_ll / k_hier_x.
-template <bool TAIL, int LAG, bool FLG>
+template <bool TAIL, int LAG, bool FLG, bool CH>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
@@ -1313,7 +1319,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res[2][kHierXChunk][TV];   // two chunks of results
+    __shared__ __attribute__((aligned(16))) uint4 res[CH ? 2 : 1][kHierXChunk][TV];   // two chunks of results
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane % TV, q = lane / TV;
@@ -1322,7 +1328,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
     const uint64_t G = gridDim.x;
     const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    const int nch = (mine + kHierXChunk - 1) / kHierXChunk;
+    const int nch = CH ? (mine + kHierXChunk - 1) / kHierXChunk : (mine > 0 ? 1 : 0);
     auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
     auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
     auto issue = [&](uint64_t t, int b) {
@@ -1333,7 +1339,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     };
     // rows of tile j of bucket `dst` from its chunk's slot (lanes of wave w, half q: rows RPW w + q + RPI k)
     auto store_rows = [&](uint16_t* dst, int j) {
-        const uint4 rv = res[(j / kHierXChunk) & 1][j % kHierXChunk][c];
+        const uint4 rv = CH ? res[(j / kHierXChunk) & 1][j % kHierXChunk][c] : res[0][j][c];
 #pragma unroll
         for (int k = 0; k < OPS; ++k)
             st_nt(reinterpret_cast<uint4*>(dst + row_off + (uint64_t)(RPI * k) * stride) + tile_of(j) * TV + c, rv);
@@ -1396,21 +1402,22 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     // old's results of chunk ch -> its slot
     auto poll_old = [&](int ch) {
         if (!act_in(ch)) return;
+        uint4& slot = res[CH ? ch & 1 : 0][jr][c];
         if constexpr (FLG) {
-            res[ch & 1][jr][c] = ld_sys16(dslot(lo.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
+            slot = ld_sys16(dslot(lo.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
             return;
         }
         const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
-        res[ch & 1][jr][c] = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
+        slot = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
     };
     if constexpr (FLG) {
         if (!TAIL) all_owned_sums();
         if (old) {   // every owner's results of old are out (raised one launch ago)
             xflag_wait(xf.f[me], po, 1, W, eold, status);
             poll_old(0);
-            if (nch > 1) poll_old(1);
+            if (CH && nch > 1) poll_old(1);
         }
     } else {
         uint64_t wo[4];
@@ -1419,7 +1426,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
         if (old && act_in(0))
             res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
-        if (old && nch > 1) poll_old(1);
+        if (CH && old && nch > 1) poll_old(1);
     }
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
     // (the polls before them have returned, and with them both tiles' loads).  With
@@ -1462,7 +1469,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         }
         // ---- cur's tile j+2 in, old's tile j - LAG out, interleaved op by op
         const int sj = j - LAG;   // the tile whose rows this iteration stores
-        if (old && sj >= kHierXChunk && sj % kHierXChunk == 0) {
+        if (CH && old && sj >= kHierXChunk && sj % kHierXChunk == 0) {
             // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
             // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1.
             // Its tiles' partials of cur are pushed in later iterations (sj + 8 > j)
@@ -1472,7 +1479,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
         const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
         const bool st = old && sj >= 0;
-        const uint4 rv = st ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : make_uint4(0, 0, 0, 0);
+        const uint4 rv = st ? (CH ? res[(sj / kHierXChunk) & 1][sj % kHierXChunk][c] : res[0][sj][c]) : make_uint4(0, 0, 0, 0);
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {
             if (cur && j + 2 < mine)
@@ -1498,9 +1505,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             __syncthreads();   // every wave has read the slot's previous results
             if (act_in(ch)) {
                 if constexpr (FLG)
-                    res[ch & 1][jr][c] = ld_sys16(dslot(lm.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
+                    res[CH ? ch & 1 : 0][jr][c] = ld_sys16(dslot(lm.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
                 else
-                    res[ch & 1][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
+                    res[CH ? ch & 1 : 0][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
             }
             lds_barrier();
             for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
@@ -1804,7 +1811,18 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
     if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
     const bool lag = tune(Tune::hier_x_lag) != 0;
-    auto* kern = xfl ? (lag ? k_hier_x<1, true> : k_hier_x<0, true>) : (lag ? k_hier_x<1, false> : k_hier_x<0, false>);
+    const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
+    decltype(&k_hier_x<0, false, false>) kern;
+    switch ((xfl ? 4 : 0) + (lag ? 2 : 0) + (ch ? 1 : 0)) {
+        case 7: kern = k_hier_x<1, true, true>; break;
+        case 6: kern = k_hier_x<1, true, false>; break;
+        case 5: kern = k_hier_x<0, true, true>; break;
+        case 4: kern = k_hier_x<0, true, false>; break;
+        case 3: kern = k_hier_x<1, false, true>; break;
+        case 2: kern = k_hier_x<1, false, false>; break;
+        case 1: kern = k_hier_x<0, false, true>; break;
+        default: kern = k_hier_x<0, false, false>; break;
+    }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
                        box_words, ecur, eprev, status, xf, parities);
@@ -1833,16 +1851,25 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
     for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
     const int form = (tune(Tune::hier_x2_tail) ? 2 : 0) + (tune(Tune::hier_x_lag) ? 1 : 0) + (xfl ? 4 : 0);
     if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
-    decltype(&k_hier_x2<false, 0, false>) kern;
-    switch (form) {
-        case 7: kern = k_hier_x2<true, 1, true>; break;
-        case 6: kern = k_hier_x2<true, 0, true>; break;
-        case 5: kern = k_hier_x2<false, 1, true>; break;
-        case 4: kern = k_hier_x2<false, 0, true>; break;
-        case 3: kern = k_hier_x2<true, 1, false>; break;
-        case 2: kern = k_hier_x2<true, 0, false>; break;
-        case 1: kern = k_hier_x2<false, 1, false>; break;
-        default: kern = k_hier_x2<false, 0, false>; break;
+    const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
+    decltype(&k_hier_x2<false, 0, false, false>) kern;
+    switch (form * 2 + (ch ? 1 : 0)) {
+        case 15: kern = k_hier_x2<true, 1, true, true>; break;
+        case 14: kern = k_hier_x2<true, 1, true, false>; break;
+        case 13: kern = k_hier_x2<true, 0, true, true>; break;
+        case 12: kern = k_hier_x2<true, 0, true, false>; break;
+        case 11: kern = k_hier_x2<false, 1, true, true>; break;
+        case 10: kern = k_hier_x2<false, 1, true, false>; break;
+        case 9: kern = k_hier_x2<false, 0, true, true>; break;
+        case 8: kern = k_hier_x2<false, 0, true, false>; break;
+        case 7: kern = k_hier_x2<true, 1, false, true>; break;
+        case 6: kern = k_hier_x2<true, 1, false, false>; break;
+        case 5: kern = k_hier_x2<true, 0, false, true>; break;
+        case 4: kern = k_hier_x2<true, 0, false, false>; break;
+        case 3: kern = k_hier_x2<false, 1, false, true>; break;
+        case 2: kern = k_hier_x2<false, 1, false, false>; break;
+        case 1: kern = k_hier_x2<false, 0, false, true>; break;
+        default: kern = k_hier_x2<false, 0, false, false>; break;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
                        box_words, ecur, emid, eold, llm ? 1 : 0, status, xf, parities);

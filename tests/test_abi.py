@@ -129,6 +129,7 @@ def test_tune_entry_point():
     assert t.tune("steps_groups") == 0
     # round-4 keys: defaults are the product forms / no fault injection
     assert t.tune("hier_handoff") == 0
+    assert t.tune("hier_x_chunked") == 0
     assert (t.tune("rccl_fault"), t.tune("multi_fault")) == (0, 0)
     for key, bad in (("hier_handoff", 2), ("rccl_fault", 8)):
         with pytest.raises(t.AllredError):

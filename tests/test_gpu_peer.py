@@ -416,10 +416,10 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(8):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL parities
-            bufs = [x.clone() for x in data]
+        for rep in range(10):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL
+            bufs = [x.clone() for x in data]   # parities; the chunked form forced (reps 8, 9)
             prev = None
-            with t.tuned(hier_x_lag=rep % 2, hier_handoff=rep // 4):
+            with t.tuned(hier_x_lag=rep % 2, hier_handoff=(rep // 4) % 2, hier_x_chunked=int(rep >= 8)):
                 for b in bufs:
                     peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
                     prev = b.data_ptr()
@@ -572,8 +572,9 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(8):   # owned sums at the start / the end of a launch; LL / flag hand-offs
-            with t.tuned(hier_x2_tail=(rep // 2) % 2, hier_x_lag=rep % 2, hier_handoff=rep // 4):
+        for rep in range(12):   # owned sums at the start / the end of a launch; LL / flag hand-offs; chunked form forced
+            with t.tuned(hier_x2_tail=(rep // 2) % 2, hier_x_lag=rep % 2, hier_handoff=(rep // 4) % 2,
+                         hier_x_chunked=int(rep >= 8)):
                 bufs = [x.clone() for x in data]
                 for b in bufs:
                     peer.allreduce_pipelined2(b.data_ptr(), n, s)

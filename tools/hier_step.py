@@ -28,7 +28,14 @@ peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_ll_flg": (0, 1), "hier_pipe": (0, 2)}
-res = {k: [] for k in list(arms) + ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]}
+# pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _flg: flag
+# hand-offs; _ch: the chunked form at <= 8 tiles per workgroup (tune hier_x_chunked)
+PIPE = ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]
+if os.environ.get("HIER_ARMS"):   # a subset, comma separated (any of the names above, + _ch variants)
+    sel = os.environ["HIER_ARMS"].split(",")
+    arms = {k: v for k, v in arms.items() if k in sel}
+    PIPE = [k for k in sel if k.startswith("hier_x")]
+res = {k: [] for k in list(arms) + PIPE}
 host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
 SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -50,10 +57,11 @@ def pipelined(k, deep):   # k buckets in k + 1 calls: k_hier_x (each call finish
 
 
 for _ in range(rounds):
-    for name, deep in (("hier_x", False), ("hier_x_flg", False), ("hier_x2", True), ("hier_x2_tail", True),
-                       ("hier_x2_flg", True), ("hier_x2_tail_flg", True)):
+    for name in PIPE:
+        deep = name.startswith("hier_x2")
         t.tune("hier_x2_tail", int(name.startswith("hier_x2_tail")))
-        t.tune("hier_handoff", int(name.endswith("_flg")))   # k_hier_x2 hand-offs: LL words / data + flags
+        t.tune("hier_handoff", int("_flg" in name))   # hand-offs: LL words / data + flags
+        t.tune("hier_x_chunked", int("_ch" in name))
         pipelined(20, deep)
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
