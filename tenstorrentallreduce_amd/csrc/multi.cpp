@@ -139,6 +139,7 @@ class DeviceBackend : public Backend {
         return ALLRED_OK;
     }
     void close(Group& gr) override {
+        (void)hipSetDevice(gr.dev);
         for (auto& e : gr.ev)
             if (e) (void)hipEventDestroy(e);
         if (gr.ws) (void)hipFree(gr.ws);
@@ -514,6 +515,16 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
             for (int q = 0; q < G; ++q) all = all && ok[(size_t)q];
             return all;
         };
+        // ALLRED_MULTI_TRACE=1: every thread's host-side phases on stderr (ms since the start)
+        const bool trace = std::getenv("ALLRED_MULTI_TRACE") && std::atoi(std::getenv("ALLRED_MULTI_TRACE")) != 0;
+        const auto t_start = std::chrono::steady_clock::now();
+        std::mutex trace_mu;
+        auto mark = [&](int g, const char* what, int s) {
+            if (!trace) return;
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+            std::lock_guard<std::mutex> l(trace_mu);
+            std::fprintf(stderr, "multi-trace g%d %-12s %9.3f ms status %d\n", g, what, ms, s);
+        };
         for (int g = 0; g < G; ++g) {
             grs[(size_t)g].g = g;
             grs[(size_t)g].dev = devs[(size_t)g];
@@ -522,25 +533,29 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 int& s = status[(size_t)g];
                 const uint16_t* in = h_in + (size_t)g * L * n;
                 s = be->open(gr);
+                mark(g, "open", s);
                 // warm-up on a scratch copy (connection setup, code-object loads stay untimed)
                 if (s == ALLRED_OK) s = be->put(gr, gr.tmp, in, mine);
+                mark(g, "put", s);
                 // every thread agrees before any exchange: one failed setup ends all
                 if (!agree(g, s)) {
                     if (s == ALLRED_OK) s = ALLRED_ERR_TRANSPORT;   // another GPU failed to set up
-                    be->close(gr);
                     return;
                 }
+                mark(g, "agree1", s);
                 if (a->run_kernel) s = be->reduce(gr, gr.tmp);
+                mark(g, "warm-launch", s);
                 if (s == ALLRED_OK) s = be->drain(gr);
+                mark(g, "warm-drain", s);
                 // ... and again after the warm-up (a GPU whose warm-up failed must not
                 // leave the others alone in the timed exchanges)
                 if (!agree(g, s)) {
                     if (s == ALLRED_OK) s = ALLRED_ERR_TRANSPORT;
-                    be->close(gr);
                     return;
                 }
                 // timed: H2D | allreduce | D2H (the reference's EnqueueWriteBuffer,
                 // EnqueueProgram + Finish, EnqueueReadBuffer; allred_helper.hpp:84-96)
+                mark(g, "agree2", s);
                 auto step = [&](int x) { if (s == ALLRED_OK) s = x; };
                 step(be->mark(gr, 0));
                 step(be->put(gr, gr.buf, in, mine));
@@ -548,17 +563,23 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 // fault injection (tests): GPU multi_fault - 1 fails its timed allreduce before any
                 // exchange, while its peers are inside theirs: every thread must still return
                 if (a->run_kernel && tune(Tune::multi_fault) == g + 1) step(ALLRED_ERR_TRANSPORT);
+                mark(g, "timed-put", s);
                 if (a->run_kernel) step(be->reduce(gr, gr.buf));
+                mark(g, "timed-launch", s);
                 step(be->mark(gr, 2));
                 step(be->get(gr, h_out + (size_t)g * L * n, gr.buf, mine));
                 step(be->mark(gr, 3));
                 step(be->drain(gr));
+                mark(g, "timed-drain", s);
                 step(be->times(gr));
                 if (s != ALLRED_OK) be->fail();
-                be->close(gr);
             });
         }
         for (auto& x : th) x.join();
+        // the groups' memory, events and streams released once every thread is done: a
+        // hipFree synchronises the device, which groups sharing one GPU must not do while
+        // another group still has work queued behind it
+        for (Group& gr : grs) be->close(gr);
         for (int g = 0; g < G && st == ALLRED_OK; ++g) st = status[(size_t)g];
         // a thread that failed first reports its own status, not the others' TRANSPORT
         for (int g = 0; g < G; ++g)

@@ -523,9 +523,12 @@ int allred_peer_status(allred_peer* p, uint32_t* out) {
 
 int allred_peer_check(allred_peer* p, void* stream) {
     if (!p) return ALLRED_ERR_ARG;
-    if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return ALLRED_ERR_HIP;
+    // the status word read on the caller's stream: nothing on the null stream, which every
+    // thread of the process shares (in-process peers on one GPU must not queue behind each other)
     uint32_t st = 0;
-    if (hipMemcpy(&st, p->status, 4, hipMemcpyDeviceToHost) != hipSuccess) return ALLRED_ERR_HIP;
+    if (hipMemcpyAsync(&st, p->status, 4, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return ALLRED_ERR_HIP;
     return (st & ALLRED_PEER_TIMEOUT) ? ALLRED_ERR_TRANSPORT : ALLRED_OK;
 }
 
