@@ -567,6 +567,12 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 if (a->run_kernel) step(be->reduce(gr, gr.buf));
                 mark(g, "timed-launch", s);
                 step(be->mark(gr, 2));
+                // Finish before the read-back, as the reference's helper does: a D2H copy
+                // queued behind a waiting allreduce can hold the copy engine that another
+                // group's H2D (which its allreduce waits for) is queued behind (groups
+                // sharing one GPU share its SDMA engines: profiles/r04_multi_share_trace.txt)
+                step(be->drain(gr));
+                mark(g, "timed-finish", s);
                 step(be->get(gr, h_out + (size_t)g * L * n, gr.buf, mine));
                 step(be->mark(gr, 3));
                 step(be->drain(gr));

@@ -44,7 +44,8 @@ def _env(g, nodes):
     return e
 
 
-CASES = [(g, *inv) for g in (2, 4) for inv in invocations(g)]
+GROUPS = [int(x) for x in os.environ.get("ALLRED_TEST_SHARE_GROUPS", "2,4").split(",")]
+CASES = [(g, *inv) for g in GROUPS for inv in invocations(g)]
 
 
 @pytest.mark.parametrize("g,name,variant,argv,nodes", CASES, ids=[f"g{c[0]}-{c[1]}" for c in CASES])
