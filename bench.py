@@ -820,10 +820,8 @@ def cli_config3(world: int, share: bool = False) -> dict:
     RCCL between them), every GPU's ranks checked with validate_result_vector.
     share (--share-gpu rehearsal): ALLRED_GPUS = world groups on the one GPU over
     the in-process peer windows (ALLRED_TRANSPORT=peer, ALLRED_SHARE_GPU=1), the
-    same G-thread orchestration with the exchange the hardware allows, at most
-    4 groups: 8 mutually waiting groups in one process do not stay co-scheduled
-    on one GPU's hardware queues (profiles/r04_multi_share_probe.txt)."""
-    gpus = min(world, 4) if share else min(world, torch.cuda.device_count())
+    same G-thread orchestration with the exchange the hardware allows."""
+    gpus = world if share else min(world, torch.cuda.device_count())
     env = {"ALLRED_NODES": "8", "ALLRED_GPUS": str(gpus), "ALLRED_REPORT": "1", "ALLRED_CHECK_ALL": "1",
            "ALLRED_STRICT": "1"}
     if share:

@@ -12,7 +12,7 @@
 //     hardware), or the host twin (host memory, allred_dist_allreduce_host
 //     with an in-memory exchange; no HIP call at all).
 // Everything between the two — input generation (allred_helper.cpp:277-285),
-// the G threads and their barriers, per-GPU H2D / D2H slices, the timed region
+// the G threads and their barriers, per-GPU H2D / D2H slices, the timed region (Finish before the read-back)
 // (EnqueueWriteBuffer | EnqueueProgram + Finish | EnqueueReadBuffer,
 // allred_helper.hpp:84-96), the status agreement, validation
 // (validate_result_vector, allred_helper.cpp:18-120) — is shared, so the host

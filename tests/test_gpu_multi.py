@@ -11,13 +11,11 @@ exchange and the waits (csrc/multi.cpp).
 Each case runs in a process of its own (the executable, or
 tests/gpu_multi_child.py) with GPU_MAX_HW_QUEUES above G + 1 so that the G
 threads' mutually waiting kernels never share a hardware queue; every peer
-wait is bounded (a stall ends as ALLRED_ERR_TRANSPORT, not a hang).  G = 2
-and 4 here: 8 mutually waiting groups in one process are not kept
-co-scheduled by one GPU's hardware queue scheduler (a group's kernel waits
-seconds for a queue slot at any GPU_MAX_HW_QUEUES from 4 to 32,
-profiles/r04_multi_share_probe.txt), so G = 8 runs only as the host twin
-(tests/test_multi_host.py) and on the 8-GPU node, where every group has a
-GPU of its own.
+wait is bounded (a stall ends as ALLRED_ERR_TRANSPORT, not a hang).  The
+timed region finishes the allreduce before the read-back (the reference's
+RunProgram order): a D2H queued behind a waiting allreduce held a copy engine
+another group's H2D was queued behind, and the groups deadlocked until the
+4 s wait bound (profiles/r04_multi_share_trace.txt).
 Reference: allred_BO_2D.cpp:7-29, allred_helper.cpp:205-220,
 allred_helper.hpp:84-96."""
 import os
@@ -44,7 +42,7 @@ def _env(g, nodes):
     return e
 
 
-GROUPS = [int(x) for x in os.environ.get("ALLRED_TEST_SHARE_GROUPS", "2,4").split(",")]
+GROUPS = [int(x) for x in os.environ.get("ALLRED_TEST_SHARE_GROUPS", "2,4,8").split(",")]
 CASES = [(g, *inv) for g in GROUPS for inv in invocations(g)]
 
 
