@@ -259,8 +259,6 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     the R phase's flag wait); a sequence keeps the form of its first call
  *   hier_x_chunked    0: k_hier_x / k_hier_x2 stage results in chunks of 8 tiles only when a workgroup
  *                     has more than 8 tiles; 1: always (A/B timing of the chunk bookkeeping)
- *   steps_early       0: k_steps_reg stages its programs, then issues the first strip's loads; 1: the
- *                     loads first (their latency overlaps the staging's)
  *   multi_fault       0; fault injection (tests only): GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return)
  *   rccl_fault        0; fault injection of the bounded RCCL waits (tests only), a bit mask: 1 init,

@@ -1217,9 +1217,7 @@ constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), in LDS; pairs unused.
 // MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
-// EARLY (tune steps_early): the first strip's loads issued before the programs are staged
-// (they depend only on the step-0 pairs), so their latency overlaps the staging's.
-template <int P, bool BO, int MINW, bool EARLY>
+template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
@@ -1247,6 +1245,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     };
     uint32_t pra[IPW], prb[IPW];   // this lane's step-0 pairs: first / second rank
     if constexpr (BO) {
+        for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
+            reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
             const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;
@@ -1254,6 +1254,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
             prb[t] = pairs[2 * u + 1];
         }
     } else {
+        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
         const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tab);
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
@@ -1263,6 +1264,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
             prb[t] = e >> 8;
         }
     }
+    __syncthreads();   // the program(s) in LDS (the only barrier)
+    uint4* tile = work[w];
     const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
     const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
     auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
@@ -1280,18 +1283,9 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 B[t] = ld_nt(grow(prb[t]) + c0);
             }
     };
-    uint4 A[IPW], B[IPW];
-    if (EARLY && mine > 0) load(0, A, B);
-    if constexpr (BO) {
-        for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
-            reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
-    } else {
-        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
-    }
-    __syncthreads();   // the program(s) in LDS (the only barrier)
-    uint4* tile = work[w];
     // strip j: step 0 from A / B (registers), then strip j+1's loads into the same registers (free once
     // step 0 has written the pair rows), the later phases among the pair rows, result rows stored
+    uint4 A[IPW], B[IPW];
     auto body = [&](int j) {
         const uint64_t s = strip_of(j);
         const bool st_on = stamps && s % Q == 0 && lane == 0;
@@ -1345,7 +1339,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
-    if (!EARLY && mine > 0) load(0, A, B);
+    if (mine > 0) load(0, A, B);
     for (int j = 0; j < mine; ++j) body(j);
 }
 
@@ -1470,11 +1464,8 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
-    const bool early = tune(Tune::steps_early) != 0;
-#define TSA_SR(PP, BOV, MW) do { if (early) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, true>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps); \
-                                 else hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, false>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps); } while (0)
+#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
+                                               pairs, bv, slices, units, stamps)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)
