@@ -502,17 +502,21 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
     st = be->open_all(devs);
     if (st == ALLRED_OK) {
         HostBarrier bar(G);
-        std::vector<int> ok((size_t)G, 0);
+        // one verdict slot per thread and round: a thread already in round 2 must not
+        // change what a slower thread still reads for round 1
+        std::vector<int> ok(2 * (size_t)G, 0);
         std::vector<int> status((size_t)G, ALLRED_OK);
         std::vector<std::thread> th;
         const size_t mine = (size_t)L * bytes;
-        // every thread calls bar.wait() exactly twice, whatever fails, so none waits forever
-        auto agree = [&](int g, int s) {
-            ok[(size_t)g] = s == ALLRED_OK;
+        // every thread reaches bar.wait() of round 1, and of round 2 iff round 1 agreed
+        // everywhere (every thread reads the same round-1 slots), so none waits forever
+        auto agree = [&](int g, int s, int round) {
+            int* v = ok.data() + (size_t)round * G;
+            v[g] = s == ALLRED_OK;
             if (s != ALLRED_OK) be->fail();
             bar.wait();
             bool all = true;
-            for (int q = 0; q < G; ++q) all = all && ok[(size_t)q];
+            for (int q = 0; q < G; ++q) all = all && v[q];
             return all;
         };
         // ALLRED_MULTI_TRACE=1: every thread's host-side phases on stderr (ms since the start)
@@ -538,7 +542,7 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 if (s == ALLRED_OK) s = be->put(gr, gr.tmp, in, mine);
                 mark(g, "put", s);
                 // every thread agrees before any exchange: one failed setup ends all
-                if (!agree(g, s)) {
+                if (!agree(g, s, 0)) {
                     if (s == ALLRED_OK) s = ALLRED_ERR_TRANSPORT;   // another GPU failed to set up
                     return;
                 }
@@ -549,7 +553,7 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 mark(g, "warm-drain", s);
                 // ... and again after the warm-up (a GPU whose warm-up failed must not
                 // leave the others alone in the timed exchanges)
-                if (!agree(g, s)) {
+                if (!agree(g, s, 1)) {
                     if (s == ALLRED_OK) s = ALLRED_ERR_TRANSPORT;
                     return;
                 }
