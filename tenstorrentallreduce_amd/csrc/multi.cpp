@@ -548,6 +548,9 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 }
                 mark(g, "agree1", s);
                 if (a->run_kernel) s = be->reduce(gr, gr.tmp);
+                // fault injection (tests): GPU multi_fault - 33 fails its warm-up; every
+                // thread must skip the timed region and return
+                if (s == ALLRED_OK && tune(Tune::multi_fault) == 33 + g) s = ALLRED_ERR_TRANSPORT;
                 mark(g, "warm-launch", s);
                 if (s == ALLRED_OK) s = be->drain(gr);
                 mark(g, "warm-drain", s);

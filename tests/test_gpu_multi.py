@@ -87,10 +87,11 @@ def test_across_gpus_bit_exact_vs_oracle_composition(tmp_path, g, name, variant,
     assert bad == 0, f"{name} G={g}: {bad} elements differ"
 
 
-@pytest.mark.parametrize("g,bad", [(2, 2), (4, 1)])
+@pytest.mark.parametrize("g,bad", [(2, 2), (4, 1), (4, 35)])
 def test_failed_gpu_ends_every_thread_on_the_gpu(g, bad):
-    """One group fails its timed allreduce (tune multi_fault) while the other
-    groups' peer kernels wait for it: their waits are bounded (4 s of
+    """One group fails its timed allreduce (tune multi_fault 1..32) while the other
+    groups' peer kernels wait for it, or its warm-up (33..64: every thread
+    skips the timed region): their waits are bounded (4 s of
     s_memrealtime), every thread returns and the executable exits 1 with the
     transport error instead of hanging."""
     import time

@@ -169,3 +169,21 @@ def test_host_twin_failed_gpu_ends_every_thread(monkeypatch, g, bad):
     assert dt < 20, dt   # cancelled, not the 60 s exchange deadline
     rep, out = t.run_multi(argv, t.BO, gpus=g, transport=t.TRANSPORT_HOST)   # and the next run is fine
     assert rep.mismatches == 0
+
+
+@pytest.mark.parametrize("g,bad", [(2, 0), (4, 3), (8, 5)])
+def test_host_twin_failed_warmup_skips_the_timed_region(monkeypatch, g, bad):
+    """One GPU's warm-up fails (tune multi_fault = 33 + GPU): the status
+    agreement after the warm-up sends every thread home before the timed
+    region (none waits in an exchange with a thread that will not come), and
+    the call returns the transport error at once."""
+    import time
+    _env(monkeypatch, None)
+    argv = ["x", "1", "1", "8", "13", "5", "32", "0", "1"]
+    with t.tuned(multi_fault=33 + bad):
+        t0 = time.monotonic()
+        with pytest.raises(t.AllredError) as e:
+            t.run_multi(argv, t.BO, gpus=g, transport=t.TRANSPORT_HOST, timeout_ms=60000, outputs=False)
+        dt = time.monotonic() - t0
+    assert e.value.status == t._lib.ERR_TRANSPORT
+    assert dt < 20, dt
