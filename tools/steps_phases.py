@@ -48,6 +48,21 @@ def main():
            "unit_total_us_p50": round(float(np.median(u[:, -1] - u[:, 0])) / 100, 2),
            "phase_us_p50": [round(float(np.median(d[:, q])) / 1000, 3) for q in range(d.shape[1])],
            "phase_us_p90": [round(float(np.percentile(d[:, q], 90)) / 1000, 3) for q in range(d.shape[1])]}
+    # k_steps_reg: unit u's stamps are those of wave 0 of workgroup u % grid, strip u // grid
+    # of that wave (a persistent grid of `grid` workgroups): split by strip index
+    grid = int(os.environ.get("STEPS_GRID", "0"))
+    if grid:
+        for j in range(int(np.ceil(u.shape[0] / grid))):
+            sel = u[j * grid:(j + 1) * grid]
+            dd = np.diff(sel, axis=1) * 10
+            out[f"strip{j}"] = {"units": int(sel.shape[0]),
+                                "start_us_p50_max": [round(float(np.median(sel[:, 0] - t0)) / 100, 2),
+                                                     round(float((sel[:, 0] - t0).max()) / 100, 2)],
+                                "end_us_p50_max": [round(float(np.median(sel[:, -1] - t0)) / 100, 2),
+                                                   round(float((sel[:, -1] - t0).max()) / 100, 2)],
+                                "step0_us_p50": round(float(np.median(dd[:, 0])) / 1000, 3),
+                                "chain_us_p50": round(float(np.median(dd[:, 1:-1 if variant == t.BO else None].sum(axis=1))) / 1000, 3),
+                                "stores_us_p50": round(float(np.median(dd[:, -1])) / 1000, 3) if variant == t.BO else None}
     print(json.dumps(out))
 
 
