@@ -1222,7 +1222,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
                                                          uint64_t slices, uint64_t units, uint64_t* __restrict__ stamps,
-                                                         int per_unit) {
+                                                         int flags) {
     constexpr int NW = 4, TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
     constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
     constexpr int NPH = BO ? 2 * S - 2 : S - 1;
@@ -1245,22 +1245,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         return o;
     };
     uint32_t pra[IPW], prb[IPW];   // this lane's step-0 pairs: first / second rank
-    // BO per_unit (tune steps_tab): the workgroup's units are blockIdx + j * grid (its four waves take
-    // the unit's four strips), so only their J blocks' programs are staged, tabs[j] for unit j, when
-    // J < P (config 2: 1-2 programs, 256-512 bytes, instead of all P blocks' 16 KiB)
-    const int J = blockIdx.x < units ? (int)((units - 1 - blockIdx.x) / gridDim.x + 1) : 0;
-    const bool perj = BO && per_unit && J < P;
     if constexpr (BO) {
-        if (perj) {
-            for (int i = threadIdx.x; i < J * (kBoPipeTab / 16); i += NW * 64) {
-                const int jj = i / (kBoPipeTab / 16), k = i % (kBoPipeTab / 16);
-                const uint64_t blk = (blockIdx.x + (uint64_t)jj * gridDim.x) / slices;
-                reinterpret_cast<uint4*>(&tabs[jj][0])[k] = reinterpret_cast<const uint4*>(tab + blk * kBoPipeTab)[k];
-            }
-        } else {
-            for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
-                reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
-        }
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
             const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;
@@ -1268,7 +1253,6 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
             prb[t] = pairs[2 * u + 1];
         }
     } else {
-        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
         const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tab);
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
@@ -1278,8 +1262,6 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
             prb[t] = e >> 8;
         }
     }
-    __syncthreads();   // the program(s) in LDS (the only barrier)
-    uint4* tile = work[w];
     const uint64_t GW = (uint64_t)gridDim.x * NW, gw = (uint64_t)blockIdx.x * NW + w, strips = units * Q;
     const int mine = gw < strips ? (int)((strips - 1 - gw) / GW + 1) : 0;
     auto strip_of = [&](int j) { return gw + (uint64_t)j * GW; };
@@ -1297,9 +1279,33 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 B[t] = ld_nt(grow(prb[t]) + c0);
             }
     };
+    uint4 A[IPW], B[IPW];
+    // flags bit 1 (tune steps_early): the first strip's loads go out before the programs are staged
+    const bool early = (flags & 2) != 0;
+    if (early && mine > 0) load(0, A, B);
+    // BO flags bit 0 (tune steps_tab): the workgroup's units are blockIdx + j * grid (its four waves
+    // take the unit's four strips), so only their J blocks' programs are staged, tabs[j] for unit j,
+    // when J < P (config 2: 1-2 programs, 256-512 bytes, instead of all P blocks' 16 KiB)
+    const int J = blockIdx.x < units ? (int)((units - 1 - blockIdx.x) / gridDim.x + 1) : 0;
+    const bool perj = BO && (flags & 1) && J < P;
+    if constexpr (BO) {
+        if (perj) {
+            for (int i = threadIdx.x; i < J * (kBoPipeTab / 16); i += NW * 64) {
+                const int jj = i / (kBoPipeTab / 16), k = i % (kBoPipeTab / 16);
+                const uint64_t blk = (blockIdx.x + (uint64_t)jj * gridDim.x) / slices;
+                reinterpret_cast<uint4*>(&tabs[jj][0])[k] = reinterpret_cast<const uint4*>(tab + blk * kBoPipeTab)[k];
+            }
+        } else {
+            for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
+                reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
+        }
+    } else {
+        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
+    }
+    __syncthreads();   // the program(s) in LDS (the only barrier)
+    uint4* tile = work[w];
     // strip j: step 0 from A / B (registers), then strip j+1's loads into the same registers (free once
     // step 0 has written the pair rows), the later phases among the pair rows, result rows stored
-    uint4 A[IPW], B[IPW];
     auto body = [&](int j) {
         const uint64_t s = strip_of(j);
         const bool st_on = stamps && s % Q == 0 && lane == 0;
@@ -1353,7 +1359,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
-    if (mine > 0) load(0, A, B);
+    if (!early && mine > 0) load(0, A, B);
     for (int j = 0; j < mine; ++j) body(j);
 }
 
@@ -1478,9 +1484,9 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
-    const int per_unit = (int)tune(Tune::steps_tab);
+    const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (tune(Tune::steps_early) ? 2 : 0);
 #define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
-                                               pairs, bv, slices, units, stamps, per_unit)
+                                               pairs, bv, slices, units, stamps, flags)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)
