@@ -259,9 +259,10 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     the R phase's flag wait); a sequence keeps the form of its first call
  *   hier_x_chunked    0: k_hier_x / k_hier_x2 stage results in chunks of 8 tiles only when a workgroup
  *                     has more than 8 tiles; 1: always (A/B timing of the chunk bookkeeping)
- *   steps_tab         0: k_steps_reg (BO) stages every block's program (P x 256 bytes) per workgroup;
- *                     1: only the programs of its own units' blocks (when fewer than P)
- *   steps_early       0: k_steps_reg stages its programs, then issues the first strip's loads; 1: loads first
+ *   steps_tab         1: k_steps_reg (BO) stages only the programs of its own units' blocks (when fewer
+ *                     than P); 0: every block's program (P x 256 bytes) per workgroup (round 3)
+ *   steps_early       1: k_steps_reg issues the first strip's loads, then stages its programs; 0: the
+ *                     programs first (round 3)
  *   multi_fault       0; fault injection (tests only): 1..32: GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return);
  *                     33..64: GPU value - 33 fails its warm-up (every thread skips the timed region)

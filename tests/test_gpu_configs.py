@@ -91,8 +91,8 @@ def test_config5_reference_inputs(n):
 
 
 # ------------------------------------------------------------------ schedule form
-@pytest.mark.parametrize("steps_form,groups,tabs", [(0, 0, 0), (0, 3, 0), (0, 4, 0), (0, 5, 0), (1, 0, 0), (2, 0, 0),
-                                                    (0, 0, 1), (0, 5, 1), (2, 0, 1), (0, 0, 3), (0, 4, 2)])
+@pytest.mark.parametrize("steps_form,groups,tabs", [(0, 0, 3), (0, 3, 3), (0, 4, 3), (0, 5, 3), (1, 0, 3), (2, 0, 3),
+                                                    (0, 0, 0), (0, 5, 1), (2, 0, 1), (0, 4, 2)])
 @pytest.mark.parametrize("variant", ["bo", "lo"])
 @pytest.mark.parametrize("algo,grid,n", [(t.SWING, (8, 64), 327680), (t.RECDUB, (8, 64), 327680),
                                          (t.SWING, (8, 64), 64 * 8 * 3), (t.SWING, (4, 8), 8 * 8 * 5),
@@ -105,8 +105,9 @@ def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, groups, tab
     128-byte strips of whole 512-byte units of 8..64 ranks, step 0 from
     registers, the later steps among LDS rows; other shapes fall back to
     k_bo_steps / k_lo_steps) at the auto grid and at 3 / 4 / 5 workgroups per
-    CU (steps_groups), staging only its units' programs (steps_tab 1) and
-    with the first strip's loads ahead of the staging (steps_early 1), with
+    CU (steps_groups), staging only its units' programs (steps_tab, default
+    1) and with the first strip's loads ahead of the staging (steps_early,
+    default 1) or not (the round-3 order), with
     every unit resident at once (steps_form 2) and as
     one launch per step (steps_form 1, the round-1 kernels), on slices
     narrower than a unit (3 and 5 vectors per block), odd unit counts and at
