@@ -1245,6 +1245,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         return o;
     };
     uint32_t pra[IPW], prb[IPW];   // this lane's step-0 pairs: first / second rank
+    if constexpr (!BO)   // LO: the one step program (<= 448 bytes) staged first, as in round 3
+        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
     if constexpr (BO) {
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
@@ -1299,8 +1301,6 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
             for (int i = threadIdx.x; i < P * kBoPipeTab / 16; i += NW * 64)
                 reinterpret_cast<uint4*>(&tabs[0][0])[i] = reinterpret_cast<const uint4*>(tab)[i];
         }
-    } else {
-        for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
     }
     __syncthreads();   // the program(s) in LDS (the only barrier)
     uint4* tile = work[w];
