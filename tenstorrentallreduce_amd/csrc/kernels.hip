@@ -1217,8 +1217,7 @@ constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), in LDS; pairs unused.
 // MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
-// LOR (LO, tune steps_lo_rows): every lane's partner / result rows read out of the LDS program once.
-template <int P, bool BO, int MINW, bool LOR>
+template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
@@ -1305,31 +1304,6 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     }
     __syncthreads();   // the program(s) in LDS (the only barrier)
     uint4* tile = work[w];
-    // LO LOR (tune steps_lo_rows): the one step program is the same for every strip, so each
-    // lane's partner rows of every phase (4 items, a byte each) and its result rows are read out of
-    // LDS once, here, instead of once per strip and phase
-    constexpr bool lo_rows = !BO && LOR;
-    uint32_t lrow[lo_rows ? NPH : 1], rrow[lo_rows ? (OPS + 3) / 4 : 1];
-    if constexpr (lo_rows) {
-        {
-            const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tabs[0]);
-#pragma unroll
-            for (int ph = 1; ph <= NPH; ++ph) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CW) v |= (uint32_t)(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8) << (8 * m);
-                lrow[ph - 1] = v;
-            }
-#pragma unroll
-            for (int k4 = 0; k4 < (OPS + 3) / 4; ++k4) {
-                uint32_t v = 0;
-#pragma unroll
-                for (int k = 4 * k4; k < 4 * k4 + 4 && k < OPS; ++k) v |= (uint32_t)tabs[0][off_of(NPH + 1) + RPO * k + rl] << (8 * (k - 4 * k4));
-                rrow[k4] = v;
-            }
-        }
-    }
     // strip j: step 0 from A / B (registers), then strip j+1's loads into the same registers (free once
     // step 0 has written the pair rows), the later phases among the pair rows, result rows stored
     auto body = [&](int j) {
@@ -1367,12 +1341,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 uint4 oth[IPW];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
-                    if (lane + 64 * m < H * CW) {
-                        uint32_t row;
-                        if constexpr (lo_rows) row = (lrow[ph - 1] >> (8 * m)) & 255u;
-                        else row = (uint32_t)(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8);
-                        oth[m] = tile[row * CW + cl];
-                    }
+                    if (lane + 64 * m < H * CW) oth[m] = tile[(t16[off_of(ph) / 2 + (lane + 64 * m) / CW] >> 8) * CW + cl];
 #pragma unroll
                 for (int m = 0; m < IPW; ++m)
                     if (lane + 64 * m < H * CW) {
@@ -1385,10 +1354,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         const uint64_t cs = col0(s) + cl;
 #pragma unroll
         for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
-            int fin;
-            if constexpr (lo_rows) fin = (int)((rrow[k / 4] >> (8 * (k % 4))) & 255u);
-            else fin = tb[off_of(NPH + 1) + RPO * k + rl];
-            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs, tile[fin * CW + cl]);
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs,
+                  tile[(int)tb[off_of(NPH + 1) + RPO * k + rl] * CW + cl]);
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
@@ -1518,11 +1485,8 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
     const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (tune(Tune::steps_early) ? 2 : 0);
-    const bool lor = !bo && tune(Tune::steps_lo_rows) != 0;
-#define TSA_SR(PP, BOV, MW) do { if (lor) hipLaunchKernelGGL((k_steps_reg<PP, false, MW, true>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps, flags); \
-                                 else hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, false>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps, flags); } while (0)
+#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
+                                               pairs, bv, slices, units, stamps, flags)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)
