@@ -263,8 +263,6 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     than P); 0: every block's program (P x 256 bytes) per workgroup (round 3)
  *   steps_early       1: k_steps_reg issues the first strip's loads, then stages its programs; 0: the
  *                     programs first (round 3)
- *   steps_depth       1: k_steps_reg (BO) loads the next strip into its one register set after a strip's
- *                     step 0; 2: two sets, strips loaded two ahead
  *   multi_fault       0; fault injection (tests only): 1..32: GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return);
  *                     33..64: GPU value - 33 fails its warm-up (every thread skips the timed region)

@@ -1217,8 +1217,7 @@ constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), in LDS; pairs unused.
 // MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
-// D2 (BO, tune steps_depth 2): strips loaded two ahead into two register sets instead of one.
-template <int P, bool BO, int MINW, bool D2>
+template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
@@ -1282,11 +1281,10 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 B[t] = ld_nt(grow(prb[t]) + c0);
             }
     };
-    uint4 A[IPW], B[IPW], A2[IPW], B2[IPW];   // A2 / B2: D2's second register set
+    uint4 A[IPW], B[IPW];
     // flags bit 1 (tune steps_early): the first strip's loads go out before the programs are staged
     const bool early = (flags & 2) != 0;
     if (early && mine > 0) load(0, A, B);
-    if (D2 && early && mine > 1) load(1, A2, B2);
     // BO flags bit 0 (tune steps_tab): the workgroup's units are blockIdx + j * grid (its four waves
     // take the unit's four strips), so only their J blocks' programs are staged, tabs[j] for unit j,
     // when J < P (config 2: 1-2 programs, 256-512 bytes, instead of all P blocks' 16 KiB)
@@ -1308,7 +1306,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     uint4* tile = work[w];
     // strip j: step 0 from A / B (registers), then strip j+1's loads into the same registers (free once
     // step 0 has written the pair rows), the later phases among the pair rows, result rows stored
-    auto body = [&](int j, uint4 (&A)[IPW], uint4 (&B)[IPW]) {
+    auto body = [&](int j) {
         const uint64_t s = strip_of(j);
         const bool st_on = stamps && s % Q == 0 && lane == 0;
         if (st_on) stamps[(s / Q) * STAMPS] = __builtin_amdgcn_s_memrealtime();
@@ -1327,8 +1325,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 }
             }
         if (st_on) stamps[(s / Q) * STAMPS + 1] = __builtin_amdgcn_s_memrealtime();
-        constexpr int D = D2 ? 2 : 1;   // the strip these registers take next
-        if (j + D < mine) load(j + D, A, B);   // in flight behind this strip's step chain and stores
+        if (j + 1 < mine) load(j + 1, A, B);   // in flight behind this strip's step chain and stores
 #pragma unroll
         for (int ph = 1; ph <= NPH; ++ph) {
             if constexpr (BO) {   // RS 1 .. S-1 (a += c), AG S-1 .. 1 (a = c); a step's pairs are disjoint
@@ -1363,11 +1360,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };
     if (!early && mine > 0) load(0, A, B);
-    if (D2 && !early && mine > 1) load(1, A2, B2);
-    for (int j = 0; j < mine; ++j) {
-        if (!D2 || (j & 1) == 0) body(j, A, B);
-        else body(j, A2, B2);
-    }
+    for (int j = 0; j < mine; ++j) body(j);
 }
 
 // One launch per step (allred_tune_set("steps_form", 1), the round-1 form, A/B):
@@ -1492,11 +1485,8 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
     const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (tune(Tune::steps_early) ? 2 : 0);
-    const bool d2 = bo && tune(Tune::steps_depth) == 2;
-#define TSA_SR(PP, BOV, MW) do { if (d2) hipLaunchKernelGGL((k_steps_reg<PP, true, MW, true>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps, flags); \
-                                 else hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW, false>), grid, dim3(256), 0, st, \
-                                     ranks, stride, tab, pairs, bv, slices, units, stamps, flags); } while (0)
+#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
+                                               pairs, bv, slices, units, stamps, flags)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)

@@ -46,7 +46,6 @@ const Key kKeys[] = {
     {"hier_x_chunked", 0, 0, 1},      // k_hier_x / k_hier_x2: 1 the chunked form even at <= 8 tiles per workgroup (A/B)
     {"steps_tab", 1, 0, 1},           // k_steps_reg BO: 1 stages only its units' block programs (J < P), 0 every block's
     {"steps_early", 1, 0, 1},         // k_steps_reg: 1 the first strip's loads issued before the programs are staged
-    {"steps_depth", 1, 1, 2},         // k_steps_reg BO: strips loaded 1 or 2 ahead (two register sets)
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");
