@@ -1314,7 +1314,11 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
-                                                    int has_mid, uint32_t* status, XFPtrs xf, uint32_t par) {
+                                                    int mid_flags, uint32_t* status, XFPtrs xf, uint32_t par) {
+    // mid_flags: bit 0 = bucket i-1 is pending (its owned sums are due); bit 1 (TAIL, LL hand-offs,
+    // tune hier_x2_tail=2): the owned sums run before the last iteration's row stores, not after them
+    const int has_mid = mid_flags & 1;
+    const bool tl2 = TAIL && !FLG && (mid_flags & 2) != 0;
     // FLG: par = the LL parities of cur / mid / old in bits 0 / 1 / 2
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
@@ -1467,6 +1471,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                 else ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
             }
         }
+        // tl2: mid's owned sums ahead of the last iteration's row stores, so their polls and pushes
+        // overlap those stores instead of queueing behind every store of the launch
+        if (tl2 && j == mine - 1)
+            for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
         // ---- cur's tile j+2 in, old's tile j - LAG out, interleaved op by op
         const int sj = j - LAG;   // the tile whose rows this iteration stores
         if (CH && old && sj >= kHierXChunk && sj % kHierXChunk == 0) {
@@ -1496,7 +1504,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         if (cur) xflag_raise(xf, pc, 0, me, W, ecur);
     if (TAIL) {   // TAIL: mid's partials arrived during the launch i-1
         if constexpr (FLG) all_owned_sums();
-        else
+        else if (!tl2 || mine == 0)
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
     }
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
@@ -1872,7 +1880,8 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         default: kern = k_hier_x2<false, 0, false, false>; break;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, emid, eold, llm ? 1 : 0, status, xf, parities);
+                       box_words, ecur, emid, eold, (llm ? 1 : 0) | (tune(Tune::hier_x2_tail) == 2 ? 2 : 0), status, xf,
+                       parities);
     return peer_last_error();
 }
 

@@ -112,7 +112,7 @@ def worker(rank, world, port, q):
                                                      ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
-                                                     ("hier_x2_tail", 0, 0, 0),
+                                                     ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0),
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
                                                      ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
@@ -134,7 +134,8 @@ def worker(rank, world, port, q):
                 buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
-                    with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
+                    with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
+                                 hier_handoff=int("flg" in mode)):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
                     with t.tuned(hier_handoff=int("flg" in mode)):
@@ -146,7 +147,8 @@ def worker(rank, world, port, q):
                                        ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
-                with t.tuned(hier_x2_tail=int(mode.startswith("hier_x2_tail")), hier_handoff=int("flg" in mode)):
+                with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
+                                 hier_handoff=int("flg" in mode)):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
                 with t.tuned(hier_handoff=int("flg" in mode)):
@@ -572,9 +574,10 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(12):   # owned sums at the start / the end of a launch; LL / flag hand-offs; chunked form forced
-            with t.tuned(hier_x2_tail=(rep // 2) % 2, hier_x_lag=rep % 2, hier_handoff=(rep // 4) % 2,
-                         hier_x_chunked=int(rep >= 8)):
+        for rep in range(14):   # owned sums at the start / the end of a launch / before its last stores (12, 13);
+            # LL / flag hand-offs; chunked form forced
+            with t.tuned(hier_x2_tail=2 if rep >= 12 else (rep // 2) % 2, hier_x_lag=rep % 2,
+                         hier_handoff=(rep // 4) % 2 if rep < 12 else 0, hier_x_chunked=int(8 <= rep < 12)):
                 bufs = [x.clone() for x in data]
                 for b in bufs:
                     peer.allreduce_pipelined2(b.data_ptr(), n, s)
