@@ -1308,17 +1308,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // + 1 polled when chunk k's row stores begin — before cur's partial of any of
 // its tiles is pushed, so the order above holds per tile).
 // Same bits as k_hier_ll / k_hier_x.
-template <bool TAIL, int LAG, bool FLG, bool CH>
+// TAIL: 0 mid's owned sums at the launch start, 1 at its end, 2 before its last row stores (LL only)
+template <int TAIL, int LAG, bool FLG, bool CH>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
-                                                    int mid_flags, uint32_t* status, XFPtrs xf, uint32_t par) {
-    // mid_flags: bit 0 = bucket i-1 is pending (its owned sums are due); bit 1 (TAIL, LL hand-offs,
-    // tune hier_x2_tail=2): the owned sums run before the last iteration's row stores, not after them
-    const int has_mid = mid_flags & 1;
-    const bool tl2 = TAIL && !FLG && (mid_flags & 2) != 0;
+                                                    int has_mid, uint32_t* status, XFPtrs xf, uint32_t par) {
+    // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
+    // stores, not after them
+    constexpr bool tl2 = TAIL == 2 && !FLG;
     // FLG: par = the LL parities of cur / mid / old in bits 0 / 1 / 2
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
@@ -1857,31 +1857,38 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
     }
     XFPtrs xf{};
     for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
-    const int form = (tune(Tune::hier_x2_tail) ? 2 : 0) + (tune(Tune::hier_x_lag) ? 1 : 0) + (xfl ? 4 : 0);
+    // TAIL 2 is an LL-form placement: the flag form takes TAIL 1
+    const int tail = (int)tune(Tune::hier_x2_tail) == 2 && !xfl ? 2 : (tune(Tune::hier_x2_tail) ? 1 : 0);
+    const int lag = tune(Tune::hier_x_lag) ? 1 : 0;
     if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
     const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    decltype(&k_hier_x2<false, 0, false, false>) kern;
-    switch (form * 2 + (ch ? 1 : 0)) {
-        case 15: kern = k_hier_x2<true, 1, true, true>; break;
-        case 14: kern = k_hier_x2<true, 1, true, false>; break;
-        case 13: kern = k_hier_x2<true, 0, true, true>; break;
-        case 12: kern = k_hier_x2<true, 0, true, false>; break;
-        case 11: kern = k_hier_x2<false, 1, true, true>; break;
-        case 10: kern = k_hier_x2<false, 1, true, false>; break;
-        case 9: kern = k_hier_x2<false, 0, true, true>; break;
-        case 8: kern = k_hier_x2<false, 0, true, false>; break;
-        case 7: kern = k_hier_x2<true, 1, false, true>; break;
-        case 6: kern = k_hier_x2<true, 1, false, false>; break;
-        case 5: kern = k_hier_x2<true, 0, false, true>; break;
-        case 4: kern = k_hier_x2<true, 0, false, false>; break;
-        case 3: kern = k_hier_x2<false, 1, false, true>; break;
-        case 2: kern = k_hier_x2<false, 1, false, false>; break;
-        case 1: kern = k_hier_x2<false, 0, false, true>; break;
-        default: kern = k_hier_x2<false, 0, false, false>; break;
+    decltype(&k_hier_x2<0, 0, false, false>) kern = nullptr;
+    // index: tail (0..2) x 8 + lag x 4 + flags x 2 + chunked
+    switch (tail * 8 + lag * 4 + (xfl ? 2 : 0) + (ch ? 1 : 0)) {
+        case 0: kern = k_hier_x2<0, 0, false, false>; break;
+        case 1: kern = k_hier_x2<0, 0, false, true>; break;
+        case 2: kern = k_hier_x2<0, 0, true, false>; break;
+        case 3: kern = k_hier_x2<0, 0, true, true>; break;
+        case 4: kern = k_hier_x2<0, 1, false, false>; break;
+        case 5: kern = k_hier_x2<0, 1, false, true>; break;
+        case 6: kern = k_hier_x2<0, 1, true, false>; break;
+        case 7: kern = k_hier_x2<0, 1, true, true>; break;
+        case 8: kern = k_hier_x2<1, 0, false, false>; break;
+        case 9: kern = k_hier_x2<1, 0, false, true>; break;
+        case 10: kern = k_hier_x2<1, 0, true, false>; break;
+        case 11: kern = k_hier_x2<1, 0, true, true>; break;
+        case 12: kern = k_hier_x2<1, 1, false, false>; break;
+        case 13: kern = k_hier_x2<1, 1, false, true>; break;
+        case 14: kern = k_hier_x2<1, 1, true, false>; break;
+        case 15: kern = k_hier_x2<1, 1, true, true>; break;
+        case 16: kern = k_hier_x2<2, 0, false, false>; break;
+        case 17: kern = k_hier_x2<2, 0, false, true>; break;
+        case 20: kern = k_hier_x2<2, 1, false, false>; break;
+        case 21: kern = k_hier_x2<2, 1, false, true>; break;
+        default: return ALLRED_ERR_ARG;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, emid, eold, (llm ? 1 : 0) | (tune(Tune::hier_x2_tail) == 2 ? 2 : 0), status, xf,
-                       parities);
+                       box_words, ecur, emid, eold, llm ? 1 : 0, status, xf, parities);
     return peer_last_error();
 }
 
