@@ -944,6 +944,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #                 owned tiles, writes bucket i-2; every poll waits for the previous launch)
     #   peer_hier_x2t the same with bucket i-1's owned sums at the END of launch i (tune
     #                 hier_x2_tail: its polls never wait; the result polls wait like k_hier_x's)
+    #   peer_hier_x2t2  the owned sums before launch i's last row stores (hier_x2_tail=2)
     # Every transport runs only once verified on THIS machine (verify_transport: the
     # exact sum of per-row 0/1 inputs and the reference's closed form, both computed
     # without any transport); the one-kernel peer forms must also equal the launch
@@ -961,10 +962,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     handoff = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
-    def x2_tail(on):   # the host-side switch between the two k_hier_x2 forms, read at launch
-        if tail[0] != on:
-            t.tune("hier_x2_tail", int(on))
-            tail[0] = on
+    def x2_tail(v):   # the host-side switch between the k_hier_x2 owned-sum placements, read at launch
+        if tail[0] != v:
+            t.tune("hier_x2_tail", int(v))
+            tail[0] = v
 
     def set_handoff(flg):   # LL words / data + flags (k_hier_x, k_hier_x2; latched per sequence)
         if handoff[0] != flg:
@@ -972,7 +973,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             handoff[0] = flg
 
     def x2_kind(kind):   # tail / hand-off form of a k_hier_x2 transport
-        x2_tail(kind in ("peer_hier_x2t", "peer_hier_x2tf"))
+        x2_tail(2 if kind == "peer_hier_x2t2" else int(kind in ("peer_hier_x2t", "peer_hier_x2tf")))
         set_handoff(int(kind in ("peer_hier_x2f", "peer_hier_x2tf")))
 
     def flush():
@@ -1265,9 +1266,10 @@ FALLBACK_DONE = threading.Event()
 ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_llf": "k_hier_ll<flags>",
               "peer_hier_pipe": "k_hier_pipe",
               "peer_hier_x": "k_hier_x", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
+              "peer_hier_x2t2": "k_hier_x2<true>",
               "peer_hier_x2f": "k_hier_x2<false, flags>", "peer_hier_x2tf": "k_hier_x2<true, flags>"}
 # the k_hier_x2 transports: owned sums at the start / the end (t) of a launch, LL / flag (f) hand-offs
-X2_KINDS = ("peer_hier_x2", "peer_hier_x2t", "peer_hier_x2f", "peer_hier_x2tf")
+X2_KINDS = ("peer_hier_x2", "peer_hier_x2t", "peer_hier_x2t2", "peer_hier_x2f", "peer_hier_x2tf")
 
 
 def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> dict:
@@ -1311,6 +1313,8 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                             "timed region): launch i reads bucket i, writes bucket i-2's rows and at its end sums "
                             "bucket i-1's owned tiles, mem_2D one-shot across GPUs with LL pushes into peer-mapped "
                             "xGMI windows",
+           "peer_hier_x2t2": "ONE kernel per bucket, two buckets deep (as peer_hier_x2t) with bucket i-1's owned "
+                             "sums before the launch's last row stores, LL pushes into peer-mapped xGMI windows",
            "peer_hier_xf": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with flag "
                            "hand-offs: plain data pushes into peer-mapped xGMI windows, one flag per workgroup and peer",
            "peer_hier_x2f": "ONE kernel per bucket, two buckets deep (as peer_hier_x2) with flag hand-offs: plain "

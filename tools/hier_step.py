@@ -31,7 +31,7 @@ arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_ll
 # pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _flg: flag
 # hand-offs; _ch: the chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned
 # sums before the last iteration's row stores (tune hier_x2_tail=2)
-PIPE = ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_flg", "hier_x2_tail_flg"]
+PIPE = ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_tail2", "hier_x2_flg", "hier_x2_tail_flg"]
 if os.environ.get("HIER_ARMS"):   # a subset, comma separated (any of the names above, + _ch variants)
     sel = os.environ["HIER_ARMS"].split(",")
     arms = {k: v for k, v in arms.items() if k in sel}
