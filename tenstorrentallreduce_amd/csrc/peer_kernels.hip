@@ -1112,7 +1112,9 @@ constexpr int kHierXChunk = 8;
 // CH: the chunked form (a workgroup with more than kHierXChunk tiles); !CH holds one chunk's
 // results and none of the chunk bookkeeping (the launcher picks it when every workgroup has
 // at most kHierXChunk tiles: the staging costs ~0.3 us a launch at W = 1, profiles/r04_hier_x_chunk_ab.txt)
-template <int LAG, bool FLG, bool CH>
+// RE (LL form, LAG 1; tune hier_x_rearly): R(cur) ahead of prev's last tile's row stores, so its polls and
+// result pushes overlap those stores instead of queueing behind them
+template <int LAG, bool FLG, bool CH, bool RE>
 __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
@@ -1228,6 +1230,49 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             if (st) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
         }
     }
+    // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
+    // partial (during this launch's loop): W partials summed (fp32, owner first,
+    // one rounding), the result pushed to every GPU's box for the next launch.
+    // FLG: this workgroup's partials are out (flag to every owner), then every
+    // GPU's partials of this workgroup's tiles are in (W flags)
+    auto r_cur = [&]() {
+        if constexpr (FLG)
+            if (cur) {
+                xflag_raise(xf, pc, 0, me, W, ecur);
+                xflag_wait(xf.f[me], pc, 0, W, ecur, status);
+            }
+        for (int j0 = 0; cur && j0 < mine && (CH || j0 == 0); j0 += kHierXChunk) {
+            if (j0 + jr >= mine) break;
+            const uint64_t t = tile_of(j0 + jr);
+            if (owner_of(t) == me) {
+                const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
+                uint4 y[kLLMaxGpus];
+                if constexpr (FLG) {
+#pragma unroll
+                    for (int src = 0; src < kLLMaxGpus; ++src)
+                        if (src < W) y[src] = ld_sys16(dslot(lc.ll[me], lr * W + src));
+                } else {
+                    uint64_t wr[kLLMaxGpus][4];
+#pragma unroll
+                    for (int src = 0; src < kLLMaxGpus; ++src)
+                        if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
+#pragma unroll
+                    for (int src = 0; src < kLLMaxGpus; ++src)
+                        if (src < W)
+                            y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
+                                                             : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
+                }
+                const uint4 o = owner_sum(y, W, me);
+#pragma unroll
+                for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                    if (dst < W) {
+                        if constexpr (FLG) st_sys16(dslot(lc.ll[dst] + box_words, t), o);
+                        else ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
+                    }
+            }
+        }
+    };
+    if constexpr (RE) r_cur();
     if (LAG && prev && mine > 0) {   // prev's last tile
         if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
         const uint4 rv = rslot(mine - 1);
@@ -1236,46 +1281,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         for (int k = 0; k < OPS; ++k)
             st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
     }
-    // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
-    // partial (during this launch's loop): W partials summed (fp32, owner first,
-    // one rounding), the result pushed to every GPU's box for the next launch.
-    // FLG: this workgroup's partials are out (flag to every owner), then every
-    // GPU's partials of this workgroup's tiles are in (W flags)
-    if constexpr (FLG)
-        if (cur) {
-            xflag_raise(xf, pc, 0, me, W, ecur);
-            xflag_wait(xf.f[me], pc, 0, W, ecur, status);
-        }
-    for (int j0 = 0; cur && j0 < mine && (CH || j0 == 0); j0 += kHierXChunk) {
-        if (j0 + jr >= mine) break;
-        const uint64_t t = tile_of(j0 + jr);
-        if (owner_of(t) == me) {
-            const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
-            uint4 y[kLLMaxGpus];
-            if constexpr (FLG) {
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) y[src] = ld_sys16(dslot(lc.ll[me], lr * W + src));
-            } else {
-                uint64_t wr[kLLMaxGpus][4];
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W)
-                        y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
-                                                         : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
-            }
-            const uint4 o = owner_sum(y, W, me);
-#pragma unroll
-            for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W) {
-                    if constexpr (FLG) st_sys16(dslot(lc.ll[dst] + box_words, t), o);
-                    else ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
-                }
-        }
-    }
+    if constexpr (!RE) r_cur();
     if constexpr (FLG)   // this workgroup's results are out: every GPU told (read by its next launch)
         if (cur) xflag_raise(xf, pc, 1, me, W, ecur);
 }
@@ -1820,16 +1826,19 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
     const bool lag = tune(Tune::hier_x_lag) != 0;
     const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    decltype(&k_hier_x<0, false, false>) kern;
-    switch ((xfl ? 4 : 0) + (lag ? 2 : 0) + (ch ? 1 : 0)) {
-        case 7: kern = k_hier_x<1, true, true>; break;
-        case 6: kern = k_hier_x<1, true, false>; break;
-        case 5: kern = k_hier_x<0, true, true>; break;
-        case 4: kern = k_hier_x<0, true, false>; break;
-        case 3: kern = k_hier_x<1, false, true>; break;
-        case 2: kern = k_hier_x<1, false, false>; break;
-        case 1: kern = k_hier_x<0, false, true>; break;
-        default: kern = k_hier_x<0, false, false>; break;
+    const bool re = !xfl && lag && tune(Tune::hier_x_rearly) != 0;
+    decltype(&k_hier_x<0, false, false, false>) kern;
+    switch ((xfl ? 4 : 0) + (lag ? 2 : 0) + (ch ? 1 : 0) + (re ? 8 : 0)) {
+        case 11: kern = k_hier_x<1, false, true, true>; break;
+        case 10: kern = k_hier_x<1, false, false, true>; break;
+        case 7: kern = k_hier_x<1, true, true, false>; break;
+        case 6: kern = k_hier_x<1, true, false, false>; break;
+        case 5: kern = k_hier_x<0, true, true, false>; break;
+        case 4: kern = k_hier_x<0, true, false, false>; break;
+        case 3: kern = k_hier_x<1, false, true, false>; break;
+        case 2: kern = k_hier_x<1, false, false, false>; break;
+        case 1: kern = k_hier_x<0, false, true, false>; break;
+        default: kern = k_hier_x<0, false, false, false>; break;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,

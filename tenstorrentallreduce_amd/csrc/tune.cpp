@@ -46,6 +46,7 @@ const Key kKeys[] = {
     {"hier_x_chunked", 0, 0, 1},      // k_hier_x / k_hier_x2: 1 the chunked form even at <= 8 tiles per workgroup (A/B)
     {"steps_tab", 1, 0, 1},           // k_steps_reg BO: 1 stages only its units' block programs (J < P), 0 every block's
     {"steps_early", 1, 0, 1},         // k_steps_reg: 1 the first strip's loads issued before the programs are staged
+    {"hier_x_rearly", 0, 0, 1},       // k_hier_x (LL, lag 1): 1 R(cur) ahead of the previous bucket's last row stores
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

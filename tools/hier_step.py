@@ -30,7 +30,8 @@ s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_ll_flg": (0, 1), "hier_pipe": (0, 2)}
 # pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _flg: flag
 # hand-offs; _ch: the chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned
-# sums before the last iteration's row stores (tune hier_x2_tail=2)
+# sums before the last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last
+# tile's row stores (tune hier_x_rearly)
 PIPE = ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_tail2", "hier_x2_flg", "hier_x2_tail_flg"]
 if os.environ.get("HIER_ARMS"):   # a subset, comma separated (any of the names above, + _ch variants)
     sel = os.environ["HIER_ARMS"].split(",")
@@ -63,6 +64,7 @@ for _ in range(rounds):
         t.tune("hier_x2_tail", 2 if name.startswith("hier_x2_tail2") else int(name.startswith("hier_x2_tail")))
         t.tune("hier_handoff", int("_flg" in name))   # hand-offs: LL words / data + flags
         t.tune("hier_x_chunked", int("_ch" in name))
+        t.tune("hier_x_rearly", int("_re" in name))
         pipelined(20, deep)
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
