@@ -945,6 +945,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   peer_hier_x2t the same with bucket i-1's owned sums at the END of launch i (tune
     #                 hier_x2_tail: its polls never wait; the result polls wait like k_hier_x's)
     #   peer_hier_x2t2  the owned sums before launch i's last row stores (hier_x2_tail=2)
+    #   peer_hier_xr  k_hier_x with R(cur) ahead of bucket i-1's last row stores (hier_x_rearly)
     # Every transport runs only once verified on THIS machine (verify_transport: the
     # exact sum of per-row 0/1 inputs and the reference's closed form, both computed
     # without any transport); the one-kernel peer forms must also equal the launch
@@ -953,7 +954,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     peer_box = [None]
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
-    pend_kind = [None]   # its transport (peer_hier_x / peer_hier_xf)
+    pend_kind = [None]   # its transport (peer_hier_x / peer_hier_xr / peer_hier_xf)
+    rearly = [None]
     pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
     pend3 = [False]   # rccl_x: a bucket is started and not finished (flush())
     pend4 = [None, 0]   # peer_mem_x: the started bucket and the partial slot it used (flush())
@@ -972,6 +974,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             t.tune("hier_handoff", flg)
             handoff[0] = flg
 
+    def set_rearly(v):   # k_hier_x: R(cur) ahead of the previous bucket's last row stores (read at launch)
+        if rearly[0] != v:
+            t.tune("hier_x_rearly", v)
+            rearly[0] = v
+
     def x2_kind(kind):   # tail / hand-off form of a k_hier_x2 transport
         x2_tail(2 if kind == "peer_hier_x2t2" else int(kind in ("peer_hier_x2t", "peer_hier_x2tf")))
         set_handoff(int(kind in ("peer_hier_x2f", "peer_hier_x2tf")))
@@ -986,6 +993,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             pend4[0] = None
         if pend[0] is not None:
             set_handoff(int(pend_kind[0] == "peer_hier_xf"))
+            set_rearly(int(pend_kind[0] == "peer_hier_xr"))
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
         if pend2[0]:
@@ -1020,10 +1028,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce(out.data_ptr(), ELEMS, stream)   # the partial: mem_2D across the GPUs
             pend4[0], pend4[1] = b.data_ptr(), slot
             return
-        if kind in ("peer_hier_x", "peer_hier_xf"):   # buckets pipelined: this call finishes the previous one
+        if kind in ("peer_hier_x", "peer_hier_xr", "peer_hier_xf"):   # buckets pipelined: this call finishes the previous one
             if pend2[0] or pend3[0] or pend4[0] is not None or (pend[0] is not None and pend_kind[0] != kind):
                 flush()
             set_handoff(int(kind == "peer_hier_xf"))
+            set_rearly(int(kind == "peer_hier_xr"))
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
             pend[0], pend_kind[0] = b.data_ptr(), kind
             return
@@ -1119,7 +1128,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
     if peer is not None:
         for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier", "peer_hier_ll",
-                                  "peer_hier_llf", "peer_hier_pipe", "peer_hier_x", "peer_hier_xf", *X2_KINDS)):
+                                  "peer_hier_llf", "peer_hier_pipe", "peer_hier_x", "peer_hier_xr", "peer_hier_xf", *X2_KINDS)):
             if check(kind, 9100 + 10 * i):
                 candidates.append(kind)
     if not candidates:
@@ -1265,7 +1274,7 @@ FALLBACK_DONE = threading.Event()
 # the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
 ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_llf": "k_hier_ll<flags>",
               "peer_hier_pipe": "k_hier_pipe",
-              "peer_hier_x": "k_hier_x", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
+              "peer_hier_x": "k_hier_x", "peer_hier_xr": "k_hier_x", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
               "peer_hier_x2t2": "k_hier_x2<true>",
               "peer_hier_x2f": "k_hier_x2<false, flags>", "peer_hier_x2tf": "k_hier_x2<true, flags>"}
 # the k_hier_x2 transports: owned sums at the start / the end (t) of a launch, LL / flag (f) hand-offs
@@ -1315,6 +1324,8 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                             "xGMI windows",
            "peer_hier_x2t2": "ONE kernel per bucket, two buckets deep (as peer_hier_x2t) with bucket i-1's owned "
                              "sums before the launch's last row stores, LL pushes into peer-mapped xGMI windows",
+           "peer_hier_xr": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with the owned "
+                           "sums ahead of the previous bucket's last row stores, LL pushes into peer-mapped xGMI windows",
            "peer_hier_xf": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with flag "
                            "hand-offs: plain data pushes into peer-mapped xGMI windows, one flag per workgroup and peer",
            "peer_hier_x2f": "ONE kernel per bucket, two buckets deep (as peer_hier_x2) with flag hand-offs: plain "
