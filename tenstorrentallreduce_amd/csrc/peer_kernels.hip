@@ -1112,9 +1112,11 @@ constexpr int kHierXChunk = 8;
 // CH: the chunked form (a workgroup with more than kHierXChunk tiles); !CH holds one chunk's
 // results and none of the chunk bookkeeping (the launcher picks it when every workgroup has
 // at most kHierXChunk tiles: the staging costs ~0.3 us a launch at W = 1, profiles/r04_hier_x_chunk_ab.txt)
-// RE (LL form, LAG 1; tune hier_x_rearly): R(cur) ahead of prev's last tile's row stores, so its polls and
-// result pushes overlap those stores instead of queueing behind them
-template <int LAG, bool FLG, bool CH, bool RE>
+// RE (LL form, LAG 1), bit 0 (tune hier_x_rearly): R(cur) ahead of prev's last tile's row stores, so
+// its polls and result pushes overlap those stores instead of queueing behind them; bit 1 (tune
+// hier_x_latepoll): prev's results polled after tile 0's tree (they are first read by iteration 1's
+// stores) instead of at the start, where the polls' wait also waited for tile 1's loads
+template <int LAG, bool FLG, bool CH, int RE>
 __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
@@ -1173,12 +1175,14 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         ll_load(at, wd);
         slot = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
     };
-    if (prev) {
+    // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
+    const bool lp = (RE & 2) && LAG == 1 && !FLG && cur;
+    if (prev && !lp) {
         if constexpr (FLG) xflag_wait(xf.f[me], pp, 1, W, eprev, status);   // raised at the end of the last launch
         poll_prev(0);
         if (CH && mine > kHierXChunk) poll_prev(1);
     }
-    lds_barrier();   // order bytes and results in LDS
+    lds_barrier();   // order bytes (and results) in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
             // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
@@ -1209,6 +1213,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                 if constexpr (FLG) st_sys16(dslot(lc.ll[o], slot), pr);
                 else ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
             }
+        }
+        if (lp && j == 0 && prev) {   // read first by iteration 1's stores, behind its A-phase barrier
+            poll_prev(0);
+            if (CH && mine > kHierXChunk) poll_prev(1);
         }
         // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
         const int sj = j - LAG;   // the tile whose rows this iteration stores
@@ -1272,7 +1280,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             }
         }
     };
-    if constexpr (RE) r_cur();
+    if constexpr ((RE & 1) != 0) r_cur();
     if (LAG && prev && mine > 0) {   // prev's last tile
         if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
         const uint4 rv = rslot(mine - 1);
@@ -1281,7 +1289,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         for (int k = 0; k < OPS; ++k)
             st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
     }
-    if constexpr (!RE) r_cur();
+    if constexpr ((RE & 1) == 0) r_cur();
     if constexpr (FLG)   // this workgroup's results are out: every GPU told (read by its next launch)
         if (cur) xflag_raise(xf, pc, 1, me, W, ecur);
 }
@@ -1826,19 +1834,23 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
     const bool lag = tune(Tune::hier_x_lag) != 0;
     const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    const bool re = !xfl && lag && tune(Tune::hier_x_rearly) != 0;
-    decltype(&k_hier_x<0, false, false, false>) kern;
-    switch ((xfl ? 4 : 0) + (lag ? 2 : 0) + (ch ? 1 : 0) + (re ? 8 : 0)) {
-        case 11: kern = k_hier_x<1, false, true, true>; break;
-        case 10: kern = k_hier_x<1, false, false, true>; break;
-        case 7: kern = k_hier_x<1, true, true, false>; break;
-        case 6: kern = k_hier_x<1, true, false, false>; break;
-        case 5: kern = k_hier_x<0, true, true, false>; break;
-        case 4: kern = k_hier_x<0, true, false, false>; break;
-        case 3: kern = k_hier_x<1, false, true, false>; break;
-        case 2: kern = k_hier_x<1, false, false, false>; break;
-        case 1: kern = k_hier_x<0, false, true, false>; break;
-        default: kern = k_hier_x<0, false, false, false>; break;
+    const int re = !xfl && lag ? (tune(Tune::hier_x_rearly) ? 1 : 0) | (tune(Tune::hier_x_latepoll) ? 2 : 0) : 0;
+    decltype(&k_hier_x<0, false, false, 0>) kern;
+    switch ((xfl ? 4 : 0) + (lag ? 2 : 0) + (ch ? 1 : 0) + re * 8) {
+        case 27: kern = k_hier_x<1, false, true, 3>; break;
+        case 26: kern = k_hier_x<1, false, false, 3>; break;
+        case 19: kern = k_hier_x<1, false, true, 2>; break;
+        case 18: kern = k_hier_x<1, false, false, 2>; break;
+        case 11: kern = k_hier_x<1, false, true, 1>; break;
+        case 10: kern = k_hier_x<1, false, false, 1>; break;
+        case 7: kern = k_hier_x<1, true, true, 0>; break;
+        case 6: kern = k_hier_x<1, true, false, 0>; break;
+        case 5: kern = k_hier_x<0, true, true, 0>; break;
+        case 4: kern = k_hier_x<0, true, false, 0>; break;
+        case 3: kern = k_hier_x<1, false, true, 0>; break;
+        case 2: kern = k_hier_x<1, false, false, 0>; break;
+        case 1: kern = k_hier_x<0, false, true, 0>; break;
+        default: kern = k_hier_x<0, false, false, 0>; break;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,

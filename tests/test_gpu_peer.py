@@ -113,6 +113,7 @@ def worker(rank, world, port, q):
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
+                                                     ("hier_x_re_lp", 0, 0, 0), ("hier_x_re_lp_one_group", 0, 0, 1),
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
                                                      ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
@@ -138,7 +139,8 @@ def worker(rank, world, port, q):
                                  hier_handoff=int("flg" in mode)):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
-                    with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode)):
+                    with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode),
+                                 hier_x_latepoll=int("_lp" in mode)):
                         peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
                                                  torch.cuda.current_stream())
                 else:
@@ -151,7 +153,8 @@ def worker(rank, world, port, q):
                                  hier_handoff=int("flg" in mode)):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
-                with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode)):
+                with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode),
+                                 hier_x_latepoll=int("_lp" in mode)):
                     peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
             torch.cuda.synchronize()
             for rep, (data, buf, _) in enumerate(runs):
@@ -418,11 +421,12 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(12):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL
-            bufs = [x.clone() for x in data]   # parities; the chunked form forced (reps 8, 9); R early (10, 11)
-            prev = None
+        for rep in range(14):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL
+            bufs = [x.clone() for x in data]   # parities; the chunked form forced (reps 8, 9); R early (10, 11);
+            prev = None                        # late result polls (12: alone, 13: with R early)
             with t.tuned(hier_x_lag=rep % 2 if rep < 10 else 1, hier_handoff=(rep // 4) % 2 if rep < 10 else 0,
-                         hier_x_chunked=int(8 <= rep < 10), hier_x_rearly=int(rep >= 10)):
+                         hier_x_chunked=int(8 <= rep < 10), hier_x_rearly=int(rep in (10, 11, 13)),
+                         hier_x_latepoll=int(rep >= 12)):
                 for b in bufs:
                     peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
                     prev = b.data_ptr()

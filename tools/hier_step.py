@@ -65,6 +65,7 @@ for _ in range(rounds):
         t.tune("hier_handoff", int("_flg" in name))   # hand-offs: LL words / data + flags
         t.tune("hier_x_chunked", int("_ch" in name))
         t.tune("hier_x_rearly", int("_re" in name))
+        t.tune("hier_x_latepoll", int("_lp" in name))
         pipelined(20, deep)
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
