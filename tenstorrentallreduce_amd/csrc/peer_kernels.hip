@@ -1282,7 +1282,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     };
     if constexpr ((RE & 1) != 0) r_cur();
     if (LAG && prev && mine > 0) {   // prev's last tile
-        if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
+        // a flush launch has no other barrier behind its chunk's poll, nor a one-tile workgroup
+        // behind its late polls (iteration 0 is its only A phase)
+        if (!cur || (lp && mine == 1)) lds_barrier();
         const uint4 rv = rslot(mine - 1);
         const int sj = mine - 1;
 #pragma unroll
