@@ -266,8 +266,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     programs first (round 3)
  *   hier_x_rearly     0: k_hier_x sums its owned tiles after the previous bucket's last row stores;
  *                     1: ahead of them (LL hand-offs, hier_x_lag 1)
- *   hier_x_latepoll   0: k_hier_x polls the previous bucket's results at its start; 1: after tile 0's
- *                     tree (LL hand-offs, hier_x_lag 1; a flush launch polls at its start)
+ *   hier_x_latepoll   1: k_hier_x / k_hier_x2 poll the results of the bucket they write after tile 0's
+ *                     tree (LL hand-offs, hier_x_lag 1; a flush launch polls at its start); 0: at the start
  *   multi_fault       0; fault injection (tests only): 1..32: GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return);
  *                     33..64: GPU value - 33 fails its warm-up (every thread skips the timed region)

@@ -1324,7 +1324,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // + 1 polled when chunk k's row stores begin — before cur's partial of any of
 // its tiles is pushed, so the order above holds per tile).
 // Same bits as k_hier_ll / k_hier_x.
-// TAIL: 0 mid's owned sums at the launch start, 1 at its end, 2 before its last row stores (LL only)
+// TAIL & 3: 0 mid's owned sums at the launch start, 1 at its end, 2 before its last row stores (LL only);
+// TAIL & 4 (LL, LAG 1, tune hier_x_latepoll): old's results polled after tile 0's tree, not at the start
 template <int TAIL, int LAG, bool FLG, bool CH>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
@@ -1334,7 +1335,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                                     int has_mid, uint32_t* status, XFPtrs xf, uint32_t par) {
     // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
     // stores, not after them
-    constexpr bool tl2 = TAIL == 2 && !FLG;
+    constexpr bool tl2 = (TAIL & 3) == 2 && !FLG;
+    // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
+    const bool lp = (TAIL & 4) && LAG == 1 && !FLG && cur;
     // FLG: par = the LL parities of cur / mid / old in bits 0 / 1 / 2
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
@@ -1433,7 +1436,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         slot = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
     };
     if constexpr (FLG) {
-        if (!TAIL) all_owned_sums();
+        if ((TAIL & 3) == 0) all_owned_sums();
         if (old) {   // every owner's results of old are out (raised one launch ago)
             xflag_wait(xf.f[me], po, 1, W, eold, status);
             poll_old(0);
@@ -1441,19 +1444,20 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         }
     } else {
         uint64_t wo[4];
-        if (old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
-        if (!TAIL)
+        const bool early_old = old && !lp;   // lp: polled in A(cur 0), ahead of its partial push
+        if (early_old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
+        if ((TAIL & 3) == 0)
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
-        if (old && act_in(0))
+        if (early_old && act_in(0))
             res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
-        if (CH && old && nch > 1) poll_old(1);
+        if (CH && early_old && nch > 1) poll_old(1);
     }
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
     // (the polls before them have returned, and with them both tiles' loads).  With
     // several chunks an earlier chunk's pushes may be in flight too: counting none
     // only waits longer (the loads of tile j are never waited for too little).  FLG:
     // the flag raise has drained them
-    const int pushed = !FLG && !TAIL && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
+    const int pushed = !FLG && (TAIL & 3) == 0 && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
@@ -1475,6 +1479,12 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
+            // lp: old's results of chunks 0 (and 1), ahead of this launch's first partial push (the
+            // order above holds per tile); first read by iteration 1's stores, behind its A barrier
+            if (lp && j == 0 && old) {
+                poll_old(0);
+                if (CH && nch > 1) poll_old(1);
+            }
             // the partial -> its owner's inbox: LL, wave w writing word w of every column;
             // FLG, wave w writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
             if (q == 0 && (!FLG || (c >> 3) == w)) {
@@ -1513,12 +1523,14 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         }
     }
     if (LAG && old && mine > 0) {   // old's last tile
-        if (!cur) lds_barrier();   // a flush launch has no other barrier behind its chunk's poll
+        // a flush launch has no other barrier behind its chunk's poll, nor a one-tile workgroup
+        // behind its late polls
+        if (!cur || (lp && mine == 1)) lds_barrier();
         store_rows(old, mine - 1);
     }
     if constexpr (FLG)   // cur's partials of this workgroup are out: every owner told
         if (cur) xflag_raise(xf, pc, 0, me, W, ecur);
-    if (TAIL) {   // TAIL: mid's partials arrived during the launch i-1
+    if ((TAIL & 3) != 0) {   // TAIL: mid's partials arrived during the launch i-1
         if constexpr (FLG) all_owned_sums();
         else if (!tl2 || mine == 0)
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
@@ -1880,14 +1892,15 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
     }
     XFPtrs xf{};
     for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
-    // TAIL 2 is an LL-form placement: the flag form takes TAIL 1
+    // TAIL 2 is an LL-form placement: the flag form takes TAIL 1; + 4: late result polls (LL, lag 1)
     const int tail = (int)tune(Tune::hier_x2_tail) == 2 && !xfl ? 2 : (tune(Tune::hier_x2_tail) ? 1 : 0);
     const int lag = tune(Tune::hier_x_lag) ? 1 : 0;
+    const int late = !xfl && lag && tune(Tune::hier_x_latepoll) ? 4 : 0;
     if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
     const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
     decltype(&k_hier_x2<0, 0, false, false>) kern = nullptr;
-    // index: tail (0..2) x 8 + lag x 4 + flags x 2 + chunked
-    switch (tail * 8 + lag * 4 + (xfl ? 2 : 0) + (ch ? 1 : 0)) {
+    // index: (tail + late) x 8 + lag x 4 + flags x 2 + chunked
+    switch ((tail + late) * 8 + lag * 4 + (xfl ? 2 : 0) + (ch ? 1 : 0)) {
         case 0: kern = k_hier_x2<0, 0, false, false>; break;
         case 1: kern = k_hier_x2<0, 0, false, true>; break;
         case 2: kern = k_hier_x2<0, 0, true, false>; break;
@@ -1908,6 +1921,12 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         case 17: kern = k_hier_x2<2, 0, false, true>; break;
         case 20: kern = k_hier_x2<2, 1, false, false>; break;
         case 21: kern = k_hier_x2<2, 1, false, true>; break;
+        case 36: kern = k_hier_x2<4, 1, false, false>; break;
+        case 37: kern = k_hier_x2<4, 1, false, true>; break;
+        case 44: kern = k_hier_x2<5, 1, false, false>; break;
+        case 45: kern = k_hier_x2<5, 1, false, true>; break;
+        case 52: kern = k_hier_x2<6, 1, false, false>; break;
+        case 53: kern = k_hier_x2<6, 1, false, true>; break;
         default: return ALLRED_ERR_ARG;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,

@@ -47,7 +47,7 @@ const Key kKeys[] = {
     {"steps_tab", 1, 0, 1},           // k_steps_reg BO: 1 stages only its units' block programs (J < P), 0 every block's
     {"steps_early", 1, 0, 1},         // k_steps_reg: 1 the first strip's loads issued before the programs are staged
     {"hier_x_rearly", 0, 0, 1},       // k_hier_x (LL, lag 1): 1 R(cur) ahead of the previous bucket's last row stores
-    {"hier_x_latepoll", 0, 0, 1},     // k_hier_x (LL, lag 1): 1 the previous bucket's results polled after tile 0's tree
+    {"hier_x_latepoll", 1, 0, 1},     // k_hier_x / k_hier_x2 (LL, lag 1): 1 the earlier bucket's results polled after tile 0's tree
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

@@ -114,6 +114,8 @@ def worker(rank, world, port, q):
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
                                                      ("hier_x_re_lp", 0, 0, 0), ("hier_x_re_lp_one_group", 0, 0, 1),
+                                                     ("hier_x_lp", 0, 0, 0), ("hier_x2_tail2_lp", 0, 0, 0),
+                                                     ("hier_x2_tail_lp_one_group", 0, 0, 1),
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
                                                      ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
@@ -136,7 +138,7 @@ def worker(rank, world, port, q):
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
                     with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
-                                 hier_handoff=int("flg" in mode)):
+                                 hier_handoff=int("flg" in mode), hier_x_latepoll=int("_lp" in mode)):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
                     with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode),
@@ -150,7 +152,7 @@ def worker(rank, world, port, q):
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
                 with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
-                                 hier_handoff=int("flg" in mode)):
+                                 hier_handoff=int("flg" in mode), hier_x_latepoll=int("_lp" in mode)):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
                 with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode),
@@ -423,10 +425,10 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
         s = torch.cuda.current_stream()
         for rep in range(14):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL
             bufs = [x.clone() for x in data]   # parities; the chunked form forced (reps 8, 9); R early (10, 11);
-            prev = None                        # late result polls (12: alone, 13: with R early)
+            prev = None                        # result polls at the start (12), R early + late polls (13)
             with t.tuned(hier_x_lag=rep % 2 if rep < 10 else 1, hier_handoff=(rep // 4) % 2 if rep < 10 else 0,
                          hier_x_chunked=int(8 <= rep < 10), hier_x_rearly=int(rep in (10, 11, 13)),
-                         hier_x_latepoll=int(rep >= 12)):
+                         hier_x_latepoll=int(rep != 12)):
                 for b in bufs:
                     peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
                     prev = b.data_ptr()
@@ -579,10 +581,11 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(14):   # owned sums at the start / the end of a launch / before its last stores (12, 13);
-            # LL / flag hand-offs; chunked form forced
+        for rep in range(16):   # owned sums at the start / the end of a launch / before its last stores (12-15);
+            # LL / flag hand-offs; chunked form forced; results polled at the start (14, 15) or after tile 0
             with t.tuned(hier_x2_tail=2 if rep >= 12 else (rep // 2) % 2, hier_x_lag=rep % 2,
-                         hier_handoff=(rep // 4) % 2 if rep < 12 else 0, hier_x_chunked=int(8 <= rep < 12)):
+                         hier_handoff=(rep // 4) % 2 if rep < 12 else 0, hier_x_chunked=int(8 <= rep < 12),
+                         hier_x_latepoll=int(rep < 14)):
                 bufs = [x.clone() for x in data]
                 for b in bufs:
                     peer.allreduce_pipelined2(b.data_ptr(), n, s)
