@@ -240,9 +240,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   fused_chunk_tiles 1280: the persistent fused 64-rank passes run a bucket of T 256-element
  *                     tiles as max(1, round(T / 1280)) launches over consecutive tile ranges
  *                     (0 = one launch); allred_plan_launches counts them
- *   hier_x2_tail      0; 1: k_hier_x2 (allred_peer_allreduce_pipelined2) sums the owned tiles of
- *                     the middle bucket at the end of each launch instead of its start; 2: before
- *                     the launch's last row stores (LL hand-offs; the flag form takes 1)
+ *   hier_x2_tail      2: k_hier_x2 (allred_peer_allreduce_pipelined2) sums the owned tiles of the
+ *                     middle bucket before the launch's last row stores (LL hand-offs; the flag form
+ *                     takes 1); 1: at the end of each launch; 0: at its start
  *   lo_tree_min_tiles 64: a 64-rank rank-uniform LO plan (every RecDub schedule) takes the BO tree
  *                     pass from this many 256-element tiles per rank, the register butterfly below
  *   tree_bcast_lag    1: k_tree_bcast_x (allred_dist_allreduce_pipelined) stores the previous

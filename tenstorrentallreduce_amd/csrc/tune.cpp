@@ -34,7 +34,7 @@ const Key kKeys[] = {
     {"lo_dag_reg_min_tiles", 64, 1, 1ll << 40},   // 256-element tiles per rank (64: 32 kB)
     {"check", 0, 0, 1},               // N > 1 programs: verify against the partners', poison receive regions
     {"fused_chunk_tiles", 1280, 0, 1ll << 40},   // persistent fused passes: tiles per launch (0: one launch)
-    {"hier_x2_tail", 0, 0, 2},        // k_hier_x2: owned sums at the start | 1 the end of the launch | 2 before its last row stores
+    {"hier_x2_tail", 2, 0, 2},        // k_hier_x2: owned sums at the start | 1 the end of the launch | 2 before its last row stores
     {"lo_tree_min_tiles", 64, 0, 1ll << 40},   // 64-rank rank-uniform LO: tree pass from this many 256-element tiles
     {"tree_bcast_lag", 1, 0, 1},      // k_tree_bcast_x: the row stores one iteration behind the tree (0: same iteration)
     {"tree_bcast_bal", 0, 0, 1},      // k_tree_bcast_x: every wave stages / stores 8 result columns (0: wave 0 all)
