@@ -1274,8 +1274,8 @@ FALLBACK_DONE = threading.Event()
 # the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
 ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_llf": "k_hier_ll<flags>",
               "peer_hier_pipe": "k_hier_pipe",
-              "peer_hier_x": "k_hier_x", "peer_hier_xr": "k_hier_x", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
-              "peer_hier_x2t2": "k_hier_x2<true>",
+              "peer_hier_x": "k_hier_x", "peer_hier_xr": "k_hier_x<re,late>", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
+              "peer_hier_x2t2": "k_hier_x2<tail2,late>",
               "peer_hier_x2f": "k_hier_x2<false, flags>", "peer_hier_x2tf": "k_hier_x2<true, flags>"}
 # the k_hier_x2 transports: owned sums at the start / the end (t) of a launch, LL / flag (f) hand-offs
 X2_KINDS = ("peer_hier_x2", "peer_hier_x2t", "peer_hier_x2t2", "peer_hier_x2f", "peer_hier_x2tf")
