@@ -1143,6 +1143,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         quick[kind] = round(statistics.median(
             timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
             for _ in range(3)), 4)
+        if peer is not None and kind.startswith("peer") and peer.status() & t.PEER_TIMEOUT:
+            note(rank, f"peer wait timed out during the quick timing of {kind}")
     transport = choose_transport(quick, verify)
 
     def step(i):

@@ -115,6 +115,7 @@ def worker(rank, world, port, q):
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
                                                      ("hier_x_re_lp", 0, 0, 0), ("hier_x_re_lp_one_group", 0, 0, 1),
                                                      ("hier_x_lp", 0, 0, 0), ("hier_x2_tail2_lp", 0, 0, 0),
+                                                     ("hier_x2_lp", 0, 0, 0), ("hier_x2_tail_lp", 0, 0, 0),
                                                      ("hier_x2_tail_lp_one_group", 0, 0, 1),
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
