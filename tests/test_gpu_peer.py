@@ -171,6 +171,8 @@ def worker(rank, world, port, q):
                 bad = sum(int((got[i] != partials[rank]).sum()) for i in range(local))
                 if bad:
                     fails.append((mode, rep, bad))
+            if peer.status() & t.PEER_TIMEOUT and not any(f[0] == "timeout" for f in fails):
+                fails.append(("timeout", mode, 0))   # the first mode whose peer waits gave up
             dist.barrier()
         peer.set_hier_ll(0)
         peer.set_max_groups(0)
