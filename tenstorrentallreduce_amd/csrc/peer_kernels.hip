@@ -1484,11 +1484,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             if (lp && j == 0 && old) {
                 poll_old(0);
                 if (CH && nch > 1) poll_old(1);
-                // the polls have read their slots before this launch pushes any partial: relaxed
-                // atomics to different addresses may otherwise be reordered (compiler or memory
-                // system), and an owner that already has this partial may overwrite the slot polled.
-                // Costs nothing the polls' own wait did not (they were issued behind L(1))
+                // every wave's polls have read their slots before ANY wave pushes a word of this
+                // launch's partials: a tile's partial words come from all four waves, and the
+                // owner's inbox slot they overwrite is free only once old's result of that tile
+                // exists (the owner read the slot's previous partial first).  vmcnt(0): relaxed
+                // atomics to different addresses are not ordered; the barrier: the other waves
+                // (only the lanes of a chunk's tiles poll).  Costs little the polls' own wait did
+                // not (they were issued behind L(1))
                 wait_vm<0>();
+                lds_barrier();
             }
             // the partial -> its owner's inbox: LL, wave w writing word w of every column;
             // FLG, wave w writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
