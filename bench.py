@@ -1143,8 +1143,18 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         quick[kind] = round(statistics.median(
             timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
             for _ in range(3)), 4)
-        if peer is not None and kind.startswith("peer") and peer.status() & t.PEER_TIMEOUT:
-            note(rank, f"peer wait timed out during the quick timing of {kind}")
+        if peer is not None and kind.startswith("peer"):
+            # a peer wait that gave up means wrong bytes: the candidate is out (every rank agrees),
+            # and the sticky status bit is cleared so the next candidates wait normally again
+            torch.cuda.synchronize()
+            st0 = torch.tensor([peer.status() & t.PEER_TIMEOUT], dtype=torch.int64)
+            dist.all_reduce(st0, op=dist.ReduceOp.MAX)
+            if st0.item():
+                note(rank, f"peer wait timed out during the quick timing of {kind}: dropped")
+                quick.pop(kind, None)
+                verify.setdefault(kind, {}).update(verified=False, quick_timing_timeout=True)
+                peer.clear_status()
+                dist.barrier()
     transport = choose_transport(quick, verify)
 
     def step(i):

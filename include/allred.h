@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define ALLRED_ABI_VERSION 4
+#define ALLRED_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------- */
 #define ALLRED_OK 0
@@ -628,6 +628,11 @@ int allred_peer_status(allred_peer* peer, uint32_t* status);
 /* Synchronises `stream` and returns ALLRED_ERR_TRANSPORT if any call so far
  * timed out (ALLRED_PEER_TIMEOUT), else ALLRED_OK. */
 int allred_peer_check(allred_peer* peer, void* stream);
+/* Clears the status word (ALLRED_PEER_TIMEOUT is sticky: once set, every later bounded
+ * wait of this peer gives up at once).  Call with no kernel of this peer in flight (after
+ * allred_peer_check): the calls that follow start from a clean status, new epochs and
+ * fresh LL words, so one timed-out sequence does not poison the next.  ABI 5. */
+int allred_peer_clear_status(allred_peer* peer);
 int allred_peer_destroy(allred_peer* peer);
 
 #ifdef __cplusplus

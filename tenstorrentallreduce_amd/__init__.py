@@ -501,6 +501,10 @@ class Peer:
         check(lib.allred_peer_status(self._h, C.byref(v)), "peer_status")
         return v.value
 
+    def clear_status(self) -> None:
+        """allred_peer_clear_status: the sticky timeout bit cleared (no kernel of this peer in flight)"""
+        check(lib.allred_peer_clear_status(self._h), "peer_clear_status")
+
     def close(self):
         if self._h:
             lib.allred_peer_destroy(self._h)

@@ -38,7 +38,7 @@ BO, LO, MEM = 0, 1, 2
 STEPS_REG = 0x100   # allred_steps_program: | ALLRED_BO -> the register-staged form's program
 EXEC_STEPS, EXEC_FUSED = 0, 1
 ACC_FP32, ACC_BF16 = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_NODES, MAX_STEPS = 64, 6
 UNIQUE_ID_BYTES = 128
 MULTI_FLAT, MULTI_HIER, MULTI_LOCAL = 0, 1, 2          # allred_multi_plan.mode
@@ -192,6 +192,7 @@ SIGNATURES = [
     ("allred_peer_set_sched_push", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_dist_allreduce", C.c_int, [_P, C.POINTER(DistDesc), _u16p, _P, _P]),
     ("allred_peer_status", C.c_int, [_P, C.POINTER(C.c_uint32)]),
+    ("allred_peer_clear_status", C.c_int, [_P]),
     ("allred_peer_check", C.c_int, [_P, _P]),
     ("allred_peer_destroy", C.c_int, [_P]),
 ]

@@ -521,6 +521,15 @@ int allred_peer_status(allred_peer* p, uint32_t* out) {
     return ALLRED_OK;
 }
 
+int allred_peer_clear_status(allred_peer* p) {
+    if (!p) return ALLRED_ERR_ARG;
+    DeviceGuard guard(p->device);
+    // the null stream only (no device-wide sync: other groups of this process may be mid-exchange)
+    if (hipMemsetAsync(p->status, 0, 4, nullptr) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess)
+        return ALLRED_ERR_HIP;
+    return ALLRED_OK;
+}
+
 int allred_peer_check(allred_peer* p, void* stream) {
     if (!p) return ALLRED_ERR_ARG;
     // the status word read on the caller's stream: nothing on the null stream, which every

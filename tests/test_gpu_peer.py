@@ -486,6 +486,42 @@ def test_peer_knob_argument_errors():
         peer.close()
 
 
+def test_peer_timeout_is_cleared():
+    """A partner that never arrives: rank 0 of an in-process two-peer set
+    allreduces alone, its bounded wait gives up (ALLRED_PEER_TIMEOUT, sticky),
+    allred_peer_clear_status clears it, and both peers then allreduce together
+    correctly — the bench drops a candidate this way without poisoning the next."""
+    sys.path.insert(0, ROOT)
+    import tenstorrentallreduce_amd as t
+    peers = [t.Peer(2, r, 0, 1 << 14) for r in range(2)]
+    t.Peer.connect_all(peers)
+    try:
+        n = 1 << 12
+        bufs = [torch.full((n,), 0x3F80, dtype=torch.int16, device="cuda:0") for _ in range(2)]
+        s = torch.cuda.current_stream()
+        peers[0].allreduce(bufs[0].data_ptr(), n, s)   # rank 1 does not come in time
+        torch.cuda.synchronize()
+        assert peers[0].status() & t.PEER_TIMEOUT
+        peers[1].allreduce(bufs[1].data_ptr(), n, s)   # its late call (the epochs stay paired)
+        torch.cuda.synchronize()
+        for p in peers:
+            p.clear_status()
+            assert not p.status() & t.PEER_TIMEOUT
+        # a fresh pair of calls (both ranks, two streams: the two kernels wait for each other)
+        s1 = torch.cuda.Stream()
+        vals = [torch.full((n,), v, dtype=torch.int16, device="cuda:0") for v in (0x3F80, 0x4000)]   # 1.0, 2.0
+        with torch.cuda.stream(s1):
+            peers[1].allreduce(vals[1].data_ptr(), n, s1)
+        peers[0].allreduce(vals[0].data_ptr(), n, s)
+        torch.cuda.synchronize()
+        assert not (peers[0].status() | peers[1].status()) & t.PEER_TIMEOUT
+        for v in vals:   # 1.0 + 2.0 = 3.0 = 0x4040
+            assert int((v.cpu() != 0x4040).sum()) == 0
+    finally:
+        for p in peers:
+            p.close()
+
+
 def config35_worker(rank, world, port, q):
     """BASELINE config 3 (8-rank RecDub BO, 655,360 B per rank; one channel and
     all 7 link-spreading channels) and config 5 (8-rank Swing LO at 2 / 8 / 32 /
