@@ -268,8 +268,6 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     1: ahead of them (LL hand-offs, hier_x_lag 1)
  *   hier_x_latepoll   1: k_hier_x / k_hier_x2 poll the results of the bucket they write after tile 0's
  *                     tree (LL hand-offs, hier_x_lag 1; a flush launch polls at its start); 0: at the start
- *   steps_pairs_arg   0: k_steps_reg reads its step-0 pairs from a device table; 1: from its kernel
- *                     arguments
  *   multi_fault       0; fault injection (tests only): 1..32: GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return);
  *                     33..64: GPU value - 33 fails its warm-up (every thread skips the timed region)

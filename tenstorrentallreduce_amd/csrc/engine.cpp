@@ -51,8 +51,6 @@ struct allred_plan {
     uint8_t* d_steps_tab = nullptr;         // schedule form, one launch: BO per-block phase ranks / LO step pairs
     uint8_t* d_steps_pipe_tab = nullptr;    // the same programs in the pipelined form's layout (k_steps_pipe)
     bool steps_reg_tab = false;             // BO: k_steps_reg's program appended to d_steps_pipe_tab
-    uint8_t h_pairs[64] = {};               // k_steps_reg: the step-0 pairs' ranks (2 bytes each), kernel args
-    bool h_pairs_ok = false;
     bool steps_persistent = false;          // schedule form as one launch (k_bo_steps / k_lo_steps)
     size_t ws_bytes = 0;
     int launches = 0;
@@ -598,13 +596,6 @@ int allred_plan_create(const allred_plan_desc* desc, allred_plan** out) {
             const std::vector<uint8_t> reg = bo_steps_reg_table(pipe, p->sched, total);
             pipe.insert(pipe.end(), reg.begin(), reg.end());
             p->steps_reg_tab = !reg.empty();
-            if (!reg.empty() && (size_t)total <= sizeof(p->h_pairs)) {   // the table ends with the H pairs
-                std::memcpy(p->h_pairs, reg.data() + reg.size() - (size_t)total, (size_t)total);
-                p->h_pairs_ok = true;
-            }
-        } else if (desc->variant != ALLRED_BO && pipe.size() >= (size_t)total && (size_t)total <= sizeof(p->h_pairs)) {
-            std::memcpy(p->h_pairs, pipe.data(), (size_t)total);   // step 0's (r, p) pairs open the LO program
-            p->h_pairs_ok = true;
         }
         if ((st = upload(&p->d_steps_tab, tab)) || (st = upload(&p->d_steps_pipe_tab, pipe))) {
             free_plan(p);
@@ -755,11 +746,9 @@ int allred_plan_execute_profiled(allred_plan* p, uint16_t* ranks, uint64_t strid
         if (p->desc.variant == ALLRED_BO)
             return launch_bo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab,
                                    p->steps_reg_tab ? p->d_steps_pipe_tab + (size_t)kBoPipeTabBytes * N : nullptr,
-                                   p->h_pairs_ok ? p->h_pairs : nullptr,
                                    p->block_elems,
                                    stamps, stream);
-        return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab,
-                               p->h_pairs_ok ? p->h_pairs : nullptr, p->n, stamps, stream);
+        return launch_lo_steps(ranks, stride, N, steps, p->d_steps_tab, p->d_steps_pipe_tab, p->n, stamps, stream);
     }
     if (p->desc.variant == ALLRED_BO) {
         for (int k = 0; k < steps && st == ALLRED_OK; ++k)

@@ -41,7 +41,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
-    rccl_fault, hier_handoff, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll, steps_pairs_arg,
+    rccl_fault, hier_handoff, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll,
     count
 };
 int64_t tune(Tune key);
@@ -105,14 +105,12 @@ int write_profile_log(const char* path, int N, int side, const uint64_t* start, 
 constexpr int kBoPipeTabBytes = 256;   // the schedule form's BO program bytes per block (4N - 4 <= 252)
 // d_pipe_tab: the pipelined form's table (engine.cpp bo_steps_pipe_table / lo_steps_pipe_table), or null;
 // d_reg_tab: k_steps_reg's program (bo_steps_reg_table: N x 256 bytes, then the step-0 pairs), or null
-// h_pairs (nullable): the step-0 pairs' ranks on the host (2 bytes each, total bytes), passed to
-// k_steps_reg as kernel arguments
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    const uint8_t* d_pipe_tab, const uint8_t* d_reg_tab, const uint8_t* h_pairs, size_t block_elems,
-                    uint64_t* stamps, void* stream);
+                    const uint8_t* d_pipe_tab, const uint8_t* d_reg_tab, size_t block_elems, uint64_t* stamps,
+                    void* stream);
 uint64_t bo_steps_units(size_t block_elems, int total);
 int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs,
-                    const uint8_t* d_pipe_tab, const uint8_t* h_pairs, size_t n, uint64_t* stamps, void* stream);
+                    const uint8_t* d_pipe_tab, size_t n, uint64_t* stamps, void* stream);
 uint64_t lo_steps_units(size_t n);
 
 // peer flag area (uint32 words): [0, 64) the multi-kernel barrier, then the

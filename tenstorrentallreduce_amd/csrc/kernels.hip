@@ -1216,20 +1216,13 @@ constexpr int log2_of() { return P <= 1 ? 0 : 1 + log2_of<P / 2>(); }
 //   result rows — in LDS for the workgroup; pairs: H x (lower rank, higher rank).
 //   LO: there are no blocks; tab = lo_steps_pipe_table (its step-0 (r, p) give
 //   the loads), in LDS; pairs unused.
-// the step-0 pairs' ranks (2 bytes per pair) as kernel arguments (flags bit 2, tune steps_pairs_arg):
-// read from the kernarg segment through the scalar cache instead of one global-load latency per
-// workgroup ahead of its first strip's loads
-struct StepPairs {
-    uint8_t b[64];
-};
-
 // MINW: waves per SIMD the compiler must allow = workgroups per CU (3, 4, 5).
 template <int P, bool BO, int MINW>
 __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ ranks, uint64_t stride,
                                                          const uint8_t* __restrict__ tab,
                                                          const uint8_t* __restrict__ pairs, uint64_t bv,
                                                          uint64_t slices, uint64_t units, uint64_t* __restrict__ stamps,
-                                                         int flags, StepPairs sp) {
+                                                         int flags) {
     constexpr int NW = 4, TV = 32, CW = 8, Q = TV / CW, RPO = 64 / CW, OPS = P / RPO, H = P / 2, S = log2_of<P>();
     constexpr int IPW = (H * CW + 63) / 64;   // step-0 items (pair, column) per lane
     constexpr int NPH = BO ? 2 * S - 2 : S - 1;
@@ -1254,24 +1247,7 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     uint32_t pra[IPW], prb[IPW];   // this lane's step-0 pairs: first / second rank
     if constexpr (!BO)   // LO: the one step program (<= 448 bytes) staged first, as in round 3
         for (int i = threadIdx.x; i < LOTAB; i += NW * 64) tabs[0][i] = tab[i];
-    if (flags & 4) {   // from the kernel arguments: uniform words, each lane selects its pair's two bytes
-        uint32_t sw[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            sw[k] = (uint32_t)sp.b[4 * k] | ((uint32_t)sp.b[4 * k + 1] << 8) | ((uint32_t)sp.b[4 * k + 2] << 16) |
-                    ((uint32_t)sp.b[4 * k + 3] << 24);
-#pragma unroll
-        for (int t = 0; t < IPW; ++t) {
-            const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;   // pair u: word u / 2, half u % 2
-            uint32_t v = 0;
-#pragma unroll
-            for (int k = 0; k < (H + 1) / 2 && k < 16; ++k)
-                if (u / 2 == k) v = sw[k];
-            v >>= 16 * (u & 1);
-            pra[t] = v & 255u;
-            prb[t] = (v >> 8) & 255u;
-        }
-    } else if constexpr (BO) {
+    if constexpr (BO) {
 #pragma unroll
         for (int t = 0; t < IPW; ++t) {
             const int i = lane + 64 * t, u = i < H * CW ? i / CW : 0;
@@ -1505,15 +1481,12 @@ unsigned persistent_grid(uint64_t tiles, uint64_t dflt) {
 // the schedule form with register-staged strips (k_steps_reg): 8..64 ranks; false if the shape has no instance.
 // per_cu: four-wave workgroups per CU (3, 4 or 5; 5 x 32 KiB of LDS at 64 ranks fills the CU's 160 KiB)
 bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int total, const uint8_t* tab,
-                      const uint8_t* pairs, const uint8_t* h_pairs, uint64_t bv, uint64_t slices, uint64_t units,
-                      uint64_t* stamps, hipStream_t st) {
+                      const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
+                      hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
-    StepPairs sp{};
-    const bool arg_pairs = h_pairs && total <= (int)sizeof(sp.b) && tune(Tune::steps_pairs_arg) != 0;
-    if (arg_pairs) std::memcpy(sp.b, h_pairs, (size_t)total);
-    const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (tune(Tune::steps_early) ? 2 : 0) | (arg_pairs ? 4 : 0);
+    const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (tune(Tune::steps_early) ? 2 : 0);
 #define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
-                                               pairs, bv, slices, units, stamps, flags, sp)
+                                               pairs, bv, slices, units, stamps, flags)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)
@@ -1751,8 +1724,8 @@ int launch_broadcast(uint16_t* ranks, uint64_t stride, size_t n, int total, cons
 }
 
 int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_tab,
-                    const uint8_t* d_pipe_tab, const uint8_t* d_reg_tab, const uint8_t* h_pairs, size_t block_elems,
-                    uint64_t* stamps, void* stream) {
+                    const uint8_t* d_pipe_tab, const uint8_t* d_reg_tab, size_t block_elems, uint64_t* stamps,
+                    void* stream) {
     if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
     if (block_elems % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t bv = block_elems / 8, slices = (bv + kStepSV - 1) / kStepSV, units = slices * (uint64_t)total;
@@ -1762,7 +1735,7 @@ int launch_bo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (d_reg_tab && tune(Tune::steps_form) == 0 && bv % kStepSV == 0 && (1 << steps) == total) {
         const int g = (int)tune(Tune::steps_groups);
         if (launch_steps_reg(true, g ? g : 3, ranks, stride, total, d_reg_tab, d_reg_tab + (size_t)kBoPipeTabBytes * total,
-                             h_pairs, bv, slices, units, stamps, st))
+                             bv, slices, units, stamps, st))
             return last_error();
     }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);
@@ -1776,7 +1749,7 @@ uint64_t bo_steps_units(size_t block_elems, int total) {
 }
 
 int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, const uint8_t* d_pairs,
-                    const uint8_t* d_pipe_tab, const uint8_t* h_pairs, size_t n, uint64_t* stamps, void* stream) {
+                    const uint8_t* d_pipe_tab, size_t n, uint64_t* stamps, void* stream) {
     if (steps == 0) return ALLRED_OK;   // one rank: nothing to exchange
     if (n % 8 || stride % 8 || !aligned16(ranks) || total < 2 || total > ALLRED_MAX_NODES) return ALLRED_ERR_ARG;
     const uint64_t nv = n / 8, units = (nv + kStepSV - 1) / kStepSV;
@@ -1787,7 +1760,7 @@ int launch_lo_steps(uint16_t* ranks, uint64_t stride, int total, int steps, cons
     if (d_pipe_tab && tune(Tune::steps_form) == 0 && nv % kStepSV == 0 && (1 << steps) == total) {
         const int g = (int)tune(Tune::steps_groups);
         const int per_cu = g ? g : (units > 768 && units <= 1024 ? 3 : 4);
-        if (launch_steps_reg(false, per_cu, ranks, stride, total, d_pipe_tab, nullptr, h_pairs, 0, 1, units, stamps, st))
+        if (launch_steps_reg(false, per_cu, ranks, stride, total, d_pipe_tab, nullptr, 0, 1, units, stamps, st))
             return last_error();
     }
     const unsigned grid = (unsigned)(units < (uint64_t)kMaxGrid ? units : (uint64_t)kMaxGrid);

@@ -48,7 +48,6 @@ const Key kKeys[] = {
     {"steps_early", 1, 0, 1},         // k_steps_reg: 1 the first strip's loads issued before the programs are staged
     {"hier_x_rearly", 0, 0, 1},       // k_hier_x (LL, lag 1): 1 R(cur) ahead of the previous bucket's last row stores
     {"hier_x_latepoll", 1, 0, 1},     // k_hier_x / k_hier_x2 (LL, lag 1): 1 the earlier bucket's results polled after tile 0's tree
-    {"steps_pairs_arg", 0, 0, 1},     // k_steps_reg: 1 the step-0 pairs as kernel arguments instead of a device table
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");
