@@ -262,8 +262,9 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     has more than 8 tiles; 1: always (A/B timing of the chunk bookkeeping)
  *   steps_tab         1: k_steps_reg (BO) stages only the programs of its own units' blocks (when fewer
  *                     than P); 0: every block's program (P x 256 bytes) per workgroup (round 3)
- *   steps_early       1: k_steps_reg issues the first strip's loads, then stages its programs; 0: the
- *                     programs first (round 3)
+ *   steps_early       1: k_steps_reg issues the first strip's loads before it stages its programs when
+ *                     its grid is full (units >= workgroups), else after; 2: always before; 0: always
+ *                     after (round 3)
  *   hier_x_rearly     0: k_hier_x sums its owned tiles after the previous bucket's last row stores;
  *                     1: ahead of them (LL hand-offs, hier_x_lag 1)
  *   hier_x_latepoll   1: k_hier_x / k_hier_x2 poll the results of the bucket they write after tile 0's

@@ -1484,7 +1484,12 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
                       const uint8_t* pairs, uint64_t bv, uint64_t slices, uint64_t units, uint64_t* stamps,
                       hipStream_t st) {
     const dim3 grid(persistent_grid(units, 256 * (uint64_t)per_cu));
-    const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (tune(Tune::steps_early) ? 2 : 0);
+    // early first-strip loads (tune steps_early: 0 never, 1 auto, 2 always): auto when the grid is full
+    // (units >= its workgroups), where they win 0.8 us at config 2; with fewer units every wave has
+    // one strip and the program staging behind that burst costs 0.3-0.8 us (profiles/r04_steps_small_ab.txt)
+    const int64_t early = tune(Tune::steps_early);
+    const bool early_on = early == 2 || (early == 1 && units >= 256 * (uint64_t)per_cu);
+    const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (early_on ? 2 : 0);
 #define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
                                                pairs, bv, slices, units, stamps, flags)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \

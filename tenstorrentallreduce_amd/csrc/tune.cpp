@@ -45,7 +45,7 @@ const Key kKeys[] = {
     {"multi_fault", 0, 0, 64},        // fault injection (tests): 1..32 GPU value - 1 fails its timed allreduce, 33..64 its warm-up
     {"hier_x_chunked", 0, 0, 1},      // k_hier_x / k_hier_x2: 1 the chunked form even at <= 8 tiles per workgroup (A/B)
     {"steps_tab", 1, 0, 1},           // k_steps_reg BO: 1 stages only its units' block programs (J < P), 0 every block's
-    {"steps_early", 1, 0, 1},         // k_steps_reg: 1 the first strip's loads issued before the programs are staged
+    {"steps_early", 1, 0, 2},         // k_steps_reg: the first strip's loads before the program staging: 0 never | 1 auto (full grid) | 2 always
     {"hier_x_rearly", 0, 0, 1},       // k_hier_x (LL, lag 1): 1 R(cur) ahead of the previous bucket's last row stores
     {"hier_x_latepoll", 1, 0, 1},     // k_hier_x / k_hier_x2 (LL, lag 1): 1 the earlier bucket's results polled after tile 0's tree
 };

@@ -122,16 +122,18 @@ def test_schedule_form_bit_exact(algo, grid, n, variant, steps_form, groups, tab
     assert np.array_equal(got, np.stack(want))
 
 
-@pytest.mark.parametrize("cap", [1, 16, 32, 200])
+@pytest.mark.parametrize("cap,early", [(1, 1), (16, 1), (32, 1), (200, 1), (0, 2), (0, 0)])
 @pytest.mark.parametrize("variant", ["bo", "lo"])
-def test_schedule_form_capped_grids(variant, cap):
+def test_schedule_form_capped_grids(variant, cap, early):
     """k_steps_reg at config 2 on capped grids (tune pipe_grid): a workgroup
     with 40 units stages 40 block programs (steps_tab), one with 80 or 1280
     (>= P blocks) stages every block's program instead, and 200 workgroups
-    leave some with one unit fewer — all bit-exact against the oracle."""
+    leave some with one unit fewer; the default grid with the first strip's
+    loads always / never ahead of the program staging — all bit-exact against
+    the oracle."""
     side, total, n = 8, 64, 327680
     ranks = rand_ranks(total, n, seed=cap + 5)
-    with t.tuned(pipe_grid=cap):
+    with t.tuned(pipe_grid=cap, steps_early=early):
         got = run_plan(t.SWING, {"bo": t.BO, "lo": t.LO}[variant], side, total, ranks, t.EXEC_STEPS)
     want = [r.copy() for r in ranks]
     oracle.allreduce(variant, t.SWING, side, want, total)
