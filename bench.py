@@ -1156,6 +1156,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                 peer.clear_status()
                 dist.barrier()
     transport = choose_transport(quick, verify)
+    if transport is None:   # every verified candidate had a peer wait give up in its timing
+        raise RuntimeError(f"no transport timed without a peer timeout on this machine: {verify}")
 
     def step(i):
         run(transport, bufs[i % len(bufs)])
