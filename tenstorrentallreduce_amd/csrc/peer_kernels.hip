@@ -1314,6 +1314,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 //   fin:     (the flush launch, cur null) mid's results — pushed by the owned
 //            sums at the start of every GPU's flush launch — polled, mid's rows
 //            written
+// (the order of the TAIL 0 form without late polls; TAIL 1 / 2 move the owned
+// sums to the launch end / ahead of its last row stores, and late polls
+// (TAIL & 4, the default with TAIL 2) move old's result polls into A(cur 0),
+// between tile 0's tree and its partial push, behind a workgroup barrier)
 // Hand-offs per tile are ordered by the workgroup that serves the tile on every
 // GPU (the same index): GPU g polls old = bucket i-2's result of tile t before
 // it pushes bucket i's partial of t, and the owner reads bucket i's partials of
