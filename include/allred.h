@@ -630,9 +630,11 @@ int allred_peer_status(allred_peer* peer, uint32_t* status);
  * timed out (ALLRED_PEER_TIMEOUT), else ALLRED_OK. */
 int allred_peer_check(allred_peer* peer, void* stream);
 /* Clears the status word (ALLRED_PEER_TIMEOUT is sticky: once set, every later bounded
- * wait of this peer gives up at once).  Call with no kernel of this peer in flight (after
- * allred_peer_check): the calls that follow start from a clean status, new epochs and
- * fresh LL words, so one timed-out sequence does not poison the next.  ABI 5. */
+ * wait of this peer gives up at once) through the null stream, and nothing else.  Call
+ * with no kernel of this peer in flight (after allred_peer_check).  The call counter
+ * keeps advancing, so the next call's LL words and flags carry epochs no timed-out call
+ * wrote.  Returns ALLRED_ERR_ARG while a pipelined sequence (allred_peer_hier_x /
+ * allred_peer_hier_x2) is pending: finish it first.  ABI 5. */
 int allred_peer_clear_status(allred_peer* peer);
 int allred_peer_destroy(allred_peer* peer);
 

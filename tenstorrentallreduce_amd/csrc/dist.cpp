@@ -574,6 +574,8 @@ int allred_comm_init_all(int ndev, const int* devices, allred_comm** out) {
         cs[(size_t)i]->device = devices[i];
     }
     int st = ALLRED_OK;
+    int prev_dev = 0;   // the caller's current device, restored below (ncclCommInitAll leaves it alone)
+    if (hipGetDevice(&prev_dev) != hipSuccess) prev_dev = -1;
     if (ncclGroupStart() != ncclSuccess) st = ALLRED_ERR_RCCL;
     for (int i = 0; i < ndev && st == ALLRED_OK; ++i) {
         ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
@@ -583,6 +585,7 @@ int allred_comm_init_all(int ndev, const int* devices, allred_comm** out) {
         if (r != ncclSuccess && r != ncclInProgress) st = ALLRED_ERR_RCCL;
     }
     const ncclResult_t ge = ncclGroupEnd();
+    if (prev_dev >= 0) (void)hipSetDevice(prev_dev);
     if (st == ALLRED_OK && ge != ncclSuccess && ge != ncclInProgress) st = ALLRED_ERR_RCCL;
     for (int i = 0; i < ndev && st == ALLRED_OK; ++i) st = settle(cs[(size_t)i], init_timeout_ms(cs[(size_t)i]), Fault::init);
     if (st != ALLRED_OK) {

@@ -461,6 +461,11 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
     R->bytes_per_rank = bytes;
     R->total_nodes = N;
     if (o->share_device && o->transport == ALLRED_TRANSPORT_RCCL && G > 1) return ALLRED_ERR_UNSUPPORTED;
+    // the peer windows sum mem_2D in fp32 only (allred_peer_dist_allreduce): refused here,
+    // before any GPU memory is allocated, not in every group's warm-up
+    if (o->transport == ALLRED_TRANSPORT_PEER && plan.variant == ALLRED_MEM && plan.mode != ALLRED_MULTI_LOCAL &&
+        plan.desc.mem_accum == ALLRED_ACC_BF16)
+        return ALLRED_ERR_UNSUPPORTED;
     const int dev0 = a->device > 0 ? a->device : 0;
     std::vector<int> devs((size_t)G);
     for (int g = 0; g < G; ++g) devs[(size_t)g] = o->share_device ? dev0 : dev0 + g;
@@ -536,64 +541,83 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 Group& gr = grs[(size_t)g];
                 int& s = status[(size_t)g];
                 const uint16_t* in = h_in + (size_t)g * L * n;
-                s = be->open(gr);
+                // every call runs only while this thread is healthy; the first failure
+                // raises the shared cancel at once (the peers' waits give up instead of
+                // running into their deadlines) and this thread skips its own exchanges
+                auto step = [&](auto&& call) {
+                    if (s != ALLRED_OK) return;
+                    s = call();
+                    if (s != ALLRED_OK) be->fail();
+                };
+                // every way out of a failed thread: one more cancel-aware drain, so work
+                // it already queued (RCCL kernels waiting for aborted peers) is aborted
+                // before close() frees the memory it points at (a hipFree syncs the device)
+                bool opened = false;
+                auto leave = [&] {
+                    if (s != ALLRED_OK && opened) (void)be->drain(gr);
+                };
+                step([&] { return be->open(gr); });
+                opened = s == ALLRED_OK;
                 mark(g, "open", s);
                 // warm-up on a scratch copy (connection setup, code-object loads stay untimed)
-                if (s == ALLRED_OK) s = be->put(gr, gr.tmp, in, mine);
+                step([&] { return be->put(gr, gr.tmp, in, mine); });
                 mark(g, "put", s);
                 // every thread agrees before any exchange: one failed setup ends all
                 if (!agree(g, s, 0)) {
                     if (s == ALLRED_OK) s = ALLRED_ERR_TRANSPORT;   // another GPU failed to set up
-                    return;
+                    return leave();
                 }
                 mark(g, "agree1", s);
-                if (a->run_kernel) s = be->reduce(gr, gr.tmp);
+                if (a->run_kernel) step([&] { return be->reduce(gr, gr.tmp); });
                 // fault injection (tests): GPU multi_fault - 33 fails its warm-up; every
                 // thread must skip the timed region and return
-                if (s == ALLRED_OK && tune(Tune::multi_fault) == 33 + g) s = ALLRED_ERR_TRANSPORT;
+                if (tune(Tune::multi_fault) == 33 + g) step([] { return (int)ALLRED_ERR_TRANSPORT; });
                 mark(g, "warm-launch", s);
-                if (s == ALLRED_OK) s = be->drain(gr);
+                step([&] { return be->drain(gr); });
                 mark(g, "warm-drain", s);
                 // ... and again after the warm-up (a GPU whose warm-up failed must not
                 // leave the others alone in the timed exchanges)
                 if (!agree(g, s, 1)) {
                     if (s == ALLRED_OK) s = ALLRED_ERR_TRANSPORT;
-                    return;
+                    return leave();
                 }
                 // timed: H2D | allreduce | D2H (the reference's EnqueueWriteBuffer,
                 // EnqueueProgram + Finish, EnqueueReadBuffer; allred_helper.hpp:84-96)
                 mark(g, "agree2", s);
-                auto step = [&](int x) { if (s == ALLRED_OK) s = x; };
-                step(be->mark(gr, 0));
-                step(be->put(gr, gr.buf, in, mine));
-                step(be->mark(gr, 1));
+                step([&] { return be->mark(gr, 0); });
+                step([&] { return be->put(gr, gr.buf, in, mine); });
+                step([&] { return be->mark(gr, 1); });
                 // fault injection (tests): GPU multi_fault - 1 fails its timed allreduce before any
-                // exchange, while its peers are inside theirs: every thread must still return
-                if (a->run_kernel && tune(Tune::multi_fault) == g + 1) step(ALLRED_ERR_TRANSPORT);
+                // exchange, while its peers are inside theirs: it never joins them, they are
+                // cancelled, and every thread still returns
+                if (a->run_kernel && tune(Tune::multi_fault) == g + 1) step([] { return (int)ALLRED_ERR_TRANSPORT; });
                 mark(g, "timed-put", s);
-                if (a->run_kernel) step(be->reduce(gr, gr.buf));
+                if (a->run_kernel) step([&] { return be->reduce(gr, gr.buf); });
                 mark(g, "timed-launch", s);
-                step(be->mark(gr, 2));
+                step([&] { return be->mark(gr, 2); });
                 // Finish before the read-back, as the reference's helper does: a D2H copy
                 // queued behind a waiting allreduce can hold the copy engine that another
                 // group's H2D (which its allreduce waits for) is queued behind (groups
                 // sharing one GPU share its SDMA engines: profiles/r04_multi_share_trace.txt)
-                step(be->drain(gr));
+                step([&] { return be->drain(gr); });
                 mark(g, "timed-finish", s);
-                step(be->get(gr, h_out + (size_t)g * L * n, gr.buf, mine));
-                step(be->mark(gr, 3));
-                step(be->drain(gr));
+                step([&] { return be->get(gr, h_out + (size_t)g * L * n, gr.buf, mine); });
+                step([&] { return be->mark(gr, 3); });
+                step([&] { return be->drain(gr); });
                 mark(g, "timed-drain", s);
-                step(be->times(gr));
-                if (s != ALLRED_OK) be->fail();
+                step([&] { return be->times(gr); });
+                leave();
             });
         }
         for (auto& x : th) x.join();
+        for (int g = 0; g < G && st == ALLRED_OK; ++g) st = status[(size_t)g];
+        // after a failure the communicators / peer windows go first: an aborted
+        // communicator's kernels have left their waits before any group's memory is freed
+        if (st != ALLRED_OK) be->close_all();
         // the groups' memory, events and streams released once every thread is done: a
         // hipFree synchronises the device, which groups sharing one GPU must not do while
         // another group still has work queued behind it
         for (Group& gr : grs) be->close(gr);
-        for (int g = 0; g < G && st == ALLRED_OK; ++g) st = status[(size_t)g];
         // a thread that failed first reports its own status, not the others' TRANSPORT
         for (int g = 0; g < G; ++g)
             if (status[(size_t)g] != ALLRED_OK && status[(size_t)g] != ALLRED_ERR_TRANSPORT) {

@@ -523,6 +523,7 @@ int allred_peer_status(allred_peer* p, uint32_t* out) {
 
 int allred_peer_clear_status(allred_peer* p) {
     if (!p) return ALLRED_ERR_ARG;
+    if (p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;   // a pipelined sequence is open: flush it first
     DeviceGuard guard(p->device);
     // the null stream only (no device-wide sync: other groups of this process may be mid-exchange)
     if (hipMemsetAsync(p->status, 0, 4, nullptr) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess)

@@ -187,3 +187,39 @@ def test_host_twin_failed_warmup_skips_the_timed_region(monkeypatch, g, bad):
         dt = time.monotonic() - t0
     assert e.value.status == t._lib.ERR_TRANSPORT
     assert dt < 20, dt
+
+
+@pytest.mark.parametrize("g,bad", [(2, 1), (4, 3)])
+def test_host_twin_failed_gpu_skips_its_exchange(monkeypatch, capfd, g, bad):
+    """The failed GPU's thread never enters its timed exchange (its reduce is
+    skipped, not merely overruled), so every other thread's exchange is ended
+    by the cancel, not completed: their timed-launch status is the transport
+    error (ALLRED_MULTI_TRACE phases).  Advisor r04: the status guard must skip
+    the call itself."""
+    _env(monkeypatch, None)
+    monkeypatch.setenv("ALLRED_MULTI_TRACE", "1")
+    argv = ["x", "1", "1", "8", "13", "5", "32", "0", "1"]
+    with t.tuned(multi_fault=bad):
+        with pytest.raises(t.AllredError) as e:
+            t.run_multi(argv, t.BO, gpus=g, transport=t.TRANSPORT_HOST, timeout_ms=60000, outputs=False)
+    assert e.value.status == t._lib.ERR_TRANSPORT
+    err = capfd.readouterr().err
+    launch = {}
+    for line in err.splitlines():
+        f = line.split()
+        if len(f) >= 6 and f[0] == "multi-trace" and f[2] == "timed-launch":
+            launch[int(f[1][1:])] = int(f[-1])
+    assert sorted(launch) == list(range(g)), err
+    assert all(s == t._lib.ERR_TRANSPORT for s in launch.values()), launch
+
+
+def test_peer_mem_bf16_refused_before_any_gpu_call(monkeypatch):
+    """mem_2D with bf16 accumulation over the peer windows (fp32 only there) is
+    refused by allred_run_multi before the backend opens: on this GPU-less
+    container the call returns ERR_UNSUPPORTED, not a HIP error."""
+    _env(monkeypatch, None)
+    monkeypatch.setenv("ALLRED_MEM_ACC", "bf16")
+    with pytest.raises(t.AllredError) as e:
+        t.run_multi(["x", "1", "1", "4", "13", "40", "32"], t.MEM, gpus=8, transport=t.TRANSPORT_PEER,
+                    outputs=False)
+    assert e.value.status == t._lib.ERR_UNSUPPORTED
