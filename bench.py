@@ -935,17 +935,17 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   peer_mem_x  consecutive buckets pipelined: bucket i's broadcast and bucket i+1's tree in
     #               one pass (k_tree_bcast_x), then bucket i+1's partial through the one-kernel
     #               mem_2D exchange over the peer windows (k_peer_oneshot)
-    #   peer_hier   ONE kernel: tree -> mem_2D across GPUs -> broadcast (k_hier_oneshot)
-    #   peer_hier_ll  the same step, every cross-GPU hand-off an LL push (k_hier_ll)
-    #   peer_hier_pipe  the same LL hand-offs on the lagged-store pipeline (k_hier_pipe)
+    #   peer_hier_ll  ONE kernel: tree -> mem_2D across GPUs -> broadcast, every cross-GPU
+    #                 hand-off an LL push (k_hier_ll)
     #   peer_hier_x   the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
     #                 reads bucket i+1 while it writes bucket i; the last flush is timed)
-    #   peer_hier_x2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
-    #                 owned tiles, writes bucket i-2; every poll waits for the previous launch)
-    #   peer_hier_x2t the same with bucket i-1's owned sums at the END of launch i (tune
-    #                 hier_x2_tail: its polls never wait; the result polls wait like k_hier_x's)
-    #   peer_hier_x2t2  the owned sums before launch i's last row stores (hier_x2_tail=2)
     #   peer_hier_xr  k_hier_x with R(cur) ahead of bucket i-1's last row stores (hier_x_rearly)
+    #   peer_hier_x2t2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
+    #                 owned tiles before its last row stores, writes bucket i-2; every poll waits
+    #                 for the previous launch)
+    # (retired in round 5, every measurement slower — profiles/README.md: the per-tile flag
+    # form k_hier_oneshot, the pipelined LL form k_hier_pipe, the flag hand-off forms of
+    # k_hier_ll / _x / _x2, and k_hier_x2's owned sums at the launch start / end)
     # Every transport runs only once verified on THIS machine (verify_transport: the
     # exact sum of per-row 0/1 inputs and the reference's closed form, both computed
     # without any transport); the one-kernel peer forms must also equal the launch
@@ -954,14 +954,13 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     peer_box = [None]
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
     pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
-    pend_kind = [None]   # its transport (peer_hier_x / peer_hier_xr / peer_hier_xf)
+    pend_kind = [None]   # its transport (peer_hier_x / peer_hier_xr)
     rearly = [None]
-    pend2 = [False]   # peer_hier_x2 / _x2t: the kind whose buckets are started and not finished (flush())
+    pend2 = [False]   # peer_hier_x2t2: the kind whose buckets are started and not finished (flush())
     pend3 = [False]   # rccl_x: a bucket is started and not finished (flush())
     pend4 = [None, 0]   # peer_mem_x: the started bucket and the partial slot it used (flush())
     mem_parts = [torch.empty(ELEMS, dtype=torch.int16, device=dev) for _ in range(2)]
     tail = [None]
-    handoff = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
     def x2_tail(v):   # the host-side switch between the k_hier_x2 owned-sum placements, read at launch
@@ -969,19 +968,13 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             t.tune("hier_x2_tail", int(v))
             tail[0] = v
 
-    def set_handoff(flg):   # LL words / data + flags (k_hier_x, k_hier_x2; latched per sequence)
-        if handoff[0] != flg:
-            t.tune("hier_handoff", flg)
-            handoff[0] = flg
-
     def set_rearly(v):   # k_hier_x: R(cur) ahead of the previous bucket's last row stores (read at launch)
         if rearly[0] != v:
             t.tune("hier_x_rearly", v)
             rearly[0] = v
 
-    def x2_kind(kind):   # tail / hand-off form of a k_hier_x2 transport
-        x2_tail(2 if kind == "peer_hier_x2t2" else int(kind in ("peer_hier_x2t", "peer_hier_x2tf")))
-        set_handoff(int(kind in ("peer_hier_x2f", "peer_hier_x2tf")))
+    def x2_kind(kind):   # owned-sum placement of a k_hier_x2 transport
+        x2_tail(2)
 
     def flush():
         peer = peer_box[0]
@@ -992,7 +985,6 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             t.broadcast(pend4[0], ELEMS, ELEMS, RANKS, mem_parts[pend4[1]].data_ptr(), stream)
             pend4[0] = None
         if pend[0] is not None:
-            set_handoff(int(pend_kind[0] == "peer_hier_xf"))
             set_rearly(int(pend_kind[0] == "peer_hier_xr"))
             peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
             pend[0] = None
@@ -1028,10 +1020,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce(out.data_ptr(), ELEMS, stream)   # the partial: mem_2D across the GPUs
             pend4[0], pend4[1] = b.data_ptr(), slot
             return
-        if kind in ("peer_hier_x", "peer_hier_xr", "peer_hier_xf"):   # buckets pipelined: this call finishes the previous one
+        if kind in ("peer_hier_x", "peer_hier_xr"):   # buckets pipelined: this call finishes the previous one
             if pend2[0] or pend3[0] or pend4[0] is not None or (pend[0] is not None and pend_kind[0] != kind):
                 flush()
-            set_handoff(int(kind == "peer_hier_xf"))
             set_rearly(int(kind == "peer_hier_xr"))
             peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
             pend[0], pend_kind[0] = b.data_ptr(), kind
@@ -1051,9 +1042,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         else:
             if mode[0] != kind:
                 peer.set_oneshot_max(0 if kind == "peer_launches" else (4 << 20))
-                peer.set_hier_ll({"peer_hier_ll": 1, "peer_hier_llf": 1, "peer_hier_pipe": 2}.get(kind, 0))
+                peer.set_hier_ll(int(kind == "peer_hier_ll"))
                 mode[0] = kind
-            set_handoff(int(kind == "peer_hier_llf"))   # read at launch (the x / x2 kinds set it too)
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
     verify = {}
@@ -1127,8 +1117,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                            f", peer windows: {peer_err}")
     candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
     if peer is not None:
-        for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier", "peer_hier_ll",
-                                  "peer_hier_llf", "peer_hier_pipe", "peer_hier_x", "peer_hier_xr", "peer_hier_xf", *X2_KINDS)):
+        for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier_ll", "peer_hier_x",
+                                  "peer_hier_xr", *X2_KINDS)):
             if check(kind, 9100 + 10 * i):
                 candidates.append(kind)
     if not candidates:
@@ -1286,13 +1276,10 @@ HEADLINE_DONE = threading.Event()
 FALLBACK_DONE = threading.Event()
 
 # the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
-ONE_LAUNCH = {"peer_hier": "k_hier_oneshot", "peer_hier_ll": "k_hier_ll", "peer_hier_llf": "k_hier_ll<flags>",
-              "peer_hier_pipe": "k_hier_pipe",
-              "peer_hier_x": "k_hier_x", "peer_hier_xr": "k_hier_x<re,late>", "peer_hier_xf": "k_hier_x<flags>", "peer_hier_x2": "k_hier_x2<false>", "peer_hier_x2t": "k_hier_x2<true>",
-              "peer_hier_x2t2": "k_hier_x2<tail2,late>",
-              "peer_hier_x2f": "k_hier_x2<false, flags>", "peer_hier_x2tf": "k_hier_x2<true, flags>"}
-# the k_hier_x2 transports: owned sums at the start / the end (t) of a launch, LL / flag (f) hand-offs
-X2_KINDS = ("peer_hier_x2", "peer_hier_x2t", "peer_hier_x2t2", "peer_hier_x2f", "peer_hier_x2tf")
+ONE_LAUNCH = {"peer_hier_ll": "k_hier_ll", "peer_hier_x": "k_hier_x", "peer_hier_xr": "k_hier_x<re,late>",
+              "peer_hier_x2t2": "k_hier_x2<tail2,late>"}
+# the k_hier_x2 transports (owned sums before a launch's last row stores)
+X2_KINDS = ("peer_hier_x2t2",)
 
 
 def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> dict:
@@ -1322,34 +1309,17 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                      "2D Swing BO over RCCL/xGMI",
            "peer_launches": "on-GPU tree reduce, mem_2D across GPUs over peer-mapped windows (launches), broadcast",
            "peer_swing": "on-GPU tree reduce, 2D Swing BO over peer-mapped xGMI windows (one kernel), broadcast",
-           "peer_hier": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs over peer-mapped xGMI "
-                        "windows, broadcast (per-tile flags)",
-           "peer_hier_pipe": "ONE kernel, pipelined per tile: on-GPU tree reduce, mem_2D one-shot across GPUs with LL "
-                             "pushes into peer-mapped xGMI windows, broadcast (tile j read, j-1 summed, j-2 written)",
            "peer_hier_x": "ONE kernel per bucket, consecutive buckets pipelined (K buckets in K + 1 launches, all "
                           "inside the timed region): on-GPU tree reduce of bucket i+1 while bucket i's rows are written, "
                           "mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
-           "peer_hier_x2": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
-                           "timed region): launch i reads bucket i, sums bucket i-1's owned tiles and writes bucket "
-                           "i-2's rows, mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
-           "peer_hier_x2t": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
-                            "timed region): launch i reads bucket i, writes bucket i-2's rows and at its end sums "
-                            "bucket i-1's owned tiles, mem_2D one-shot across GPUs with LL pushes into peer-mapped "
-                            "xGMI windows",
-           "peer_hier_x2t2": "ONE kernel per bucket, two buckets deep (as peer_hier_x2t) with bucket i-1's owned "
-                             "sums before the launch's last row stores, LL pushes into peer-mapped xGMI windows",
+           "peer_hier_x2t2": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
+                             "timed region): launch i reads bucket i, writes bucket i-2's rows and, before its last "
+                             "row stores, sums bucket i-1's owned tiles; mem_2D one-shot across GPUs with LL pushes "
+                             "into peer-mapped xGMI windows",
            "peer_hier_xr": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with the owned "
                            "sums ahead of the previous bucket's last row stores, LL pushes into peer-mapped xGMI windows",
-           "peer_hier_xf": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with flag "
-                           "hand-offs: plain data pushes into peer-mapped xGMI windows, one flag per workgroup and peer",
-           "peer_hier_x2f": "ONE kernel per bucket, two buckets deep (as peer_hier_x2) with flag hand-offs: plain "
-                            "data pushes into peer-mapped xGMI windows, one flag per workgroup and peer",
-           "peer_hier_x2tf": "ONE kernel per bucket, two buckets deep, owned sums at the end of a launch (as "
-                             "peer_hier_x2t) with flag hand-offs: plain data pushes, one flag per workgroup and peer",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
-                           "(data+epoch words) into peer-mapped xGMI windows, broadcast",
-           "peer_hier_llf": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with plain data pushes "
-                            "into peer-mapped xGMI windows and one flag per workgroup and peer, broadcast"}[transport]
+                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
     v = extras.get("transport_verified", {}).get(transport, {})
     return {
         "metric": METRIC,

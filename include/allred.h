@@ -241,8 +241,8 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     tiles as max(1, round(T / 1280)) launches over consecutive tile ranges
  *                     (0 = one launch); allred_plan_launches counts them
  *   hier_x2_tail      2: k_hier_x2 (allred_peer_allreduce_pipelined2) sums the owned tiles of the
- *                     middle bucket before the launch's last row stores (LL hand-offs; the flag form
- *                     takes 1); 1: at the end of each launch; 0: at its start
+ *                     middle bucket before the launch's last row stores; 1: at the end of each
+ *                     launch; 0: at its start
  *   lo_tree_min_tiles 64: a 64-rank rank-uniform LO plan (every RecDub schedule) takes the BO tree
  *                     pass from this many 256-element tiles per rank, the register butterfly below
  *   tree_bcast_lag    1: k_tree_bcast_x (allred_dist_allreduce_pipelined) stores the previous
@@ -255,9 +255,6 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   hier_x_lag        1: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
  *                     iteration after the tree of the matching tile of the bucket being read; 0: in
  *                     the same iteration
- *   hier_handoff      0: k_hier_x / k_hier_x2 hand-offs as LL words (4 data bytes + epoch per 8 bytes);
- *                     1: plain data + one flag per workgroup and peer (read one launch later, or after
- *                     the R phase's flag wait); a sequence keeps the form of its first call
  *   hier_x_chunked    0: k_hier_x / k_hier_x2 stage results in chunks of 8 tiles only when a workgroup
  *                     has more than 8 tiles; 1: always (A/B timing of the chunk bookkeeping)
  *   steps_tab         1: k_steps_reg (BO) stages only the programs of its own units' blocks (when fewer
@@ -578,11 +575,12 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * (allred_mem_2D semantics over the per-GPU trees).  Every rank must use the
  * same setting.  Replaces nothing in the reference (its mem_2D phases sync
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
-/* 0 = off, 1 = k_hier_ll (all tiles read, owned tiles summed, all tiles
- * written: three phases), 2 = k_hier_pipe (the same hand-offs on the
- * lagged-store pipeline: iteration j reads tile j, sums owned tile j-1 and
- * writes tile j-2).  (The specialised-wave form of round 1 lives in
- * tools/ubench/ws_trace.hip: 27-38 us vs 18 at W = 1, never a candidate.) */
+/* 0 = off (tree, the mem_2D exchange, broadcast as launches), 1 = k_hier_ll
+ * (all tiles read, owned tiles summed, all tiles written: three phases);
+ * other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
+ * profiles/README.md — the per-tile flag form k_hier_oneshot, 19.9 us at
+ * W = 1, and the pipelined LL form k_hier_pipe, 17.8 us, in round 5; the
+ * specialised-wave form of round 1, 27-38 us.) */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
 /* Caps the grid of the hierarchical one-kernel forms, k_peer_mem_ll and the
  * scheduled form (allred_peer_dist_allreduce) at `groups` workgroups (0 =

@@ -41,7 +41,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
-    rccl_fault, hier_handoff, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll,
+    rccl_fault, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll,
     count
 };
 int64_t tune(Tune key);
@@ -153,41 +153,26 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
 int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint32_t* const* flags, int me,
                            uint16_t* bucket, const PeerProg& prog, uint32_t base_epoch, uint32_t* status,
                            unsigned max_groups, void* stream);
-// hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast.
-// wins[q] = GPU q's window for this parity ([partial n][result n]); hflags[q]: [tiles][nranks + 1]
-int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
-                        uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
-                        unsigned max_grid, void* stream);
-// the same step with LL (push) hand-offs: ll[q] = GPU q's LL area for this parity,
-// [inbox box_words words][result box box_words words]; nranks <= 8; epoch grows by 1 per call
-// xfl: null = LL hand-offs, else every GPU's hand-off flag block (kXFlagBytes; parity = this call's LL parity)
+// hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast with LL
+// (push) hand-offs: ll[q] = GPU q's LL area for this parity, [inbox box_words words][result box
+// box_words words]; nranks <= 8; epoch grows by 1 per call
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   uint32_t* const* xfl, uint32_t parity, void* stream);
-// the same step on the lagged-store pipeline (k_hier_pipe): tree / owner sum / row stores of
-// tiles j, j-1, j-2 in one iteration; same arguments and bits as launch_hier_ll
-int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                     size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                     void* stream);
-// k_hier_x / k_hier_x2 hand-off flag block per GPU: [2 parities][2 kinds][8 GPUs][512 workgroups] u32
-constexpr size_t kXFlagBytes = 4 * 2 * 2 * 8 * 512;
+                   void* stream);
 // the hierarchical step across consecutive buckets (k_hier_x): finishes `prev` (may be null)
 // and starts `cur` (may be null) in one launch; llc / llp: every GPU's LL area of cur's /
 // prev's parity; ALLRED_ERR_UNSUPPORTED beyond kHierXMaxTiles tiles per workgroup
 int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
                   uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                  uint32_t* status, unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream);
+                  uint32_t* status, unsigned max_grid, void* stream);
 // the same step two buckets deep (k_hier_x2): starts `cur`, sums the owned tiles of the bucket
 // the previous launch started (llm non-null: its parity's LL areas), writes `old` (started two
 // launches ago; llo: its parity); the flush launch (cur null) also writes that middle bucket
 // `fin` from its results
-// xfl: null = LL hand-offs; else every GPU's hand-off flag block (kXFlagBytes, the FLG form: data
-// in the LL slots without epochs, one flag per workgroup and peer; parities = the LL parities of
-// cur / mid / old in bits 0 / 1 / 2)
 int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
                    uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
-                   unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream);
+                   unsigned max_grid, void* stream);
 // allred_mem_2D across GPUs with LL pushes (k_peer_mem_ll): area_words >= 8 * (n / 8 rounded up to 32)
 int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket, size_t n, uint64_t area_words,
                        uint32_t epoch, uint32_t* status, unsigned max_groups, void* stream);

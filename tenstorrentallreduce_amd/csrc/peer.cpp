@@ -15,9 +15,9 @@
 // Buckets up to allred_peer_set_oneshot_max() bytes (default 4 MiB) run the
 // same three phases as ONE kernel (k_peer_oneshot): workgroup g syncs only
 // with workgroup g of the peers, through per-workgroup flag slots.  With 64
-// local ranks per GPU the local tree and the broadcast join that kernel too
-// (k_hier_oneshot, per-tile flags; k_hier_ll, the same step with LL push
-// hand-offs, LL boxes; both live in the flag allocation behind the flags).
+// local ranks per GPU the local tree and the broadcast join one kernel with LL
+// push hand-offs (k_hier_ll, k_hier_x, k_hier_x2; the LL boxes live in the
+// flag allocation behind the flags).
 // Windows are double-buffered by call parity: call k+2 can only overwrite a
 // window after every peer passed call k+1's first barrier, i.e. finished
 // reading call k's windows.
@@ -38,12 +38,9 @@ struct allred_peer {
     // process hung on the MI355X boxes (tools/peer_open_probe.py)
     uint16_t* win[2] = {};
     uint16_t* stage = nullptr;      // staging window of the push form (k_peer_sched_push), max_elems
-    uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp, then hfl and LL
+    uint32_t* flags = nullptr;      // own flag area (uncached), layout in internal.hpp, then the LL boxes
     uint32_t* status = nullptr;     // device status word
     bool flags_uncached = false, win_uncached = false;
-    size_t hfl_off = 0;             // byte offset of the per-tile flags in the flag allocation
-    size_t hfl_bytes = 0;
-    uint32_t* peer_hfl[ALLRED_MAX_NODES] = {};
     uint16_t* peer_win[ALLRED_MAX_NODES][2] = {};
     uint16_t* peer_stage[ALLRED_MAX_NODES] = {};
     uint64_t sched_push_min = 0;    // BO buckets of at least this many bytes take the push form (0: never)
@@ -60,9 +57,7 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
-    size_t xfl_off = 0;             // k_hier_x2's hand-off flags (FLG form) behind the LL boxes
-    uint32_t* peer_xfl[ALLRED_MAX_NODES] = {};
-    int hier_ll = 0;                // 0 off, 1 k_hier_ll (LL push hand-offs), 2 k_hier_pipe (the same, pipelined)
+    int hier_ll = 0;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
@@ -71,14 +66,12 @@ struct allred_peer {
     uint32_t pipe_k = 0;            // that bucket's call number (epoch pipe_k + 1, LL parity pipe_k & 1)
     uint16_t* pipe_buf = nullptr;   // that bucket, and its size: the next call must finish exactly it
     uint64_t pipe_elems = 0;
-    bool pipe_flg = false;          // the sequence's hand-off form (tune hier_handoff at its first call)
     // allred_peer_allreduce_pipelined2: up to two started, unfinished buckets, older
     // first; with two, the older one's owned tiles are summed already
     int x2_n = 0;
     uint16_t* x2_buf[2] = {};
     uint32_t x2_k[2] = {};          // their call numbers
     uint64_t x2_elems = 0;          // the sequence's bucket size
-    bool x2_flg = false;            // the sequence's hand-off form (tune hier_handoff at its first call)
 };
 
 extern "C" {
@@ -99,17 +92,13 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     p->max_elems = (max_elems + 127) / 128 * 128;  // LO halves stay 64-element aligned (still <= 2^29)
     // windows are uncached too: peers read them over xGMI straight from HBM, so
     // no write may linger in one of this GPU's eight per-XCD L2s.  The flag
-    // allocation holds, behind the flags of internal.hpp: the hierarchical
-    // form's per-tile flags, [tiles][nranks + 1] for up to max_elems / 2
-    // elements per call (256-element tiles), and the LL boxes for buckets of up
-    // to min(max_elems, 4 Mi) elements (128 words per 256-element tile).
-    p->hfl_off = ((size_t)kPeerFlagBytes + 255) / 256 * 256;
-    p->hfl_bytes = 4 * (size_t)(nranks + 1) * (p->max_elems / 2 / 256 + 1);
+    // allocation holds, behind the flags of internal.hpp, the LL boxes for
+    // buckets of up to min(max_elems, 4 Mi) elements (128 words per
+    // 256-element tile), two parities of [inbox][result box].
     const uint64_t ll_elems = p->max_elems < (4ull << 20) ? p->max_elems : (4ull << 20);
-    p->ll_off = (p->hfl_off + p->hfl_bytes + 255) / 256 * 256;
+    p->ll_off = ((size_t)kPeerFlagBytes + 255) / 256 * 256;
     p->ll_box_words = (ll_elems / 256) * 128;
-    p->xfl_off = (p->ll_off + 2 * 2 * p->ll_box_words * 8 + 255) / 256 * 256;
-    const size_t flag_bytes = p->xfl_off + kXFlagBytes;
+    const size_t flag_bytes = p->ll_off + 2 * 2 * p->ll_box_words * 8;
     const size_t win_bytes = p->max_elems * 2;
     auto release = [p]() {
         for (uint16_t* w : p->win) (void)hipFree(w);
@@ -202,9 +191,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
             p->opened[q] = true;
         }
         uint8_t* f = reinterpret_cast<uint8_t*>(p->peer_flags[q]);
-        p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + p->hfl_off);
         p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + p->ll_off);
-        p->peer_xfl[q] = reinterpret_cast<uint32_t*>(f + p->xfl_off);
     }
     p->connected = true;
     return ALLRED_OK;
@@ -230,9 +217,7 @@ int allred_peer_connect_all(int nranks, allred_peer* const* peers) {
             p->peer_flags[q] = o->flags;
             p->peer_stage[q] = o->stage;
             uint8_t* f = reinterpret_cast<uint8_t*>(o->flags);
-            p->peer_hfl[q] = reinterpret_cast<uint32_t*>(f + o->hfl_off);
             p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + o->ll_off);
-            p->peer_xfl[q] = reinterpret_cast<uint32_t*>(f + o->xfl_off);
         }
     }
     for (int q = 0; q < nranks; ++q) peers[q]->connected = true;   // opened[] stays false: nothing to close
@@ -272,11 +257,8 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
         llc[q] = p->peer_ll[q] + (kc & 1u) * 2 * p->ll_box_words;
         llp[q] = p->peer_ll[q] + (kp & 1u) * 2 * p->ll_box_words;
     }
-    if (!prev) p->pipe_flg = tune(Tune::hier_handoff) != 0;   // a sequence keeps its hand-off form
-    const uint32_t parities = (kc & 1u) | ((kp & 1u) << 1);
     st = launch_hier_x(cur, prev, n, order, cur ? llc : nullptr, prev ? llp : nullptr, p->nranks, p->rank, n,
-                       p->ll_box_words, kc + 1u, kp + 1u, p->status, p->max_groups,
-                       p->pipe_flg ? p->peer_xfl : nullptr, parities, stream);
+                       p->ll_box_words, kc + 1u, kp + 1u, p->status, p->max_groups, stream);
     if (st != ALLRED_OK) return st;
     if (cur) {
         p->pipe_k = kc;
@@ -318,11 +300,9 @@ int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t ele
     area(ko, llo);
     uint16_t* old = has_old ? p->x2_buf[0] : nullptr;
     uint16_t* fin = !cur ? p->x2_buf[p->x2_n - 1] : nullptr;
-    if (p->x2_n == 0) p->x2_flg = tune(Tune::hier_handoff) != 0;   // a sequence keeps its hand-off form
-    const uint32_t parities = (kc & 1u) | ((km & 1u) << 1) | ((ko & 1u) << 2);
     st = launch_hier_x2(cur, old, fin, n, order, cur ? llc : nullptr, p->x2_n > 0 ? llm : nullptr,
                         has_old ? llo : nullptr, p->nranks, p->rank, n, p->ll_box_words, kc + 1u, km + 1u, ko + 1u,
-                        p->status, p->max_groups, p->x2_flg ? p->peer_xfl : nullptr, parities, stream);
+                        p->status, p->max_groups, stream);
     if (st != ALLRED_OK) return st;
     if (!cur) {   // flushed: nothing pending
         p->x2_n = 0;
@@ -358,33 +338,14 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
         for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
-        if (p->hier_ll == 2)
-            st = launch_hier_pipe(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
-                                  p->max_groups, stream);
-        else   // tune hier_handoff 1: plain data + one flag per workgroup and peer (same bits)
-            st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
-                                p->max_groups, tune(Tune::hier_handoff) ? p->peer_xfl : nullptr, p->calls & 1u, stream);
+        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
+                            p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
         return ALLRED_OK;
     }
     const bool one_kernel = n * 2 <= p->oneshot_max && p->win_uncached && p->flags_uncached;
-    if (one_kernel && local_ranks == 64 && n % (256 * (size_t)p->nranks) == 0 && 2 * n <= p->max_elems) {
-        // the whole hierarchical step in one launch (k_hier_oneshot): same bits as
-        // tree_reduce + the mem_2D exchange + broadcast below
-        const uint8_t* order = nullptr;
-        st = local_tree_order(local_algo, local_side, local_ranks, &order);
-        if (st != ALLRED_OK) return st;
-        uint16_t* wins[ALLRED_MAX_NODES];
-        parity_windows(p, wins);
-        st = launch_hier_oneshot(buf, n, order, wins, p->peer_hfl, p->nranks, p->rank, n, p->calls + 1u, p->status,
-                                 p->max_groups, stream);
-        if (st != ALLRED_OK) return st;
-        ++p->calls;
-        p->last_all_peer = true;
-        return ALLRED_OK;
-    }
     if (local_ranks > 1) {
         if (!workspace) return ALLRED_ERR_ARG;
         bucket = static_cast<uint16_t*>(workspace);
@@ -484,7 +445,7 @@ int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
 
 int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
-    if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
+    if (enable < 0 || enable > 1) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
     return ALLRED_OK;
 }

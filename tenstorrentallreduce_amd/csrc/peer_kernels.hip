@@ -423,186 +423,20 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched_push(PeerPtrs pp, PeerSta
     }
 }
 
-// ---- hierarchical one-kernel form: 64 local ranks per GPU -------------------
+// ---- hierarchical one-kernel form: 64 local ranks per GPU, LL (push) hand-offs
 // The whole hierarchical step (local tree of the 64 virtual ranks -> mem_2D
 // across the W GPUs -> broadcast back to the 64 ranks) as ONE persistent
-// launch with per-tile flags, so the xGMI latency of one tile hides behind
-// the HBM streaming of the others.  Tile = 256 elements (512 B per rank row);
-// owner(t) = t / (tiles / W), i.e. the block ownership of allred_mem_2D, so
-// the bits equal tree_reduce + allred_peer_allreduce + broadcast.
-//   A (all my tiles, double-buffered LDS as k_tree_lds_pipe): partial of tile
-//     t -> my window's partial region (local, uncached); flagA[t][me] -> owner.
-//   R (my tiles that I own): wait flagA[t][*]; read the W partials (remote
-//     loads), fp32 sum owner first then ascending, one rounding -> my result
-//     region; flagB[t] -> every GPU.
-//   B (all my tiles): wait flagB[t]; read the result from the owner's window;
-//     store it to the 64 rank rows.
-// A never waits, R waits only for A, B only for R: with the grid resident
-// (2 workgroups per CU) every wait is reached and satisfied.
-struct HierPtrs {
-    uint16_t* win[ALLRED_MAX_NODES];   // GPU q's window, this parity: [partial n][result n]
-    uint32_t* hfl[ALLRED_MAX_NODES];   // GPU q's per-tile flags: [tile][W + 1]
-};
-
-__device__ inline void hier_wait(const uint32_t* f, uint32_t epoch, uint32_t* status) {
-    uint64_t t0 = 0;
-    for (uint64_t spin = 0;; ++spin) {
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) return;
-        if (peer_give_up(spin, t0, status)) return;
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_hier_oneshot(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                         const uint8_t* __restrict__ order, HierPtrs hp, int W, int me,
-                                                         uint64_t n, uint64_t ntiles, uint64_t tiles_per_owner,
-                                                         uint32_t epoch, uint32_t* status) {
-    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    if (threadIdx.x < ALLRED_MAX_NODES) ord_lds[threadIdx.x] = order[threadIdx.x];
-    __syncthreads();
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
-    auto issue = [&](uint64_t t, int b) {
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) {
-            const int r = RPW * w + 2 * k + h;
-            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
-            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
-        }
-    };
-    const uint64_t G = gridDim.x, nvec = n / 8;
-    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    const uint32_t F = (uint32_t)W + 1;
-    uint4* my_partial = reinterpret_cast<uint4*>(hp.win[me]);
-    uint4* my_result = my_partial + nvec;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
-    // ---- A: local trees, partials published.  Each iteration starts with
-    // vmcnt(0): tile j's LDS-DMA and tile j-1's partial store are then done, so
-    // tile j-1's flag goes out there, one iteration late, without draining the
-    // prefetch of tile j+1 (issued after that wait).  (Interleaving R and B
-    // into this loop measured slower: 22.6 vs 19.6 us at W = 1 — each
-    // uncached round trip is then paid once per tile instead of once per batch.)
-    auto publish = [&](uint64_t t) {
-        if (threadIdx.x == 0)
-            __hip_atomic_store(hp.hfl[owner_of(t)] + t * F + me, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    if (mine > 0) issue(tile_of(0), 0);
-    for (int j = 0; j < mine; ++j) {
-        wait_vm<0>();
-        lds_barrier();
-        if (j > 0) publish(tile_of(j - 1));
-        if (j + 1 < mine) issue(tile_of(j + 1), (j + 1) & 1);
-        const uint4* tile = buf[j & 1];
-        const uint64_t v0 = tile_of(j) * TV;
-        const uint8_t* ord = ord_lds + RPW * w + LPL * h;
-        uint4 x[LPL];
-#pragma unroll
-        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
-#pragma unroll
-        for (int s2 = 1; s2 < LPL; s2 *= 2)
-#pragma unroll
-            for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
-        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
-        if (h == 0) part[w * TV + c] = pw;
-        lds_barrier();
-        if (w == 0 && h == 0)
-            st_nt(my_partial + v0 + c,
-                  add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c])));
-    }
-    wait_vm<0>();
-    if (mine > 0) publish(tile_of(mine - 1));
-    // ---- R: the tiles I own, 8 at a time: every flag, then every remote load in flight at once
-    {
-        int owned[8];
-        int no = 0;
-        auto flush = [&]() {
-            for (int i = threadIdx.x; i < no * W; i += kBlock)
-                hier_wait(hp.hfl[me] + tile_of(owned[i / W]) * F + i % W, epoch, status);
-            lds_barrier();
-            const int b = threadIdx.x / TV;
-            if (b < no) {
-                const uint64_t v0 = tile_of(owned[b]) * TV;
-                const uint4 s0 = ld_nt(my_partial + v0 + c);
-                float a[8] = {lo_f(s0.x), hi_f(s0.x), lo_f(s0.y), hi_f(s0.y),
-                              lo_f(s0.z), hi_f(s0.z), lo_f(s0.w), hi_f(s0.w)};
-                for (int q0 = 0; q0 < W; q0 += 8) {   // 8 remote partials in flight at once
-                    uint4 y[8];
-#pragma unroll
-                    for (int i = 0; i < 8; ++i)
-                        if (q0 + i < W && q0 + i != me) y[i] = ld_nt(reinterpret_cast<const uint4*>(hp.win[q0 + i]) + v0 + c);
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        if (q0 + i >= W || q0 + i == me) continue;
-                        a[0] += lo_f(y[i].x); a[1] += hi_f(y[i].x);
-                        a[2] += lo_f(y[i].y); a[3] += hi_f(y[i].y);
-                        a[4] += lo_f(y[i].z); a[5] += hi_f(y[i].z);
-                        a[6] += lo_f(y[i].w); a[7] += hi_f(y[i].w);
-                    }
-                }
-                uint4 o;
-                o.x = pack_rne(a[0], a[1]);
-                o.y = pack_rne(a[2], a[3]);
-                o.z = pack_rne(a[4], a[5]);
-                o.w = pack_rne(a[6], a[7]);
-                st_nt(my_result + v0 + c, o);
-            }
-            wait_vm<0>();     // results are in HBM (uncached) before their flags
-            lds_barrier();
-            for (int i = threadIdx.x; i < no * W; i += kBlock)
-                __hip_atomic_store(hp.hfl[i % W] + tile_of(owned[i / W]) * F + W, epoch, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            no = 0;
-        };
-        for (int j = 0; j < mine; ++j) {
-            if (owner_of(tile_of(j)) != me) continue;
-            owned[no++] = j;
-            if (no == 8) flush();
-        }
-        if (no) flush();
-    }
-    // ---- B: results back to the 64 rank rows, 4 tiles' remote loads in flight at once
-    constexpr int BB = 4;
-    for (int j0 = 0; j0 < mine; j0 += BB) {
-        const int nb = mine - j0 < BB ? mine - j0 : BB;
-        if (threadIdx.x < (unsigned)nb) hier_wait(hp.hfl[me] + tile_of(j0 + (int)threadIdx.x) * F + W, epoch, status);
-        lds_barrier();
-        uint4 res[BB];
-#pragma unroll
-        for (int b = 0; b < BB; ++b) {
-            if (b >= nb) break;
-            const uint64_t t = tile_of(j0 + b);
-            res[b] = ld_nt(reinterpret_cast<const uint4*>(hp.win[owner_of(t)]) + nvec + t * TV + c);
-        }
-#pragma unroll
-        for (int b = 0; b < BB; ++b) {
-            if (b >= nb) break;
-            const uint64_t v0 = tile_of(j0 + b) * TV;
-#pragma unroll
-            for (int k = 0; k < OPS; ++k) {
-                const int r = RPW * w + 2 * k + h;
-                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, res[b]);
-            }
-        }
-    }
-}
-
-// ---- hierarchical one-kernel form, LL (push) variant ------------------------
-// Same bits as k_hier_oneshot (local tree per tile -> mem_2D across the W GPUs,
-// fp32 owner first then ascending, one rounding -> every GPU's 64 rank rows),
-// but every cross-GPU transfer is a PUSH of self-validating 8-byte words
-// (4 bytes of data + the call's epoch, RCCL's "LL" idea): the producer's
+// launch; the same bits as tree_reduce + the mem_2D exchange + broadcast
+// (fp32 owner first then ascending, one rounding).  Tile = 256 elements (512 B
+// per rank row); owner(t) = t / (tiles / W), the block ownership of
+// allred_mem_2D.  Every cross-GPU transfer is a PUSH of self-validating 8-byte
+// words (4 bytes of data + the call's epoch, RCCL's "LL" idea): the producer's
 // relaxed system-scope stores go straight into the consumer's uncached LL
 // area and the consumer polls its OWN memory until every word carries the
 // epoch.  No flag follows the data and no remote load is ever waited for, so
-// each hand-off costs one one-way xGMI trip instead of a flag trip plus a
-// remote read round trip (k_hier_oneshot: A publish -> R remote loads -> B
-// remote loads).
+// each hand-off costs one one-way xGMI trip.  (A per-tile flag form — publish,
+// then remote loads — ran 19.9 us at W = 1 and a pipelined LL form 17.8 us;
+// both were removed in round 5, profiles/README.md.)
 //   A (all my tiles, double-buffered LDS): tile t's partial -> owner o's inbox
 //     slot [t - o*tpo][me] (1 KiB of LL words per tile).
 //   R (my tiles that I own): poll the W slots, fp32 sum owner first then
@@ -661,7 +495,7 @@ __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_
     return make_uint4((uint32_t)w0, (uint32_t)w1, (uint32_t)w2, (uint32_t)w3);
 }
 
-// one poll of an LL slot without waiting (k_hier_pipe / k_hier_x / k_hier_x2 / k_hier_ll R)
+// one poll of an LL slot without waiting (k_hier_x / k_hier_x2 / k_hier_ll R)
 __device__ __forceinline__ void ll_load(const uint64_t* src, uint64_t (&wd)[4]) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -693,70 +527,10 @@ __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, 
     return make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
 }
 
-// ---- hand-off flags (FLG forms of k_hier_ll / k_hier_x / k_hier_x2, tune hier_handoff = 1)
-// LL words carry 4 data bytes + a 4-byte epoch each: every hand-off moves twice
-// its data.  In the FLG form the data go as plain system-coherent 16-byte
-// stores (sc0 sc1, the LL stores' policy) into the first 512 bytes of the same
-// LL slot, and each workgroup raises ONE flag per peer GPU when every wave's
-// hand-off stores of the launch have completed (s_waitcnt vmcnt(0): the one
-// in-order counter — the ordering k_peer_oneshot's barriers already rely on).
-// The consumer is the same workgroup index on the peer (tile t is served by
-// workgroup t mod G on every GPU) one launch later: it polls its W flags, then
-// reads the data.  Flags: [parity][0 partials | 1 results][GPU][workgroup] in
-// each GPU's flag allocation; values = the bucket's epoch (monotonic).
-constexpr int kXFlagGroups = 512;
-constexpr size_t kXFlagWords = 2 * 2 * kLLMaxGpus * kXFlagGroups;
-static_assert(kXFlagWords * 4 == kXFlagBytes, "internal.hpp kXFlagBytes: the flag block the host allocates");
-struct XFPtrs {
-    uint32_t* f[kLLMaxGpus];   // GPU q's hand-off flag block
-};
-__device__ __forceinline__ uint32_t* xflag(uint32_t* base, uint32_t parity, int kind, int q) {
-    return base + (((parity * 2 + kind) * kLLMaxGpus + q) * kXFlagGroups + blockIdx.x);
-}
-// two system-scope 8-byte stores (global_store_dwordx2 sc0 sc1, the LL stores' policy): compiler-issued,
-// so the compiler also keeps the data VGPRs alive until the stores have read them (an inline-asm
-// dwordx4 store hid that from it and corrupted data); FLG push accounting counts 2 ops per store
-constexpr int kSys16Ops = 2;
-__device__ __forceinline__ void st_sys16(uint4* p, uint4 v) {
-    uint64_t* q = reinterpret_cast<uint64_t*>(p);
-    __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ uint4 ld_sys16(const uint4* p) {
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(p);
-    const uint64_t a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
-}
-// every wave's stores so far have completed; then lane q raises the flag in GPU q's block
-__device__ __forceinline__ void xflag_raise(const XFPtrs& xf, uint32_t parity, int kind, int me, int W, uint32_t e) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    if ((int)threadIdx.x < W)
-        __hip_atomic_store(xflag(xf.f[threadIdx.x], parity, kind, me), e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-// lane q waits for GPU q's flag in this GPU's block, then the workgroup goes on (bounded)
-__device__ __forceinline__ void xflag_wait(uint32_t* mine, uint32_t parity, int kind, int W, uint32_t e,
-                                           uint32_t* status) {
-    if ((int)threadIdx.x < W) {
-        const uint32_t* f = xflag(mine, parity, kind, threadIdx.x);
-        uint64_t t0 = 0;
-        for (uint64_t spin = 0;; ++spin) {
-            if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= e) break;
-            if (peer_give_up(spin, t0, status)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    lds_barrier();
-}
-
-template <bool FLG>
 __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status, XFPtrs xf, uint32_t par) {
-    // FLG: par = this call's LL parity; partials / results move as plain data, one flag per workgroup and peer
-    auto dslot = [&](uint64_t* base, uint64_t slot, int col) { return reinterpret_cast<uint4*>(base + slot * 128) + col; };
+                                                    uint32_t epoch, uint32_t* status) {
     constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
@@ -809,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
     for (int j = 0; j < mine; ++j) {
         // in flight after tile j's loads: this wave's LL store of tile j-1
-        if (j > 0) { if constexpr (FLG) wait_vm<kSys16Ops>(); else wait_vm<1>(); } else wait_vm<0>();
+        if (j > 0) wait_vm<1>(); else wait_vm<0>();
         lds_barrier();
         if (j + 1 < mine) issue(tile_a(j + 1), (j + 1) & 1);
         const uint4* tile = buf[j & 1];
@@ -825,71 +599,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
         if (h == 0) part[w * TV + c] = pw;
         lds_barrier();
-        // the partial -> its owner's inbox: LL, wave w writing word w of every column; FLG, wave w
-        // writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
-        if (h == 0 && (!FLG || (c >> 3) == w)) {
+        // the partial -> its owner's inbox: wave w writing word w of every column (one store
+        // instruction per wave)
+        if (h == 0) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
             const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-            if constexpr (FLG) st_sys16(dslot(lp.ll[o], slot, c), res);
-            else ll_put_word(lp.ll[o] + slot * 128 + c, res, epoch, w);
+            ll_put_word(lp.ll[o] + slot * 128 + c, res, epoch, w);
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
     uint4* xs = buf[0];   // [8][32] results of a batch
-    if constexpr (FLG) {
-        // R: this workgroup's partials are out (flag to every owner), every GPU's partials of
-        // its tiles are in (W flags); owned tiles summed batch by batch, results pushed to the
-        // other GPUs' boxes, their rows stored.  B: every owner's results are in; the other
-        // tiles' rows.  (The LL form interleaves R and B per batch; here each waits once.)
-        constexpr int BB = 8;
-        xflag_raise(xf, par, 0, me, W, epoch);
-        xflag_wait(xf.f[me], par, 0, W, epoch, status);
-        const int b = threadIdx.x >> 5, cc = threadIdx.x & 31;
-        auto rows = [&](int j0, int nb, bool owned) {
-#pragma unroll
-            for (int bb = 0; bb < BB; ++bb) {
-                if (bb >= nb) break;
-                if ((owner_of(tile_of(j0 + bb)) == me) != owned) continue;
-                const uint4 rv = xs[bb * 32 + c];
-                const uint64_t v0 = tile_of(j0 + bb) * TV;
-#pragma unroll
-                for (int k = 0; k < OPS; ++k)
-                    st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPW * w + 2 * k + h) * stride) + v0 + c, rv);
-            }
-        };
-        for (int j0 = 0; j0 < mine; j0 += BB) {
-            const int nb = mine - j0 < BB ? mine - j0 : BB;
-            const uint64_t t = tile_of(j0 + b);
-            if (b < nb && owner_of(t) == me) {
-                const uint64_t li = t - (uint64_t)me * tiles_per_owner;
-                uint4 y[kLLMaxGpus];
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) y[src] = ld_sys16(dslot(lp.ll[me], li * W + src, cc));
-                const uint4 val = owner_sum(y, W, me);
-#pragma unroll
-                for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                    if (dst < W && dst != me) st_sys16(dslot(lp.ll[dst] + box_words, t, cc), val);
-                xs[b * 32 + cc] = val;
-            }
-            __syncthreads();
-            rows(j0, nb, true);
-            __syncthreads();   // xs is reused by the next batch
-        }
-        if (W == 1) return;
-        xflag_raise(xf, par, 1, me, W, epoch);
-        xflag_wait(xf.f[me], par, 1, W, epoch, status);
-        for (int j0 = 0; j0 < mine; j0 += BB) {
-            const int nb = mine - j0 < BB ? mine - j0 : BB;
-            const uint64_t t = tile_of(j0 + b);
-            if (b < nb && owner_of(t) != me) xs[b * 32 + cc] = ld_sys16(dslot(lp.ll[me] + box_words, t, cc));
-            __syncthreads();
-            rows(j0, nb, false);
-            __syncthreads();
-        }
-        return;
-    }
     // ---- R + B, 8 tiles at a time; lane (jr, c) serves tile jr of the batch, column c.
     // R: for a tile I own, the W partials of its column are polled from my inbox
     // (all in flight at once), summed and pushed to every OTHER GPU's box; the
@@ -953,132 +673,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
 }
 
-// ---- hierarchical one-kernel form, LL hand-offs, pipelined -------------------
-// k_hier_pipe: the same step and the same bits as k_hier_ll, on k_tree_lds_lag's
-// pipeline instead of three phases.  k_hier_ll first reads every tile (A), then
-// sums the owned ones (R), then writes every tile (B): the chip reads only,
-// then writes only (17.6 us at W = 1 vs 14.1 for the fused one-GPU pass, whose
-// reads and writes overlap).  Here iteration j of a workgroup (two per CU, two
-// 32 KiB tiles of LDS) does
-//   A(j)    tile j's local tree -> its partial pushed to the owner's inbox
-//   R(j-1)  if this GPU owns tile j-1: the W partials polled from the inbox,
-//           summed (fp32, owner first, one rounding), pushed to every GPU's box
-//   B(j-2)  tile j-2's result polled from this GPU's box, its 64 rank rows
-//           stored interleaved with tile j+2's LDS-DMA loads
-// and two drain iterations finish R / B.  A poll is a VMEM load, and CDNA
-// retires a wave's VMEM operations in order, so a poll issued behind the next
-// tile's loads would wait for them.  Hence the tile parity split: waves 0-1
-// load, poll, push and store the even tiles, waves 2-3 the odd ones (16 row
-// loads / stores per wave and tile; all four waves reduce every tile).  At
-// iteration j the waves of tile j's parity have nothing else outstanding, so
-// their polls wait for the polled words only, while tile j+1's loads (the
-// other pair's) stay in flight.  Every poll waits for strictly earlier
-// iterations of the same workgroup index on every GPU (A(j-1) before R(j-1),
-// R(j-2) before B(j-2)), and the grid is resident, so every wait is reached
-// and satisfied; the hand-offs have one (R) and two (B) iterations of local
-// work to arrive in.
-__global__ __launch_bounds__(kBlock) void k_hier_pipe(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                      const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
-                                                      uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                      uint32_t epoch, uint32_t* status) {
-    constexpr int P = 64, NW = 4, TV = 32, RPW = P / NW, LPL = 8, OPS = 16;   // OPS: row ops per wave and tile
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[NW * TV];
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane % TV, q = lane / TV;
-    const int par = __builtin_amdgcn_readfirstlane(w >> 1), li = (w & 1) * 64 + lane;   // tile parity; lane in the pair
-    // rows of a pair wave: 32 (w & 1) + 2k + q, k < 16
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(32 * (w & 1) * TV * 16));
-    auto row = [&](int k) { return ranks + (uint64_t)(32 * (w & 1) + 2 * k + q) * stride; };
-    const uint64_t G = gridDim.x;
-    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
-    uint64_t* const my_ll = lp.ll[me];
-    auto issue = [&](uint64_t t, int b) {
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            lds_dma16(reinterpret_cast<const uint4*>(row(k)) + t * TV + c, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
-    };
-    uint32_t ob = 0;
-    if (w == 0) ob = order_byte_load(order, lane);
-    if (mine > par) issue(tile_of(par), par);   // tile 0 by waves 0-1, tile 1 by waves 2-3
-    if (w == 0) {   // the order byte (tile 0's loads may stay in flight); read after the loop's barrier
-        if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
-        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
-        ord_lds[lane] = (uint8_t)ob;
-    }
-    for (int j = 0; j < mine + 2; ++j) {
-        const bool mp = par == (j & 1);   // this wave serves tile j's parity (wave-uniform)
-        const bool own_r = j >= 1 && j - 1 < mine && owner_of(tile_of(j - 1)) == me;   // workgroup-uniform
-        const bool do_b = j >= 2 && j - 2 < mine;
-        const bool rl = mp && own_r && li < TV;   // this lane sums column c of tile j-1
-        // polls of R(j-1) (the W partials of column c) and B(j-2) (tile j-2's result
-        // in column c, every lane of the pair), issued before the tree: their
-        // latency hides behind it.  The pair has no other VMEM operation in flight.
-        uint64_t wr[kLLMaxGpus][4], wb[4];
-        if (mp) {
-            if (j < mine) wait_vm<0>();   // this pair's loads of tile j (and its older stores) are done
-            if (rl) {
-                const uint64_t lr = tile_of(j - 1) - (uint64_t)me * tiles_per_owner;
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) ll_load(my_ll + (lr * W + src) * 128 + c, wr[src]);
-            }
-            if (do_b) ll_load(my_ll + box_words + tile_of(j - 2) * 128 + c, wb);
-        }
-        if (j < mine) {   // ---- A(j): every wave reduces
-            lds_barrier();   // tile j is in LDS
-            const uint4* tile = buf[j & 1];
-            const uint8_t* ord = ord_lds + RPW * w + LPL * q;
-            uint4 x[LPL];
-#pragma unroll
-            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
-#pragma unroll
-            for (int s2 = 1; s2 < LPL; s2 *= 2)
-#pragma unroll
-                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
-            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
-            if (q == 0) part[w * TV + c] = pw;
-            lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            if (mp && li < TV) {   // the partial of tile j -> its owner's inbox
-                const uint64_t t = tile_of(j);
-                const int o = owner_of(t);
-                const uint4 pr = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-                ll_put(lp.ll[o] + ((t - (uint64_t)o * tiles_per_owner) * W + me) * 128 + c, pr, epoch);
-            }
-        }
-        if (!mp) continue;
-        if (rl) {   // ---- R(j-1): owner first, then ascending; fp32, one rounding -> every GPU's box
-            const uint64_t t = tile_of(j - 1), lr = t - (uint64_t)me * tiles_per_owner;
-            uint4 y[kLLMaxGpus];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src) {
-                if (src >= W) continue;
-                const uint64_t* at = my_ll + (lr * W + src) * 128 + c;
-                y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(at, epoch, status);
-            }
-            const uint4 o = owner_sum(y, W, me);
-#pragma unroll
-            for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W) ll_put(lp.ll[dst] + box_words + t * 128 + c, o, epoch);
-        }
-        uint4 res = make_uint4(0, 0, 0, 0);
-        if (do_b) res = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + tile_of(j - 2) * 128 + c, epoch, status);
-        // tile j+2's loads and tile j-2's stores, interleaved op by op (both of this parity)
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(j - 2);
-        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) {
-            if (j + 2 < mine)
-                lds_dma16(reinterpret_cast<const uint4*>(row(k)) + tl * TV + c, bl + (uint32_t)(2 * k * TV * 16));
-            if (do_b) st_nt(reinterpret_cast<uint4*>(row(k)) + ts * TV + c, res);
-        }
-    }
-}
-
 // ---- hierarchical step across consecutive buckets ----------------------------
 // k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
 // hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
@@ -1116,13 +710,12 @@ constexpr int kHierXChunk = 8;
 // its polls and result pushes overlap those stores instead of queueing behind them; bit 1 (tune
 // hier_x_latepoll): prev's results polled after tile 0's tree (they are first read by iteration 1's
 // stores) instead of at the start, where the polls' wait also waited for tile 1's loads
-template <int LAG, bool FLG, bool CH, int RE>
+template <int LAG, bool CH, int RE>
 __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                    uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                                                   uint32_t* status, XFPtrs xf, uint32_t par) {
-    // FLG: par = the LL parities of cur / prev in bits 0 / 1
+                                                   uint32_t* status) {
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
@@ -1159,26 +752,18 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     const int jr = threadIdx.x / TV;
     // tile j's results in LDS, column c
     auto rslot = [&](int j) { return CH ? res[(j / kHierXChunk) & 1][j % kHierXChunk][c] : res[0][j][c]; };
-    const uint32_t pc = par & 1u, pp = (par >> 1) & 1u;
-    // a hand-off slot's data in the FLG form: the first 512 bytes of its 1 KiB LL slot
-    auto dslot = [&](uint64_t* base, uint64_t slot) { return reinterpret_cast<uint4*>(base + slot * 128) + c; };
     auto poll_prev = [&](int ch) {
         const int j = ch * kHierXChunk + jr;
         if (j >= mine) return;
         uint4& slot = res[CH ? ch & 1 : 0][jr][c];
-        if constexpr (FLG) {   // every owner's flag was waited for
-            slot = ld_sys16(dslot(lpv.ll[me] + box_words, tile_of(j)));
-            return;
-        }
         const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
         slot = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
     };
     // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
-    const bool lp = (RE & 2) && LAG == 1 && !FLG && cur;
+    const bool lp = (RE & 2) && LAG == 1 && cur;
     if (prev && !lp) {
-        if constexpr (FLG) xflag_wait(xf.f[me], pp, 1, W, eprev, status);   // raised at the end of the last launch
         poll_prev(0);
         if (CH && mine > kHierXChunk) poll_prev(1);
     }
@@ -1188,7 +773,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
             // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
             wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
-                     (j >= 1 ? (FLG ? kSys16Ops : 1) : 0));
+                     (j >= 1 ? 1 : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -1202,16 +787,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            // the partial -> its owner's inbox: LL, wave w writing word w of every column;
-            // FLG, wave w writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
-            if (q == 0 && (!FLG || (c >> 3) == w)) {
+            // the partial -> its owner's inbox: wave w writing word w of every column (one
+            // store instruction per wave)
+            if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pt = part[j & 1];
                 const uint4 pr = add8(add8(pt[0 * TV + c], pt[1 * TV + c]), add8(pt[2 * TV + c], pt[3 * TV + c]));
                 const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                if constexpr (FLG) st_sys16(dslot(lc.ll[o], slot), pr);
-                else ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
+                ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
             }
         }
         if (lp && j == 0 && prev) {   // read first by iteration 1's stores, behind its A-phase barrier
@@ -1241,42 +825,26 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
     // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
     // partial (during this launch's loop): W partials summed (fp32, owner first,
     // one rounding), the result pushed to every GPU's box for the next launch.
-    // FLG: this workgroup's partials are out (flag to every owner), then every
-    // GPU's partials of this workgroup's tiles are in (W flags)
     auto r_cur = [&]() {
-        if constexpr (FLG)
-            if (cur) {
-                xflag_raise(xf, pc, 0, me, W, ecur);
-                xflag_wait(xf.f[me], pc, 0, W, ecur, status);
-            }
         for (int j0 = 0; cur && j0 < mine && (CH || j0 == 0); j0 += kHierXChunk) {
             if (j0 + jr >= mine) break;
             const uint64_t t = tile_of(j0 + jr);
             if (owner_of(t) == me) {
                 const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
                 uint4 y[kLLMaxGpus];
-                if constexpr (FLG) {
+                uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
-                    for (int src = 0; src < kLLMaxGpus; ++src)
-                        if (src < W) y[src] = ld_sys16(dslot(lc.ll[me], lr * W + src));
-                } else {
-                    uint64_t wr[kLLMaxGpus][4];
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
 #pragma unroll
-                    for (int src = 0; src < kLLMaxGpus; ++src)
-                        if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
-#pragma unroll
-                    for (int src = 0; src < kLLMaxGpus; ++src)
-                        if (src < W)
-                            y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
-                                                             : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
-                }
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W)
+                        y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
+                                                         : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
                 const uint4 o = owner_sum(y, W, me);
 #pragma unroll
                 for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                    if (dst < W) {
-                        if constexpr (FLG) st_sys16(dslot(lc.ll[dst] + box_words, t), o);
-                        else ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
-                    }
+                    if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
             }
         }
     };
@@ -1292,8 +860,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
     }
     if constexpr ((RE & 1) == 0) r_cur();
-    if constexpr (FLG)   // this workgroup's results are out: every GPU told (read by its next launch)
-        if (cur) xflag_raise(xf, pc, 1, me, W, ecur);
 }
 
 // ---- hierarchical step, two-deep bucket pipeline ----------------------------
@@ -1328,21 +894,20 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // + 1 polled when chunk k's row stores begin — before cur's partial of any of
 // its tiles is pushed, so the order above holds per tile).
 // Same bits as k_hier_ll / k_hier_x.
-// TAIL & 3: 0 mid's owned sums at the launch start, 1 at its end, 2 before its last row stores (LL only);
-// TAIL & 4 (LL, LAG 1, tune hier_x_latepoll): old's results polled after tile 0's tree, not at the start
-template <int TAIL, int LAG, bool FLG, bool CH>
+// TAIL & 3: 0 mid's owned sums at the launch start, 1 at its end, 2 before its last row stores;
+// TAIL & 4 (LAG 1, tune hier_x_latepoll): old's results polled after tile 0's tree, not at the start
+template <int TAIL, int LAG, bool CH>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
-                                                    int has_mid, uint32_t* status, XFPtrs xf, uint32_t par) {
+                                                    int has_mid, uint32_t* status) {
     // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
     // stores, not after them
-    constexpr bool tl2 = (TAIL & 3) == 2 && !FLG;
+    constexpr bool tl2 = (TAIL & 3) == 2;
     // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
-    const bool lp = (TAIL & 4) && LAG == 1 && !FLG && cur;
-    // FLG: par = the LL parities of cur / mid / old in bits 0 / 1 / 2
+    const bool lp = (TAIL & 4) && LAG == 1 && cur;
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
@@ -1385,68 +950,35 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     auto act_in = [&](int ch) { return ch * kHierXChunk + jr < mine; };
     auto rmid_in = [&](int ch) { return has_mid && act_in(ch) && owner_of(tile_of(ch * kHierXChunk + jr)) == me; };
     // mid's owned sums of chunk ch: polls of its W partials, owner sum, pushed to every GPU's box
-    const uint32_t pc = par & 1u, pm = (par >> 1) & 1u, po = (par >> 2) & 1u;
-    // a hand-off slot's data in the FLG form: the first 512 bytes of its 1 KiB LL slot
-    auto dslot = [&](uint64_t* base, uint64_t slot) { return reinterpret_cast<uint4*>(base + slot * 128) + c; };
     auto owned_sums = [&](int ch) {
         if (!rmid_in(ch)) return;
         const uint64_t tr = tile_of(ch * kHierXChunk + jr);
         const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
         uint4 y[kLLMaxGpus];
-        if constexpr (FLG) {   // the W flags were waited for: plain loads
+        uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) y[src] = ld_sys16(dslot(lm.ll[me], lr * W + src));
-        } else {
-            uint64_t wr[kLLMaxGpus][4];
+        for (int src = 0; src < kLLMaxGpus; ++src)
+            if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
 #pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W)
-                    y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
-                                                     : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
-        }
+        for (int src = 0; src < kLLMaxGpus; ++src)
+            if (src < W)
+                y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
+                                                 : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
         const uint4 o = owner_sum(y, W, me);
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
-            if (dst < W) {
-                if constexpr (FLG) st_sys16(dslot(lm.ll[dst] + box_words, tr), o);
-                else ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
-            }
-    };
-    // FLG: mid's partials have arrived from every GPU (their previous launch raised its
-    // flag after its loop); the owned sums; every GPU told that this workgroup's sums are out
-    auto all_owned_sums = [&]() {
-        if constexpr (FLG) {
-            if (!has_mid) return;
-            xflag_wait(xf.f[me], pm, 0, W, emid, status);
-        }
-        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
-        if constexpr (FLG) xflag_raise(xf, pm, 1, me, W, emid);
+            if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
     };
     // old's results of chunk ch -> its slot
     auto poll_old = [&](int ch) {
         if (!act_in(ch)) return;
         uint4& slot = res[CH ? ch & 1 : 0][jr][c];
-        if constexpr (FLG) {
-            slot = ld_sys16(dslot(lo.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
-            return;
-        }
         const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c;
         uint64_t wd[4];
         ll_load(at, wd);
         slot = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
     };
-    if constexpr (FLG) {
-        if ((TAIL & 3) == 0) all_owned_sums();
-        if (old) {   // every owner's results of old are out (raised one launch ago)
-            xflag_wait(xf.f[me], po, 1, W, eold, status);
-            poll_old(0);
-            if (CH && nch > 1) poll_old(1);
-        }
-    } else {
+    {
         uint64_t wo[4];
         const bool early_old = old && !lp;   // lp: polled in A(cur 0), ahead of its partial push
         if (early_old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
@@ -1459,9 +991,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
     // (the polls before them have returned, and with them both tiles' loads).  With
     // several chunks an earlier chunk's pushes may be in flight too: counting none
-    // only waits longer (the loads of tile j are never waited for too little).  FLG:
-    // the flag raise has drained them
-    const int pushed = !FLG && (TAIL & 3) == 0 && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
+    // only waits longer (the loads of tile j are never waited for too little)
+    const int pushed = (TAIL & 3) == 0 && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
@@ -1469,7 +1000,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             // partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG), this
             // wave's owned-sum pushes (j < 2)
             wait_any((j >= 2 + LAG && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && old ? OPS : 0) +
-                     (j >= 1 ? (FLG ? kSys16Ops : 1) : 0) + (j < 2 ? pushed : 0));
+                     (j >= 1 ? 1 : 0) + (j < 2 ? pushed : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -1498,16 +1029,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                 wait_vm<0>();
                 lds_barrier();
             }
-            // the partial -> its owner's inbox: LL, wave w writing word w of every column;
-            // FLG, wave w writing columns 8w .. 8w+7 whole (one store instruction per wave either way)
-            if (q == 0 && (!FLG || (c >> 3) == w)) {
+            // the partial -> its owner's inbox: wave w writing word w of every column (one
+            // store instruction per wave)
+            if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
                 const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                if constexpr (FLG) st_sys16(dslot(lc.ll[o], slot), pr);
-                else ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
+                ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
             }
         }
         // tl2: mid's owned sums ahead of the last iteration's row stores, so their polls and pushes
@@ -1541,23 +1071,13 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         if (!cur || (lp && mine == 1)) lds_barrier();
         store_rows(old, mine - 1);
     }
-    if constexpr (FLG)   // cur's partials of this workgroup are out: every owner told
-        if (cur) xflag_raise(xf, pc, 0, me, W, ecur);
-    if ((TAIL & 3) != 0) {   // TAIL: mid's partials arrived during the launch i-1
-        if constexpr (FLG) all_owned_sums();
-        else if (!tl2 || mine == 0)
-            for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
-    }
+    if ((TAIL & 3) != 0 && (!tl2 || mine == 0))   // TAIL: mid's partials arrived during the launch i-1
+        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
-        if constexpr (FLG) xflag_wait(xf.f[me], pm, 1, W, emid, status);
         for (int ch = 0; ch < nch; ++ch) {
             __syncthreads();   // every wave has read the slot's previous results
-            if (act_in(ch)) {
-                if constexpr (FLG)
-                    res[CH ? ch & 1 : 0][jr][c] = ld_sys16(dslot(lm.ll[me] + box_words, tile_of(ch * kHierXChunk + jr)));
-                else
-                    res[CH ? ch & 1 : 0][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
-            }
+            if (act_in(ch))
+                res[CH ? ch & 1 : 0][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
             lds_barrier();
             for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
         }
@@ -1786,28 +1306,9 @@ int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket,
     return peer_last_error();
 }
 
-int launch_hier_oneshot(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint16_t* const* wins,
-                        uint32_t* const* hflags, int nranks, int me, size_t n, uint32_t epoch, uint32_t* status,
-                        unsigned max_grid, void* stream) {
-    const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > ALLRED_MAX_NODES || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks))
-        return ALLRED_ERR_ARG;
-    HierPtrs hp{};
-    for (int q = 0; q < nranks; ++q) {
-        hp.win[q] = wins[q];
-        hp.hfl[q] = hflags[q];
-    }
-    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
-    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    hipLaunchKernelGGL(k_hier_oneshot, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, hp,
-                       nranks, me, (uint64_t)n, ntiles, ntiles / nranks, epoch, status);
-    return peer_last_error();
-}
-
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   uint32_t* const* xfl, uint32_t parity, void* stream) {
+                   void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
         ntiles * 128 > box_words)
@@ -1817,33 +1318,14 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    XFPtrs xf{};
-    for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
-    hipLaunchKernelGGL(xfl ? k_hier_ll<true> : k_hier_ll<false>, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks,
-                       stride, order, lp, nranks, me, ntiles, ntiles / nranks, box_words, epoch, status, xf, parity);
-    return peer_last_error();
-}
-
-int launch_hier_pipe(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                     size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                     void* stream) {
-    const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
-        ntiles * 128 > box_words)
-        return ALLRED_ERR_ARG;
-    LLPtrs lp{};
-    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
-    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
-    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    hipLaunchKernelGGL(k_hier_pipe, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
+    hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
                        me, ntiles, ntiles / nranks, box_words, epoch, status);
     return peer_last_error();
 }
 
 int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
                   uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                  uint32_t* status, unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream) {
+                  uint32_t* status, unsigned max_grid, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
         (!cur && !prev) || (cur && !aligned16(cur)) || (prev && !aligned16(prev)))
@@ -1856,39 +1338,32 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
         lc.ll[q] = llc ? llc[q] : nullptr;
         lp.ll[q] = llp ? llp[q] : nullptr;
     }
-    XFPtrs xf{};
-    for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
-    if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
     const bool lag = tune(Tune::hier_x_lag) != 0;
     const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    const int re = !xfl && lag ? (tune(Tune::hier_x_rearly) ? 1 : 0) | (tune(Tune::hier_x_latepoll) ? 2 : 0) : 0;
-    decltype(&k_hier_x<0, false, false, 0>) kern;
-    switch ((xfl ? 4 : 0) + (lag ? 2 : 0) + (ch ? 1 : 0) + re * 8) {
-        case 27: kern = k_hier_x<1, false, true, 3>; break;
-        case 26: kern = k_hier_x<1, false, false, 3>; break;
-        case 19: kern = k_hier_x<1, false, true, 2>; break;
-        case 18: kern = k_hier_x<1, false, false, 2>; break;
-        case 11: kern = k_hier_x<1, false, true, 1>; break;
-        case 10: kern = k_hier_x<1, false, false, 1>; break;
-        case 7: kern = k_hier_x<1, true, true, 0>; break;
-        case 6: kern = k_hier_x<1, true, false, 0>; break;
-        case 5: kern = k_hier_x<0, true, true, 0>; break;
-        case 4: kern = k_hier_x<0, true, false, 0>; break;
-        case 3: kern = k_hier_x<1, false, true, 0>; break;
-        case 2: kern = k_hier_x<1, false, false, 0>; break;
-        case 1: kern = k_hier_x<0, false, true, 0>; break;
-        default: kern = k_hier_x<0, false, false, 0>; break;
+    const int re = lag ? (tune(Tune::hier_x_rearly) ? 1 : 0) | (tune(Tune::hier_x_latepoll) ? 2 : 0) : 0;
+    decltype(&k_hier_x<0, false, 0>) kern;
+    switch ((lag ? 2 : 0) + (ch ? 1 : 0) + re * 4) {
+        case 15: kern = k_hier_x<1, true, 3>; break;
+        case 14: kern = k_hier_x<1, false, 3>; break;
+        case 11: kern = k_hier_x<1, true, 2>; break;
+        case 10: kern = k_hier_x<1, false, 2>; break;
+        case 7: kern = k_hier_x<1, true, 1>; break;
+        case 6: kern = k_hier_x<1, false, 1>; break;
+        case 3: kern = k_hier_x<1, true, 0>; break;
+        case 2: kern = k_hier_x<1, false, 0>; break;
+        case 1: kern = k_hier_x<0, true, 0>; break;
+        default: kern = k_hier_x<0, false, 0>; break;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, eprev, status, xf, parities);
+                       box_words, ecur, eprev, status);
     return peer_last_error();
 }
 
 int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride, const uint8_t* order,
                    uint64_t* const* llc, uint64_t* const* llm, uint64_t* const* llo, int nranks, int me, size_t n,
                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
-                   unsigned max_grid, uint32_t* const* xfl, uint32_t parities, void* stream) {
+                   unsigned max_grid, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
         (!cur && !old && !fin) || (cur && !llc) || (old && !llo) || (fin && (cur || !llm)) ||
@@ -1903,47 +1378,36 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         lm.ll[q] = llm ? llm[q] : nullptr;
         lo.ll[q] = llo ? llo[q] : nullptr;
     }
-    XFPtrs xf{};
-    for (int q = 0; q < nranks && xfl; ++q) xf.f[q] = xfl[q];
-    // TAIL 2 is an LL-form placement: the flag form takes TAIL 1; + 4: late result polls (LL, lag 1)
-    const int tail = (int)tune(Tune::hier_x2_tail) == 2 && !xfl ? 2 : (tune(Tune::hier_x2_tail) ? 1 : 0);
+    // + 4: late result polls (lag 1)
+    const int tail = (int)tune(Tune::hier_x2_tail);
     const int lag = tune(Tune::hier_x_lag) ? 1 : 0;
-    const int late = !xfl && lag && tune(Tune::hier_x_latepoll) ? 4 : 0;
-    if (xfl && grid > (unsigned)kXFlagGroups) return ALLRED_ERR_ARG;
+    const int late = lag && tune(Tune::hier_x_latepoll) ? 4 : 0;
     const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    decltype(&k_hier_x2<0, 0, false, false>) kern = nullptr;
-    // index: (tail + late) x 8 + lag x 4 + flags x 2 + chunked
-    switch ((tail + late) * 8 + lag * 4 + (xfl ? 2 : 0) + (ch ? 1 : 0)) {
-        case 0: kern = k_hier_x2<0, 0, false, false>; break;
-        case 1: kern = k_hier_x2<0, 0, false, true>; break;
-        case 2: kern = k_hier_x2<0, 0, true, false>; break;
-        case 3: kern = k_hier_x2<0, 0, true, true>; break;
-        case 4: kern = k_hier_x2<0, 1, false, false>; break;
-        case 5: kern = k_hier_x2<0, 1, false, true>; break;
-        case 6: kern = k_hier_x2<0, 1, true, false>; break;
-        case 7: kern = k_hier_x2<0, 1, true, true>; break;
-        case 8: kern = k_hier_x2<1, 0, false, false>; break;
-        case 9: kern = k_hier_x2<1, 0, false, true>; break;
-        case 10: kern = k_hier_x2<1, 0, true, false>; break;
-        case 11: kern = k_hier_x2<1, 0, true, true>; break;
-        case 12: kern = k_hier_x2<1, 1, false, false>; break;
-        case 13: kern = k_hier_x2<1, 1, false, true>; break;
-        case 14: kern = k_hier_x2<1, 1, true, false>; break;
-        case 15: kern = k_hier_x2<1, 1, true, true>; break;
-        case 16: kern = k_hier_x2<2, 0, false, false>; break;
-        case 17: kern = k_hier_x2<2, 0, false, true>; break;
-        case 20: kern = k_hier_x2<2, 1, false, false>; break;
-        case 21: kern = k_hier_x2<2, 1, false, true>; break;
-        case 36: kern = k_hier_x2<4, 1, false, false>; break;
-        case 37: kern = k_hier_x2<4, 1, false, true>; break;
-        case 44: kern = k_hier_x2<5, 1, false, false>; break;
-        case 45: kern = k_hier_x2<5, 1, false, true>; break;
-        case 52: kern = k_hier_x2<6, 1, false, false>; break;
-        case 53: kern = k_hier_x2<6, 1, false, true>; break;
+    decltype(&k_hier_x2<0, 0, false>) kern = nullptr;
+    // index: (tail + late) x 4 + lag x 2 + chunked
+    switch ((tail + late) * 4 + lag * 2 + (ch ? 1 : 0)) {
+        case 0: kern = k_hier_x2<0, 0, false>; break;
+        case 1: kern = k_hier_x2<0, 0, true>; break;
+        case 2: kern = k_hier_x2<0, 1, false>; break;
+        case 3: kern = k_hier_x2<0, 1, true>; break;
+        case 4: kern = k_hier_x2<1, 0, false>; break;
+        case 5: kern = k_hier_x2<1, 0, true>; break;
+        case 6: kern = k_hier_x2<1, 1, false>; break;
+        case 7: kern = k_hier_x2<1, 1, true>; break;
+        case 8: kern = k_hier_x2<2, 0, false>; break;
+        case 9: kern = k_hier_x2<2, 0, true>; break;
+        case 10: kern = k_hier_x2<2, 1, false>; break;
+        case 11: kern = k_hier_x2<2, 1, true>; break;
+        case 18: kern = k_hier_x2<4, 1, false>; break;
+        case 19: kern = k_hier_x2<4, 1, true>; break;
+        case 22: kern = k_hier_x2<5, 1, false>; break;
+        case 23: kern = k_hier_x2<5, 1, true>; break;
+        case 26: kern = k_hier_x2<6, 1, false>; break;
+        case 27: kern = k_hier_x2<6, 1, true>; break;
         default: return ALLRED_ERR_ARG;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, emid, eold, llm ? 1 : 0, status, xf, parities);
+                       box_words, ecur, emid, eold, llm ? 1 : 0, status);
     return peer_last_error();
 }
 

@@ -41,7 +41,6 @@ const Key kKeys[] = {
     {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
     {"steps_groups", 0, 0, 5},        // k_steps_reg: workgroups per CU, 0 auto (BO 3, LO 4 or 3) | 3 | 4 | 5
     {"rccl_fault", 0, 0, 7},          // fault injection (tests): 1 init, 2 group end, 4 stream drain never settle
-    {"hier_handoff", 0, 0, 1},        // k_hier_x / k_hier_x2 hand-offs: 0 LL words (data + epoch) | 1 data + one flag per workgroup
     {"multi_fault", 0, 0, 64},        // fault injection (tests): 1..32 GPU value - 1 fails its timed allreduce, 33..64 its warm-up
     {"hier_x_chunked", 0, 0, 1},      // k_hier_x / k_hier_x2: 1 the chunked form even at <= 8 tiles per workgroup (A/B)
     {"steps_tab", 1, 0, 1},           // k_steps_reg BO: 1 stages only its units' block programs (J < P), 0 every block's

@@ -128,12 +128,14 @@ def test_tune_entry_point():
             t.tune("steps_groups", v)
     assert t.tune("steps_groups") == 0
     # round-4 keys: defaults are the product forms / no fault injection
-    assert t.tune("hier_handoff") == 0
     assert t.tune("hier_x_chunked") == 0
     assert (t.tune("rccl_fault"), t.tune("multi_fault")) == (0, 0)
-    for key, bad in (("hier_handoff", 2), ("rccl_fault", 8)):
+    for key, bad in (("hier_x2_tail", 3), ("rccl_fault", 8)):
         with pytest.raises(t.AllredError):
             t.tune(key, bad)
+    # round 5: the flag hand-off forms are gone with their key (the trimmed table)
+    with pytest.raises(t.AllredError):
+        t.tune("hier_handoff")
 
 
 def test_mem_program_stats_one_rank_has_no_launch():

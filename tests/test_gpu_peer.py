@@ -100,16 +100,14 @@ def worker(rank, world, port, q):
         if not all(np.array_equal(got[i], partials[rank]) for i in range(local)):
             fails.append(("hier", 0, 1))
         # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form
-        # (k_hier_oneshot, per-tile flags), the LL push form (k_hier_ll), its
-        # pipelined form (k_hier_pipe), the launch form and the bucket pipelines (k_hier_x, k_hier_x2), two or
-        # three calls back to back each (then LL once more after the launch form: its LL boxes must not accept
-        # the older calls' words)
+        # with LL push hand-offs (k_hier_ll), the launch form (the mem_2D exchange as one kernel or as
+        # launches) and the bucket pipelines (k_hier_x, k_hier_x2), two or three calls back to back each
+        # (then LL once more after the launch form: its LL boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
         # in full and capped grids (a capped grid gives every workgroup many tiles)
-        for mi, (mode, limit, ll, cap) in enumerate((("hier_one_kernel", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
+        for mi, (mode, limit, ll, cap) in enumerate((("hier_oneshot_exchange", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
-                                                     ("hier_ll_capped", 0, 1, 2), ("hier_one_kernel_capped", 1 << 40, 0, 1),
-                                                     ("hier_pipe", 0, 2, 0), ("hier_pipe_capped", 0, 2, 2),
+                                                     ("hier_ll_capped", 0, 1, 2), ("hier_oneshot_exchange_capped", 1 << 40, 0, 1),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
@@ -120,12 +118,7 @@ def worker(rank, world, port, q):
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
                                                      ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
-                                                     ("hier_x2_tail_one_group", 0, 0, 1),
-                                                     # the flag hand-offs (tune hier_handoff 1)
-                                                     ("hier_x2_flg", 0, 0, 0), ("hier_x2_tail_flg", 0, 0, 0),
-                                                     ("hier_x2_flg_one_group", 0, 0, 1), ("hier_x_flg", 0, 0, 0),
-                                                     ("hier_x_flg_one_group", 0, 0, 1), ("hier_ll_flg", 0, 1, 0),
-                                                     ("hier_ll_flg_capped", 0, 1, 2))):
+                                                     ("hier_x2_tail_one_group", 0, 0, 1))):
             if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
@@ -139,25 +132,21 @@ def worker(rank, world, port, q):
                 ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
                     with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
-                                 hier_handoff=int("flg" in mode), hier_x_latepoll=int("_lp" in mode)):
+                                 hier_x_latepoll=int("_lp" in mode)):
                         peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
-                    with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode),
-                                 hier_x_latepoll=int("_lp" in mode)):
+                    with t.tuned(hier_x_rearly=int("_re" in mode), hier_x_latepoll=int("_lp" in mode)):
                         peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
                                                  torch.cuda.current_stream())
                 else:
-                    with t.tuned(hier_handoff=int("flg" in mode)):
-                        peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING,
-                                       ws.data_ptr())
+                    peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
                 with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
-                                 hier_handoff=int("flg" in mode), hier_x_latepoll=int("_lp" in mode)):
+                             hier_x_latepoll=int("_lp" in mode)):
                     peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             elif mode.startswith("hier_x"):
-                with t.tuned(hier_handoff=int("flg" in mode), hier_x_rearly=int("_re" in mode),
-                                 hier_x_latepoll=int("_lp" in mode)):
+                with t.tuned(hier_x_rearly=int("_re" in mode), hier_x_latepoll=int("_lp" in mode)):
                     peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
             torch.cuda.synchronize()
             for rep, (data, buf, _) in enumerate(runs):
@@ -356,8 +345,8 @@ def t_timeout_bit():
 
 @pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
 def test_hier_forms_single_gpu_bit_exact(n, cap):
-    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll, its pipelined
-    form k_hier_pipe, the flag form k_hier_oneshot and the launch form give the same
+    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll and the launch
+    form (mem_2D exchange as one kernel or as launches) give the same
     bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
     mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
     (both LL parities).  Config-2 size full grid and with capped grids (many
@@ -378,19 +367,17 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit, flg in ((1, 0, 0), (0, 1 << 40, 0), (0, 0, 0), (2, 0, 0), (1, 0, 0), (2, 0, 0), (1, 0, 1),
-                               (1, 0, 0), (1, 0, 1)):
+        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (1, 0), (0, 1 << 40), (1, 0)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
             torch.cuda.synchronize()
-            with t.tuned(hier_handoff=flg):   # k_hier_ll: LL words / plain data + flags
-                for b in bufs:   # back to back: both LL parities / epochs
-                    peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+            for b in bufs:   # back to back: both LL parities / epochs
+                peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
             torch.cuda.synchronize()
             for rep, (b, (_, want)) in enumerate(zip(bufs, cases)):
                 bad = int((b.cpu().numpy().view(np.uint16) != want[None, :]).sum())
-                assert bad == 0, (ll, limit, flg, rep, bad)
+                assert bad == 0, (ll, limit, rep, bad)
         assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.set_hier_ll(0)
@@ -405,7 +392,7 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
     bucket while it reads the next), buckets + 1 calls, every bucket bit-exact
     vs the oracle (tree of local rank 0, the mem_2D sum of one partial, rows
     overwritten with it); full and capped grids (one workgroup with 40 tiles:
-    five chunks of staged results); LL and flag hand-offs (tune hier_handoff).
+    five chunks of staged results).
     Protocol errors: a prev that is not the pending bucket, another peer call
     while a bucket is pending, finishing with nothing pending."""
     sys.path.insert(0, ROOT)
@@ -426,10 +413,10 @@ def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(14):   # row stores with the tree's tile / one behind; LL / flag hand-offs; both LL
+        for rep in range(14):   # row stores with the tree's tile / one behind; both LL
             bufs = [x.clone() for x in data]   # parities; the chunked form forced (reps 8, 9); R early (10, 11);
             prev = None                        # result polls at the start (12), R early + late polls (13)
-            with t.tuned(hier_x_lag=rep % 2 if rep < 10 else 1, hier_handoff=(rep // 4) % 2 if rep < 10 else 0,
+            with t.tuned(hier_x_lag=rep % 2 if rep < 10 else 1,
                          hier_x_chunked=int(8 <= rep < 10), hier_x_rearly=int(rep in (10, 11, 13)),
                          hier_x_latepoll=int(rep != 12)):
                 for b in bufs:
@@ -471,7 +458,7 @@ def test_peer_knob_argument_errors():
     peer.connect([peer.handle()])
     try:
         with pytest.raises(_lib.AllredError):
-            peer.set_hier_ll(3)            # 0 off, 1 k_hier_ll, 2 k_hier_pipe
+            peer.set_hier_ll(2)            # 0 off, 1 k_hier_ll (k_hier_pipe is gone)
         with pytest.raises(_lib.AllredError):
             peer.set_hier_ll(-1)
         peer.set_lo_ll_max(0)
@@ -598,8 +585,8 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
     sums bucket i-1's owned tiles and writes bucket i-2), buckets + 1 calls
     (1 bucket: the flush sums and writes it; 2: the flush writes both), every
     bucket bit-exact vs the oracle; full and capped grids (one workgroup with
-    40 tiles: five chunks of staged results), LL and flag hand-offs (tune
-    hier_handoff), the sequence repeated (both LL parities reused).  Protocol errors:
+    40 tiles: five chunks of staged results), the sequence repeated (both LL
+    parities reused).  Protocol errors:
     another peer call or the one-deep pipeline while buckets are pending, a
     different bucket size mid-sequence, a flush with nothing pending."""
     sys.path.insert(0, ROOT)
@@ -621,9 +608,9 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             want.append(loc[0])
         s = torch.cuda.current_stream()
         for rep in range(16):   # owned sums at the start / the end of a launch / before its last stores (12-15);
-            # LL / flag hand-offs; chunked form forced; results polled at the start (14, 15) or after tile 0
+            # chunked form forced; results polled at the start (14, 15) or after tile 0
             with t.tuned(hier_x2_tail=2 if rep >= 12 else (rep // 2) % 2, hier_x_lag=rep % 2,
-                         hier_handoff=(rep // 4) % 2 if rep < 12 else 0, hier_x_chunked=int(8 <= rep < 12),
+                         hier_x_chunked=int(8 <= rep < 12),
                          hier_x_latepoll=int(rep < 14)):
                 bufs = [x.clone() for x in data]
                 for b in bufs:

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
-x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_oneshot,
-k_hier_ll, k_hier_pipe, k_hier_x and k_hier_x2 (buckets pipelined one / two
-deep, k_hier_x2 with its owned sums at the start or the end of a launch, LL or
-flag hand-offs: K buckets in K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
+x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ll, k_hier_x
+and k_hier_x2 (buckets pipelined one / two deep, k_hier_x2 with its owned sums
+at the start, the end or before the last row stores of a launch: K buckets in
+K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
 hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
 kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
 arms interleaved.   python tools/hier_step.py [steps] [rounds]   (HIER_CAP: grid cap)"""
@@ -27,12 +27,12 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
-arms = {"launches": (0, 0), "oneshot": (1 << 40, 0), "hier_ll": (0, 1), "hier_ll_flg": (0, 1), "hier_pipe": (0, 2)}
-# pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _flg: flag
-# hand-offs; _ch: the chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned
-# sums before the last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last
-# tile's row stores (tune hier_x_rearly)
-PIPE = ["hier_x", "hier_x_flg", "hier_x2", "hier_x2_tail", "hier_x2_tail2", "hier_x2_flg", "hier_x2_tail_flg"]
+arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ll": (0, 1)}
+# pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _ch: the
+# chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned sums before the
+# last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last tile's row
+# stores (tune hier_x_rearly); _lp: late result polls (tune hier_x_latepoll)
+PIPE = ["hier_x_lp", "hier_x_re_lp", "hier_x2_tail2_lp"]
 if os.environ.get("HIER_ARMS"):   # a subset, comma separated (any of the names above, + _ch variants)
     sel = os.environ["HIER_ARMS"].split(",")
     arms = {k: v for k, v in arms.items() if k in sel}
@@ -62,7 +62,6 @@ for _ in range(rounds):
     for name in PIPE:
         deep = name.startswith("hier_x2")
         t.tune("hier_x2_tail", 2 if name.startswith("hier_x2_tail2") else int(name.startswith("hier_x2_tail")))
-        t.tune("hier_handoff", int("_flg" in name))   # hand-offs: LL words / data + flags
         t.tune("hier_x_chunked", int("_ch" in name))
         t.tune("hier_x_rearly", int("_re" in name))
         t.tune("hier_x_latepoll", int("_lp" in name))
@@ -80,7 +79,6 @@ for _ in range(rounds):
     for name, (limit, ll) in arms.items():
         peer.set_oneshot_max(limit)
         peer.set_hier_ll(ll)
-        t.tune("hier_handoff", int(name.endswith("_flg")))   # k_hier_ll: LL words / data + flags
         for i in range(20):
             peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
         torch.cuda.synchronize()
