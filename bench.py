@@ -696,7 +696,7 @@ def best_arms(out: dict) -> dict:
         if not isinstance(v, dict) or v.get("verified") is not True or "ms" not in v or v.get("peer_timeout"):
             continue
         cfg = key
-        for pre in ("peer_sched_", "peer_oneshot_", "peer_push_", "peer_"):
+        for pre in ("peer_sched_", "peer_oneshot_", "peer_push_", "peer_fenced_", "peer_"):
             if cfg.startswith(pre):
                 cfg = cfg[len(pre):]
                 break
@@ -758,6 +758,12 @@ def xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, name, algo,
                 timed("peer_push_" + name, peer_fn, variant == t.LO, status)
             finally:
                 peer.set_sched_push(0)
+            # the same program with tune peer_fence=1 (release / acquire fences around every flag)
+            t.tune("peer_fence", 1)
+            try:
+                timed("peer_fenced_" + name, peer_fn, variant == t.LO, status)
+            finally:
+                t.tune("peer_fence", 0)
         if name.startswith("config5"):   # the same LO program without LL hand-offs (k_peer_sched)
             peer.set_lo_ll_max(0)
             try:
@@ -805,6 +811,28 @@ def cpu_baseline_multi() -> dict:
                        "640 kB, config 4 Swing BO at 64 MiB per rank (reduced from 1 GiB, <= 5 reps), "
                        "config 5 Swing LO 2/8/32/128 kB; value = config 3, bytes of all 8 ranks / median time"),
             "online_cpus": os.sysconf("SC_NPROCESSORS_ONLN"), "configs": res}
+
+
+def dropped_candidates(verify: dict) -> list:
+    """xgmi.dropped: every transport whose verdict is not verified, with why —
+    a peer wait that gave up in its quick timing, bits that differ from the
+    form of the same semantics, a failed exact-sum / closed-form check."""
+    out = []
+    for kind, v in verify.items():
+        if v.get("verified") is True:
+            continue
+        if v.get("quick_timing_timeout"):
+            why = "quick_timing_timeout: a peer wait gave up during its timing"
+        elif any(k.startswith("matches_") and v[k] is False for k in v):
+            why = "differs from " + next(k[len("matches_"):] for k in v if k.startswith("matches_") and v[k] is False)
+        elif v.get("exact_sum") is False:
+            why = "exact_sum check failed"
+        elif v.get("closed_form") is False:
+            why = "closed_form check failed"
+        else:
+            why = "verification failed"
+        out.append({"transport": kind, "reason": why})
+    return out
 
 
 def choose_transport(quick: dict, verify: dict):
@@ -943,6 +971,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   peer_hier_x2t2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
     #                 owned tiles before its last row stores, writes bucket i-2; every poll waits
     #                 for the previous launch)
+    #   <peer kind>_fenced  the same kernel with tune peer_fence=1: a system-scope release
+    #                 fence before every cross-GPU hand-off, an acquire fence after every wait
+    #                 (same bits; the form that stays correct on a node that breaks the ordering
+    #                 argument of DESIGN.md §5) — verified and timed for every relaxed form that
+    #                 failed and for the two fastest that passed
     # (retired in round 5, every measurement slower — profiles/README.md: the per-tile flag
     # form k_hier_oneshot, the pipelined LL form k_hier_pipe, the flag hand-off forms of
     # k_hier_ll / _x / _x2, and k_hier_x2's owned sums at the launch start / end)
@@ -961,12 +994,18 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     pend4 = [None, 0]   # peer_mem_x: the started bucket and the partial slot it used (flush())
     mem_parts = [torch.empty(ELEMS, dtype=torch.int16, device=dev) for _ in range(2)]
     tail = [None]
+    fence = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
 
     def x2_tail(v):   # the host-side switch between the k_hier_x2 owned-sum placements, read at launch
         if tail[0] != v:
             t.tune("hier_x2_tail", int(v))
             tail[0] = v
+
+    def set_fence(v):   # tune peer_fence, read at every peer launch
+        if fence[0] != v:
+            t.tune("peer_fence", v)
+            fence[0] = v
 
     def set_rearly(v):   # k_hier_x: R(cur) ahead of the previous bucket's last row stores (read at launch)
         if rearly[0] != v:
@@ -997,6 +1036,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         peer = peer_box[0]
         if fresh:   # b was just written on torch's current stream
             stream.wait_stream(torch.cuda.current_stream())
+        if kind.startswith("peer"):   # <kind>_fenced: the same kernel with the fences
+            base = kind[:-len("_fenced")] if kind.endswith("_fenced") else kind
+            set_fence(int(base != kind))
+            kind = base
         if kind == "rccl_x":   # buckets pipelined: this call writes the previous one's rows
             if pend[0] is not None or pend2[0] or pend4[0] is not None:
                 flush()
@@ -1058,7 +1101,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
 
         status = (lambda: peer.status() & t.PEER_TIMEOUT) if kind.startswith("peer") else None
         v = verify_transport(once, vbuf, world, rank, RANKS, SIDE, side, seed, status=status)
-        same_as = {"peer_swing": "rccl", "rccl_x": "rccl"}.get(kind, None if kind in ("rccl", "peer_launches")
+        base = kind[:-len("_fenced")] if kind.endswith("_fenced") else kind
+        same_as = {"peer_swing": "rccl", "rccl_x": "rccl"}.get(base, None if base in ("rccl", "peer_launches")
                                                                      else "peer_launches")
         if same_as == "rccl" and not verify.get("rccl", {}).get("verified"):
             same_as = None   # --share-gpu: no RCCL to compare with (the Swing trees differ from mem_2D's)
@@ -1115,36 +1159,64 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     if peer is None and not rccl_ok:
         raise RuntimeError("no verified transport: RCCL " + (comm_err or ("unverified" if comm else "absent")) +
                            f", peer windows: {peer_err}")
+    def drop(kind, reason):   # on stderr as it happens; xgmi.dropped lists them all (dropped_candidates)
+        note(rank, f"DROPPED {kind}: {reason}")
+
     candidates = (["rccl"] if rccl_ok else []) + (["rccl_x"] if rccl_x_ok else [])
-    if peer is not None:
-        for i, kind in enumerate(("peer_launches", "peer_swing", "peer_mem_x", "peer_hier_ll", "peer_hier_x",
-                                  "peer_hier_xr", *X2_KINDS)):
-            if check(kind, 9100 + 10 * i):
-                candidates.append(kind)
-    if not candidates:
-        raise RuntimeError(f"no transport passed verification on this machine: {verify}")
+    for kind, ok in (("rccl", rccl_ok), ("rccl_x", rccl_x_ok)):
+        if comm is not None and kind in verify and not ok:
+            drop(kind, "verification failed")
     quick = {}
     # each candidate timed the way the headline is: K steps with the pipelined forms'
     # finishing launch inside (it weighs 1/K per step), median of three
     qk = max(args.steps, 10)
-    for kind in candidates:
-        note(rank, f"quick timing: {kind}")
-        it = iter(range(1 << 30))
-        quick[kind] = round(statistics.median(
-            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
-            for _ in range(3)), 4)
-        if peer is not None and kind.startswith("peer"):
-            # a peer wait that gave up means wrong bytes: the candidate is out (every rank agrees),
-            # and the sticky status bit is cleared so the next candidates wait normally again
-            torch.cuda.synchronize()
-            st0 = torch.tensor([peer.status() & t.PEER_TIMEOUT], dtype=torch.int64)
-            dist.all_reduce(st0, op=dist.ReduceOp.MAX)
-            if st0.item():
-                note(rank, f"peer wait timed out during the quick timing of {kind}: dropped")
-                quick.pop(kind, None)
-                verify.setdefault(kind, {}).update(verified=False, quick_timing_timeout=True)
-                peer.clear_status()
-                dist.barrier()
+
+    def quick_time(kinds):
+        for kind in kinds:
+            note(rank, f"quick timing: {kind}")
+            it = iter(range(1 << 30))
+            quick[kind] = round(statistics.median(
+                timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
+                for _ in range(3)), 4)
+            if peer is not None and kind.startswith("peer"):
+                # a peer wait that gave up means wrong bytes: the candidate is out (every rank agrees),
+                # and the sticky status bit is cleared so the next candidates wait normally again
+                torch.cuda.synchronize()
+                st0 = torch.tensor([peer.status() & t.PEER_TIMEOUT], dtype=torch.int64)
+                dist.all_reduce(st0, op=dist.ReduceOp.MAX)
+                if st0.item():
+                    drop(kind, "quick_timing_timeout: a peer wait gave up during its timing")
+                    quick.pop(kind, None)
+                    verify.setdefault(kind, {}).update(verified=False, quick_timing_timeout=True)
+                    peer.clear_status()
+                    dist.barrier()
+
+    quick_time(list(candidates))
+    if peer is not None:
+        relaxed = ("peer_launches", "peer_swing", "peer_mem_x", "peer_hier_ll", "peer_hier_x", "peer_hier_xr",
+                   *X2_KINDS)
+        passed = []
+        for i, kind in enumerate(relaxed):
+            if check(kind, 9100 + 10 * i):
+                passed.append(kind)
+            else:
+                drop(kind, "verification failed")
+        quick_time(passed)
+        # the fenced twins: of every relaxed form that failed (verification or timing) and of
+        # the two fastest that passed, so a node that breaks the relaxed ordering still
+        # leaves a verified peer form behind
+        failed = [k for k in relaxed if k not in quick]
+        fastest = sorted((k for k in relaxed if k in quick), key=lambda k: quick[k])[:2]
+        fenced = []
+        for i, kind in enumerate(failed + fastest):
+            if check(kind + "_fenced", 9300 + 10 * i):
+                fenced.append(kind + "_fenced")
+            else:
+                drop(kind + "_fenced", "verification failed")
+        quick_time(fenced)
+        set_fence(0)
+    if not quick:
+        raise RuntimeError(f"no transport passed verification on this machine: {verify}")
     transport = choose_transport(quick, verify)
     if transport is None:   # every verified candidate had a peer wait give up in its timing
         raise RuntimeError(f"no transport timed without a peer timeout on this machine: {verify}")
@@ -1183,6 +1255,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     if peer is not None:   # defaults again for the extras below
         peer.set_oneshot_max(4 << 20)
         peer.set_hier_ll(0)
+        set_fence(0)
         mode[0] = None
     fused_local = transport in ("rccl_x", "peer_mem_x")
     local_ms = local_phases_ms(fused=fused_local)
@@ -1192,6 +1265,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     HEADLINE_DONE.set()
 
     extras = {"headline_transport": transport, "transport_verified": verify, "transport_quick_ms": quick,
+              "dropped": dropped_candidates(verify),
               "peer_timeout_in_timed_loop": peer_timeout,
               "local_phases_ms": {"tree_then_broadcast": round(local_split_ms, 6),
                                   **({"tree_broadcast_fused": round(local_ms, 6)} if fused_local else {})},
@@ -1286,11 +1360,13 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
     """rank 0's JSON line of the N > 1 bench"""
     bytes_all = world * RANKS * ELEMS * 2
     local_bytes = 2 * RANKS * ELEMS * 2 + 2 * ELEMS * 2
-    if transport in ONE_LAUNCH:   # the step IS one launch: its HBM bytes over its time
-        kern = ONE_LAUNCH[transport]
+    fenced = transport.endswith("_fenced")   # the same kernel with tune peer_fence=1
+    base = transport[:-len("_fenced")] if fenced else transport
+    if base in ONE_LAUNCH:   # the step IS one launch: its HBM bytes over its time
+        kern = ONE_LAUNCH[base]
         roof = {"kernel": f"{kern} (whole step)", "algorithmic_bytes_per_launch": 2 * RANKS * ELEMS * 2,
                 "achieved": 2 * RANKS * ELEMS * 2 / (ms_per_step * 1e-3) / 1e9, "traffic": pmc_traffic(kern)}
-    elif transport in ("rccl_x", "peer_mem_x"):   # the local HBM pass: bucket i's broadcast + i+1's tree, one kernel
+    elif base in ("rccl_x", "peer_mem_x"):   # the local HBM pass: bucket i's broadcast + i+1's tree, one kernel
         roof = {"kernel": "k_tree_bcast_x (local phases of consecutive buckets, one pass)",
                 "algorithmic_bytes_per_launch": local_bytes, "achieved": local_bytes / (local_ms * 1e-3) / 1e9,
                 "traffic": pmc_traffic("k_tree_bcast_x<1>")}
@@ -1319,7 +1395,9 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
            "peer_hier_xr": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with the owned "
                            "sums ahead of the previous bucket's last row stores, LL pushes into peer-mapped xGMI windows",
            "peer_hier_ll": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
-                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[transport]
+                           "(data+epoch words) into peer-mapped xGMI windows, broadcast"}[base]
+    if fenced:
+        via += " (peer_fence: release / acquire fences around every cross-GPU hand-off)"
     v = extras.get("transport_verified", {}).get(transport, {})
     return {
         "metric": METRIC,

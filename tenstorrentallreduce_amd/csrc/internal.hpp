@@ -41,7 +41,7 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
-    rccl_fault, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll,
+    rccl_fault, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll, peer_fence,
     count
 };
 int64_t tune(Tune key);
@@ -130,6 +130,7 @@ constexpr int kPeerMaxChannels = 7;
 constexpr int kPeerMaxSteps = 6;
 struct PeerProg {
     int S = 0, C = 1, N = 1, lo = 0;
+    int fence = 0;   // tune peer_fence (set by the launchers): release / acquire fences around every flag
     int peer[kPeerMaxChannels][kPeerMaxSteps] = {};       // real rank, [channel][step]
     uint64_t recv[kPeerMaxChannels][kPeerMaxSteps] = {};  // block masks in the channel's labels
     uint64_t send[kPeerMaxChannels][kPeerMaxSteps] = {};

@@ -24,6 +24,21 @@ struct PeerPtrs {
     uint32_t* flags[ALLRED_MAX_NODES];   // flag array of rank q, as mapped here
 };
 
+// tune peer_fence = 1 (the `fence` argument of every peer kernel): a system-scope
+// release fence before every store that hands data or progress to another GPU
+// and an acquire fence after every wait on another GPU's store.  The default
+// (0) relies on the ordering argument of DESIGN.md §5 instead — every hand-off
+// goes to uncached (MTYPE UC) memory, so a store acknowledged to s_waitcnt is
+// in the target's HBM before the workgroup barrier that precedes the flag, and
+// an LL word is its own flag.  Same bits either way; the fenced form is the one
+// a node that breaks the argument still runs correctly.
+__device__ __forceinline__ void peer_release(uint32_t fence) {
+    if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+__device__ __forceinline__ void peer_acquire(uint32_t fence) {
+    if (fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+
 // one workgroup: tell every peer "rank `me` reached `epoch`", then wait for all.
 // Bounded: on timeout bit 0 of *status is set and the kernel returns.
 __global__ void k_peer_barrier(PeerPtrs pp, int nranks, int me, uint32_t epoch, uint32_t* status) {
@@ -115,8 +130,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_ag(PeerPtrs pp, int me, uint16_
 // L2 writeback / invalidate, which cost ~20 us at 128 KiB).  allred_peer
 // only selects this form when both allocations really are uncached.
 __device__ inline void peer_signal_wait(const PeerPtrs& pp, int nranks, int me, uint32_t slot_base, uint32_t epoch,
-                                        uint32_t* status) {
+                                        uint32_t* status, uint32_t fence) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    peer_release(fence);
     __syncthreads();
     const int t = threadIdx.x;
     if (t < nranks)
@@ -131,11 +147,12 @@ __device__ inline void peer_signal_wait(const PeerPtrs& pp, int nranks, int me, 
         }
     }
     __syncthreads();
+    peer_acquire(fence);
 }
 
 __global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks, int me, uint16_t* __restrict__ bucket,
                                                          uint64_t blk_vec, uint64_t chunk, uint32_t epoch,
-                                                         uint32_t* status) {
+                                                         uint32_t* status, uint32_t fence) {
     const int g = blockIdx.x;
     const uint64_t lo = (uint64_t)g * chunk;
     const uint64_t hi = lo + chunk < blk_vec ? lo + chunk : blk_vec;
@@ -149,7 +166,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks
     }
     const uint32_t base0 = kPeerFusedFlagOff + (uint32_t)g * 64u;
     const uint32_t base1 = kPeerFusedFlagOff + (uint32_t)(kPeerFusedMaxGroups + g) * 64u;
-    peer_signal_wait(pp, nranks, me, base0, epoch, status);
+    peer_signal_wait(pp, nranks, me, base0, epoch, status, fence);
     // 2. reduce my block's sub-slice g
     const uint64_t off = (uint64_t)me * blk_vec;
     for (uint64_t v = lo + threadIdx.x; v < hi; v += blockDim.x) {
@@ -178,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks
         st_nt(mywin + off + v, o);
         st_nt(reinterpret_cast<uint4*>(bucket) + off + v, o);
     }
-    peer_signal_wait(pp, nranks, me, base1, epoch, status);
+    peer_signal_wait(pp, nranks, me, base1, epoch, status, fence);
     // 3. gather every other block's sub-slice g from its owner
     for (uint64_t i = threadIdx.x; i < (uint64_t)nranks * len; i += blockDim.x) {
         const uint64_t q = i / len, v = q * blk_vec + lo + i % len;
@@ -204,6 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_oneshot(PeerPtrs pp, int nranks
 __device__ inline void sched_signal(const PeerPtrs& pp, const PeerProg& pr, int c, int me, uint32_t slot,
                                     uint32_t value) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    peer_release(pr.fence);
     __syncthreads();
     const int t = threadIdx.x;
     if (t < pr.S)
@@ -211,7 +229,7 @@ __device__ inline void sched_signal(const PeerPtrs& pp, const PeerProg& pr, int 
 }
 
 __device__ inline void sched_wait(const PeerPtrs& pp, int me, uint32_t slot, int q0, int q1, uint32_t value,
-                                  uint32_t* status) {
+                                  uint32_t* status, uint32_t fence) {
     const int t = threadIdx.x;
     const int q = t == 0 ? q0 : (t == 1 ? q1 : -1);
     if (q >= 0) {
@@ -224,6 +242,7 @@ __device__ inline void sched_wait(const PeerPtrs& pp, int me, uint32_t slot, int
         }
     }
     __syncthreads();
+    peer_acquire(fence);
 }
 
 __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
@@ -244,7 +263,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
         sched_signal(pp, pr, c, me, slot, base + 1);
         for (int k = 0; k < S; ++k) {  // reduce-scatter
             const int p = pr.peer[c][k];
-            sched_wait(pp, me, slot, p, -1, base + 1 + k, status);
+            sched_wait(pp, me, slot, p, -1, base + 1 + k, status, pr.fence);
             const uint4* theirs = reinterpret_cast<const uint4*>(pp.win[p]);
             const bool last = k == S - 1;
             for (uint64_t m = pr.recv[c][k]; m; m &= m - 1) {
@@ -272,7 +291,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
         for (int t = 0; t < S; ++t) {  // all-gather, steps in reverse
             const int i = S - 1 - t, pos = S + t;
             const int p = pr.peer[c][i];
-            sched_wait(pp, me, slot, p, -1, base + 1 + pos, status);
+            sched_wait(pp, me, slot, p, -1, base + 1 + pos, status, pr.fence);
             const uint4* theirs = reinterpret_cast<const uint4*>(pp.win[p]);
             const bool keep = t < S - 1;  // later partners read these blocks from my window
             for (uint64_t m = pr.send[c][i]; m; m &= m - 1) {
@@ -304,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched(PeerPtrs pp, PeerProg pr,
     for (int k = 0; k < S; ++k) {
         const int p = pr.peer[c][k];
         const bool last = k == S - 1;
-        sched_wait(pp, me, slot, p, (k >= 1 && !last) ? pr.peer[c][k - 1] : -1, base + 1 + k, status);
+        sched_wait(pp, me, slot, p, (k >= 1 && !last) ? pr.peer[c][k - 1] : -1, base + 1 + k, status, pr.fence);
         const uint4* a = mine + (k & 1) * half_vec;
         const uint4* b = reinterpret_cast<const uint4*>(pp.win[p]) + (k & 1) * half_vec;
         uint4* dst = last ? bk : mine + ((k + 1) & 1) * half_vec;
@@ -341,8 +360,9 @@ struct PeerStage {
     uint16_t* st[ALLRED_MAX_NODES];   // GPU q's staging window, as mapped here
 };
 
-__device__ inline void push_signal(const PeerPtrs& pp, int p, int me, uint32_t slot, uint32_t value) {
+__device__ inline void push_signal(const PeerPtrs& pp, int p, int me, uint32_t slot, uint32_t value, uint32_t fence) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's pushes have completed
+    peer_release(fence);
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(pp.flags[p] + kPeerSchedPushOff + slot + me, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -384,10 +404,10 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched_push(PeerPtrs pp, PeerSta
     sched_signal(pp, pr, c, me, slot, base + 1);
     for (int k = 0; k < S; ++k) {  // reduce-scatter
         const int p = pr.peer[c][k];
-        sched_wait(pp, me, slot, p, -1, base + 1 + k, status);                 // p's staging is free
+        sched_wait(pp, me, slot, p, -1, base + 1 + k, status, pr.fence);                 // p's staging is free
         move(pr.send[c][k], mine, reinterpret_cast<uint4*>(ps.st[p]));         // my blocks -> p's staging
-        push_signal(pp, p, me, gs, base + 1 + k);
-        sched_wait(pp, me, kPeerSchedPushOff + gs, p, -1, base + 1 + k, status);   // p's blocks are in mine
+        push_signal(pp, p, me, gs, base + 1 + k, pr.fence);
+        sched_wait(pp, me, kPeerSchedPushOff + gs, p, -1, base + 1 + k, status, pr.fence);   // p's blocks are in mine
         const bool last = k == S - 1;
         for (uint64_t m = pr.recv[c][k]; m; m &= m - 1) {
             const int b = __builtin_ctzll(m);
@@ -414,10 +434,10 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched_push(PeerPtrs pp, PeerSta
     for (int t = 0; t < S; ++t) {  // all-gather, steps in reverse
         const int i = S - 1 - t, pos = S + t;
         const int p = pr.peer[c][i];
-        sched_wait(pp, me, slot, p, -1, base + 1 + pos, status);               // p is past its RS step i
+        sched_wait(pp, me, slot, p, -1, base + 1 + pos, status, pr.fence);               // p is past its RS step i
         move(pr.recv[c][i], mine, reinterpret_cast<uint4*>(pp.win[p]));        // my owned blocks -> p's window
-        push_signal(pp, p, me, gs, base + 1 + pos);
-        sched_wait(pp, me, kPeerSchedPushOff + gs, p, -1, base + 1 + pos, status);
+        push_signal(pp, p, me, gs, base + 1 + pos, pr.fence);
+        sched_wait(pp, me, kPeerSchedPushOff + gs, p, -1, base + 1 + pos, status, pr.fence);
         move(pr.send[c][i], mine, bk);                                          // p's blocks, now in mine -> bucket
         if (t < S - 1) sched_signal(pp, pr, c, me, slot, base + 2 + pos);
     }
@@ -530,7 +550,7 @@ __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, 
 __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status) {
+                                                    uint32_t epoch, uint32_t* status, uint32_t fence) {
     constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
@@ -601,6 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         lds_barrier();
         // the partial -> its owner's inbox: wave w writing word w of every column (one store
         // instruction per wave)
+        peer_release(fence);
         if (h == 0) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
@@ -636,7 +657,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             for (int src = 0; src < kLLMaxGpus; ++src)
                 if (src < W)
                     y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(my_ll + (li * W + src) * 128 + c, epoch, status);
+            peer_acquire(fence);
             val = owner_sum(y, W, me);
+            peer_release(fence);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
                 if (dst < W && dst != me) ll_put(lp.ll[dst] + box_words + t * 128 + c, val, epoch);
@@ -667,6 +690,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         };
         store_batch(true);
         if (!own && b < nb) xs[b * 32 + c] = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + t * 128 + c, epoch, status);
+        peer_acquire(fence);
         __syncthreads();
         store_batch(false);
         __syncthreads();   // xs is reused by the next batch
@@ -715,7 +739,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                    uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                                                   uint32_t* status) {
+                                                   uint32_t* status, uint32_t fence) {
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
@@ -760,6 +784,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         uint64_t wd[4];
         ll_load(at, wd);
         slot = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+        peer_acquire(fence);
     };
     // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
     const bool lp = (RE & 2) && LAG == 1 && cur;
@@ -789,6 +814,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
             // the partial -> its owner's inbox: wave w writing word w of every column (one
             // store instruction per wave)
+            peer_release(fence);
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
@@ -841,7 +867,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                     if (src < W)
                         y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
                                                          : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
+                peer_acquire(fence);
                 const uint4 o = owner_sum(y, W, me);
+                peer_release(fence);
 #pragma unroll
                 for (int dst = 0; dst < kLLMaxGpus; ++dst)
                     if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
@@ -902,7 +930,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
-                                                    int has_mid, uint32_t* status) {
+                                                    int has_mid, uint32_t* status, uint32_t fence) {
     // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
     // stores, not after them
     constexpr bool tl2 = (TAIL & 3) == 2;
@@ -964,7 +992,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             if (src < W)
                 y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
                                                  : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
+        peer_acquire(fence);
         const uint4 o = owner_sum(y, W, me);
+        peer_release(fence);
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
             if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
@@ -977,6 +1007,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         uint64_t wd[4];
         ll_load(at, wd);
         slot = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
+        peer_acquire(fence);
     };
     {
         uint64_t wo[4];
@@ -986,6 +1017,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
         if (early_old && act_in(0))
             res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
+        peer_acquire(fence);
         if (CH && early_old && nch > 1) poll_old(1);
     }
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
@@ -1031,6 +1063,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             }
             // the partial -> its owner's inbox: wave w writing word w of every column (one
             // store instruction per wave)
+            peer_release(fence);
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
@@ -1078,6 +1111,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             __syncthreads();   // every wave has read the slot's previous results
             if (act_in(ch))
                 res[CH ? ch & 1 : 0][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
+            peer_acquire(fence);
             lds_barrier();
             for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
         }
@@ -1100,11 +1134,13 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
 __host__ __device__ constexpr uint64_t ll_padded(uint64_t slots) { return (slots + 31) / 32 * 32; }
 
 __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me, uint16_t* __restrict__ bucket,
-                                                        uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status) {
+                                                        uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status,
+                                                        uint32_t fence) {
     const uint64_t gt = gtid(), GT = gthreads();
     uint4* bk = reinterpret_cast<uint4*>(bucket);
     uint64_t* const my_ll = lp.ll[me];
     const uint64_t box = ll_padded(nv) * 4;   // words
+    peer_release(fence);
     for (uint64_t v = gt; v < nv; v += GT) {   // A
         const int o = (int)(v / bv);
         // the owner's area by an unrolled select over the (scalar) kernarg pointers: a
@@ -1139,6 +1175,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
             if (peer_give_up(spin, t0, status)) break;
             __builtin_amdgcn_s_sleep(1);
         }
+        peer_acquire(fence);
         float a[8];
 #pragma unroll
         for (int q = 0; q < kLLMaxGpus; ++q) {
@@ -1156,9 +1193,14 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
         }
         const uint4 r = make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
         const uint64_t v = (uint64_t)me * bv + u;
+        peer_release(fence);
         for (int q = 0; q < W; ++q) ll_put(ll_slot(lp.ll[q] + box, v), r, epoch);
     }
-    for (uint64_t v = gt; v < nv; v += GT) st_nt(bk + v, ll_get(ll_slot(my_ll + box, v), epoch, status));   // B
+    for (uint64_t v = gt; v < nv; v += GT) {   // B
+        const uint4 r = ll_get(ll_slot(my_ll + box, v), epoch, status);
+        peer_acquire(fence);
+        st_nt(bk + v, r);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1176,6 +1218,7 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
                                                        uint64_t nv, uint32_t epoch, uint32_t* status) {
+    const uint32_t fence = pr.fence;
     const uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (v >= nv) return;
     uint4* bk = reinterpret_cast<uint4*>(bucket);
@@ -1184,8 +1227,11 @@ __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, i
     const uint64_t per_step = ll_padded(nv);   // slots
     for (int k = 0; k < pr.S; ++k) {
         const int p = pr.peer[0][k];
+        peer_release(fence);
         ll_put(ll_slot(lp.ll[p], (uint64_t)k * per_step + v), cur, epoch);
-        cur = add8(cur, ll_get(ll_slot(mine, (uint64_t)k * per_step + v), epoch, status));
+        const uint4 y = ll_get(ll_slot(mine, (uint64_t)k * per_step + v), epoch, status);
+        peer_acquire(fence);
+        cur = add8(cur, y);
     }
     st_nt(bk + v, cur);
 }
@@ -1248,7 +1294,9 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
     const uint64_t gmax = cap / prog.C > 0 ? cap / prog.C : 1;
     if (gc > gmax) gc = gmax;
     if (gc < 1) gc = 1;
-    hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, prog, me,
+    PeerProg pf = prog;
+    pf.fence = (int)tune(Tune::peer_fence);
+    hipLaunchKernelGGL(k_peer_sched, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, pf, me,
                        bucket, half_vec, base_epoch, status);
     return peer_last_error();
 }
@@ -1273,8 +1321,10 @@ int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint3
     const uint64_t gmax = cap / prog.C > 0 ? cap / prog.C : 1;
     if (gc > gmax) gc = gmax;
     if (gc < 1) gc = 1;
+    PeerProg pf = prog;
+    pf.fence = (int)tune(Tune::peer_fence);
     hipLaunchKernelGGL(k_peer_sched_push, dim3((unsigned)(gc * prog.C)), dim3(kBlock), 0, (hipStream_t)stream, pp, ps,
-                       prog, me, bucket, base_epoch, status);
+                       pf, me, bucket, base_epoch, status);
     return peer_last_error();
 }
 
@@ -1289,7 +1339,7 @@ int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket
     const uint64_t cap = max_groups && max_groups < kPeerFusedMaxGroups ? max_groups : kPeerFusedMaxGroups;
     if (groups > cap) groups = cap;   // resident: every wait is reached
     hipLaunchKernelGGL(k_peer_mem_ll, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, lp, nranks, me,
-                       bucket, nv, nv / nranks, epoch, status);
+                       bucket, nv, nv / nranks, epoch, status, (uint32_t)tune(Tune::peer_fence));
     return peer_last_error();
 }
 
@@ -1301,8 +1351,10 @@ int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket,
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    PeerProg pf = prog;
+    pf.fence = (int)tune(Tune::peer_fence);
     hipLaunchKernelGGL(k_peer_lo_ll, dim3((unsigned)((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)stream, lp, prog, me, bucket, nv, epoch, status);
+                       (hipStream_t)stream, lp, pf, me, bucket, nv, epoch, status);
     return peer_last_error();
 }
 
@@ -1319,7 +1371,7 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
-                       me, ntiles, ntiles / nranks, box_words, epoch, status);
+                       me, ntiles, ntiles / nranks, box_words, epoch, status, (uint32_t)tune(Tune::peer_fence));
     return peer_last_error();
 }
 
@@ -1356,7 +1408,7 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, eprev, status);
+                       box_words, ecur, eprev, status, (uint32_t)tune(Tune::peer_fence));
     return peer_last_error();
 }
 
@@ -1407,7 +1459,7 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         default: return ALLRED_ERR_ARG;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, emid, eold, llm ? 1 : 0, status);
+                       box_words, ecur, emid, eold, llm ? 1 : 0, status, (uint32_t)tune(Tune::peer_fence));
     return peer_last_error();
 }
 
@@ -1425,7 +1477,7 @@ int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nrank
     if (groups < 1) groups = 1;
     const uint64_t chunk = (bv + groups - 1) / groups;
     hipLaunchKernelGGL(k_peer_oneshot, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, pp, nranks, me,
-                       bucket, bv, chunk, epoch, status);
+                       bucket, bv, chunk, epoch, status, (uint32_t)tune(Tune::peer_fence));
     return peer_last_error();
 }
 

@@ -133,9 +133,15 @@ def test_tune_entry_point():
     for key, bad in (("hier_x2_tail", 3), ("rccl_fault", 8)):
         with pytest.raises(t.AllredError):
             t.tune(key, bad)
-    # round 5: the flag hand-off forms are gone with their key (the trimmed table)
+    # round 5: the flag hand-off forms are gone with their key (the trimmed table); peer_fence
+    # (release / acquire fences around every cross-GPU hand-off) is off by default, 0 / 1 only
     with pytest.raises(t.AllredError):
         t.tune("hier_handoff")
+    assert t.tune("peer_fence") == 0
+    with t.tuned(peer_fence=1):
+        assert t.tune("peer_fence") == 1
+    with pytest.raises(t.AllredError):
+        t.tune("peer_fence", 2)
 
 
 def test_mem_program_stats_one_rank_has_no_launch():

@@ -138,6 +138,26 @@ def test_closed_form_is_the_references_expected_value():
     assert torch.equal(cf, ref)
 
 
+def test_dropped_candidates_are_listed_with_a_reason():
+    """xgmi.dropped: a form that failed verification or whose quick timing had a
+    peer wait give up is listed (and never chosen); verified forms are not."""
+    verify = {"rccl": {"verified": True, "exact_sum": True, "closed_form": True},
+              "peer_hier_x": {"verified": False, "quick_timing_timeout": True},
+              "peer_hier_ll": {"verified": False, "exact_sum": True, "closed_form": True,
+                               "matches_peer_launches": False},
+              "peer_swing": {"verified": False, "exact_sum": False, "closed_form": True},
+              "peer_hier_x_fenced": {"verified": True, "exact_sum": True, "closed_form": True,
+                                     "matches_peer_launches": True}}
+    quick = {"rccl": 1.0, "peer_hier_x_fenced": 0.6}
+    assert bench.choose_transport(quick, verify) == "peer_hier_x_fenced"
+    got = {d["transport"]: d["reason"] for d in bench.dropped_candidates(verify)}
+    assert set(got) == {"peer_hier_x", "peer_hier_ll", "peer_swing"}
+    assert got["peer_hier_x"].startswith("quick_timing_timeout")
+    assert got["peer_hier_ll"] == "differs from peer_launches"
+    assert got["peer_swing"] == "exact_sum check failed"
+    assert bench.dropped_candidates({"rccl": {"verified": True}}) == []
+
+
 def test_unverified_never_headline_nor_roofline():
     quick = {"rccl": 1.0, "peer_hier_ll": 0.5, "peer_swing": 0.8}
     verify = {"rccl": {"verified": True}, "peer_hier_ll": {"verified": False}, "peer_swing": {"verified": True}}

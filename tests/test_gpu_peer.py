@@ -24,7 +24,43 @@ def free_port():
     return p
 
 
-def worker(rank, world, port, q):
+def placement(rank, world, devs, tunes):
+    """A worker's device (devs[rank]; None: every rank on device 0, the one-GPU
+    rehearsal) and the tune keys every rank sets before its first call
+    (bit-identical forms, e.g. peer_fence).  Returns (devs, "cuda:i", shared)."""
+    import tenstorrentallreduce_amd as t
+    devs = list(devs) if devs else [0] * world
+    torch.cuda.set_device(devs[rank])
+    for k, v in (tunes or {}).items():
+        t.tune(k, v)
+    return devs, f"cuda:{devs[rank]}", len(set(devs)) < world
+
+
+def run_world(target, world, timeout, devs=None, tunes=None):
+    """world spawned processes running target(rank, world, port, q, devs, tunes);
+    every rank must report no failure and a clean peer status word."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q, devs, tunes)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = []
+    try:
+        for _ in procs:
+            results.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, fails, status in results:
+        assert fails == [], (rank, fails)
+        assert status == 0, (rank, status)
+
+
+def worker(rank, world, port, q, devs=None, tunes=None):
     try:
         import torch.distributed as dist
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -32,17 +68,18 @@ def worker(rank, world, port, q):
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import tenstorrentallreduce_amd as t
         import oracle
+        devs, dev, shared = placement(rank, world, devs, tunes)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         unit = 8 * world
         sizes = [unit, unit * 64 * 5, unit * 3, unit * 8200, unit * 64 * 5]   # 8200 vectors: > 128 groups x 64
         n = unit * 64 * 5
-        peer = t.Peer(world, rank, 0, max(sizes))
+        peer = t.Peer(world, rank, devs[rank], max(sizes))
         handles = [None] * world
         dist.all_gather_object(handles, peer.handle())
         peer.connect(handles)
         # the one-kernel forms wait across processes: every process's grid must be
         # resident at once on the shared GPU (one GPU per process needs no cap)
-        peer.set_max_groups(256 // world)
+        peer.set_max_groups(256 // world if shared else 0)
         fails = []
         call = 0
         for mode, limit, ll_max in (("oneshot", 1 << 40, 0), ("steps", 0, 0), ("auto", 1 << 20, 256 << 10),
@@ -52,7 +89,7 @@ def worker(rank, world, port, q):
             for m in sizes:
                 rng = [np.random.default_rng(1000 * call + r) for r in range(world)]
                 data = [g.integers(0x3F80, 0x42C8, m).astype(np.uint16) for g in rng]
-                buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
+                buf = torch.from_numpy(data[rank].view(np.int16)).to(dev)
                 peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream())
                 torch.cuda.synchronize()
                 want = [d.copy() for d in data]
@@ -66,7 +103,7 @@ def worker(rank, world, port, q):
         bufs = []
         for k in range(6):
             d = np.random.default_rng(50 + k * world + rank).integers(0x3F80, 0x42C8, n).astype(np.uint16)
-            bufs.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
+            bufs.append(torch.from_numpy(d.view(np.int16)).to(dev))
         torch.cuda.synchronize()
         dist.barrier()
         for k, b in enumerate(bufs):   # launches / one kernel / LL pushes, interleaved
@@ -86,8 +123,8 @@ def worker(rank, world, port, q):
         local = 8
         data = [np.random.default_rng(77 + r).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
                 for r in range(world)]
-        buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
-        ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
+        buf = torch.from_numpy(data[rank].view(np.int16)).to(dev)
+        ws = torch.empty(n, dtype=torch.int16, device=dev)
         peer.allreduce(buf.data_ptr(), n, torch.cuda.current_stream(), local, 4, t.SWING, ws.data_ptr())
         torch.cuda.synchronize()
         partials = []
@@ -128,8 +165,8 @@ def worker(rank, world, port, q):
             for rep in range(3 if mode.startswith("hier_x2") else 2):   # x2: one launch with cur, mid and old
                 data = [np.random.default_rng(700 + 100 * mi + 10 * rep + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
                         for r in range(world)]
-                buf = torch.from_numpy(data[rank].view(np.int16)).to("cuda:0")
-                ws = torch.empty(m, dtype=torch.int16, device="cuda:0")
+                buf = torch.from_numpy(data[rank].view(np.int16)).to(dev)
+                ws = torch.empty(m, dtype=torch.int16, device=dev)
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
                     with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
                                  hier_x_latepoll=int("_lp" in mode)):
@@ -175,30 +212,18 @@ def worker(rank, world, port, q):
         q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
 
 
+# tune peer_fence = 1: a system-scope release fence before every cross-GPU hand-off store and an
+# acquire fence after every wait (the same bits)
+FENCES = pytest.mark.parametrize("tunes", [{}, {"peer_fence": 1}], ids=["relaxed", "fenced"])
+
+
+@FENCES
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_peer_one_shot_multi_process_one_gpu(world):
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = []
-    try:
-        for _ in procs:
-            results.append(q.get(timeout=240))
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.kill()
-    for rank, fails, status in results:
-        assert fails == [], (rank, fails)
-        assert status == 0, (rank, status)
+def test_peer_one_shot_multi_process_one_gpu(world, tunes):
+    run_world(worker, world, 240, tunes=tunes)
 
 
-def dist_worker(rank, world, port, q):
+def dist_worker(rank, world, port, q, devs=None, tunes=None):
     """allred_peer_dist_allreduce: every case of the gloo-tested RCCL program
     (tests/test_dist_host.py: Swing / RecDub / 1D schedules, BO and LO, flat and
     hierarchical, link-spreading channels) over the peer windows — read by the
@@ -212,10 +237,11 @@ def dist_worker(rank, world, port, q):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import tenstorrentallreduce_amd as t
         import test_dist_host as tdh
+        devs, dev, shared = placement(rank, world, devs, tunes)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         side, total = tdh.GRIDS[world]
         n = 8 * total * 16 * 3
-        peer = t.Peer(world, rank, 0, 4 * n * 2)
+        peer = t.Peer(world, rank, devs[rank], 4 * n * 2)
         handles = [None] * world
         dist.all_gather_object(handles, peer.handle())
         peer.connect(handles)
@@ -230,11 +256,11 @@ def dist_worker(rank, world, port, q):
             peer.set_sched_push(push)
             desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
                                local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
-            ws = torch.empty(max(t.dist_workspace_bytes(desc), 16), dtype=torch.uint8, device="cuda:0")
+            ws = torch.empty(max(t.dist_workspace_bytes(desc), 16), dtype=torch.uint8, device=dev)
             runs = []
             for rep in range(2):
                 data = tdh.inputs(world, local, n, seed=1000 * world + 10 * ci + rep)
-                buf = torch.from_numpy(np.concatenate(data[rank]).view(np.int16)).to("cuda:0")
+                buf = torch.from_numpy(np.concatenate(data[rank]).view(np.int16)).to(dev)
                 peer.dist_allreduce(desc, buf.data_ptr(), ws.data_ptr(), torch.cuda.current_stream())
                 runs.append((data, buf))
             torch.cuda.synchronize()
@@ -244,7 +270,7 @@ def dist_worker(rank, world, port, q):
                 if not np.array_equal(got, want):
                     fails.append((variant, algo, local, chans, ll_max, push, rep, int((got != want).sum())))
             # a mem_2D call (reads every window) between scheduled calls
-            m = torch.zeros(n, dtype=torch.int16, device="cuda:0")
+            m = torch.zeros(n, dtype=torch.int16, device=dev)
             peer.allreduce(m.data_ptr(), n, torch.cuda.current_stream())
         torch.cuda.synchronize()
         status = peer.status()
@@ -257,27 +283,10 @@ def dist_worker(rank, world, port, q):
         q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
 
 
+@FENCES
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_peer_scheduled_program_multi_process_one_gpu(world):
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    procs = [ctx.Process(target=dist_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = []
-    try:
-        for _ in procs:
-            results.append(q.get(timeout=300))
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.kill()
-    for rank, fails, status in results:
-        assert fails == [], (rank, fails)
-        assert status == 0, (rank, status)
+def test_peer_scheduled_program_multi_process_one_gpu(world, tunes):
+    run_world(dist_worker, world, 300, tunes=tunes)
 
 
 def big_window_worker(rank, world, port, q):
@@ -509,7 +518,7 @@ def test_peer_timeout_is_cleared():
             p.close()
 
 
-def config35_worker(rank, world, port, q):
+def config35_worker(rank, world, port, q, devs=None, tunes=None):
     """BASELINE config 3 (8-rank RecDub BO, 655,360 B per rank; one channel and
     all 7 link-spreading channels) and config 5 (8-rank Swing LO at 2 / 8 / 32 /
     128 kB; LL pushes and the scheduled flag form) through
@@ -522,9 +531,10 @@ def config35_worker(rank, world, port, q):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import tenstorrentallreduce_amd as t
         import test_dist_host as tdh
+        devs, dev, shared = placement(rank, world, devs, tunes)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         side, total = tdh.GRIDS[world]
-        peer = t.Peer(world, rank, 0, 327680)
+        peer = t.Peer(world, rank, devs[rank], 327680)
         handles = [None] * world
         dist.all_gather_object(handles, peer.handle())
         peer.connect(handles)
@@ -537,7 +547,7 @@ def config35_worker(rank, world, port, q):
             desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, side, total, n, channels=chans)
             for rep in range(2):   # both window parities
                 data = tdh.inputs(world, 1, n, seed=7000 + 10 * ci + rep)
-                buf = torch.from_numpy(data[rank][0].view(np.int16)).to("cuda:0")
+                buf = torch.from_numpy(data[rank][0].view(np.int16)).to(dev)
                 peer.dist_allreduce(desc, buf.data_ptr(), None, torch.cuda.current_stream(), check_status=True)
                 want = tdh.expected(variant, algo, world, 1, data, chans)[rank][0]
                 got = buf.cpu().numpy().view(np.uint16)
@@ -554,27 +564,9 @@ def config35_worker(rank, world, port, q):
         q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
 
 
-def test_config3_config5_eight_processes():
-    import torch.multiprocessing as mp
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = free_port()
-    world = 8
-    procs = [ctx.Process(target=config35_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = []
-    try:
-        for _ in procs:
-            results.append(q.get(timeout=240))
-    finally:
-        for p in procs:
-            p.join(timeout=60)
-            if p.is_alive():
-                p.kill()
-    for rank, fails, status in results:
-        assert fails == [], (rank, fails)
-        assert status == 0, (rank, status)
+@FENCES
+def test_config3_config5_eight_processes(tunes):
+    run_world(config35_worker, 8, 240, tunes=tunes)
 
 
 @pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 5), (327680, 0, 1), (256 * 5, 0, 2), (256 * 40, 5, 3),
