@@ -958,27 +958,28 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   rccl        tree -> 2D Swing BO over RCCL -> broadcast (3 launches + RCCL groups)
     #   rccl_x      the same, consecutive buckets pipelined: bucket i's broadcast and bucket
     #               i+1's tree in ONE pass (k_tree_bcast_x), then bucket i+1's RCCL program
-    #   peer_launches  tree -> mem_2D across GPUs over peer windows (launches) -> broadcast
+    #   peer_launches  tree -> mem_2D across GPUs over peer windows (launches) -> broadcast: verified,
+    #               the bit-identity reference of the one-kernel forms, not a candidate
     #   peer_swing  tree -> the same Swing program over peer windows (k_peer_sched) -> broadcast
     #   peer_mem_x  consecutive buckets pipelined: bucket i's broadcast and bucket i+1's tree in
     #               one pass (k_tree_bcast_x), then bucket i+1's partial through the one-kernel
     #               mem_2D exchange over the peer windows (k_peer_oneshot)
     #   peer_hier_ll  ONE kernel: tree -> mem_2D across GPUs -> broadcast, every cross-GPU
     #                 hand-off an LL push (k_hier_ll)
-    #   peer_hier_x   the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
-    #                 reads bucket i+1 while it writes bucket i; the last flush is timed)
-    #   peer_hier_xr  k_hier_x with R(cur) ahead of bucket i-1's last row stores (hier_x_rearly)
+    #   peer_hier_xr  the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
+    #                 reads bucket i+1 while it writes bucket i; the last flush is timed), R(cur)
+    #                 ahead of bucket i-1's last row stores (hier_x_rearly)
     #   peer_hier_x2t2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
     #                 owned tiles before its last row stores, writes bucket i-2; every poll waits
     #                 for the previous launch)
-    #   <peer kind>_fenced  the same kernel with tune peer_fence=1: a system-scope release
-    #                 fence before every cross-GPU hand-off, an acquire fence after every wait
-    #                 (same bits; the form that stays correct on a node that breaks the ordering
-    #                 argument of DESIGN.md §5) — verified and timed for every relaxed form that
-    #                 failed and for the two fastest that passed
+    #   peer_swing_fenced / peer_mem_x_fenced  the same kernels with tune peer_fence=1: a
+    #                 system-scope release fence before every flag store, an acquire fence after
+    #                 every flag wait (same bits; the form that stays correct on a node that breaks
+    #                 the ordering argument of DESIGN.md §5).  The LL forms have no separate flag
     # (retired in round 5, every measurement slower — profiles/README.md: the per-tile flag
     # form k_hier_oneshot, the pipelined LL form k_hier_pipe, the flag hand-off forms of
-    # k_hier_ll / _x / _x2, and k_hier_x2's owned sums at the launch start / end)
+    # k_hier_ll / _x / _x2, k_hier_x with R(cur) after the last row stores, and k_hier_x2's
+    # owned sums at the launch start / end)
     # Every transport runs only once verified on THIS machine (verify_transport: the
     # exact sum of per-row 0/1 inputs and the reference's closed form, both computed
     # without any transport); the one-kernel peer forms must also equal the launch
@@ -1090,6 +1091,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
     verify = {}
+    comparator = {}   # peer_launches: verified like a candidate, the bit-identity reference of the one-kernel forms
 
     def check(kind, seed):
         note(rank, f"verify: {kind}")
@@ -1106,6 +1108,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                                                                      else "peer_launches")
         if same_as == "rccl" and not verify.get("rccl", {}).get("verified"):
             same_as = None   # --share-gpu: no RCCL to compare with (the Swing trees differ from mem_2D's)
+        if same_as == "peer_launches" and not comparator.get("peer_launches", {}).get("verified"):
+            same_as = None   # the comparator itself did not verify (its own checks stand)
         if v["verified"] and same_as:   # random real data: bit-identical to the form of the same semantics
             ok = False
             try:
@@ -1193,8 +1197,12 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
 
     quick_time(list(candidates))
     if peer is not None:
-        relaxed = ("peer_launches", "peer_swing", "peer_mem_x", "peer_hier_ll", "peer_hier_x", "peer_hier_xr",
-                   *X2_KINDS)
+        # the launch form (tree, mem_2D exchange as launches, broadcast) first: not a candidate
+        # (slower than every one-kernel form in every measurement), the form the one-kernel
+        # forms must equal bit for bit on random data
+        check("peer_launches", 9090)
+        comparator["peer_launches"] = verify.pop("peer_launches")
+        relaxed = ("peer_swing", "peer_mem_x", "peer_hier_ll", "peer_hier_xr", *X2_KINDS)
         passed = []
         for i, kind in enumerate(relaxed):
             if check(kind, 9100 + 10 * i):
@@ -1202,13 +1210,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             else:
                 drop(kind, "verification failed")
         quick_time(passed)
-        # the fenced twins: of every relaxed form that failed (verification or timing) and of
-        # the two fastest that passed, so a node that breaks the relaxed ordering still
-        # leaves a verified peer form behind
-        failed = [k for k in relaxed if k not in quick]
-        fastest = sorted((k for k in relaxed if k in quick), key=lambda k: quick[k])[:2]
+        # the fenced twins of the flag-protocol forms, so a node that breaks the relaxed
+        # ordering still leaves a verified peer form behind
         fenced = []
-        for i, kind in enumerate(failed + fastest):
+        for i, kind in enumerate(FLAG_KINDS):
             if check(kind + "_fenced", 9300 + 10 * i):
                 fenced.append(kind + "_fenced")
             else:
@@ -1265,7 +1270,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     HEADLINE_DONE.set()
 
     extras = {"headline_transport": transport, "transport_verified": verify, "transport_quick_ms": quick,
-              "dropped": dropped_candidates(verify),
+              "dropped": dropped_candidates(verify), "comparator_verified": comparator,
               "peer_timeout_in_timed_loop": peer_timeout,
               "local_phases_ms": {"tree_then_broadcast": round(local_split_ms, 6),
                                   **({"tree_broadcast_fused": round(local_ms, 6)} if fused_local else {})},
@@ -1354,6 +1359,9 @@ ONE_LAUNCH = {"peer_hier_ll": "k_hier_ll", "peer_hier_x": "k_hier_x", "peer_hier
               "peer_hier_x2t2": "k_hier_x2<tail2,late>"}
 # the k_hier_x2 transports (owned sums before a launch's last row stores)
 X2_KINDS = ("peer_hier_x2t2",)
+# the transports whose cross-GPU hand-offs are data + a separate flag (k_peer_sched, k_peer_oneshot):
+# their tune peer_fence=1 twins are candidates too
+FLAG_KINDS = ("peer_swing", "peer_mem_x")
 
 
 def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> dict:

@@ -266,12 +266,13 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     1: ahead of them (LL hand-offs, hier_x_lag 1)
  *   hier_x_latepoll   1: k_hier_x / k_hier_x2 poll the results of the bucket they write after tile 0's
  *                     tree (LL hand-offs, hier_x_lag 1; a flush launch polls at its start); 0: at the start
- *   peer_fence        0; 1: every peer-window kernel puts a system-scope release fence before each
- *                     store that hands data or progress to another GPU (flags, LL pushes) and an
- *                     acquire fence after each wait on another GPU's store.  Same bits; the default
- *                     relies on the ordering argument of DESIGN.md §5 (uncached hand-off memory,
- *                     s_waitcnt before the workgroup barrier that precedes a flag, LL words that
- *                     carry their own epoch).  Every rank must use the same setting
+ *   peer_fence        0; 1: the flag protocols of the peer windows (k_peer_oneshot, k_peer_sched,
+ *                     k_peer_sched_push) put a system-scope release fence before every flag store
+ *                     and an acquire fence after every flag wait.  Same bits; the default relies on
+ *                     the ordering argument of DESIGN.md §5 (uncached hand-off memory, s_waitcnt
+ *                     before the workgroup barrier that precedes a flag).  The LL kernels have no
+ *                     separate flag (each word carries its epoch) and take no fence.  Every rank
+ *                     must use the same setting
  *   multi_fault       0; fault injection (tests only): 1..32: GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return);
  *                     33..64: GPU value - 33 fails its warm-up (every thread skips the timed region)

@@ -24,14 +24,18 @@ struct PeerPtrs {
     uint32_t* flags[ALLRED_MAX_NODES];   // flag array of rank q, as mapped here
 };
 
-// tune peer_fence = 1 (the `fence` argument of every peer kernel): a system-scope
-// release fence before every store that hands data or progress to another GPU
-// and an acquire fence after every wait on another GPU's store.  The default
-// (0) relies on the ordering argument of DESIGN.md §5 instead — every hand-off
-// goes to uncached (MTYPE UC) memory, so a store acknowledged to s_waitcnt is
-// in the target's HBM before the workgroup barrier that precedes the flag, and
-// an LL word is its own flag.  Same bits either way; the fenced form is the one
-// a node that breaks the argument still runs correctly.
+// tune peer_fence = 1 (the `fence` argument of the flag protocols: k_peer_oneshot's
+// peer_signal_wait, k_peer_sched's sched_signal / sched_wait, k_peer_sched_push's
+// push_signal): a system-scope release fence before every flag store that
+// publishes data written before it, and an acquire fence after every flag wait.
+// The default (0) relies on the ordering argument of DESIGN.md §5 instead: the
+// data go to uncached (MTYPE UC) memory, so a store acknowledged to s_waitcnt
+// vmcnt(0) is in the target's HBM before the workgroup barrier that precedes
+// the flag.  Same bits either way; the fenced form is the one a node that
+// breaks the argument still runs correctly.  The LL kernels take no fence: an
+// LL word is its own flag (data and epoch in one 8-byte store), so there is no
+// earlier store to order before it (measured: fences around their pushes and
+// polls cost 10x, 16 -> 161 us a step at W = 1, for no ordering they need).
 __device__ __forceinline__ void peer_release(uint32_t fence) {
     if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
@@ -550,7 +554,7 @@ __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, 
 __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status, uint32_t fence) {
+                                                    uint32_t epoch, uint32_t* status) {
     constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
@@ -621,7 +625,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         lds_barrier();
         // the partial -> its owner's inbox: wave w writing word w of every column (one store
         // instruction per wave)
-        peer_release(fence);
         if (h == 0) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
@@ -657,9 +660,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             for (int src = 0; src < kLLMaxGpus; ++src)
                 if (src < W)
                     y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(my_ll + (li * W + src) * 128 + c, epoch, status);
-            peer_acquire(fence);
             val = owner_sum(y, W, me);
-            peer_release(fence);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
                 if (dst < W && dst != me) ll_put(lp.ll[dst] + box_words + t * 128 + c, val, epoch);
@@ -690,7 +691,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         };
         store_batch(true);
         if (!own && b < nb) xs[b * 32 + c] = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + t * 128 + c, epoch, status);
-        peer_acquire(fence);
         __syncthreads();
         store_batch(false);
         __syncthreads();   // xs is reused by the next batch
@@ -739,7 +739,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                                                    uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                    uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                                                   uint32_t* status, uint32_t fence) {
+                                                   uint32_t* status) {
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
@@ -784,7 +784,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         uint64_t wd[4];
         ll_load(at, wd);
         slot = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
-        peer_acquire(fence);
     };
     // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
     const bool lp = (RE & 2) && LAG == 1 && cur;
@@ -814,7 +813,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
             // the partial -> its owner's inbox: wave w writing word w of every column (one
             // store instruction per wave)
-            peer_release(fence);
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
@@ -867,9 +865,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                     if (src < W)
                         y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
                                                          : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
-                peer_acquire(fence);
                 const uint4 o = owner_sum(y, W, me);
-                peer_release(fence);
 #pragma unroll
                 for (int dst = 0; dst < kLLMaxGpus; ++dst)
                     if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
@@ -930,7 +926,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
-                                                    int has_mid, uint32_t* status, uint32_t fence) {
+                                                    int has_mid, uint32_t* status) {
     // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
     // stores, not after them
     constexpr bool tl2 = (TAIL & 3) == 2;
@@ -992,9 +988,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             if (src < W)
                 y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
                                                  : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
-        peer_acquire(fence);
         const uint4 o = owner_sum(y, W, me);
-        peer_release(fence);
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
             if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
@@ -1007,7 +1001,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         uint64_t wd[4];
         ll_load(at, wd);
         slot = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
-        peer_acquire(fence);
     };
     {
         uint64_t wo[4];
@@ -1017,7 +1010,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
         if (early_old && act_in(0))
             res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
-        peer_acquire(fence);
         if (CH && early_old && nch > 1) poll_old(1);
     }
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
@@ -1063,7 +1055,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             }
             // the partial -> its owner's inbox: wave w writing word w of every column (one
             // store instruction per wave)
-            peer_release(fence);
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
@@ -1111,7 +1102,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             __syncthreads();   // every wave has read the slot's previous results
             if (act_in(ch))
                 res[CH ? ch & 1 : 0][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
-            peer_acquire(fence);
             lds_barrier();
             for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
         }
@@ -1134,13 +1124,11 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
 __host__ __device__ constexpr uint64_t ll_padded(uint64_t slots) { return (slots + 31) / 32 * 32; }
 
 __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me, uint16_t* __restrict__ bucket,
-                                                        uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status,
-                                                        uint32_t fence) {
+                                                        uint64_t nv, uint64_t bv, uint32_t epoch, uint32_t* status) {
     const uint64_t gt = gtid(), GT = gthreads();
     uint4* bk = reinterpret_cast<uint4*>(bucket);
     uint64_t* const my_ll = lp.ll[me];
     const uint64_t box = ll_padded(nv) * 4;   // words
-    peer_release(fence);
     for (uint64_t v = gt; v < nv; v += GT) {   // A
         const int o = (int)(v / bv);
         // the owner's area by an unrolled select over the (scalar) kernarg pointers: a
@@ -1175,7 +1163,6 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
             if (peer_give_up(spin, t0, status)) break;
             __builtin_amdgcn_s_sleep(1);
         }
-        peer_acquire(fence);
         float a[8];
 #pragma unroll
         for (int q = 0; q < kLLMaxGpus; ++q) {
@@ -1193,14 +1180,9 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
         }
         const uint4 r = make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
         const uint64_t v = (uint64_t)me * bv + u;
-        peer_release(fence);
         for (int q = 0; q < W; ++q) ll_put(ll_slot(lp.ll[q] + box, v), r, epoch);
     }
-    for (uint64_t v = gt; v < nv; v += GT) {   // B
-        const uint4 r = ll_get(ll_slot(my_ll + box, v), epoch, status);
-        peer_acquire(fence);
-        st_nt(bk + v, r);
-    }
+    for (uint64_t v = gt; v < nv; v += GT) st_nt(bk + v, ll_get(ll_slot(my_ll + box, v), epoch, status));   // B
 }
 
 // ---------------------------------------------------------------------------
@@ -1218,7 +1200,6 @@ __global__ __launch_bounds__(kBlock) void k_peer_mem_ll(LLPtrs lp, int W, int me
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, int me, uint16_t* __restrict__ bucket,
                                                        uint64_t nv, uint32_t epoch, uint32_t* status) {
-    const uint32_t fence = pr.fence;
     const uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (v >= nv) return;
     uint4* bk = reinterpret_cast<uint4*>(bucket);
@@ -1227,11 +1208,8 @@ __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, i
     const uint64_t per_step = ll_padded(nv);   // slots
     for (int k = 0; k < pr.S; ++k) {
         const int p = pr.peer[0][k];
-        peer_release(fence);
         ll_put(ll_slot(lp.ll[p], (uint64_t)k * per_step + v), cur, epoch);
-        const uint4 y = ll_get(ll_slot(mine, (uint64_t)k * per_step + v), epoch, status);
-        peer_acquire(fence);
-        cur = add8(cur, y);
+        cur = add8(cur, ll_get(ll_slot(mine, (uint64_t)k * per_step + v), epoch, status));
     }
     st_nt(bk + v, cur);
 }
@@ -1339,7 +1317,7 @@ int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket
     const uint64_t cap = max_groups && max_groups < kPeerFusedMaxGroups ? max_groups : kPeerFusedMaxGroups;
     if (groups > cap) groups = cap;   // resident: every wait is reached
     hipLaunchKernelGGL(k_peer_mem_ll, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, lp, nranks, me,
-                       bucket, nv, nv / nranks, epoch, status, (uint32_t)tune(Tune::peer_fence));
+                       bucket, nv, nv / nranks, epoch, status);
     return peer_last_error();
 }
 
@@ -1351,10 +1329,8 @@ int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket,
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
-    PeerProg pf = prog;
-    pf.fence = (int)tune(Tune::peer_fence);
     hipLaunchKernelGGL(k_peer_lo_ll, dim3((unsigned)((nv + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       (hipStream_t)stream, lp, pf, me, bucket, nv, epoch, status);
+                       (hipStream_t)stream, lp, prog, me, bucket, nv, epoch, status);
     return peer_last_error();
 }
 
@@ -1371,7 +1347,7 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
-                       me, ntiles, ntiles / nranks, box_words, epoch, status, (uint32_t)tune(Tune::peer_fence));
+                       me, ntiles, ntiles / nranks, box_words, epoch, status);
     return peer_last_error();
 }
 
@@ -1408,7 +1384,7 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
                        (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, eprev, status, (uint32_t)tune(Tune::peer_fence));
+                       box_words, ecur, eprev, status);
     return peer_last_error();
 }
 
@@ -1459,7 +1435,7 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         default: return ALLRED_ERR_ARG;
     }
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, emid, eold, llm ? 1 : 0, status, (uint32_t)tune(Tune::peer_fence));
+                       box_words, ecur, emid, eold, llm ? 1 : 0, status);
     return peer_last_error();
 }
 
