@@ -274,17 +274,27 @@ def bench_single(args) -> dict:
     # each way ("dma"), or the fused kernel reading / writing the pinned host
     # buckets in place ("zerocopy")
     argv = ["allred_BO_2D", "1", "1", str(SIDE), "13", str(TILES), "32", "0", "1"]
+    # ("dma": column chunks, chunk c's H2D | pass | D2H overlapping the neighbours', 8 chunks by
+    # default; dma_chunks_<c> the same with c chunks, 1 = one copy each way around one pass).
+    # Each the median of 3 runs
     e2e = {}
-    for mode in ("zerocopy", "dma"):
-        os.environ["ALLRED_E2E"] = mode
+    for mode, chunks in (("zerocopy", None), ("dma", None), ("dma_chunks_1", 1), ("dma_chunks_4", 4),
+                         ("dma_chunks_16", 16)):
+        os.environ["ALLRED_E2E"] = "dma" if chunks or mode == "dma" else mode
+        if chunks:
+            os.environ["ALLRED_E2E_CHUNKS"] = str(chunks)
         try:
-            rep = t.run(argv, t.BO, False, t.EXEC_FUSED)
+            reps = sorted((t.run(argv, t.BO, False, t.EXEC_FUSED) for _ in range(3)), key=lambda r: r.e2e_seconds)
+            rep = reps[1]
             e2e[mode] = {"e2e_ms": round(rep.e2e_seconds * 1e3, 4), "device_ms": round(rep.device_seconds * 1e3, 4),
-                         "value": round(bytes_all / rep.e2e_seconds / 1e9, 3), "mismatches": int(rep.mismatches)}
+                         "value": round(bytes_all / rep.e2e_seconds / 1e9, 3),
+                         "mismatches": int(max(r.mismatches for r in reps)),
+                         "e2e_ms_runs": [round(r.e2e_seconds * 1e3, 4) for r in reps]}
         except Exception as e:  # reported, never silently dropped
             e2e[mode] = {"error": repr(e)}
         finally:
             del os.environ["ALLRED_E2E"]
+            os.environ.pop("ALLRED_E2E_CHUNKS", None)
 
     # BASELINE config 1: 2x2 RecDub LO, 1 tile (2 kB per rank), seed -1 (all ones) —
     # latency-bound (no roofline): the fused one-launch plan, us per allreduce

@@ -952,6 +952,19 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     const char* e2e_mode = std::getenv("ALLRED_E2E");
     const bool zero_copy = e2e_mode ? std::strcmp(e2e_mode, "zerocopy") == 0
                                     : (variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED && N >= 8);
+    // "dma" over column chunks (ALLRED_E2E_CHUNKS, default 8; 1 = one copy each way): the
+    // fused BO pass reduces every column with the same tree (tree_order[0]), so chunk c of
+    // every rank is an allreduce of its own — H2D(c + 1) | pass(c) | D2H(c - 1) on three
+    // streams, each copy a 2D DMA straight into / out of the skewed device layout (no
+    // staging pass); same bits as the whole-bucket pass
+    int chunks = 8;
+    if (const char* c = std::getenv("ALLRED_E2E_CHUNKS")) chunks = std::max(1, std::atoi(c));
+    const size_t cs = n / (size_t)chunks;
+    const bool chunked = !zero_copy && chunks > 1 && variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED &&
+                         n % (size_t)chunks == 0 && cs % (8 * (size_t)N) == 0 && !profile_log;
+    allred_plan* cplan = nullptr;
+    hipStream_t sh = nullptr, sd = nullptr;
+    std::vector<hipEvent_t> cev;   // per chunk: H2D done, pass start, pass done
     if (a->seed < 0) {
         allred_constant_bf16_vector(bytes, 1.0f, src0.data());
         src1 = src0;
@@ -974,12 +987,53 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     HIPCK(hipEventCreate(&e1));
     HIPCK(hipEventCreate(&e2));
     HIPCK(hipEventCreate(&e3));
+    if (chunked) {
+        allred_plan_desc cd = d;
+        cd.elems_per_rank = cs;
+        ST(allred_plan_create(&cd, &cplan));
+        HIPCK(hipStreamCreateWithFlags(&sh, hipStreamNonBlocking));
+        HIPCK(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
+        cev.assign(3 * (size_t)chunks, nullptr);
+        for (auto& e : cev) HIPCK(hipEventCreate(&e));
+    }
     // warm-up on a scratch copy (first-launch code-object load stays out of the timing)
     HIPCK(hipMemcpyAsync(d_stage, h_in, all_bytes, hipMemcpyHostToDevice, s));
     ST(launch_copy_ranks(d_stage, n, d_scratch, stride, N, n, s));
     if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, stride, d_ws, s));
+    if (cplan && a->run_kernel) ST(allred_plan_execute(cplan, d_scratch, stride, d_ws, s));
     HIPCK(hipStreamSynchronize(s));
-    if (zero_copy) {
+    if (chunked) {
+        // timed: chunk c's H2D on sh, its pass on s behind it, its D2H on sd behind the
+        // pass; the two PCIe directions and the passes overlap across chunks
+        HIPCK(hipEventRecord(e0, sh));
+        for (int c = 0; c < chunks; ++c) {
+            hipEvent_t h = cev[3 * (size_t)c], k0 = cev[3 * (size_t)c + 1], k1 = cev[3 * (size_t)c + 2];
+            const size_t off = (size_t)c * cs;
+            HIPCK(hipMemcpy2DAsync(d_ranks + off, stride * 2, h_in + off, n * 2, cs * 2, (size_t)N,
+                                   hipMemcpyHostToDevice, sh));
+            HIPCK(hipEventRecord(h, sh));
+            HIPCK(hipStreamWaitEvent(s, h, 0));
+            HIPCK(hipEventRecord(k0, s));
+            if (a->run_kernel) ST(allred_plan_execute(cplan, d_ranks + off, stride, d_ws, s));
+            HIPCK(hipEventRecord(k1, s));
+            HIPCK(hipStreamWaitEvent(sd, k1, 0));
+            HIPCK(hipMemcpy2DAsync(h_out + off, n * 2, d_ranks + off, stride * 2, cs * 2, (size_t)N,
+                                   hipMemcpyDeviceToHost, sd));
+        }
+        HIPCK(hipEventRecord(e3, sd));
+        HIPCK(hipStreamSynchronize(sd));
+        // device time: the passes themselves (each from its stream reaching it to its end)
+        float dev_ms = 0;
+        for (int c = 0; c < chunks; ++c) {
+            float m = 0;
+            HIPCK(hipEventElapsedTime(&m, cev[3 * (size_t)c + 1], cev[3 * (size_t)c + 2]));
+            dev_ms += m;
+        }
+        R->device_seconds = dev_ms * 1e-3;
+        HIPCK(hipEventElapsedTime(&ms, e0, e3));
+        R->e2e_seconds = ms * 1e-3;
+        R->launches = cplan->launches * chunks;
+    } else if (zero_copy) {
         // the kernels read and write the pinned host buckets in place over PCIe
         // (both directions at once); no staging copies, no HBM round trip
         uint16_t* h_dev = nullptr;
@@ -1006,10 +1060,12 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         HIPCK(hipEventRecord(e3, s));
         HIPCK(hipStreamSynchronize(s));
     }
-    HIPCK(hipEventElapsedTime(&ms, e1, e2));
-    R->device_seconds = ms * 1e-3;
-    HIPCK(hipEventElapsedTime(&ms, e0, e3));
-    R->e2e_seconds = ms * 1e-3;
+    if (!chunked) {
+        HIPCK(hipEventElapsedTime(&ms, e1, e2));
+        R->device_seconds = ms * 1e-3;
+        HIPCK(hipEventElapsedTime(&ms, e0, e3));
+        R->e2e_seconds = ms * 1e-3;
+    }
     if (profile_log) {
         std::vector<uint64_t> zs(N, 0), ze(N, (uint64_t)(R->device_seconds * 1e8));
         if (stamp_words && a->run_kernel) {   // the schedule form's per-unit stamps -> per-rank zones
@@ -1035,6 +1091,13 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         }
     }
 done:
+    if (sh) (void)hipStreamSynchronize(sh);
+    if (sd) (void)hipStreamSynchronize(sd);
+    for (hipEvent_t e : cev)
+        if (e) (void)hipEventDestroy(e);
+    if (sh) (void)hipStreamDestroy(sh);
+    if (sd) (void)hipStreamDestroy(sd);
+    if (cplan) allred_plan_destroy(cplan);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (e2) (void)hipEventDestroy(e2);

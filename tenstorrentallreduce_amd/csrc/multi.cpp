@@ -12,7 +12,8 @@
 //     hardware), or the host twin (host memory, allred_dist_allreduce_host
 //     with an in-memory exchange; no HIP call at all).
 // Everything between the two — input generation (allred_helper.cpp:277-285),
-// the G threads and their barriers, per-GPU H2D / D2H slices, the timed region (Finish before the read-back)
+// the G threads and their barriers, per-GPU H2D / D2H slices, the timed region (Finish before the
+// read-back where groups share a GPU)
 // (EnqueueWriteBuffer | EnqueueProgram + Finish | EnqueueReadBuffer,
 // allred_helper.hpp:84-96), the status agreement, validation
 // (validate_result_vector, allred_helper.cpp:18-120) — is shared, so the host
@@ -595,11 +596,12 @@ int allred_run_multi(const allred_args* a, const allred_multi_opts* o, int verbo
                 if (a->run_kernel) step([&] { return be->reduce(gr, gr.buf); });
                 mark(g, "timed-launch", s);
                 step([&] { return be->mark(gr, 2); });
-                // Finish before the read-back, as the reference's helper does: a D2H copy
-                // queued behind a waiting allreduce can hold the copy engine that another
-                // group's H2D (which its allreduce waits for) is queued behind (groups
-                // sharing one GPU share its SDMA engines: profiles/r04_multi_share_trace.txt)
-                step([&] { return be->drain(gr); });
+                // groups sharing one GPU: Finish before the read-back, as the reference's helper
+                // does — a D2H copy queued behind a waiting allreduce can hold the copy engine
+                // that another group's H2D (which its allreduce waits for) is queued behind
+                // (they share its SDMA engines: profiles/r04_multi_share_trace.txt).  A GPU of
+                // its own queues the D2H right behind its allreduce (stream order), no host wait
+                if (o->share_device) step([&] { return be->drain(gr); });
                 mark(g, "timed-finish", s);
                 step([&] { return be->get(gr, h_out + (size_t)g * L * n, gr.buf, mine); });
                 step([&] { return be->mark(gr, 3); });
