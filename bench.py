@@ -284,12 +284,12 @@ def bench_single(args) -> dict:
         if chunks:
             os.environ["ALLRED_E2E_CHUNKS"] = str(chunks)
         try:
-            reps = sorted((t.run(argv, t.BO, False, t.EXEC_FUSED) for _ in range(3)), key=lambda r: r.e2e_seconds)
-            rep = reps[1]
+            e2e_runs = sorted((t.run(argv, t.BO, False, t.EXEC_FUSED) for _ in range(3)), key=lambda r: r.e2e_seconds)
+            rep = e2e_runs[1]
             e2e[mode] = {"e2e_ms": round(rep.e2e_seconds * 1e3, 4), "device_ms": round(rep.device_seconds * 1e3, 4),
                          "value": round(bytes_all / rep.e2e_seconds / 1e9, 3),
-                         "mismatches": int(max(r.mismatches for r in reps)),
-                         "e2e_ms_runs": [round(r.e2e_seconds * 1e3, 4) for r in reps]}
+                         "mismatches": int(max(r.mismatches for r in e2e_runs)),
+                         "e2e_ms_runs": [round(r.e2e_seconds * 1e3, 4) for r in e2e_runs]}
         except Exception as e:  # reported, never silently dropped
             e2e[mode] = {"error": repr(e)}
         finally:

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <utility>
+#include <vector>
 
 #include "device_guard.hpp"
 #include "internal.hpp"
@@ -57,6 +59,15 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
+    // the hierarchical forms' hand-off area (7 + 1 byte words, peer_kernels.hip h_word), behind
+    // the LL boxes: 2 parities x [inbox: tiles x kHSlot words][result box: same]
+    size_t hl_off = 0;
+    uint64_t hl_box_words = 0;
+    uint64_t* peer_hl[ALLRED_MAX_NODES] = {};
+    // per parity: (tiles, call) of the calls whose words may still sit in the area, largest
+    // range oldest (every call rewrites tiles [0, its tiles)); hier_area_prepare reads it
+    std::vector<std::pair<uint64_t, uint32_t>> hl_stairs[2];
+    uint64_t hl_clears = 0;         // barrier-protected clears of a parity's area so far
     int hier_ll = 0;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
@@ -98,7 +109,9 @@ int allred_peer_create(int nranks, int rank, int device, uint64_t max_elems, all
     const uint64_t ll_elems = p->max_elems < (4ull << 20) ? p->max_elems : (4ull << 20);
     p->ll_off = ((size_t)kPeerFlagBytes + 255) / 256 * 256;
     p->ll_box_words = (ll_elems / 256) * 128;
-    const size_t flag_bytes = p->ll_off + 2 * 2 * p->ll_box_words * 8;
+    p->hl_off = (p->ll_off + 2 * 2 * p->ll_box_words * 8 + 255) / 256 * 256;
+    p->hl_box_words = (ll_elems / 256) * kHSlot;
+    const size_t flag_bytes = p->hl_off + 2 * 2 * p->hl_box_words * 8;
     const size_t win_bytes = p->max_elems * 2;
     auto release = [p]() {
         for (uint16_t* w : p->win) (void)hipFree(w);
@@ -192,6 +205,7 @@ int allred_peer_connect(allred_peer* p, const uint8_t* all) {
         }
         uint8_t* f = reinterpret_cast<uint8_t*>(p->peer_flags[q]);
         p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + p->ll_off);
+        p->peer_hl[q] = reinterpret_cast<uint64_t*>(f + p->hl_off);
     }
     p->connected = true;
     return ALLRED_OK;
@@ -218,6 +232,7 @@ int allred_peer_connect_all(int nranks, allred_peer* const* peers) {
             p->peer_stage[q] = o->stage;
             uint8_t* f = reinterpret_cast<uint8_t*>(o->flags);
             p->peer_ll[q] = reinterpret_cast<uint64_t*>(f + o->ll_off);
+            p->peer_hl[q] = reinterpret_cast<uint64_t*>(f + o->hl_off);
         }
     }
     for (int q = 0; q < nranks; ++q) peers[q]->connected = true;   // opened[] stays false: nothing to close
@@ -232,6 +247,54 @@ void parity_windows(allred_peer* p, uint16_t** wins) {
     for (int q = 0; q < p->nranks; ++q) wins[q] = p->peer_win[q][parity];
 }
 
+// every GPU's hand-off area of call k's parity (the hierarchical forms)
+void hier_areas(const allred_peer* p, uint32_t k, uint64_t** hl) {
+    for (int q = 0; q < p->nranks; ++q) hl[q] = p->peer_hl[q] + (k & 1u) * 2 * p->hl_box_words;
+}
+
+// A bucket of `tiles` tiles starts at call k on parity k & 1 of the hand-off area.  Its
+// readers accept a word whose 8-bit epoch is h_epoch(k + 1) = (k + 1) % 255 + 1; a slot of
+// its range still holding a word of an older same-parity call k' with k' = k (mod 255) —
+// k - k' a multiple of 510 — would be taken as this call's.  Every call rewrites all slots
+// of its own range, so the oldest word in [0, tiles) is the one the newest call covering
+// slot tiles - 1 wrote (never written: zero, epoch 0, never awaited).  If that call is 510
+// or more calls back, the parity's area is cleared first, between two barriers of the whole
+// peer set (every GPU runs the same calls, so all take this path together): after the first
+// no GPU is still writing into any area (each finished its previous launches, whose words
+// every consumer had taken), before the second every GPU has cleared its own.  Call with
+// no pipelined bucket pending on that parity.
+void hier_area_note(allred_peer* p, uint64_t tiles, uint32_t k) {
+    auto& st = p->hl_stairs[k & 1u];
+    while (!st.empty() && st.back().first <= tiles) st.pop_back();
+    st.emplace_back(tiles, k);
+}
+
+int hier_area_prepare(allred_peer* p, uint64_t tiles, uint32_t k, void* stream) {
+    auto& st = p->hl_stairs[k & 1u];
+    uint32_t newest = 0;
+    bool covered = false;
+    for (auto it = st.rbegin(); it != st.rend(); ++it)
+        if (it->first >= tiles) {
+            newest = it->second;
+            covered = true;
+            break;
+        }
+    if (covered && k - newest >= 510u) {
+        const uint32_t e = 2u * p->calls + 1u;   // barrier epochs: monotonic with every other barrier user
+        int rc = launch_peer_barrier(p->peer_flags, p->nranks, p->rank, e, p->status, stream);
+        if (rc != ALLRED_OK) return rc;
+        if (hipMemsetAsync(p->peer_hl[p->rank] + (k & 1u) * 2 * p->hl_box_words, 0, 2 * p->hl_box_words * 8,
+                           (hipStream_t)stream) != hipSuccess)
+            return ALLRED_ERR_HIP;
+        rc = launch_peer_barrier(p->peer_flags, p->nranks, p->rank, e + 1u, p->status, stream);
+        if (rc != ALLRED_OK) return rc;
+        st.clear();
+        ++p->hl_clears;
+    }
+    hier_area_note(p, tiles, k);
+    return ALLRED_OK;
+}
+
 }  // namespace
 
 int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* prev, uint64_t elems, int local_ranks,
@@ -239,7 +302,7 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
     if (!p || !p->connected || (!cur && !prev) || p->x2_n) return ALLRED_ERR_ARG;
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
-    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * 128 > p->ll_box_words)
+    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * kHSlot > p->hl_box_words)
         return ALLRED_ERR_UNSUPPORTED;
     // prev must be the bucket the previous call started (same pointer, same size: the
     // launch finishes prev with this call's tile count and owner split); a started
@@ -253,12 +316,12 @@ int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* pre
     const uint32_t kc = p->calls, kp = p->pipe_k;
     uint64_t* llc[ALLRED_MAX_NODES];
     uint64_t* llp[ALLRED_MAX_NODES];
-    for (int q = 0; q < p->nranks; ++q) {
-        llc[q] = p->peer_ll[q] + (kc & 1u) * 2 * p->ll_box_words;
-        llp[q] = p->peer_ll[q] + (kp & 1u) * 2 * p->ll_box_words;
-    }
+    hier_areas(p, kc, llc);
+    hier_areas(p, kp, llp);
+    // cur's parity holds nothing pending (prev, if any, is on the other one)
+    if (cur && (st = hier_area_prepare(p, n / 256, kc, stream)) != ALLRED_OK) return st;
     st = launch_hier_x(cur, prev, n, order, cur ? llc : nullptr, prev ? llp : nullptr, p->nranks, p->rank, n,
-                       p->ll_box_words, kc + 1u, kp + 1u, p->status, p->max_groups, stream);
+                       p->hl_box_words, kc + 1u, kp + 1u, p->status, p->max_groups, stream);
     if (st != ALLRED_OK) return st;
     if (cur) {
         p->pipe_k = kc;
@@ -279,15 +342,13 @@ int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t ele
     if (!p || !p->connected || p->pipe_pending) return ALLRED_ERR_ARG;
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
-    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * 128 > p->ll_box_words)
+    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * kHSlot > p->hl_box_words)
         return ALLRED_ERR_UNSUPPORTED;
     if ((p->x2_n > 0 && n != p->x2_elems) || (!cur && p->x2_n == 0)) return ALLRED_ERR_ARG;
     const uint8_t* order = nullptr;
     int st = local_tree_order(local_algo, local_side, local_ranks, &order);
     if (st != ALLRED_OK) return st;
-    auto area = [&](uint32_t k, uint64_t** ll) {   // every GPU's LL area of call k's parity
-        for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (k & 1u) * 2 * p->ll_box_words;
-    };
+    auto area = [&](uint32_t k, uint64_t** ll) { hier_areas(p, k, ll); };   // every GPU's area of call k's parity
     // mid: the newest pending bucket (its owned tiles are summed by this launch);
     // old: the older one when two are pending (its rows are written by this launch)
     const bool has_old = p->x2_n == 2;
@@ -300,8 +361,12 @@ int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t ele
     area(ko, llo);
     uint16_t* old = has_old ? p->x2_buf[0] : nullptr;
     uint16_t* fin = !cur ? p->x2_buf[p->x2_n - 1] : nullptr;
+    // cur's parity is old's: a sequence's buckets share one size, so only its first two starts
+    // (nothing pending on cur's parity yet) can meet slots an earlier, smaller bucket left
+    if (cur && p->x2_n < 2 && (st = hier_area_prepare(p, n / 256, kc, stream)) != ALLRED_OK) return st;
+    if (cur && p->x2_n == 2) hier_area_note(p, n / 256, kc);
     st = launch_hier_x2(cur, old, fin, n, order, cur ? llc : nullptr, p->x2_n > 0 ? llm : nullptr,
-                        has_old ? llo : nullptr, p->nranks, p->rank, n, p->ll_box_words, kc + 1u, km + 1u, ko + 1u,
+                        has_old ? llo : nullptr, p->nranks, p->rank, n, p->hl_box_words, kc + 1u, km + 1u, ko + 1u,
                         p->status, p->max_groups, stream);
     if (st != ALLRED_OK) return st;
     if (!cur) {   // flushed: nothing pending
@@ -331,14 +396,15 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
     uint16_t* bucket = buf;
     int st = ALLRED_OK;
     if (p->hier_ll && local_ranks == 64 && p->nranks <= 8 && p->flags_uncached && n % (256 * (size_t)p->nranks) == 0 &&
-        (n / 256) * 128 <= p->ll_box_words) {
+        (n / 256) * kHSlot <= p->hl_box_words) {
         // the hierarchical step in one launch with LL (push) hand-offs (k_hier_ll): same bits
         const uint8_t* order = nullptr;
         st = local_tree_order(local_algo, local_side, local_ranks, &order);
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
-        for (int q = 0; q < p->nranks; ++q) ll[q] = p->peer_ll[q] + (p->calls & 1u) * 2 * p->ll_box_words;
-        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->ll_box_words, p->calls + 1u, p->status,
+        hier_areas(p, p->calls, ll);
+        if ((st = hier_area_prepare(p, n / 256, p->calls, stream)) != ALLRED_OK) return st;
+        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->hl_box_words, p->calls + 1u, p->status,
                             p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;

@@ -495,12 +495,6 @@ __device__ __forceinline__ void ll_put(uint64_t* dst, uint4 v, uint32_t e) {
     __hip_atomic_store(dst + 3 * kLLGroup, hi | v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// word k of an LL slot (the four waves of a workgroup push one word each)
-__device__ __forceinline__ void ll_put_word(uint64_t* dst, uint4 v, uint32_t e, int k) {
-    const uint32_t d = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-    __hip_atomic_store(dst + k * kLLGroup, ((uint64_t)e << 32) | d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // poll 4 LL words until all carry epoch e (bounded: status bit 0 on timeout)
 __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_t* status) {
     uint64_t w0, w1, w2, w3;
@@ -519,17 +513,88 @@ __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_
     return make_uint4((uint32_t)w0, (uint32_t)w1, (uint32_t)w2, (uint32_t)w3);
 }
 
-// one poll of an LL slot without waiting (k_hier_x / k_hier_x2 / k_hier_ll R)
-__device__ __forceinline__ void ll_load(const uint64_t* src, uint64_t (&wd)[4]) {
+// ---- the hierarchical forms' hand-off words (round 5) -------------------------
+// A tile's 512-byte partial or result crosses as kHWords = 74 self-validating
+// 8-byte words: word i = bytes 7i .. 7i+6 of the tile (zero past its end) in
+// bits 0..55 and the call's 8-bit epoch in bits 56..63 — 1.16x the data bytes
+// instead of the 2x of the 4 + 4 LL word above.  A tile's words are contiguous
+// (kHSlot per slot), so the 32 lanes of a tile write 32 consecutive words
+// (256 bytes) per instruction.  Writer lanes each hold one 16-byte column; a
+// word spans at most two columns, taken from the column lanes by ds_bpermute.
+// A reader lane rebuilds its column from the four words covering it (16c / 7
+// .. + 3).  One 8-byte store is the unit of visibility, as for the LL words:
+// a word carries its own epoch and needs no flag.  The 8-bit epoch repeats
+// every 255 calls: the host clears a parity's area, between two barriers of
+// the peer set, before a bucket whose slots could still hold a word of an
+// older same-parity call with the same epoch (peer.cpp hier_area_prepare;
+// every call rewrites all of its own slots, so only a bucket larger than the
+// recent ones can meet such a word).
+__device__ __forceinline__ uint32_t h_epoch(uint32_t e) { return e % 255u + 1u; }
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
+    return make_uint4((uint32_t)__shfl((int)v.x, src), (uint32_t)__shfl((int)v.y, src), (uint32_t)__shfl((int)v.z, src),
+                      (uint32_t)__shfl((int)v.w, src));
+}
+constexpr uint64_t kH56 = 0x00FFFFFFFFFFFFFFull;
+// word i of a tile whose column c is `v` in lane base + c of this wave; all 32 of those lanes call it
+__device__ __forceinline__ uint64_t h_word(uint4 v, int base, int i, uint32_t e8) {
+    const int a = min((7 * i) >> 4, 31), o = (7 * i) & 15;
+    const uint4 ca = shfl4(v, base + a);
+    const uint4 cn = shfl4(v, base + min(a + 1, 31));
+    const bool last = a == 31 || i >= kHWords;   // the word reaches past the tile: zeros
+    const uint64_t q0 = ca.x | ((uint64_t)ca.y << 32), q1 = ca.z | ((uint64_t)ca.w << 32);
+    const uint64_t q2 = last ? 0 : (cn.x | ((uint64_t)cn.y << 32));
+    const int r = (o & 7) * 8;
+    const uint64_t lo = o >= 8 ? q1 : q0, hi = o >= 8 ? q2 : q1;
+    const uint64_t x = r ? (lo >> r) | (hi << (64 - r)) : lo;
+    return (x & kH56) | ((uint64_t)e8 << 56);
+}
+// the four words that cover column c of the tile at `tile`: one poll, no wait
+__device__ __forceinline__ void h_load(const uint64_t* tile, int c, uint64_t (&wd)[4]) {
+    const uint64_t* w0 = tile + (16 * c) / 7;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(src + k * kLLGroup, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(w0 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ bool ll_fresh(const uint64_t (&wd)[4], uint32_t e) {
-    return (uint32_t)(wd[0] >> 32) == e && (uint32_t)(wd[1] >> 32) == e && (uint32_t)(wd[2] >> 32) == e &&
-           (uint32_t)(wd[3] >> 32) == e;
+__device__ __forceinline__ bool h_fresh(const uint64_t (&wd)[4], uint32_t e8) {
+    return (uint32_t)(wd[0] >> 56) == e8 && (uint32_t)(wd[1] >> 56) == e8 && (uint32_t)(wd[2] >> 56) == e8 &&
+           (uint32_t)(wd[3] >> 56) == e8;
 }
-__device__ __forceinline__ uint4 ll_data(const uint64_t (&wd)[4]) {
-    return make_uint4((uint32_t)wd[0], (uint32_t)wd[1], (uint32_t)wd[2], (uint32_t)wd[3]);
+// column c from its four words: stream bytes o .. o+15, o = 16c - 7 (16c / 7)
+__device__ __forceinline__ uint4 h_data(const uint64_t (&wd)[4], int c) {
+    const int o = 16 * c - 7 * ((16 * c) / 7);
+    const uint64_t p0 = wd[0] & kH56, p1 = wd[1] & kH56, p2 = wd[2] & kH56, p3 = wd[3] & kH56;
+    auto get8 = [&](int b) {   // 8 bytes from stream byte b (b <= 14)
+        const int j = b / 7, r = (b % 7) * 8;
+        const uint64_t x = j == 0 ? p0 : (j == 1 ? p1 : p2), y = j == 0 ? p1 : (j == 1 ? p2 : p3);
+        return (x >> r) | (y << (56 - r));
+    };
+    const uint64_t lo = get8(o), hi = get8(o + 8);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+// poll until all four words carry e8 (bounded: status bit 0 on timeout), then the column
+__device__ __forceinline__ uint4 h_get(const uint64_t* tile, int c, uint32_t e8, uint32_t* status) {
+    uint64_t wd[4];
+    uint64_t t0 = 0;
+    for (uint64_t spin = 0;; ++spin) {
+        h_load(tile, c, wd);
+        if (h_fresh(wd, e8)) break;
+        if (peer_give_up(spin, t0, status)) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return h_data(wd, c);
+}
+__device__ __forceinline__ uint4 h_take(const uint64_t (&wd)[4], const uint64_t* tile, int c, uint32_t e8,
+                                        uint32_t* status) {
+    return h_fresh(wd, e8) ? h_data(wd, c) : h_get(tile, c, e8, status);
+}
+// the words c, c + 32, c + 64 of the tile whose column c is `v` in lane base + c (all 32 lanes call)
+__device__ __forceinline__ void h_words(uint4 v, int base, int c, uint32_t e8, uint64_t (&w)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k] = h_word(v, base, c + 32 * k, e8);
+}
+__device__ __forceinline__ void h_store(uint64_t* slot, int c, const uint64_t (&w)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (c + 32 * k < kHWords) __hip_atomic_store(slot + c + 32 * k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
@@ -556,6 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
                                                     uint32_t epoch, uint32_t* status) {
     constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
+    const uint32_t e8 = h_epoch(epoch);
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
     __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
@@ -623,13 +689,16 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
         if (h == 0) part[w * TV + c] = pw;
         lds_barrier();
-        // the partial -> its owner's inbox: wave w writing word w of every column (one store
-        // instruction per wave)
+        // the partial -> its owner's inbox: lanes 0..31 of every wave hold the tile's columns,
+        // wave w writes words 19 w .. 19 w + 18 (one store instruction per wave)
         if (h == 0) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
             const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-            ll_put_word(lp.ll[o] + slot * 128 + c, res, epoch, w);
+            const int i = 19 * w + c;
+            const uint64_t wd = h_word(res, 0, i, e8);
+            if (c < 19 && i < kHWords)
+                __hip_atomic_store(lp.ll[o] + slot * kHSlot + i, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
@@ -654,16 +723,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) ll_load(my_ll + (li * W + src) * 128 + c, wr[src]);
+                if (src < W) h_load(my_ll + (li * W + src) * kHSlot, c, wr[src]);
             uint4 y[kLLMaxGpus];
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W)
-                    y[src] = ll_fresh(wr[src], epoch) ? ll_data(wr[src]) : ll_get(my_ll + (li * W + src) * 128 + c, epoch, status);
+                if (src < W) y[src] = h_take(wr[src], my_ll + (li * W + src) * kHSlot, c, e8, status);
             val = owner_sum(y, W, me);
+            uint64_t hw[3];
+            h_words(val, threadIdx.x & 32, c, e8, hw);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W && dst != me) ll_put(lp.ll[dst] + box_words + t * 128 + c, val, epoch);
+                if (dst < W && dst != me) h_store(lp.ll[dst] + box_words + t * kHSlot, c, hw);
         }
         // every owned-tile push of this wave is issued before any of its result polls:
         // a wave holds owned and other tiles, and a poll spinning ahead of the wave's
@@ -672,7 +742,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         // the other GPUs' results: polls issued now, taken after the owned tiles' rows
         // have gone out (their xGMI round trip overlaps those stores)
         uint64_t wb[4];
-        if (!own && b < nb) ll_load(my_ll + box_words + t * 128 + c, wb);
+        if (!own && b < nb) h_load(my_ll + box_words + t * kHSlot, c, wb);
         if (own) xs[b * 32 + c] = val;
         __syncthreads();
         auto store_batch = [&](bool owned) {   // the rows of the batch's owned / other tiles
@@ -690,7 +760,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             }
         };
         store_batch(true);
-        if (!own && b < nb) xs[b * 32 + c] = ll_fresh(wb, epoch) ? ll_data(wb) : ll_get(my_ll + box_words + t * 128 + c, epoch, status);
+        if (!own && b < nb) xs[b * 32 + c] = h_take(wb, my_ll + box_words + t * kHSlot, c, e8, status);
         __syncthreads();
         store_batch(false);
         __syncthreads();   // xs is reused by the next batch
@@ -740,6 +810,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                                                    LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                    uint64_t box_words, uint32_t ecur, uint32_t eprev,
                                                    uint32_t* status) {
+    const uint32_t e8c = h_epoch(ecur), e8p = h_epoch(eprev);
     constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
@@ -780,10 +851,10 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         const int j = ch * kHierXChunk + jr;
         if (j >= mine) return;
         uint4& slot = res[CH ? ch & 1 : 0][jr][c];
-        const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * 128 + c;
+        const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * kHSlot;
         uint64_t wd[4];
-        ll_load(at, wd);
-        slot = ll_fresh(wd, eprev) ? ll_data(wd) : ll_get(at, eprev, status);
+        h_load(at, c, wd);
+        slot = h_take(wd, at, c, e8p, status);
     };
     // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
     const bool lp = (RE & 2) && LAG == 1 && cur;
@@ -811,15 +882,18 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            // the partial -> its owner's inbox: wave w writing word w of every column (one
-            // store instruction per wave)
+            // the partial -> its owner's inbox: lanes 0..31 of every wave hold the tile's columns,
+            // wave w writes words 19 w .. 19 w + 18 (one store instruction per wave)
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pt = part[j & 1];
                 const uint4 pr = add8(add8(pt[0 * TV + c], pt[1 * TV + c]), add8(pt[2 * TV + c], pt[3 * TV + c]));
                 const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
+                const int i = 19 * w + c;
+                const uint64_t wd = h_word(pr, 0, i, e8c);
+                if (c < 19 && i < kHWords)
+                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + i, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         if (lp && j == 0 && prev) {   // read first by iteration 1's stores, behind its A-phase barrier
@@ -859,16 +933,16 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                 uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
                 for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) ll_load(lc.ll[me] + (lr * W + src) * 128 + c, wr[src]);
+                    if (src < W) h_load(lc.ll[me] + (lr * W + src) * kHSlot, c, wr[src]);
 #pragma unroll
                 for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W)
-                        y[src] = ll_fresh(wr[src], ecur) ? ll_data(wr[src])
-                                                         : ll_get(lc.ll[me] + (lr * W + src) * 128 + c, ecur, status);
+                    if (src < W) y[src] = h_take(wr[src], lc.ll[me] + (lr * W + src) * kHSlot, c, e8c, status);
                 const uint4 o = owner_sum(y, W, me);
+                uint64_t hw[3];
+                h_words(o, threadIdx.x & 32, c, e8c, hw);
 #pragma unroll
                 for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                    if (dst < W) ll_put(lc.ll[dst] + box_words + t * 128 + c, o, ecur);
+                    if (dst < W) h_store(lc.ll[dst] + box_words + t * kHSlot, c, hw);
             }
         }
     };
@@ -927,6 +1001,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                                     int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
                                                     int has_mid, uint32_t* status) {
+    const uint32_t e8c = h_epoch(ecur), e8m = h_epoch(emid), e8o = h_epoch(eold);
     // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
     // stores, not after them
     constexpr bool tl2 = (TAIL & 3) == 2;
@@ -982,34 +1057,34 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         uint64_t wr[kLLMaxGpus][4];
 #pragma unroll
         for (int src = 0; src < kLLMaxGpus; ++src)
-            if (src < W) ll_load(lm.ll[me] + (lr * W + src) * 128 + c, wr[src]);
+            if (src < W) h_load(lm.ll[me] + (lr * W + src) * kHSlot, c, wr[src]);
 #pragma unroll
         for (int src = 0; src < kLLMaxGpus; ++src)
-            if (src < W)
-                y[src] = ll_fresh(wr[src], emid) ? ll_data(wr[src])
-                                                 : ll_get(lm.ll[me] + (lr * W + src) * 128 + c, emid, status);
+            if (src < W) y[src] = h_take(wr[src], lm.ll[me] + (lr * W + src) * kHSlot, c, e8m, status);
         const uint4 o = owner_sum(y, W, me);
+        uint64_t hw[3];
+        h_words(o, threadIdx.x & 32, c, e8m, hw);
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
-            if (dst < W) ll_put(lm.ll[dst] + box_words + tr * 128 + c, o, emid);
+            if (dst < W) h_store(lm.ll[dst] + box_words + tr * kHSlot, c, hw);
     };
     // old's results of chunk ch -> its slot
     auto poll_old = [&](int ch) {
         if (!act_in(ch)) return;
         uint4& slot = res[CH ? ch & 1 : 0][jr][c];
-        const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c;
+        const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * kHSlot;
         uint64_t wd[4];
-        ll_load(at, wd);
-        slot = ll_fresh(wd, eold) ? ll_data(wd) : ll_get(at, eold, status);
+        h_load(at, c, wd);
+        slot = h_take(wd, at, c, e8o, status);
     };
     {
         uint64_t wo[4];
         const bool early_old = old && !lp;   // lp: polled in A(cur 0), ahead of its partial push
-        if (early_old && act_in(0)) ll_load(lo.ll[me] + box_words + tile_of(jr) * 128 + c, wo);
+        if (early_old && act_in(0)) h_load(lo.ll[me] + box_words + tile_of(jr) * kHSlot, c, wo);
         if ((TAIL & 3) == 0)
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
         if (early_old && act_in(0))
-            res[0][jr][c] = ll_fresh(wo, eold) ? ll_data(wo) : ll_get(lo.ll[me] + box_words + tile_of(jr) * 128 + c, eold, status);
+            res[0][jr][c] = h_take(wo, lo.ll[me] + box_words + tile_of(jr) * kHSlot, c, e8o, status);
         if (CH && early_old && nch > 1) poll_old(1);
     }
     // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
@@ -1053,15 +1128,18 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                 wait_vm<0>();
                 lds_barrier();
             }
-            // the partial -> its owner's inbox: wave w writing word w of every column (one
-            // store instruction per wave)
+            // the partial -> its owner's inbox: lanes 0..31 of every wave hold the tile's columns,
+            // wave w writes words 19 w .. 19 w + 18 (one store instruction per wave)
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
                 const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                ll_put_word(lc.ll[o] + slot * 128 + c, pr, ecur, w);
+                const int i = 19 * w + c;
+                const uint64_t wd = h_word(pr, 0, i, e8c);
+                if (c < 19 && i < kHWords)
+                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + i, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         // tl2: mid's owned sums ahead of the last iteration's row stores, so their polls and pushes
@@ -1101,7 +1179,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         for (int ch = 0; ch < nch; ++ch) {
             __syncthreads();   // every wave has read the slot's previous results
             if (act_in(ch))
-                res[CH ? ch & 1 : 0][jr][c] = ll_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * 128 + c, emid, status);
+                res[CH ? ch & 1 : 0][jr][c] = h_get(lm.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * kHSlot, c, e8m, status);
             lds_barrier();
             for (int j = ch * kHierXChunk; j < mine && j < (ch + 1) * kHierXChunk; ++j) store_rows(fin, j);
         }
@@ -1339,7 +1417,7 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
                    void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
     if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
-        ntiles * 128 > box_words)
+        ntiles * kHSlot > box_words)
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
@@ -1355,7 +1433,7 @@ int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t*
                   uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
                   uint32_t* status, unsigned max_grid, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * kHSlot > box_words ||
         (!cur && !prev) || (cur && !aligned16(cur)) || (prev && !aligned16(prev)))
         return ALLRED_ERR_ARG;
     // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
@@ -1393,7 +1471,7 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
                    uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold, uint32_t* status,
                    unsigned max_grid, void* stream) {
     const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * 128 > box_words ||
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * kHSlot > box_words ||
         (!cur && !old && !fin) || (cur && !llc) || (old && !llo) || (fin && (cur || !llm)) ||
         (cur && !aligned16(cur)) || (old && !aligned16(old)) || (fin && !aligned16(fin)))
         return ALLRED_ERR_ARG;

@@ -639,3 +639,47 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
         assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.close()
+
+
+def test_hier_handoff_epoch_wrap_is_cleared():
+    """The hierarchical forms' hand-off words carry an 8-bit epoch ((k + 1) % 255
+    + 1 for call k), so call k + 510 awaits the epoch call k's words carry.  A
+    large bucket at call 0, then 509 small ones, then the large bucket again at
+    call 510 on the same parity: the slots beyond the small buckets' range still
+    hold call 0's words with call 510's epoch.  The host sees it coming
+    (hier_area_prepare) and clears the parity's area between two barriers; the
+    result must be call 510's own data, bit-exact (W = 1, k_hier_ll)."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import tenstorrentallreduce_amd as t
+    import oracle
+    local, small, large = 64, 256 * 8, 256 * 64
+    peer = t.Peer(1, 0, 0, 2 * large)
+    peer.connect([peer.handle()])
+    try:
+        peer.set_hier_ll(1)
+        s = torch.cuda.current_stream()
+        ws = torch.empty(large, dtype=torch.int16, device="cuda:0")
+
+        def bucket(seed, n):
+            d = np.random.default_rng(seed).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+            loc = [x.copy() for x in d]
+            oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+            return torch.from_numpy(d.view(np.int16)).to("cuda:0"), loc[0]
+
+        first, _ = bucket(1, large)
+        peer.allreduce(first.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())    # call 0
+        sm, sm_want = bucket(2, small)
+        for _ in range(509):                                                            # calls 1 .. 509
+            peer.allreduce(sm.data_ptr(), small, s, local, 8, t.SWING, ws.data_ptr())
+        torch.cuda.synchronize()
+        assert peer.status() & t.PEER_TIMEOUT == 0
+        last, want = bucket(3, large)
+        peer.allreduce(last.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())     # call 510
+        torch.cuda.synchronize()
+        bad = int((last.cpu().numpy().view(np.uint16) != want[None, :]).sum())
+        assert bad == 0, bad
+        assert peer.status() & t.PEER_TIMEOUT == 0
+    finally:
+        peer.set_hier_ll(0)
+        peer.close()
