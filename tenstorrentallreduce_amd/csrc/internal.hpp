@@ -154,10 +154,9 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
 int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint32_t* const* flags, int me,
                            uint16_t* bucket, const PeerProg& prog, uint32_t base_epoch, uint32_t* status,
                            unsigned max_groups, void* stream);
-// the hierarchical forms' hand-off words: a tile's 512 bytes as kHWords 8-byte words (7 data
-// bytes + an 8-bit epoch each), kHSlot words per tile slot (peer_kernels.hip h_word)
-constexpr int kHWords = 74;
-constexpr int kHSlot = 80;
+// the hierarchical forms' hand-off words: a tile's 512 bytes as 3 x 32 8-byte words (6 data
+// bytes + a 16-bit epoch each), kHSlot words per tile slot (peer_kernels.hip h_pack)
+constexpr int kHSlot = 96;
 // hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast with LL
 // (push) hand-offs: ll[q] = GPU q's LL area for this parity, [inbox box_words words][result box
 // box_words words]; nranks <= 8; epoch grows by 1 per call

@@ -23,6 +23,7 @@
 // reading call k's windows.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <utility>
 #include <vector>
@@ -253,16 +254,18 @@ void hier_areas(const allred_peer* p, uint32_t k, uint64_t** hl) {
 }
 
 // A bucket of `tiles` tiles starts at call k on parity k & 1 of the hand-off area.  Its
-// readers accept a word whose 8-bit epoch is h_epoch(k + 1) = (k + 1) % 255 + 1; a slot of
-// its range still holding a word of an older same-parity call k' with k' = k (mod 255) —
-// k - k' a multiple of 510 — would be taken as this call's.  Every call rewrites all slots
-// of its own range, so the oldest word in [0, tiles) is the one the newest call covering
-// slot tiles - 1 wrote (never written: zero, epoch 0, never awaited).  If that call is 510
-// or more calls back, the parity's area is cleared first, between two barriers of the whole
-// peer set (every GPU runs the same calls, so all take this path together): after the first
-// no GPU is still writing into any area (each finished its previous launches, whose words
-// every consumer had taken), before the second every GPU has cleared its own.  Call with
-// no pipelined bucket pending on that parity.
+// readers accept a word whose 16-bit epoch is h_epoch(k + 1) = (k + 1) % 65535 + 1; a slot
+// of its range still holding a word of an older same-parity call k' with k' = k (mod 65535)
+// — k - k' a multiple of 131070 — would be taken as this call's.  Every call rewrites all
+// slots of its own range, so the oldest word in [0, tiles) is the one the newest call
+// covering slot tiles - 1 wrote (never written: zero, epoch 0, never awaited).  If that
+// call is 131070 or more calls back, the parity's area is cleared first, between two
+// barriers of the whole peer set (every GPU runs the same calls, so all take this path
+// together): after the first no GPU is still writing into any area (each finished its
+// previous launches, whose words every consumer had taken), before the second every GPU
+// has cleared its own.  Call with no pipelined bucket pending on that parity.
+constexpr uint32_t kHierWrapCalls = 131070;   // 2 x 65535: same-parity calls between equal epochs
+
 void hier_area_note(allred_peer* p, uint64_t tiles, uint32_t k) {
     auto& st = p->hl_stairs[k & 1u];
     while (!st.empty() && st.back().first <= tiles) st.pop_back();
@@ -279,7 +282,7 @@ int hier_area_prepare(allred_peer* p, uint64_t tiles, uint32_t k, void* stream) 
             covered = true;
             break;
         }
-    if (covered && k - newest >= 510u) {
+    if (covered && k - newest >= kHierWrapCalls) {
         const uint32_t e = 2u * p->calls + 1u;   // barrier epochs: monotonic with every other barrier user
         int rc = launch_peer_barrier(p->peer_flags, p->nranks, p->rank, e, p->status, stream);
         if (rc != ALLRED_OK) return rc;

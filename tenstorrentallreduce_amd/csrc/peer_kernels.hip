@@ -514,87 +514,64 @@ __device__ __forceinline__ uint4 ll_get(const uint64_t* src, uint32_t e, uint32_
 }
 
 // ---- the hierarchical forms' hand-off words (round 5) -------------------------
-// A tile's 512-byte partial or result crosses as kHWords = 74 self-validating
-// 8-byte words: word i = bytes 7i .. 7i+6 of the tile (zero past its end) in
-// bits 0..55 and the call's 8-bit epoch in bits 56..63 — 1.16x the data bytes
-// instead of the 2x of the 4 + 4 LL word above.  A tile's words are contiguous
-// (kHSlot per slot), so the 32 lanes of a tile write 32 consecutive words
-// (256 bytes) per instruction.  Writer lanes each hold one 16-byte column; a
-// word spans at most two columns, taken from the column lanes by ds_bpermute.
-// A reader lane rebuilds its column from the four words covering it (16c / 7
-// .. + 3).  One 8-byte store is the unit of visibility, as for the LL words:
-// a word carries its own epoch and needs no flag.  The 8-bit epoch repeats
-// every 255 calls: the host clears a parity's area, between two barriers of
-// the peer set, before a bucket whose slots could still hold a word of an
-// older same-parity call with the same epoch (peer.cpp hier_area_prepare;
-// every call rewrites all of its own slots, so only a bucket larger than the
-// recent ones can meet such a word).
-__device__ __forceinline__ uint32_t h_epoch(uint32_t e) { return e % 255u + 1u; }
-__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
-    return make_uint4((uint32_t)__shfl((int)v.x, src), (uint32_t)__shfl((int)v.y, src), (uint32_t)__shfl((int)v.z, src),
-                      (uint32_t)__shfl((int)v.w, src));
+// A tile's 512-byte partial or result crosses as 96 self-validating 8-byte
+// words: column c's 16 bytes as three words, bytes 0-5 / 6-11 / 12-15 of the
+// column in bits 0..47 and the call's 16-bit epoch in bits 48..63 — 1.5x the
+// data bytes instead of the 2x of the 4 + 4 LL word above.  Word k of column c
+// sits at k * 32 + c of the tile's slot (kHSlot words), so the 32 lanes of a
+// tile write or poll 256 contiguous bytes per instruction, each lane only its
+// own column (no cross-lane traffic; a 7 + 1 byte packing, 1.16x, needed two
+// columns per word and ran 0.6-0.8 us slower a step at W = 1 on the shuffles
+// and scattered polls, profiles/README.md).  One 8-byte store is the unit of
+// visibility, as for the LL words: a word carries its own epoch, no flag
+// follows it.  The 16-bit epoch repeats every 65535 calls: the host clears a
+// parity's area, between two barriers of the peer set, before a bucket whose
+// slots could still hold a word of an older same-parity call with the same
+// epoch (peer.cpp hier_area_prepare; every call rewrites all of its own slots,
+// so only a bucket larger than the recent ones can meet such a word).
+__device__ __forceinline__ uint32_t h_epoch(uint32_t e) { return e % 65535u + 1u; }
+constexpr uint64_t kH48 = 0x0000FFFFFFFFFFFFull;
+// word k of a column
+__device__ __forceinline__ uint64_t h_pack(uint4 v, int k, uint32_t e16) {
+    const uint64_t lo = v.x | ((uint64_t)v.y << 32), hi = v.z | ((uint64_t)v.w << 32);
+    const uint64_t d = k == 0 ? (lo & kH48) : k == 1 ? ((lo >> 48) | ((hi & 0xFFFFFFFFull) << 16)) : (hi >> 32);
+    return d | ((uint64_t)e16 << 48);
 }
-constexpr uint64_t kH56 = 0x00FFFFFFFFFFFFFFull;
-// word i of a tile whose column c is `v` in lane base + c of this wave; all 32 of those lanes call it
-__device__ __forceinline__ uint64_t h_word(uint4 v, int base, int i, uint32_t e8) {
-    const int a = min((7 * i) >> 4, 31), o = (7 * i) & 15;
-    const uint4 ca = shfl4(v, base + a);
-    const uint4 cn = shfl4(v, base + min(a + 1, 31));
-    const bool last = a == 31 || i >= kHWords;   // the word reaches past the tile: zeros
-    const uint64_t q0 = ca.x | ((uint64_t)ca.y << 32), q1 = ca.z | ((uint64_t)ca.w << 32);
-    const uint64_t q2 = last ? 0 : (cn.x | ((uint64_t)cn.y << 32));
-    const int r = (o & 7) * 8;
-    const uint64_t lo = o >= 8 ? q1 : q0, hi = o >= 8 ? q2 : q1;
-    const uint64_t x = r ? (lo >> r) | (hi << (64 - r)) : lo;
-    return (x & kH56) | ((uint64_t)e8 << 56);
-}
-// the four words that cover column c of the tile at `tile`: one poll, no wait
-__device__ __forceinline__ void h_load(const uint64_t* tile, int c, uint64_t (&wd)[4]) {
-    const uint64_t* w0 = tile + (16 * c) / 7;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) wd[k] = __hip_atomic_load(w0 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ bool h_fresh(const uint64_t (&wd)[4], uint32_t e8) {
-    return (uint32_t)(wd[0] >> 56) == e8 && (uint32_t)(wd[1] >> 56) == e8 && (uint32_t)(wd[2] >> 56) == e8 &&
-           (uint32_t)(wd[3] >> 56) == e8;
-}
-// column c from its four words: stream bytes o .. o+15, o = 16c - 7 (16c / 7)
-__device__ __forceinline__ uint4 h_data(const uint64_t (&wd)[4], int c) {
-    const int o = 16 * c - 7 * ((16 * c) / 7);
-    const uint64_t p0 = wd[0] & kH56, p1 = wd[1] & kH56, p2 = wd[2] & kH56, p3 = wd[3] & kH56;
-    auto get8 = [&](int b) {   // 8 bytes from stream byte b (b <= 14)
-        const int j = b / 7, r = (b % 7) * 8;
-        const uint64_t x = j == 0 ? p0 : (j == 1 ? p1 : p2), y = j == 0 ? p1 : (j == 1 ? p2 : p3);
-        return (x >> r) | (y << (56 - r));
-    };
-    const uint64_t lo = get8(o), hi = get8(o + 8);
+// the column from its three words
+__device__ __forceinline__ uint4 h_unpack(const uint64_t (&wd)[3]) {
+    const uint64_t lo = (wd[0] & kH48) | (wd[1] << 48);
+    const uint64_t hi = ((wd[1] >> 16) & 0xFFFFFFFFull) | (wd[2] << 32);
     return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
 }
-// poll until all four words carry e8 (bounded: status bit 0 on timeout), then the column
-__device__ __forceinline__ uint4 h_get(const uint64_t* tile, int c, uint32_t e8, uint32_t* status) {
-    uint64_t wd[4];
+// the three words of column c of the tile at `tile`: one poll, no wait
+__device__ __forceinline__ void h_load(const uint64_t* tile, int c, uint64_t (&wd)[3]) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) wd[k] = __hip_atomic_load(tile + 32 * k + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ bool h_fresh(const uint64_t (&wd)[3], uint32_t e16) {
+    return (uint32_t)(wd[0] >> 48) == e16 && (uint32_t)(wd[1] >> 48) == e16 && (uint32_t)(wd[2] >> 48) == e16;
+}
+// poll until all three words carry e16 (bounded: status bit 0 on timeout), then the column
+__device__ __forceinline__ uint4 h_get(const uint64_t* tile, int c, uint32_t e16, uint32_t* status) {
+    uint64_t wd[3];
     uint64_t t0 = 0;
     for (uint64_t spin = 0;; ++spin) {
         h_load(tile, c, wd);
-        if (h_fresh(wd, e8)) break;
+        if (h_fresh(wd, e16)) break;
         if (peer_give_up(spin, t0, status)) break;
         __builtin_amdgcn_s_sleep(1);
     }
-    return h_data(wd, c);
+    return h_unpack(wd);
 }
-__device__ __forceinline__ uint4 h_take(const uint64_t (&wd)[4], const uint64_t* tile, int c, uint32_t e8,
+__device__ __forceinline__ uint4 h_take(const uint64_t (&wd)[3], const uint64_t* tile, int c, uint32_t e16,
                                         uint32_t* status) {
-    return h_fresh(wd, e8) ? h_data(wd, c) : h_get(tile, c, e8, status);
+    return h_fresh(wd, e16) ? h_unpack(wd) : h_get(tile, c, e16, status);
 }
-// the words c, c + 32, c + 64 of the tile whose column c is `v` in lane base + c (all 32 lanes call)
-__device__ __forceinline__ void h_words(uint4 v, int base, int c, uint32_t e8, uint64_t (&w)[3]) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) w[k] = h_word(v, base, c + 32 * k, e8);
-}
-__device__ __forceinline__ void h_store(uint64_t* slot, int c, const uint64_t (&w)[3]) {
+// column c (v) -> its three words in the tile slot at `tile`
+__device__ __forceinline__ void h_put(uint64_t* tile, int c, uint4 v, uint32_t e16) {
 #pragma unroll
     for (int k = 0; k < 3; ++k)
-        if (c + 32 * k < kHWords) __hip_atomic_store(slot + c + 32 * k, w[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(tile + 32 * k + c, h_pack(v, k, e16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the owner's sum of one column of a tile: y[q] = GPU q's partial; fp32, owner
@@ -673,7 +650,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
     for (int j = 0; j < mine; ++j) {
         // in flight after tile j's loads: this wave's LL store of tile j-1
-        if (j > 0) wait_vm<1>(); else wait_vm<0>();
+        if (j > 0 && w < 3) wait_vm<1>(); else wait_vm<0>();
         lds_barrier();
         if (j + 1 < mine) issue(tile_a(j + 1), (j + 1) & 1);
         const uint4* tile = buf[j & 1];
@@ -689,16 +666,15 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
         if (h == 0) part[w * TV + c] = pw;
         lds_barrier();
-        // the partial -> its owner's inbox: lanes 0..31 of every wave hold the tile's columns,
-        // wave w writes words 19 w .. 19 w + 18 (one store instruction per wave)
+        // the partial -> its owner's inbox: wave w < 3 writing word w of every column (one store
+        // instruction; wave 3 none)
         if (h == 0) {
             const int o = owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
             const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-            const int i = 19 * w + c;
-            const uint64_t wd = h_word(res, 0, i, e8);
-            if (c < 19 && i < kHWords)
-                __hip_atomic_store(lp.ll[o] + slot * kHSlot + i, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (w < 3)
+                __hip_atomic_store(lp.ll[o] + slot * kHSlot + 32 * w + c, h_pack(res, w, e8), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     __syncthreads();   // every wave is past A: buf may be reused below
@@ -720,7 +696,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         uint4 val = make_uint4(0, 0, 0, 0);
         if (own) {
             const uint64_t li = t - (uint64_t)me * tiles_per_owner;
-            uint64_t wr[kLLMaxGpus][4];
+            uint64_t wr[kLLMaxGpus][3];
 #pragma unroll
             for (int src = 0; src < kLLMaxGpus; ++src)
                 if (src < W) h_load(my_ll + (li * W + src) * kHSlot, c, wr[src]);
@@ -729,11 +705,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             for (int src = 0; src < kLLMaxGpus; ++src)
                 if (src < W) y[src] = h_take(wr[src], my_ll + (li * W + src) * kHSlot, c, e8, status);
             val = owner_sum(y, W, me);
-            uint64_t hw[3];
-            h_words(val, threadIdx.x & 32, c, e8, hw);
 #pragma unroll
             for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W && dst != me) h_store(lp.ll[dst] + box_words + t * kHSlot, c, hw);
+                if (dst < W && dst != me) h_put(lp.ll[dst] + box_words + t * kHSlot, c, val, e8);
         }
         // every owned-tile push of this wave is issued before any of its result polls:
         // a wave holds owned and other tiles, and a poll spinning ahead of the wave's
@@ -741,7 +715,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         // the other GPUs' results: polls issued now, taken after the owned tiles' rows
         // have gone out (their xGMI round trip overlaps those stores)
-        uint64_t wb[4];
+        uint64_t wb[3];
         if (!own && b < nb) h_load(my_ll + box_words + t * kHSlot, c, wb);
         if (own) xs[b * 32 + c] = val;
         __syncthreads();
@@ -852,7 +826,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
         if (j >= mine) return;
         uint4& slot = res[CH ? ch & 1 : 0][jr][c];
         const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * kHSlot;
-        uint64_t wd[4];
+        uint64_t wd[3];
         h_load(at, c, wd);
         slot = h_take(wd, at, c, e8p, status);
     };
@@ -868,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
             // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
             wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
-                     (j >= 1 ? 1 : 0));
+                     (j >= 1 && w < 3 ? 1 : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -882,18 +856,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            // the partial -> its owner's inbox: lanes 0..31 of every wave hold the tile's columns,
-            // wave w writes words 19 w .. 19 w + 18 (one store instruction per wave)
+            // the partial -> its owner's inbox: wave w < 3 writing word w of every column (one
+            // store instruction; wave 3 none)
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pt = part[j & 1];
                 const uint4 pr = add8(add8(pt[0 * TV + c], pt[1 * TV + c]), add8(pt[2 * TV + c], pt[3 * TV + c]));
                 const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                const int i = 19 * w + c;
-                const uint64_t wd = h_word(pr, 0, i, e8c);
-                if (c < 19 && i < kHWords)
-                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + i, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (w < 3)
+                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + 32 * w + c, h_pack(pr, w, e8c), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         if (lp && j == 0 && prev) {   // read first by iteration 1's stores, behind its A-phase barrier
@@ -930,7 +903,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
             if (owner_of(t) == me) {
                 const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
                 uint4 y[kLLMaxGpus];
-                uint64_t wr[kLLMaxGpus][4];
+                uint64_t wr[kLLMaxGpus][3];
 #pragma unroll
                 for (int src = 0; src < kLLMaxGpus; ++src)
                     if (src < W) h_load(lc.ll[me] + (lr * W + src) * kHSlot, c, wr[src]);
@@ -938,11 +911,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
                 for (int src = 0; src < kLLMaxGpus; ++src)
                     if (src < W) y[src] = h_take(wr[src], lc.ll[me] + (lr * W + src) * kHSlot, c, e8c, status);
                 const uint4 o = owner_sum(y, W, me);
-                uint64_t hw[3];
-                h_words(o, threadIdx.x & 32, c, e8c, hw);
 #pragma unroll
                 for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                    if (dst < W) h_store(lc.ll[dst] + box_words + t * kHSlot, c, hw);
+                    if (dst < W) h_put(lc.ll[dst] + box_words + t * kHSlot, c, o, e8c);
             }
         }
     };
@@ -1054,7 +1025,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         const uint64_t tr = tile_of(ch * kHierXChunk + jr);
         const uint64_t lr = tr - (uint64_t)me * tiles_per_owner;
         uint4 y[kLLMaxGpus];
-        uint64_t wr[kLLMaxGpus][4];
+        uint64_t wr[kLLMaxGpus][3];
 #pragma unroll
         for (int src = 0; src < kLLMaxGpus; ++src)
             if (src < W) h_load(lm.ll[me] + (lr * W + src) * kHSlot, c, wr[src]);
@@ -1062,23 +1033,21 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         for (int src = 0; src < kLLMaxGpus; ++src)
             if (src < W) y[src] = h_take(wr[src], lm.ll[me] + (lr * W + src) * kHSlot, c, e8m, status);
         const uint4 o = owner_sum(y, W, me);
-        uint64_t hw[3];
-        h_words(o, threadIdx.x & 32, c, e8m, hw);
 #pragma unroll
         for (int dst = 0; dst < kLLMaxGpus; ++dst)
-            if (dst < W) h_store(lm.ll[dst] + box_words + tr * kHSlot, c, hw);
+            if (dst < W) h_put(lm.ll[dst] + box_words + tr * kHSlot, c, o, e8m);
     };
     // old's results of chunk ch -> its slot
     auto poll_old = [&](int ch) {
         if (!act_in(ch)) return;
         uint4& slot = res[CH ? ch & 1 : 0][jr][c];
         const uint64_t* at = lo.ll[me] + box_words + tile_of(ch * kHierXChunk + jr) * kHSlot;
-        uint64_t wd[4];
+        uint64_t wd[3];
         h_load(at, c, wd);
         slot = h_take(wd, at, c, e8o, status);
     };
     {
-        uint64_t wo[4];
+        uint64_t wo[3];
         const bool early_old = old && !lp;   // lp: polled in A(cur 0), ahead of its partial push
         if (early_old && act_in(0)) h_load(lo.ll[me] + box_words + tile_of(jr) * kHSlot, c, wo);
         if ((TAIL & 3) == 0)
@@ -1091,7 +1060,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
     // (the polls before them have returned, and with them both tiles' loads).  With
     // several chunks an earlier chunk's pushes may be in flight too: counting none
     // only waits longer (the loads of tile j are never waited for too little)
-    const int pushed = (TAIL & 3) == 0 && nch == 1 && __ballot(rmid_in(0)) != 0 ? 4 * W : 0;
+    const int pushed = (TAIL & 3) == 0 && nch == 1 && __ballot(rmid_in(0)) != 0 ? 3 * W : 0;
     lds_barrier();   // order bytes and old's results in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
@@ -1099,7 +1068,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             // partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG), this
             // wave's owned-sum pushes (j < 2)
             wait_any((j >= 2 + LAG && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && old ? OPS : 0) +
-                     (j >= 1 ? 1 : 0) + (j < 2 ? pushed : 0));
+                     (j >= 1 && w < 3 ? 1 : 0) + (j < 2 ? pushed : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -1128,18 +1097,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                 wait_vm<0>();
                 lds_barrier();
             }
-            // the partial -> its owner's inbox: lanes 0..31 of every wave hold the tile's columns,
-            // wave w writes words 19 w .. 19 w + 18 (one store instruction per wave)
+            // the partial -> its owner's inbox: wave w < 3 writing word w of every column (one
+            // store instruction; wave 3 none)
             if (q == 0) {
                 const uint64_t t = tile_of(j);
                 const int o = owner_of(t);
                 const uint4* pp = part[j & 1];
                 const uint4 pr = add8(add8(pp[0 * TV + c], pp[1 * TV + c]), add8(pp[2 * TV + c], pp[3 * TV + c]));
                 const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                const int i = 19 * w + c;
-                const uint64_t wd = h_word(pr, 0, i, e8c);
-                if (c < 19 && i < kHWords)
-                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + i, wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (w < 3)
+                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + 32 * w + c, h_pack(pr, w, e8c), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         // tl2: mid's owned sums ahead of the last iteration's row stores, so their polls and pushes

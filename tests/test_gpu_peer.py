@@ -642,18 +642,19 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
 
 
 def test_hier_handoff_epoch_wrap_is_cleared():
-    """The hierarchical forms' hand-off words carry an 8-bit epoch ((k + 1) % 255
-    + 1 for call k), so call k + 510 awaits the epoch call k's words carry.  A
-    large bucket at call 0, then 509 small ones, then the large bucket again at
-    call 510 on the same parity: the slots beyond the small buckets' range still
-    hold call 0's words with call 510's epoch.  The host sees it coming
-    (hier_area_prepare) and clears the parity's area between two barriers; the
-    result must be call 510's own data, bit-exact (W = 1, k_hier_ll)."""
+    """The hierarchical forms' hand-off words carry a 16-bit epoch ((k + 1) %
+    65535 + 1 for call k), so call k + 131070 (same parity) awaits the epoch
+    call k's words carry.  A large bucket at call 0, then 131069 small ones,
+    then the large bucket again at call 131070: the slots beyond the small
+    buckets' range still hold call 0's words with call 131070's epoch.  The host
+    sees it coming (hier_area_prepare) and clears the parity's area between two
+    barriers; the result must be call 131070's own data, bit-exact (W = 1,
+    k_hier_ll).  ~1 s of tiny launches."""
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import tenstorrentallreduce_amd as t
     import oracle
-    local, small, large = 64, 256 * 8, 256 * 64
+    local, small, large = 64, 256 * 2, 256 * 64
     peer = t.Peer(1, 0, 0, 2 * large)
     peer.connect([peer.handle()])
     try:
@@ -669,13 +670,15 @@ def test_hier_handoff_epoch_wrap_is_cleared():
 
         first, _ = bucket(1, large)
         peer.allreduce(first.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())    # call 0
-        sm, sm_want = bucket(2, small)
-        for _ in range(509):                                                            # calls 1 .. 509
+        sm, _ = bucket(2, small)   # reduced in place over and over: only its launches matter
+        for i in range(131069):                                                         # calls 1 .. 131069
             peer.allreduce(sm.data_ptr(), small, s, local, 8, t.SWING, ws.data_ptr())
+            if i % 16384 == 16383:
+                torch.cuda.synchronize()
         torch.cuda.synchronize()
         assert peer.status() & t.PEER_TIMEOUT == 0
         last, want = bucket(3, large)
-        peer.allreduce(last.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())     # call 510
+        peer.allreduce(last.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())     # call 131070
         torch.cuda.synchronize()
         bad = int((last.cpu().numpy().view(np.uint16) != want[None, :]).sum())
         assert bad == 0, bad
