@@ -274,12 +274,10 @@ def bench_single(args) -> dict:
     # each way ("dma"), or the fused kernel reading / writing the pinned host
     # buckets in place ("zerocopy")
     argv = ["allred_BO_2D", "1", "1", str(SIDE), "13", str(TILES), "32", "0", "1"]
-    # ("dma": column chunks, chunk c's H2D | pass | D2H overlapping the neighbours', 8 chunks by
-    # default; dma_chunks_<c> the same with c chunks, 1 = one copy each way around one pass).
-    # Each the median of 3 runs
+    # ("dma": 8 column chunks, chunk c's H2D | pass | D2H overlapping the neighbours';
+    # dma_chunks_<c> c chunks, 1 = one copy each way around one pass).  Each the median of 3 runs
     e2e = {}
-    for mode, chunks in (("zerocopy", None), ("dma", None), ("dma_chunks_1", 1), ("dma_chunks_4", 4),
-                         ("dma_chunks_16", 16)):
+    for mode, chunks in (("zerocopy", None), ("dma", None), ("dma_chunks_1", 1), ("dma_chunks_16", 16)):
         os.environ["ALLRED_E2E"] = "dma" if chunks or mode == "dma" else mode
         if chunks:
             os.environ["ALLRED_E2E_CHUNKS"] = str(chunks)

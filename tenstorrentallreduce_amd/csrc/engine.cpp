@@ -952,17 +952,29 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     const char* e2e_mode = std::getenv("ALLRED_E2E");
     const bool zero_copy = e2e_mode ? std::strcmp(e2e_mode, "zerocopy") == 0
                                     : (variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED && N >= 8);
-    // "dma" over column chunks (ALLRED_E2E_CHUNKS, default 8; 1 = one copy each way): the
-    // fused BO pass reduces every column with the same tree (tree_order[0]), so chunk c of
-    // every rank is an allreduce of its own — H2D(c + 1) | pass(c) | D2H(c - 1) on three
-    // streams, each copy a 2D DMA straight into / out of the skewed device layout (no
-    // staging pass); same bits as the whole-bucket pass
-    int chunks = 8;
-    if (const char* c = std::getenv("ALLRED_E2E_CHUNKS")) chunks = std::max(1, std::atoi(c));
-    const size_t cs = n / (size_t)chunks;
+    // "dma" over column chunks: the fused BO pass reduces every column with the same tree
+    // (tree_order[0]), so a column chunk of every rank is an allreduce of its own —
+    // H2D(c + 1) | pass(c) | D2H(c - 1) on three streams, each copy a 2D DMA straight into /
+    // out of the skewed device layout (no staging pass); same bits as the whole-bucket pass.
+    // ALLRED_E2E_CHUNKS=c equal chunks, default 8 (1 = one copy each way around one pass).
+    // Each 2D copy costs ~10 us over its bytes (measured: 8 chunks 1.09 ms, 16 1.19, 32 1.5,
+    // a 1-2-4-9-9-4-2-1 32nds ramp 1.18; profiles/r05_e2e_probe.json)
+    std::vector<size_t> csz;
+    const size_t col_unit = 8 * (size_t)N;
+    {
+        const char* c = std::getenv("ALLRED_E2E_CHUNKS");
+        const size_t k = c ? (size_t)std::max(1, std::atoi(c)) : 8;
+        if (n % k == 0 && (n / k) % col_unit == 0) csz.assign(k, n / k);
+    }
+    const int chunks = (int)csz.size();
     const bool chunked = !zero_copy && chunks > 1 && variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED &&
-                         n % (size_t)chunks == 0 && cs % (8 * (size_t)N) == 0 && !profile_log;
-    allred_plan* cplan = nullptr;
+                         !profile_log;
+    std::vector<std::pair<size_t, allred_plan*>> cplans;   // one plan per distinct chunk size
+    auto chunk_plan = [&](size_t len) -> allred_plan* {
+        for (auto& cp : cplans)
+            if (cp.first == len) return cp.second;
+        return nullptr;
+    };
     hipStream_t sh = nullptr, sd = nullptr;
     std::vector<hipEvent_t> cev;   // per chunk: H2D done, pass start, pass done
     if (a->seed < 0) {
@@ -988,9 +1000,14 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     HIPCK(hipEventCreate(&e2));
     HIPCK(hipEventCreate(&e3));
     if (chunked) {
-        allred_plan_desc cd = d;
-        cd.elems_per_rank = cs;
-        ST(allred_plan_create(&cd, &cplan));
+        for (size_t len : csz) {
+            if (chunk_plan(len)) continue;
+            allred_plan_desc cd = d;
+            cd.elems_per_rank = len;
+            allred_plan* cp = nullptr;
+            ST(allred_plan_create(&cd, &cp));
+            cplans.emplace_back(len, cp);
+        }
         HIPCK(hipStreamCreateWithFlags(&sh, hipStreamNonBlocking));
         HIPCK(hipStreamCreateWithFlags(&sd, hipStreamNonBlocking));
         cev.assign(3 * (size_t)chunks, nullptr);
@@ -1000,15 +1017,20 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     HIPCK(hipMemcpyAsync(d_stage, h_in, all_bytes, hipMemcpyHostToDevice, s));
     ST(launch_copy_ranks(d_stage, n, d_scratch, stride, N, n, s));
     if (a->run_kernel) ST(allred_plan_execute(plan, d_scratch, stride, d_ws, s));
-    if (cplan && a->run_kernel) ST(allred_plan_execute(cplan, d_scratch, stride, d_ws, s));
+    if (a->run_kernel)
+        for (auto& cp : cplans) ST(allred_plan_execute(cp.second, d_scratch, stride, d_ws, s));
     HIPCK(hipStreamSynchronize(s));
     if (chunked) {
         // timed: chunk c's H2D on sh, its pass on s behind it, its D2H on sd behind the
         // pass; the two PCIe directions and the passes overlap across chunks
         HIPCK(hipEventRecord(e0, sh));
-        for (int c = 0; c < chunks; ++c) {
+        size_t off = 0;
+        int launches = 0;
+        for (int c = 0; c < chunks; off += csz[(size_t)c], ++c) {
             hipEvent_t h = cev[3 * (size_t)c], k0 = cev[3 * (size_t)c + 1], k1 = cev[3 * (size_t)c + 2];
-            const size_t off = (size_t)c * cs;
+            const size_t cs = csz[(size_t)c];
+            allred_plan* cplan = chunk_plan(cs);
+            launches += cplan->launches;
             HIPCK(hipMemcpy2DAsync(d_ranks + off, stride * 2, h_in + off, n * 2, cs * 2, (size_t)N,
                                    hipMemcpyHostToDevice, sh));
             HIPCK(hipEventRecord(h, sh));
@@ -1032,7 +1054,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         R->device_seconds = dev_ms * 1e-3;
         HIPCK(hipEventElapsedTime(&ms, e0, e3));
         R->e2e_seconds = ms * 1e-3;
-        R->launches = cplan->launches * chunks;
+        R->launches = launches;
     } else if (zero_copy) {
         // the kernels read and write the pinned host buckets in place over PCIe
         // (both directions at once); no staging copies, no HBM round trip
@@ -1097,7 +1119,7 @@ done:
         if (e) (void)hipEventDestroy(e);
     if (sh) (void)hipStreamDestroy(sh);
     if (sd) (void)hipStreamDestroy(sd);
-    if (cplan) allred_plan_destroy(cplan);
+    for (auto& cp : cplans) allred_plan_destroy(cp.second);
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (e2) (void)hipEventDestroy(e2);

@@ -95,17 +95,17 @@ def test_config2_fused_both_end_to_end_modes(e2e):
 
 @pytest.mark.parametrize("argv", [["1", "1", "8", "13", "5", "32", "0", "1"],      # config 2, 640 kB
                                   ["0", "1", "8", "13", "40", "0", "63", "1"]])  # RecDub, 5 MiB per rank
-@pytest.mark.parametrize("chunks", ["1", "2", "5", "8", "10", "16", "3"])
+@pytest.mark.parametrize("chunks", ["default", "1", "2", "5", "10", "16", "3"])
 def test_dma_end_to_end_chunked_is_exact(argv, chunks):
-    """The DMA end-to-end form over column chunks (ALLRED_E2E_CHUNKS): chunk c's
-    2D H2D, its fused pass and its 2D D2H on three streams, overlapping across
-    chunks.  Every rank equals the reference's expected value at ERROR 0 (RNE
-    ctor, ALLRED_CHECK_ALL).  3 chunks do not divide the bucket's blocks: the
-    one-copy form runs instead (still exact)."""
+    """The DMA end-to-end form over column chunks: chunk c's 2D H2D, its fused
+    pass and its 2D D2H on three streams, overlapping across chunks — 8 by
+    default, or ALLRED_E2E_CHUNKS.  Every rank equals the reference's expected value at ERROR 0
+    (RNE ctor, ALLRED_CHECK_ALL).  3 chunks do not divide the bucket's blocks:
+    the one-copy form runs instead (still exact)."""
     argv = list(argv)
     argv[5] = "0"
-    out, rep = run("allred_BO_2D", argv, ALLRED_EXEC="fused", ALLRED_E2E="dma", ALLRED_E2E_CHUNKS=chunks,
-                   ALLRED_BF16_ROUND="rne")
+    env = {} if chunks == "default" else {"ALLRED_E2E_CHUNKS": chunks}
+    out, rep = run("allred_BO_2D", argv, ALLRED_EXEC="fused", ALLRED_E2E="dma", ALLRED_BF16_ROUND="rne", **env)
     assert out.strip() == "All values match!", out
     assert rep["mismatches"] == 0 and rep["e2e_s"] > rep["device_s"] > 0
 
