@@ -317,15 +317,6 @@ std::vector<uint8_t> lo_steps_pipe_table(const allred_schedule& s, int N) {
         row = nrow;
     }
     for (int r = 0; r < N; ++r) out.push_back((uint8_t)row[r]);
-    // then, per row x, the two ranks whose result it holds after the last step (ascending):
-    // k_steps_reg stores them straight from the register that holds row x
-    std::vector<int> got(H, 0);
-    std::vector<uint8_t> ranks_of(2 * H, 0);
-    for (int r = 0; r < N; ++r) {
-        if (row[r] < 0 || got[row[r]] >= 2) return {};
-        ranks_of[2 * row[r] + got[row[r]]++] = (uint8_t)r;
-    }
-    out.insert(out.end(), ranks_of.begin(), ranks_of.end());
     return out;
 }
 

@@ -1228,9 +1228,8 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
     constexpr int NPH = BO ? 2 * S - 2 : S - 1;
     constexpr int STAMPS = BO ? 2 * S + 1 : S + 1;
     constexpr int MPH = BO ? (P / 4 * CW + 63) / 64 : IPW;
-    // the program(s) in LDS: BO every block's (P x 256 bytes), LO the one step program (2H S + P
-    // bytes, then 2H: the two ranks of each row after the last step; <= 512 bytes)
-    constexpr int LOTAB = 2 * H * S + 2 * P;
+    // the program(s) in LDS: BO every block's (P x 256 bytes), LO the one step program (2H S + P <= 448 bytes)
+    constexpr int LOTAB = 2 * H * S + P;
     __shared__ __attribute__((aligned(16))) uint8_t tabs[BO ? P : 1][BO ? kBoPipeTab : (LOTAB + 15) / 16 * 16];
     __shared__ __attribute__((aligned(16))) uint4 work[NW][H * CW];   // per wave: the strip's pair rows
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1347,28 +1346,16 @@ __global__ __launch_bounds__(256, MINW) void k_steps_reg(uint16_t* __restrict__ 
                 for (int m = 0; m < IPW; ++m)
                     if (lane + 64 * m < H * CW) {
                         val[m] = add8(val[m], oth[m]);
-                        // the last step's rows are stored from the registers below: no LDS round trip
-                        if (ph < NPH) tile[((lane + 64 * m) / CW) * CW + cl] = val[m];
+                        tile[((lane + 64 * m) / CW) * CW + cl] = val[m];
                     }
             }
             if (st_on) stamps[(s / Q) * STAMPS + 1 + ph] = __builtin_amdgcn_s_memrealtime();
         }
         const uint64_t cs = col0(s) + cl;
-        if constexpr (BO) {
 #pragma unroll
-            for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
-                st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs,
-                      tile[(int)tb[off_of(NPH + 1) + RPO * k + rl] * CW + cl]);
-            }
-        } else {   // LO: row x's value (val) is the result of its two ranks (the table's last 2H bytes)
-            const uint8_t* two = tb + off_of(NPH + 1) + P;
-#pragma unroll
-            for (int t = 0; t < IPW; ++t)
-                if (lane + 64 * t < H * CW) {
-                    const int x = (lane + 64 * t) / CW;
-                    st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)two[2 * x] * stride) + cs, val[t]);
-                    st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)two[2 * x + 1] * stride) + cs, val[t]);
-                }
+        for (int k = 0; k < OPS; ++k) {   // rank RPO k + rl's value is row fin
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(RPO * k + rl) * stride) + cs,
+                  tile[(int)tb[off_of(NPH + 1) + RPO * k + rl] * CW + cl]);
         }
         if (BO && st_on) stamps[(s / Q) * STAMPS + 2 * S] = __builtin_amdgcn_s_memrealtime();
     };

@@ -150,11 +150,7 @@ def test_lo_program_matches_oracle(algo, grid):
     side, total = grid
     tab = program(algo, t.LO, side, total)
     S = total.bit_length() - 1
-    assert tab.size == 2 * (total // 2) * S + total + total
-    fin = tab[2 * (total // 2) * S:][:total]
-    pairs = tab[2 * (total // 2) * S + total:].reshape(total // 2, 2)   # row x -> its two ranks (round 5)
-    for x, (a, b) in enumerate(pairs):
-        assert a < b and fin[a] == x and fin[b] == x
+    assert tab.size == 2 * (total // 2) * S + total
     n = 64
     rng = np.random.default_rng(9 + total + algo)
     ranks = [rng.integers(0x3F80, 0x42C8, n).astype(np.uint16) for _ in range(total)]
