@@ -22,7 +22,11 @@
 extern "C" {
 #endif
 
-#define ALLRED_ABI_VERSION 5
+/* ABI 6 (round 5): allred_peer_set_hier_ll takes 0 / 1 only (k_hier_pipe retired), the tune
+ * keys lose hier_handoff and gain peer_fence, allred_peer_clear_status refuses while a
+ * pipelined sequence is pending, and the hierarchical forms' hand-off area moved (its own
+ * words: 6 data bytes + a 16-bit epoch) — peers of different ABIs must not connect. */
+#define ALLRED_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------- */
 #define ALLRED_OK 0

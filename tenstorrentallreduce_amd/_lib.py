@@ -38,7 +38,7 @@ BO, LO, MEM = 0, 1, 2
 STEPS_REG = 0x100   # allred_steps_program: | ALLRED_BO -> the register-staged form's program
 EXEC_STEPS, EXEC_FUSED = 0, 1
 ACC_FP32, ACC_BF16 = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_NODES, MAX_STEPS = 64, 6
 UNIQUE_ID_BYTES = 128
 MULTI_FLAT, MULTI_HIER, MULTI_LOCAL = 0, 1, 2          # allred_multi_plan.mode

@@ -47,7 +47,7 @@ def test_header_constants_match_python_bindings():
 
 
 def test_status_strings():
-    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 5
+    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 6
     for st in range(0, -8, -1):
         assert _lib.lib.allred_status_string(st)
 
