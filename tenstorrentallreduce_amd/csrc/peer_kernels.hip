@@ -593,15 +593,47 @@ __device__ __forceinline__ uint4 owner_sum(const uint4 (&y)[kLLMaxGpus], int W, 
     return make_uint4(pack_rne(a[0], a[1]), pack_rne(a[2], a[3]), pack_rne(a[4], a[5]), pack_rne(a[6], a[7]));
 }
 
-__global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
-                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status) {
+// The workgroup's tiles of the one-launch forms: blk + kG of the reducing grid G
+// (identical on every GPU).  A reduces them in a different order (tile_a):
+// within each batch of 8, the tiles other GPUs own first, its own tiles last —
+// the owned ones form the run k0 <= k < k1.  Every GPU reduces the tiles it does
+// not own first, so an owner finds the remote partials of its tiles already
+// arrived, and the result leaves after one xGMI trip (natural order: remote
+// partials of the last tiles arrive one trip after the owner's own, then the
+// result needs a second).  At W = 1 nothing moves.
+struct HierTiles {
+    uint64_t blk, G, tpo;
+    int mine, k0, k1;
+    __device__ HierTiles(uint64_t b, uint64_t g, uint64_t ntiles, uint64_t tiles_per_owner, int me)
+        : blk(b), G(g), tpo(tiles_per_owner) {
+        mine = b < ntiles ? (int)((ntiles - 1 - b) / g + 1) : 0;
+        const uint32_t tpo32 = (uint32_t)tiles_per_owner;
+        k0 = count_below((uint32_t)me * tpo32);
+        k1 = count_below((uint32_t)(me + 1) * tpo32);
+    }
+    __device__ int count_below(uint32_t t0) const {   // the workgroup's tiles below tile index t0 (< 2^20 tiles)
+        return t0 <= blk ? 0 : (int)min((uint32_t)mine, (t0 - (uint32_t)blk + (uint32_t)G - 1) / (uint32_t)G);
+    }
+    __device__ uint64_t tile_of(int k) const { return blk + (uint64_t)k * G; }
+    __device__ uint64_t tile_a(int j) const {
+        const int lo = j & ~7, hi = lo + 8 < mine ? lo + 8 : mine;
+        const int a0 = k0 < lo ? lo : (k0 > hi ? hi : k0), a1 = k1 < lo ? lo : (k1 > hi ? hi : k1);
+        const int p = j - lo, below = a0 - lo, above = hi - a1;
+        const int k = p < below ? lo + p : (p < below + above ? a1 + (p - below) : a0 + (p - below - above));
+        return tile_of(k);
+    }
+    __device__ int owner_of(uint64_t t) const { return (int)(t / tpo); }
+};
+
+// A of the one-launch forms for one reducing workgroup: its tiles' 64 rank rows
+// by LDS-DMA (double-buffered), the local tree out of LDS, each partial pushed
+// to its owner's inbox slot [t - o*tpo][me] as the 6 + 2-byte words (waves 0-2
+// one word of every column each, wave 3 none).  Never waits for a peer.
+__device__ __forceinline__ void hier_reduce(const HierTiles& ht, const uint16_t* __restrict__ ranks, uint64_t stride,
+                                            const uint8_t* __restrict__ order, const LLPtrs& lp, int W, int me,
+                                            uint32_t e8, uint4 (&buf)[2][64 * 32], uint4 (&part)[4 * 32],
+                                            uint8_t (&ord_lds)[ALLRED_MAX_NODES]) {
     constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
-    const uint32_t e8 = h_epoch(epoch);
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int c = lane & 31, h = lane >> 5;
     uint32_t ob = 0;
@@ -616,33 +648,8 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
             lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
         }
     };
-    const uint64_t G = gridDim.x;
-    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    // The workgroup's tiles are blockIdx.x + kG (tile_of, also the R / B batches of 8,
-    // identical on every GPU: B of batch i waits only for R of batch i of the owners).
-    // A reduces them in a different order (tile_a): within each batch of 8, the tiles
-    // other GPUs own first, its own tiles last — the owned ones form the run
-    // k0 <= k < k1.  Every GPU reduces the tiles it does not own first, so an owner
-    // finds the remote partials of its tiles already arrived, and the result leaves
-    // after one xGMI trip (natural order: remote partials of the last tiles arrive one
-    // trip after the owner's own, then the result needs a second).  At W = 1 nothing moves.
-    auto tile_of = [&](int k) { return blockIdx.x + (uint64_t)k * G; };
-    auto count_below = [&](uint32_t t0) {   // the workgroup's tiles below tile index t0 (32-bit: < 2^20 tiles)
-        return t0 <= blockIdx.x ? 0 : (int)min((uint32_t)mine, (t0 - blockIdx.x + (uint32_t)G - 1) / (uint32_t)G);
-    };
-    const uint32_t tpo32 = (uint32_t)tiles_per_owner;
-    const int k0 = count_below((uint32_t)me * tpo32), k1 = count_below((uint32_t)(me + 1) * tpo32);
-    auto tile_a = [&](int j) {
-        const int lo = j & ~7, hi = lo + 8 < mine ? lo + 8 : mine;
-        const int a0 = k0 < lo ? lo : (k0 > hi ? hi : k0), a1 = k1 < lo ? lo : (k1 > hi ? hi : k1);
-        const int p = j - lo, below = a0 - lo, above = hi - a1;
-        const int k = p < below ? lo + p : (p < below + above ? a1 + (p - below) : a0 + (p - below - above));
-        return tile_of(k);
-    };
-    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
-    uint64_t* const my_ll = lp.ll[me];
-    // ---- A: local trees, partials pushed to their owners
-    if (mine > 0) issue(tile_a(0), 0);
+    const int mine = ht.mine;
+    if (mine > 0) issue(ht.tile_a(0), 0);
     if (w == 0) {   // the order byte (tile 0's loads may stay in flight); read after the loop's barrier
         if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
         asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
@@ -652,9 +659,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         // in flight after tile j's loads: this wave's LL store of tile j-1
         if (j > 0 && w < 3) wait_vm<1>(); else wait_vm<0>();
         lds_barrier();
-        if (j + 1 < mine) issue(tile_a(j + 1), (j + 1) & 1);
+        if (j + 1 < mine) issue(ht.tile_a(j + 1), (j + 1) & 1);
         const uint4* tile = buf[j & 1];
-        const uint64_t t = tile_a(j);
+        const uint64_t t = ht.tile_a(j);
         const uint8_t* ord = ord_lds + RPW * w + LPL * h;
         uint4 x[LPL];
 #pragma unroll
@@ -669,14 +676,34 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         // the partial -> its owner's inbox: wave w < 3 writing word w of every column (one store
         // instruction; wave 3 none)
         if (h == 0) {
-            const int o = owner_of(t);
+            const int o = ht.owner_of(t);
             const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-            const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
+            const uint64_t slot = (t - (uint64_t)o * ht.tpo) * W + me;
             if (w < 3)
                 __hip_atomic_store(lp.ll[o] + slot * kHSlot + 32 * w + c, h_pack(res, w, e8), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
+                                                    uint32_t epoch, uint32_t* status) {
+    constexpr int TV = 32, RPW = 16, OPS = 8;
+    const uint32_t e8 = h_epoch(epoch);
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][64 * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const HierTiles ht(blockIdx.x, gridDim.x, ntiles, tiles_per_owner, me);
+    const int mine = ht.mine;
+    auto tile_of = [&](int k) { return ht.tile_of(k); };
+    auto owner_of = [&](uint64_t t) { return ht.owner_of(t); };
+    uint64_t* const my_ll = lp.ll[me];
+    // ---- A: local trees, partials pushed to their owners
+    hier_reduce(ht, ranks, stride, order, lp, W, me, e8, buf, part, ord_lds);
     __syncthreads();   // every wave is past A: buf may be reused below
     uint4* xs = buf[0];   // [8][32] results of a batch
     // ---- R + B, 8 tiles at a time; lane (jr, c) serves tile jr of the batch, column c.
@@ -738,6 +765,119 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
         __syncthreads();
         store_batch(false);
         __syncthreads();   // xs is reused by the next batch
+    }
+}
+
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
+    return make_uint4((uint32_t)__shfl((int)v.x, src), (uint32_t)__shfl((int)v.y, src), (uint32_t)__shfl((int)v.z, src),
+                      (uint32_t)__shfl((int)v.w, src));
+}
+
+// k_hier_duo: the step of k_hier_ll (same hand-offs, same bits) with its two HBM
+// phases on different workgroups.  k_hier_ll's workgroup reads all its tiles,
+// then writes them, and every workgroup starts reading at once, so the chip
+// reads, then writes (16.2 us at W = 1 against 14.2 for the fused one-GPU pass,
+// which interleaves a tile's stores with later tiles' loads).  Here workgroups
+// [0, GA) are A only (hier_reduce: never wait) and the GA / 4 workgroups after
+// them are B only: wave bw serves reducing workgroup bw's tiles — for a tile it
+// owns, the W partials polled from its inbox, summed, the result pushed to every
+// other GPU's box; for the others the result polled from its own box — and
+// writes the tile's 64 rank rows while A streams the next tiles in.
+//   A B wave keeps two cursors over its tiles, the next owned one and the next
+// other one, and each round polls both (one set of loads in flight) and
+// finishes whichever arrived.  An owned tile waits only for A (every GPU's),
+// another only for its owner's owned tile, so no wait is circular, whatever the
+// order, and nothing needs the grid resident: the reducing workgroups come
+// first in dispatch order and finish without waiting.  A round with nothing
+// arrived sleeps (SLEEP: s_sleep 1 / 4 / 16 / 64) and is bounded like every peer
+// wait (status bit 0).
+__global__ __launch_bounds__(kBlock) void k_hier_duo(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
+                                                     uint32_t epoch, uint32_t* status, uint32_t GA, int sleep_sel) {
+    constexpr int TV = 32;
+    const uint32_t e8 = h_epoch(epoch);
+    __shared__ __attribute__((aligned(16))) uint4 buf[2][64 * TV];
+    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
+    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
+    if (blockIdx.x < GA) {
+        hier_reduce(HierTiles(blockIdx.x, GA, ntiles, tiles_per_owner, me), ranks, stride, order, lp, W, me, e8, buf,
+                    part, ord_lds);
+        return;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = lane & 31, h = lane >> 5;
+    const uint64_t bw = (uint64_t)(blockIdx.x - GA) * 4 + w;
+    if (bw >= GA) return;
+    const HierTiles ht(bw, GA, ntiles, tiles_per_owner, me);
+    const int mine = ht.mine;
+    uint64_t* const my_ll = lp.ll[me];
+    auto owned = [&](int j) { return ht.owner_of(ht.tile_of(j)) == me; };
+    auto next = [&](int j, bool own) {
+        while (j < mine && owned(j) != own) ++j;
+        return j;
+    };
+    // lane (h, c): column c of rows 2k + h (half-wave rows: 512 contiguous bytes per store)
+    auto rows_out = [&](uint64_t t, uint4 v) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k)
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(2 * k + h) * stride) + t * TV + c, v);
+    };
+    int jo = next(0, true), jx = next(0, false);
+    uint64_t spin = 0, t0 = 0;
+    while (jo < mine || jx < mine) {
+        const uint64_t to = ht.tile_of(jo < mine ? jo : 0), tx = ht.tile_of(jx < mine ? jx : 0);
+        const uint64_t li = to - (uint64_t)me * tiles_per_owner;
+        uint64_t wr[kLLMaxGpus][3], wb[3];
+        if (h == 0) {   // the lower half-wave polls (one 16-byte column per lane), both cursors at once
+            if (jo < mine) {
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) h_load(my_ll + (li * W + src) * kHSlot, c, wr[src]);
+            }
+            if (jx < mine) h_load(my_ll + box_words + tx * kHSlot, c, wb);
+        }
+        bool moved = false;
+        if (jo < mine) {
+            bool f = true;
+            if (h == 0) {
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W) f = f && h_fresh(wr[src], e8);
+            }
+            if (__all(f)) {
+                uint4 val = make_uint4(0, 0, 0, 0);
+                if (h == 0) {
+                    uint4 y[kLLMaxGpus];
+#pragma unroll
+                    for (int src = 0; src < kLLMaxGpus; ++src) y[src] = src < W ? h_unpack(wr[src]) : val;
+                    val = owner_sum(y, W, me);
+#pragma unroll
+                    for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                        if (dst < W && dst != me) h_put(lp.ll[dst] + box_words + to * kHSlot, c, val, e8);
+                }
+                rows_out(to, shfl4(val, c));
+                jo = next(jo + 1, true);
+                moved = true;
+            }
+        }
+        if (jx < mine) {
+            const bool f = h != 0 || h_fresh(wb, e8);
+            if (__all(f)) {
+                rows_out(tx, shfl4(h == 0 ? h_unpack(wb) : make_uint4(0, 0, 0, 0), c));
+                jx = next(jx + 1, false);
+                moved = true;
+            }
+        }
+        if (!moved) {
+            if (peer_give_up(spin++, t0, status)) break;
+            switch (sleep_sel) {
+                case 0: __builtin_amdgcn_s_sleep(1); break;
+                case 1: __builtin_amdgcn_s_sleep(4); break;
+                case 2: __builtin_amdgcn_s_sleep(16); break;
+                default: __builtin_amdgcn_s_sleep(64); break;
+            }
+        }
     }
 }
 
@@ -1394,6 +1534,30 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
                        me, ntiles, ntiles / nranks, box_words, epoch, status);
+    return peer_last_error();
+}
+
+int launch_hier_duo(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                    void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
+        ntiles * kHSlot > box_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    // GA reducing workgroups + GA / 4 writing ones within the 2-per-CU slots (the LDS of a
+    // reducing workgroup, 66 KiB, is every workgroup's), or within max_grid when processes
+    // share the GPU (every process's reducing workgroups must find slots while the others' wait)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    unsigned ga = tune(Tune::hier_duo_grid) > 0 ? (unsigned)tune(Tune::hier_duo_grid) : 408u;
+    ga = std::min(ga, cap * 4u / 5u);
+    ga = (unsigned)std::min<uint64_t>(ga, ntiles);
+    ga = std::max(ga, 1u);
+    const unsigned gb = (ga + 3) / 4;
+    hipLaunchKernelGGL(k_hier_duo, dim3(ga + gb), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp,
+                       nranks, me, ntiles, ntiles / nranks, box_words, epoch, status, ga,
+                       tune(Tune::hier_duo_sleep));
     return peer_last_error();
 }
 
