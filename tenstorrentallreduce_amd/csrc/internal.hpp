@@ -42,7 +42,7 @@ enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
     rccl_fault, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll, peer_fence,
-    hier_duo_grid, hier_duo_sleep, count
+    count
 };
 int64_t tune(Tune key);
 
@@ -161,9 +161,6 @@ constexpr int kHSlot = 96;
 // (push) hand-offs: ll[q] = GPU q's LL area for this parity, [inbox box_words words][result box
 // box_words words]; nranks <= 8; epoch grows by 1 per call
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   void* stream);
-int launch_hier_duo(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream);
 // the hierarchical step across consecutive buckets (k_hier_x): finishes `prev` (may be null)

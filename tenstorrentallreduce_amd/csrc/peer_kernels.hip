@@ -768,119 +768,6 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
 }
 
-__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
-    return make_uint4((uint32_t)__shfl((int)v.x, src), (uint32_t)__shfl((int)v.y, src), (uint32_t)__shfl((int)v.z, src),
-                      (uint32_t)__shfl((int)v.w, src));
-}
-
-// k_hier_duo: the step of k_hier_ll (same hand-offs, same bits) with its two HBM
-// phases on different workgroups.  k_hier_ll's workgroup reads all its tiles,
-// then writes them, and every workgroup starts reading at once, so the chip
-// reads, then writes (16.2 us at W = 1 against 14.2 for the fused one-GPU pass,
-// which interleaves a tile's stores with later tiles' loads).  Here workgroups
-// [0, GA) are A only (hier_reduce: never wait) and the GA / 4 workgroups after
-// them are B only: wave bw serves reducing workgroup bw's tiles — for a tile it
-// owns, the W partials polled from its inbox, summed, the result pushed to every
-// other GPU's box; for the others the result polled from its own box — and
-// writes the tile's 64 rank rows while A streams the next tiles in.
-//   A B wave keeps two cursors over its tiles, the next owned one and the next
-// other one, and each round polls both (one set of loads in flight) and
-// finishes whichever arrived.  An owned tile waits only for A (every GPU's),
-// another only for its owner's owned tile, so no wait is circular, whatever the
-// order, and nothing needs the grid resident: the reducing workgroups come
-// first in dispatch order and finish without waiting.  A round with nothing
-// arrived sleeps (SLEEP: s_sleep 1 / 4 / 16 / 64) and is bounded like every peer
-// wait (status bit 0).
-__global__ __launch_bounds__(kBlock) void k_hier_duo(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
-                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                     uint32_t epoch, uint32_t* status, uint32_t GA, int sleep_sel) {
-    constexpr int TV = 32;
-    const uint32_t e8 = h_epoch(epoch);
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][64 * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
-    if (blockIdx.x < GA) {
-        hier_reduce(HierTiles(blockIdx.x, GA, ntiles, tiles_per_owner, me), ranks, stride, order, lp, W, me, e8, buf,
-                    part, ord_lds);
-        return;
-    }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    const uint64_t bw = (uint64_t)(blockIdx.x - GA) * 4 + w;
-    if (bw >= GA) return;
-    const HierTiles ht(bw, GA, ntiles, tiles_per_owner, me);
-    const int mine = ht.mine;
-    uint64_t* const my_ll = lp.ll[me];
-    auto owned = [&](int j) { return ht.owner_of(ht.tile_of(j)) == me; };
-    auto next = [&](int j, bool own) {
-        while (j < mine && owned(j) != own) ++j;
-        return j;
-    };
-    // lane (h, c): column c of rows 2k + h (half-wave rows: 512 contiguous bytes per store)
-    auto rows_out = [&](uint64_t t, uint4 v) {
-#pragma unroll
-        for (int k = 0; k < 32; ++k)
-            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(2 * k + h) * stride) + t * TV + c, v);
-    };
-    int jo = next(0, true), jx = next(0, false);
-    uint64_t spin = 0, t0 = 0;
-    while (jo < mine || jx < mine) {
-        const uint64_t to = ht.tile_of(jo < mine ? jo : 0), tx = ht.tile_of(jx < mine ? jx : 0);
-        const uint64_t li = to - (uint64_t)me * tiles_per_owner;
-        uint64_t wr[kLLMaxGpus][3], wb[3];
-        if (h == 0) {   // the lower half-wave polls (one 16-byte column per lane), both cursors at once
-            if (jo < mine) {
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) h_load(my_ll + (li * W + src) * kHSlot, c, wr[src]);
-            }
-            if (jx < mine) h_load(my_ll + box_words + tx * kHSlot, c, wb);
-        }
-        bool moved = false;
-        if (jo < mine) {
-            bool f = true;
-            if (h == 0) {
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) f = f && h_fresh(wr[src], e8);
-            }
-            if (__all(f)) {
-                uint4 val = make_uint4(0, 0, 0, 0);
-                if (h == 0) {
-                    uint4 y[kLLMaxGpus];
-#pragma unroll
-                    for (int src = 0; src < kLLMaxGpus; ++src) y[src] = src < W ? h_unpack(wr[src]) : val;
-                    val = owner_sum(y, W, me);
-#pragma unroll
-                    for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                        if (dst < W && dst != me) h_put(lp.ll[dst] + box_words + to * kHSlot, c, val, e8);
-                }
-                rows_out(to, shfl4(val, c));
-                jo = next(jo + 1, true);
-                moved = true;
-            }
-        }
-        if (jx < mine) {
-            const bool f = h != 0 || h_fresh(wb, e8);
-            if (__all(f)) {
-                rows_out(tx, shfl4(h == 0 ? h_unpack(wb) : make_uint4(0, 0, 0, 0), c));
-                jx = next(jx + 1, false);
-                moved = true;
-            }
-        }
-        if (!moved) {
-            if (peer_give_up(spin++, t0, status)) break;
-            switch (sleep_sel) {
-                case 0: __builtin_amdgcn_s_sleep(1); break;
-                case 1: __builtin_amdgcn_s_sleep(4); break;
-                case 2: __builtin_amdgcn_s_sleep(16); break;
-                default: __builtin_amdgcn_s_sleep(64); break;
-            }
-        }
-    }
-}
-
 // ---- hierarchical step across consecutive buckets ----------------------------
 // k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
 // hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
@@ -1534,30 +1421,6 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
                        me, ntiles, ntiles / nranks, box_words, epoch, status);
-    return peer_last_error();
-}
-
-int launch_hier_duo(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                    void* stream) {
-    const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
-        ntiles * kHSlot > box_words)
-        return ALLRED_ERR_ARG;
-    LLPtrs lp{};
-    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
-    // GA reducing workgroups + GA / 4 writing ones within the 2-per-CU slots (the LDS of a
-    // reducing workgroup, 66 KiB, is every workgroup's), or within max_grid when processes
-    // share the GPU (every process's reducing workgroups must find slots while the others' wait)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
-    unsigned ga = tune(Tune::hier_duo_grid) > 0 ? (unsigned)tune(Tune::hier_duo_grid) : 408u;
-    ga = std::min(ga, cap * 4u / 5u);
-    ga = (unsigned)std::min<uint64_t>(ga, ntiles);
-    ga = std::max(ga, 1u);
-    const unsigned gb = (ga + 3) / 4;
-    hipLaunchKernelGGL(k_hier_duo, dim3(ga + gb), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp,
-                       nranks, me, ntiles, ntiles / nranks, box_words, epoch, status, ga,
-                       tune(Tune::hier_duo_sleep));
     return peer_last_error();
 }
 

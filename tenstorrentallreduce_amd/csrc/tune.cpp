@@ -48,8 +48,6 @@ const Key kKeys[] = {
     {"hier_x_rearly", 0, 0, 1},       // k_hier_x (LL, lag 1): 1 R(cur) ahead of the previous bucket's last row stores
     {"hier_x_latepoll", 1, 0, 1},     // k_hier_x / k_hier_x2 (LL, lag 1): 1 the earlier bucket's results polled after tile 0's tree
     {"peer_fence", 0, 0, 1},          // peer kernels: 1 system-scope release / acquire fences around every cross-GPU hand-off
-    {"hier_duo_grid", 0, 0, 409},     // k_hier_duo: reducing workgroups (0 auto: 408, + a quarter as many writing ones)
-    {"hier_duo_sleep", 1, 0, 3},      // k_hier_duo: a writing wave's idle round sleeps s_sleep 1 | 4 | 16 | 64
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

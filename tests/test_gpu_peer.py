@@ -145,8 +145,6 @@ def worker(rank, world, port, q, devs=None, tunes=None):
         for mi, (mode, limit, ll, cap) in enumerate((("hier_oneshot_exchange", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
                                                      ("hier_ll_capped", 0, 1, 2), ("hier_oneshot_exchange_capped", 1 << 40, 0, 1),
-                                                     ("hier_duo", 0, 2, 0), ("hier_duo_capped", 0, 2, 2),
-                                                     ("hier_launches_then_duo", 0, 0, 0), ("hier_duo_again", 0, 2, 0),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
@@ -356,7 +354,7 @@ def t_timeout_bit():
 
 @pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
 def test_hier_forms_single_gpu_bit_exact(n, cap):
-    """One GPU (W = 1), 64 local ranks: the LL forms k_hier_ll / k_hier_duo and the launch
+    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll and the launch
     form (mem_2D exchange as one kernel or as launches) give the same
     bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
     mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
@@ -378,7 +376,7 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit in ((1, 0), (0, 1 << 40), (2, 0), (0, 0), (1, 0), (2, 0), (0, 1 << 40), (1, 0), (2, 0)):
+        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (1, 0), (0, 1 << 40), (1, 0)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
@@ -469,7 +467,7 @@ def test_peer_knob_argument_errors():
     peer.connect([peer.handle()])
     try:
         with pytest.raises(_lib.AllredError):
-            peer.set_hier_ll(3)            # 0 off, 1 k_hier_ll, 2 k_hier_duo
+            peer.set_hier_ll(2)            # 0 off, 1 k_hier_ll (k_hier_pipe is gone)
         with pytest.raises(_lib.AllredError):
             peer.set_hier_ll(-1)
         peer.set_lo_ll_max(0)

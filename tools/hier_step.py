@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
-x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ll, k_hier_duo, k_hier_x
+x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ll, k_hier_x
 and k_hier_x2 (buckets pipelined one / two deep, k_hier_x2 with its owned sums
 at the start, the end or before the last row stores of a launch: K buckets in
 K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
@@ -27,13 +27,7 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
-arms = {"launches": (0, 0, {}), "oneshot_exchange": (1 << 40, 0, {}), "hier_ll": (0, 1, {}),
-        "hier_duo": (0, 2, {})}
-# k_hier_duo variants: _s<k> the writing waves' idle sleep (tune hier_duo_sleep), _g<n> reducing workgroups
-for k in range(4):
-    arms[f"hier_duo_s{k}"] = (0, 2, {"hier_duo_sleep": k})
-for g in (256, 320, 384):
-    arms[f"hier_duo_g{g}"] = (0, 2, {"hier_duo_grid": g})
+arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ll": (0, 1)}
 # pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _ch: the
 # chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned sums before the
 # last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last tile's row
@@ -82,11 +76,9 @@ for _ in range(rounds):
         e1.record(s)
         torch.cuda.synchronize()
         res[name].append(round(e0.elapsed_time(e1) * 1e3 / steps, 3))
-    for name, (limit, ll, knobs) in arms.items():
+    for name, (limit, ll) in arms.items():
         peer.set_oneshot_max(limit)
         peer.set_hier_ll(ll)
-        t.tune("hier_duo_sleep", knobs.get("hier_duo_sleep", 1))
-        t.tune("hier_duo_grid", knobs.get("hier_duo_grid", 0))
         for i in range(20):
             peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
         torch.cuda.synchronize()

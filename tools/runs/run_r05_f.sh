@@ -6,7 +6,7 @@ out=gpurun_out/r05f
 mkdir -p $out
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_peer.py \
     -k "hier_forms_single or one_shot_multi_process or knob" > $out/tests.log 2>&1 &&
-HIER_ARMS=hier_ll,hier_duo,hier_duo_s0,hier_duo_s2,hier_duo_s3,hier_duo_g256,hier_duo_g320,hier_duo_g384,hier_x2_tail2_lp \
+HIER_ARMS=hier_ll,hier_duo,hier_duo_s2,hier_duo_g384,hier_x2_tail2_lp \
     timeout -k 10 300 python tools/hier_step.py 100 3 > $out/hier_step.json 2> $out/hier_step.err &&
 HIER_ARMS=hier_ll,hier_duo timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/prof -o run -- \
     python tools/hier_step.py 50 2 > $out/prof.log 2>&1
