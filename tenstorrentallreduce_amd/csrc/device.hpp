@@ -69,6 +69,7 @@ __device__ __forceinline__ uint4 shfl_xor4(uint4 v, int m) {
 // once and written once per pass, so nothing is worth keeping in L2 / MALL
 // (measured: the fused tree pass 19.2 -> 16.0 us, the tile-sum 5.9 -> 6.4 TB/s).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     return make_uint4(v.x, v.y, v.z, v.w);

@@ -163,6 +163,9 @@ constexpr int kHSlot = 96;
 int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream);
+int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                   void* stream);
 // the hierarchical step across consecutive buckets (k_hier_x): finishes `prev` (may be null)
 // and starts `cur` (may be null) in one launch; llc / llp: every GPU's LL area of cur's /
 // prev's parity; ALLRED_ERR_UNSUPPORTED beyond kHierXMaxTiles tiles per workgroup

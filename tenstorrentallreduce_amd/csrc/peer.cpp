@@ -69,7 +69,7 @@ struct allred_peer {
     // range oldest (every call rewrites tiles [0, its tiles)); hier_area_prepare reads it
     std::vector<std::pair<uint64_t, uint32_t>> hl_stairs[2];
     uint64_t hl_clears = 0;         // barrier-protected clears of a parity's area so far
-    int hier_ll = 0;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs)
+    int hier_ll = 0;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs), 2 k_hier_ws
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
@@ -407,8 +407,9 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
         uint64_t* ll[ALLRED_MAX_NODES];
         hier_areas(p, p->calls, ll);
         if ((st = hier_area_prepare(p, n / 256, p->calls, stream)) != ALLRED_OK) return st;
-        st = launch_hier_ll(buf, n, order, ll, p->nranks, p->rank, n, p->hl_box_words, p->calls + 1u, p->status,
-                            p->max_groups, stream);
+        st = (p->hier_ll == 2 ? launch_hier_ws : launch_hier_ll)(buf, n, order, ll, p->nranks, p->rank, n,
+                                                                 p->hl_box_words, p->calls + 1u, p->status,
+                                                                 p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -514,7 +515,7 @@ int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
 
 int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
-    if (enable < 0 || enable > 1) return ALLRED_ERR_ARG;
+    if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
     return ALLRED_OK;
 }

@@ -768,6 +768,193 @@ __global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks
     }
 }
 
+__device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
+    return make_uint4((uint32_t)__shfl((int)v.x, src), (uint32_t)__shfl((int)v.y, src), (uint32_t)__shfl((int)v.z, src),
+                      (uint32_t)__shfl((int)v.w, src));
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src) | ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32);
+}
+
+// k_hier_ws: the step of k_hier_ll (same hand-offs across GPUs, same bits) with
+// its two HBM phases on different waves of one workgroup, so every CU reads and
+// writes at once.  k_hier_ll's workgroups read all their tiles, then write
+// them: the chip reads, then writes (16.2 us at W = 1 against 14.2 for the
+// fused one-GPU pass, which interleaves a tile's stores with later tiles'
+// loads).  A workgroup here has 8 waves and no barrier after its start:
+//   wave q < 4 (A) reduces column quarter q (8 columns, 128 bytes of each rank
+//     row) of the workgroup's tiles on its own: LDS-DMA of the 64 rows of its
+//     quarter into its own two buffers (one tile ahead), 8 leaves per lane
+//     (lane = leaf group g x column c) and the tree's last three levels across
+//     lanes (xor 8, 16, 32 — the tree and operand order of k_hier_ll, whose
+//     leaf group g = 2w + h).  A partial another GPU owns is pushed to its
+//     inbox (the 6 + 2-byte words, lanes 0-23 one word each); an owned one goes
+//     to an LDS slot for wave q + 4 (the first kRing owned tiles; later ones
+//     through the own inbox), so at W = 1 nothing crosses global memory but
+//     the rank rows.
+//   wave q + 4 (B) writes quarter q of the tiles' 64 rank rows: for a tile it
+//     owns, the own partial (LDS or inbox) and the W - 1 others polled from
+//     its inbox, summed (owner first, fp32, one rounding), the result pushed
+//     to every other GPU's box; for another GPU's tile the result polled from
+//     its own box.  Two cursors (next owned, next other tile, both polled in a
+//     round, whichever arrived is finished): an owned tile waits only for A
+//     (which never waits), another only for its owner's owned tile, so no wait
+//     is circular.  Bounded like every peer wait (status bit 0).
+// Every workgroup must be resident (the B waves wait across GPUs): 2 per CU,
+// 8 waves each at <= 128 VGPRs, max_grid when processes share the GPU.
+constexpr int kWsRing = 16;
+__global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks, uint64_t stride,
+                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
+                                                    uint32_t epoch, uint32_t* status) {
+    constexpr int TV = 32, QC = 8, LPL = 8, OPS = 8;
+    __shared__ __attribute__((aligned(16))) uint4 buf[4][2][64 * QC];    // A wave q: two tiles of its quarter
+    __shared__ __attribute__((aligned(16))) uint4 res[4][kWsRing][QC];   // A -> B: owned partials of quarter q
+    __shared__ uint32_t prod[4];                                          // owned partials published per quarter
+    // the wave index as a scalar: the A / B split is a uniform branch (one role's code only per wave)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = w & 3;
+    const int cc = lane & 7, g = lane >> 3;
+    const uint32_t e8 = h_epoch(epoch);
+    const HierTiles ht(blockIdx.x, gridDim.x, ntiles, tiles_per_owner, me);
+    const int mine = ht.mine;
+    if (threadIdx.x < 4) prod[threadIdx.x] = 0;
+    __syncthreads();
+    // word k = lane / 8 (lanes 0-23) of column 8q + cc of a tile's slot
+    const int wk = g < 3 ? g : 0;
+    const uint64_t woff = 32 * (uint64_t)wk + 8 * q + cc;
+    if (w < 4) {
+        // ---- A: the leaf bytes 8g .. 8g + 7 of the tree order (one 8-byte load ahead of the tiles')
+        u32x2 ov;
+        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(ov) : "v"(order + 8 * g) : "memory");
+        const uint32_t wbase = __builtin_amdgcn_readfirstlane(
+            (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[q][0][0]);
+        auto issue = [&](uint64_t t, int b) {   // rows 8k + g, column 8q + cc: 8 rows x 128 bytes per op
+#pragma unroll
+            for (int k = 0; k < OPS; ++k)
+                lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)(8 * k + g) * stride) + t * TV + 8 * q + cc,
+                          wbase + (uint32_t)(b * 64 * QC * 16 + k * 1024));
+        };
+        if (mine > 0) issue(ht.tile_a(0), 0);
+        bool pushed = false;   // the previous tile's partial went out as a global store (one op)
+        int ko = 0;            // owned tiles so far
+        for (int j = 0; j < mine; ++j) {
+            if (pushed) wait_vm<1>(); else wait_vm<0>();
+            asm volatile("" : "+v"(ov));   // no use of ov may move above the first wait
+            if (j + 1 < mine) issue(ht.tile_a(j + 1), (j + 1) & 1);
+            const uint4* tile = buf[q][j & 1];
+            uint4 x[LPL];
+#pragma unroll
+            for (int i = 0; i < LPL; ++i) {
+                const uint32_t leaf = ((i < 4 ? ov.x : ov.y) >> (8 * (i & 3))) & 255u;
+                x[i] = tile[(int)leaf * QC + cc];
+            }
+#pragma unroll
+            for (int s2 = 1; s2 < LPL; s2 *= 2)
+#pragma unroll
+                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
+#pragma unroll
+            for (int m = 8; m < 64; m *= 2) x[0] = add8(x[0], shfl_xor4(x[0], m));
+            const uint4 pr = shfl4(x[0], cc);   // leaf group 0's sum: k_hier_ll's operand order
+            const uint64_t t = ht.tile_a(j);
+            const int o = ht.owner_of(t);
+            if (o == me && ko < kWsRing) {
+                if (g == 0) res[q][ko][cc] = pr;
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the slot before the count
+                if (lane == 0) __hip_atomic_store(&prod[q], (uint32_t)(ko + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                pushed = false;
+            } else {
+                const uint64_t slot = (t - (uint64_t)o * ht.tpo) * W + me;
+                if (g < 3)
+                    __hip_atomic_store(lp.ll[o] + slot * kHSlot + woff, h_pack(pr, wk, e8), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                pushed = true;
+            }
+            if (o == me) ++ko;
+        }
+        return;
+    }
+    // ---- B: quarter q of the tiles' rank rows
+    uint64_t* const my_ll = lp.ll[me];
+    auto owned = [&](int j) { return ht.owner_of(ht.tile_a(j)) == me; };
+    auto next = [&](int j, bool own) {
+        while (j < mine && owned(j) != own) ++j;
+        return j;
+    };
+    auto rows_out = [&](uint64_t t, uint4 v) {   // rows 8k + g, column 8q + cc
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(8 * k + g) * stride) + t * TV + 8 * q + cc, v);
+    };
+    // the column of this lane from the three words lanes cc, 8 + cc, 16 + cc polled
+    auto gather = [&](uint64_t wd) {
+        const uint64_t a[3] = {shfl64(wd, cc), shfl64(wd, 8 + cc), shfl64(wd, 16 + cc)};
+        return h_unpack(a);
+    };
+    int jo = next(0, true), jx = next(0, false), ko = 0;
+    uint64_t spin = 0, t0 = 0;
+    while (jo < mine || jx < mine) {
+        const uint64_t to = ht.tile_a(jo < mine ? jo : 0), tx = ht.tile_a(jx < mine ? jx : 0);
+        const uint64_t li = to - (uint64_t)me * tiles_per_owner;
+        const bool own_lds = ko < kWsRing;
+        // one round: every word both cursors need, in flight at once (lanes 0-23, one word each)
+        uint64_t wr[kLLMaxGpus] = {}, wb = 0;
+        if (g < 3) {
+            if (jo < mine) {
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W && (src != me || !own_lds))
+                        wr[src] = __hip_atomic_load(my_ll + (li * W + src) * kHSlot + woff, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (jx < mine)
+                wb = __hip_atomic_load(my_ll + box_words + tx * kHSlot + woff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        bool moved = false;
+        if (jo < mine) {
+            bool f = !own_lds || __hip_atomic_load(&prod[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > (uint32_t)ko;
+            if (g < 3) {
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src)
+                    if (src < W && (src != me || !own_lds)) f = f && (uint32_t)(wr[src] >> 48) == e8;
+            }
+            if (__all(f)) {
+                asm volatile("" ::: "memory");   // the slot read stays behind the count read
+                uint4 y[kLLMaxGpus];
+#pragma unroll
+                for (int src = 0; src < kLLMaxGpus; ++src) {
+                    if (src >= W) y[src] = make_uint4(0, 0, 0, 0);
+                    else if (src == me && own_lds) y[src] = res[q][ko][cc];
+                    else y[src] = gather(wr[src]);
+                }
+                const uint4 val = owner_sum(y, W, me);
+                if (g < 3) {
+#pragma unroll
+                    for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                        if (dst < W && dst != me)
+                            __hip_atomic_store(lp.ll[dst] + box_words + to * kHSlot + woff, h_pack(val, wk, e8),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+                rows_out(to, val);
+                ++ko;
+                jo = next(jo + 1, true);
+                moved = true;
+            }
+        }
+        if (jx < mine) {
+            const bool f = g >= 3 || (uint32_t)(wb >> 48) == e8;
+            if (__all(f)) {
+                rows_out(tx, gather(wb));
+                jx = next(jx + 1, false);
+                moved = true;
+            }
+        }
+        if (!moved) {
+            if (peer_give_up(spin++, t0, status)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+}
+
 // ---- hierarchical step across consecutive buckets ----------------------------
 // k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
 // hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
@@ -1421,6 +1608,23 @@ int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
                        me, ntiles, ntiles / nranks, box_words, epoch, status);
+    return peer_last_error();
+}
+
+int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
+                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
+                   void* stream) {
+    const uint64_t nv = n / 8, ntiles = nv / 32;
+    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
+        ntiles * kHSlot > box_words)
+        return ALLRED_ERR_ARG;
+    LLPtrs lp{};
+    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
+    // 2 per CU (8 waves each): the whole grid resident (max_grid < 512 when processes share the GPU)
+    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
+    hipLaunchKernelGGL(k_hier_ws, dim3(grid), dim3(512), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
+                       ntiles, ntiles / nranks, box_words, epoch, status);
     return peer_last_error();
 }
 

@@ -142,9 +142,14 @@ def worker(rank, world, port, q, devs=None, tunes=None):
         # (then LL once more after the launch form: its LL boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
         # in full and capped grids (a capped grid gives every workgroup many tiles)
-        for mi, (mode, limit, ll, cap) in enumerate((("hier_oneshot_exchange", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
+        for mi, (mode, limit, ll, cap, *more) in enumerate((("hier_oneshot_exchange", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
                                                      ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
                                                      ("hier_ll_capped", 0, 1, 2), ("hier_oneshot_exchange_capped", 1 << 40, 0, 1),
+                                                     # k_hier_ws; one workgroup with 20 tiles per owner: owned
+                                                     # partials past its 16 LDS slots go through the own inbox
+                                                     ("hier_ws", 0, 2, 0), ("hier_ws_capped", 0, 2, 2),
+                                                     ("hier_launches_then_ws", 0, 0, 0), ("hier_ws_again", 0, 2, 0),
+                                                     ("hier_ws_ring", 0, 2, 1, 20),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
@@ -156,6 +161,7 @@ def worker(rank, world, port, q, devs=None, tunes=None):
                                                      # (two chunks resident, the third reusing the first's slot)
                                                      ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
                                                      ("hier_x2_tail_one_group", 0, 0, 1))):
+            m = 256 * world * (more[0] if more else 3)
             if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
@@ -354,7 +360,7 @@ def t_timeout_bit():
 
 @pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
 def test_hier_forms_single_gpu_bit_exact(n, cap):
-    """One GPU (W = 1), 64 local ranks: the LL form k_hier_ll and the launch
+    """One GPU (W = 1), 64 local ranks: the LL forms k_hier_ll / k_hier_ws and the launch
     form (mem_2D exchange as one kernel or as launches) give the same
     bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
     mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
@@ -376,7 +382,7 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit in ((1, 0), (0, 1 << 40), (0, 0), (1, 0), (0, 1 << 40), (1, 0)):
+        for ll, limit in ((1, 0), (0, 1 << 40), (2, 0), (0, 0), (1, 0), (2, 0), (0, 1 << 40), (1, 0), (2, 0)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
@@ -467,7 +473,7 @@ def test_peer_knob_argument_errors():
     peer.connect([peer.handle()])
     try:
         with pytest.raises(_lib.AllredError):
-            peer.set_hier_ll(2)            # 0 off, 1 k_hier_ll (k_hier_pipe is gone)
+            peer.set_hier_ll(3)            # 0 off, 1 k_hier_ll, 2 k_hier_ws
         with pytest.raises(_lib.AllredError):
             peer.set_hier_ll(-1)
         peer.set_lo_ll_max(0)

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
-x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ll, k_hier_x
+x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ll, k_hier_ws, k_hier_x
 and k_hier_x2 (buckets pipelined one / two deep, k_hier_x2 with its owned sums
 at the start, the end or before the last row stores of a launch: K buckets in
 K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
@@ -27,7 +27,7 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
-arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ll": (0, 1)}
+arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ll": (0, 1), "hier_ws": (0, 2)}
 # pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _ch: the
 # chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned sums before the
 # last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last tile's row
