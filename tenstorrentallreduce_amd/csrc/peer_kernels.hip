@@ -803,6 +803,9 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // Every workgroup must be resident (the B waves wait across GPUs): 2 per CU,
 // 8 waves each at <= 128 VGPRs, max_grid when processes share the GPU.
 constexpr int kWsRing = 16;
+// AHEAD 1: tile j+1's loads issued before tile j's tree; 2: also tile j+2's, into tile j's buffer
+// right after its tree (k_tree_lds_lag's schedule)
+template <int AHEAD>
 __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
                                                     uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
@@ -835,12 +838,18 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
                           wbase + (uint32_t)(b * 64 * QC * 16 + k * 1024));
         };
         if (mine > 0) issue(ht.tile_a(0), 0);
+        if (AHEAD == 2 && mine > 1) issue(ht.tile_a(1), 1);
         bool pushed = false;   // the previous tile's partial went out as a global store (one op)
         int ko = 0;            // owned tiles so far
         for (int j = 0; j < mine; ++j) {
-            if (pushed) wait_vm<1>(); else wait_vm<0>();
+            // after L(j): AHEAD 1 the previous tile's store; AHEAD 2 that store and L(j+1)
+            if (AHEAD == 2 && j + 1 < mine) {
+                if (pushed) wait_vm<OPS + 1>(); else wait_vm<OPS>();
+            } else {
+                if (pushed) wait_vm<1>(); else wait_vm<0>();
+            }
             asm volatile("" : "+v"(ov));   // no use of ov may move above the first wait
-            if (j + 1 < mine) issue(ht.tile_a(j + 1), (j + 1) & 1);
+            if (AHEAD == 1 && j + 1 < mine) issue(ht.tile_a(j + 1), (j + 1) & 1);
             const uint4* tile = buf[q][j & 1];
             uint4 x[LPL];
 #pragma unroll
@@ -870,6 +879,7 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
                 pushed = true;
             }
             if (o == me) ++ko;
+            if (AHEAD == 2 && j + 2 < mine) issue(ht.tile_a(j + 2), j & 1);   // this wave has read tile j
         }
         return;
     }
@@ -1623,7 +1633,8 @@ int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     // 2 per CU (8 waves each): the whole grid resident (max_grid < 512 when processes share the GPU)
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    hipLaunchKernelGGL(k_hier_ws, dim3(grid), dim3(512), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
+    hipLaunchKernelGGL(tune(Tune::hier_ws_ahead) == 2 ? k_hier_ws<2> : k_hier_ws<1>, dim3(grid), dim3(512), 0,
+                       (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
                        ntiles, ntiles / nranks, box_words, epoch, status);
     return peer_last_error();
 }

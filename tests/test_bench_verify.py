@@ -143,7 +143,7 @@ def test_dropped_candidates_are_listed_with_a_reason():
     peer wait give up is listed (and never chosen); verified forms are not."""
     verify = {"rccl": {"verified": True, "exact_sum": True, "closed_form": True},
               "peer_hier_x": {"verified": False, "quick_timing_timeout": True},
-              "peer_hier_ll": {"verified": False, "exact_sum": True, "closed_form": True,
+              "peer_hier_ws": {"verified": False, "exact_sum": True, "closed_form": True,
                                "matches_peer_launches": False},
               "peer_swing": {"verified": False, "exact_sum": False, "closed_form": True},
               "peer_hier_x_fenced": {"verified": True, "exact_sum": True, "closed_form": True,
@@ -151,16 +151,16 @@ def test_dropped_candidates_are_listed_with_a_reason():
     quick = {"rccl": 1.0, "peer_hier_x_fenced": 0.6}
     assert bench.choose_transport(quick, verify) == "peer_hier_x_fenced"
     got = {d["transport"]: d["reason"] for d in bench.dropped_candidates(verify)}
-    assert set(got) == {"peer_hier_x", "peer_hier_ll", "peer_swing"}
+    assert set(got) == {"peer_hier_x", "peer_hier_ws", "peer_swing"}
     assert got["peer_hier_x"].startswith("quick_timing_timeout")
-    assert got["peer_hier_ll"] == "differs from peer_launches"
+    assert got["peer_hier_ws"] == "differs from peer_launches"
     assert got["peer_swing"] == "exact_sum check failed"
     assert bench.dropped_candidates({"rccl": {"verified": True}}) == []
 
 
 def test_unverified_never_headline_nor_roofline():
-    quick = {"rccl": 1.0, "peer_hier_ll": 0.5, "peer_swing": 0.8}
-    verify = {"rccl": {"verified": True}, "peer_hier_ll": {"verified": False}, "peer_swing": {"verified": True}}
+    quick = {"rccl": 1.0, "peer_hier_ws": 0.5, "peer_swing": 0.8}
+    verify = {"rccl": {"verified": True}, "peer_hier_ws": {"verified": False}, "peer_swing": {"verified": True}}
     assert bench.choose_transport(quick, verify) == "peer_swing"
     assert bench.choose_transport(quick, {}) is None
     arm = "config4_swing_bo_1GiB_all_links"
