@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-/* ABI 6 (round 5): allred_peer_set_hier_ll takes 0 / 1 only (k_hier_pipe retired), the tune
+/* ABI 6 (round 5): allred_peer_set_hier_ll takes 0 / 1 / 2 (k_hier_pipe retired, k_hier_ws new), the tune
  * keys lose hier_handoff and gain peer_fence, allred_peer_clear_status refuses while a
  * pipelined sequence is pending, and the hierarchical forms' hand-off area moved (its own
  * words: 6 data bytes + a 16-bit epoch) — peers of different ABIs must not connect. */
@@ -587,8 +587,10 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * same setting.  Replaces nothing in the reference (its mem_2D phases sync
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
 /* 0 = off (tree, the mem_2D exchange, broadcast as launches), 1 = k_hier_ll
- * (all tiles read, owned tiles summed, all tiles written: three phases);
- * other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
+ * (all tiles read, owned tiles summed, all tiles written: three phases),
+ * 2 = k_hier_ws (round 5: the same hand-offs with reducing and writing waves
+ * in every workgroup, so each CU reads and writes at once: 15.0 vs 16.2 us at
+ * W = 1); other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
  * profiles/README.md — the per-tile flag form k_hier_oneshot, 19.9 us at
  * W = 1, and the pipelined LL form k_hier_pipe, 17.8 us, in round 5; the
  * specialised-wave form of round 1, 27-38 us.) */
