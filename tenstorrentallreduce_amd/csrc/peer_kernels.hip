@@ -781,89 +781,114 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
 // writes at once.  k_hier_ll's workgroups read all their tiles, then write
 // them: the chip reads, then writes (16.2 us at W = 1 against 14.2 for the
 // fused one-GPU pass, which interleaves a tile's stores with later tiles'
-// loads).  A workgroup here has 8 waves and no barrier after its start:
-//   wave q < 4 (A) reduces column quarter q (8 columns, 128 bytes of each rank
-//     row) of the workgroup's tiles on its own: LDS-DMA of the 64 rows of its
-//     quarter into its own two buffers (one tile ahead), 8 leaves per lane
-//     (lane = leaf group g x column c) and the tree's last three levels across
-//     lanes (xor 8, 16, 32 — the tree and operand order of k_hier_ll, whose
-//     leaf group g = 2w + h).  A partial another GPU owns is pushed to its
-//     inbox (the 6 + 2-byte words, lanes 0-23 one word each); an owned one goes
-//     to an LDS slot for wave q + 4 (the first kRing owned tiles; later ones
-//     through the own inbox), so at W = 1 nothing crosses global memory but
-//     the rank rows.
-//   wave q + 4 (B) writes quarter q of the tiles' 64 rank rows: for a tile it
-//     owns, the own partial (LDS or inbox) and the W - 1 others polled from
+// loads).  A workgroup has 2 * NQ waves and no barrier after its start; the
+// tile's 32 columns (16 bytes each) split into NQ = 32 / CW groups of CW:
+//   wave q < NQ (A) reduces columns CW q .. CW q + CW - 1 of the workgroup's
+//     tiles on its own: LDS-DMA of those columns of the 64 rank rows into its
+//     own two buffers (one tile ahead), CW leaves per lane (lane = leaf group g
+//     x column c) and the tree's last levels across lanes (xor CW .. 32 — the
+//     tree and operand order of k_hier_ll, whose lanes hold 8 leaves each).  A
+//     partial another GPU owns is pushed to its inbox (the 6 + 2-byte words,
+//     one per lane); an owned one goes to an LDS slot for wave q + NQ (the
+//     first kWsRing owned tiles; later ones through the own inbox), so at W = 1
+//     nothing crosses global memory but the rank rows.
+//   wave q + NQ (B) writes those columns of the tiles' 64 rank rows: for a tile
+//     it owns, the own partial (LDS or inbox) and the W - 1 others polled from
 //     its inbox, summed (owner first, fp32, one rounding), the result pushed
 //     to every other GPU's box; for another GPU's tile the result polled from
 //     its own box.  Two cursors (next owned, next other tile, both polled in a
 //     round, whichever arrived is finished): an owned tile waits only for A
 //     (which never waits), another only for its owner's owned tile, so no wait
 //     is circular.  Bounded like every peer wait (status bit 0).
-// Every workgroup must be resident (the B waves wait across GPUs): 2 per CU,
-// 8 waves each at <= 128 VGPRs, max_grid when processes share the GPU.
+// CW = 16 (halves: 4 waves, 256-byte row segments) is the default: 14.5-14.7 us a
+// step at W = 1 against 14.8-15.0 for quarters (8 waves, 128-byte segments) and
+// 16.2 for whole tiles (2 waves: too few in flight); profiles/r05_hier_ws_step_w1.json.
+// Every workgroup must be resident (the B waves wait across GPUs): 2 per CU (the
+// A buffers' 64 KiB of LDS), max_grid when processes share the GPU.
 constexpr int kWsRing = 16;
 // AHEAD 1: tile j+1's loads issued before tile j's tree; 2: also tile j+2's, into tile j's buffer
-// right after its tree (k_tree_lds_lag's schedule)
-template <int AHEAD>
-__global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
-                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status) {
-    constexpr int TV = 32, QC = 8, LPL = 8, OPS = 8;
-    __shared__ __attribute__((aligned(16))) uint4 buf[4][2][64 * QC];    // A wave q: two tiles of its quarter
-    __shared__ __attribute__((aligned(16))) uint4 res[4][kWsRing][QC];   // A -> B: owned partials of quarter q
-    __shared__ uint32_t prod[4];                                          // owned partials published per quarter
+// right after its tree (k_tree_lds_lag's schedule).  CW: columns (16-byte vectors) of a tile per
+// reducing wave — 8 (a quarter: 8 waves per workgroup, 128-byte row segments, 8 leaves per
+// lane), 16 (a half: 4 waves, 256-byte segments, 16 leaves) or 32 (the whole tile: 2 waves,
+// 512-byte segments, 32 leaves)
+template <int AHEAD, int CW>
+__global__ __launch_bounds__(128 * (32 / CW), (CW == 8 ? 4 : CW == 16 ? 2 : 1)) void k_hier_ws(
+    uint16_t* __restrict__ ranks, uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
+    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words, uint32_t epoch, uint32_t* status) {
+    constexpr int TV = 32, NQ = TV / CW, GR = 64 / CW, LPL = CW, OPS = CW;
+    constexpr int NWR = (3 * CW + 63) / 64;   // word rounds: a tile's 3 CW hand-off words of this wave's columns
+    static_assert(CW == 8 || CW == 16 || CW == 32, "a quarter, a half or the whole tile per reducing wave");
+    __shared__ __attribute__((aligned(16))) uint4 buf[NQ][2][64 * CW];    // A wave q: two tiles of its columns
+    __shared__ __attribute__((aligned(16))) uint4 res[NQ][kWsRing][CW];   // A -> B: owned partials
+    __shared__ uint32_t prod[NQ];                                          // owned partials published per wave
     // the wave index as a scalar: the A / B split is a uniform branch (one role's code only per wave)
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = w & 3;
-    const int cc = lane & 7, g = lane >> 3;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), q = w % NQ;
+    const int cc = lane % CW, g = lane / CW;
     const uint32_t e8 = h_epoch(epoch);
     const HierTiles ht(blockIdx.x, gridDim.x, ntiles, tiles_per_owner, me);
     const int mine = ht.mine;
-    if (threadIdx.x < 4) prod[threadIdx.x] = 0;
+    if (threadIdx.x < NQ) prod[threadIdx.x] = 0;
     __syncthreads();
-    // word k = lane / 8 (lanes 0-23) of column 8q + cc of a tile's slot
-    const int wk = g < 3 ? g : 0;
-    const uint64_t woff = 32 * (uint64_t)wk + 8 * q + cc;
-    if (w < 4) {
-        // ---- A: the leaf bytes 8g .. 8g + 7 of the tree order (one 8-byte load ahead of the tiles')
-        u32x2 ov;
-        asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(ov) : "v"(order + 8 * g) : "memory");
+    // hand-off word i = lane + 64 r of this wave's columns: word i / CW of column CW q + i % CW
+    // (column i % CW = cc: every lane packs its own column)
+    auto wvalid = [&](int r) { return lane + 64 * r < 3 * CW; };
+    auto wkey = [&](int r) { return (lane + 64 * r) / CW; };
+    auto woff = [&](int r) { return (uint64_t)(32 * wkey(r) + CW * q + cc); };
+    if (w < NQ) {
+        // ---- A: the leaf bytes CW g .. CW g + CW - 1 of the tree order (loaded ahead of the tiles')
+        uint32_t ob[CW / 4];
+        if constexpr (CW == 8) {
+            u32x2 ov;
+            asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(ov) : "v"(order + CW * g) : "memory");
+            ob[0] = ov.x;
+            ob[1] = ov.y;
+        } else {
+#pragma unroll
+            for (int h = 0; h < CW / 16; ++h) {
+                u32x4 ov;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(ov) : "v"(order + CW * g + 16 * h) : "memory");
+                ob[4 * h + 0] = ov.x;
+                ob[4 * h + 1] = ov.y;
+                ob[4 * h + 2] = ov.z;
+                ob[4 * h + 3] = ov.w;
+            }
+        }
         const uint32_t wbase = __builtin_amdgcn_readfirstlane(
             (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[q][0][0]);
-        auto issue = [&](uint64_t t, int b) {   // rows 8k + g, column 8q + cc: 8 rows x 128 bytes per op
+        auto issue = [&](uint64_t t, int b) {   // rows GR k + g, column CW q + cc: GR rows x 16 CW bytes per op
 #pragma unroll
             for (int k = 0; k < OPS; ++k)
-                lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)(8 * k + g) * stride) + t * TV + 8 * q + cc,
-                          wbase + (uint32_t)(b * 64 * QC * 16 + k * 1024));
+                lds_dma16(reinterpret_cast<const uint4*>(ranks + (uint64_t)(GR * k + g) * stride) + t * TV + CW * q + cc,
+                          wbase + (uint32_t)(b * 64 * CW * 16 + k * 1024));
         };
         if (mine > 0) issue(ht.tile_a(0), 0);
         if (AHEAD == 2 && mine > 1) issue(ht.tile_a(1), 1);
-        bool pushed = false;   // the previous tile's partial went out as a global store (one op)
+        bool pushed = false;   // the previous tile's partial went out as global stores (NWR ops)
         int ko = 0;            // owned tiles so far
         for (int j = 0; j < mine; ++j) {
-            // after L(j): AHEAD 1 the previous tile's store; AHEAD 2 that store and L(j+1)
+            // after L(j): AHEAD 1 the previous tile's stores; AHEAD 2 those and L(j+1)
             if (AHEAD == 2 && j + 1 < mine) {
-                if (pushed) wait_vm<OPS + 1>(); else wait_vm<OPS>();
+                if (pushed) wait_vm<OPS + NWR>(); else wait_vm<OPS>();
             } else {
-                if (pushed) wait_vm<1>(); else wait_vm<0>();
+                if (pushed) wait_vm<NWR>(); else wait_vm<0>();
             }
-            asm volatile("" : "+v"(ov));   // no use of ov may move above the first wait
+#pragma unroll
+            for (int i = 0; i < CW / 4; ++i) asm volatile("" : "+v"(ob[i]));   // no use may move above the first wait
             if (AHEAD == 1 && j + 1 < mine) issue(ht.tile_a(j + 1), (j + 1) & 1);
             const uint4* tile = buf[q][j & 1];
             uint4 x[LPL];
 #pragma unroll
             for (int i = 0; i < LPL; ++i) {
-                const uint32_t leaf = ((i < 4 ? ov.x : ov.y) >> (8 * (i & 3))) & 255u;
-                x[i] = tile[(int)leaf * QC + cc];
+                const uint32_t leaf = (ob[i / 4] >> (8 * (i & 3))) & 255u;
+                x[i] = tile[(int)leaf * CW + cc];
             }
 #pragma unroll
             for (int s2 = 1; s2 < LPL; s2 *= 2)
 #pragma unroll
                 for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
 #pragma unroll
-            for (int m = 8; m < 64; m *= 2) x[0] = add8(x[0], shfl_xor4(x[0], m));
-            const uint4 pr = shfl4(x[0], cc);   // leaf group 0's sum: k_hier_ll's operand order
+            for (int m = CW; m < 64; m *= 2) x[0] = add8(x[0], shfl_xor4(x[0], m));
+            const uint4 pr = CW == 32 ? x[0] : shfl4(x[0], cc);   // leaf group 0's sum: k_hier_ll's operand order
             const uint64_t t = ht.tile_a(j);
             const int o = ht.owner_of(t);
             if (o == me && ko < kWsRing) {
@@ -872,10 +897,12 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
                 if (lane == 0) __hip_atomic_store(&prod[q], (uint32_t)(ko + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 pushed = false;
             } else {
-                const uint64_t slot = (t - (uint64_t)o * ht.tpo) * W + me;
-                if (g < 3)
-                    __hip_atomic_store(lp.ll[o] + slot * kHSlot + woff, h_pack(pr, wk, e8), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                uint64_t* const slot = lp.ll[o] + ((t - (uint64_t)o * ht.tpo) * W + me) * kHSlot;
+#pragma unroll
+                for (int r = 0; r < NWR; ++r)
+                    if (wvalid(r))
+                        __hip_atomic_store(slot + woff(r), h_pack(pr, wkey(r), e8), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
                 pushed = true;
             }
             if (o == me) ++ko;
@@ -883,21 +910,33 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
         }
         return;
     }
-    // ---- B: quarter q of the tiles' rank rows
+    // ---- B: columns CW q .. CW q + CW - 1 of the tiles' rank rows
     uint64_t* const my_ll = lp.ll[me];
     auto owned = [&](int j) { return ht.owner_of(ht.tile_a(j)) == me; };
     auto next = [&](int j, bool own) {
         while (j < mine && owned(j) != own) ++j;
         return j;
     };
-    auto rows_out = [&](uint64_t t, uint4 v) {   // rows 8k + g, column 8q + cc
+    auto rows_out = [&](uint64_t t, uint4 v) {   // rows GR k + g, column CW q + cc
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(8 * k + g) * stride) + t * TV + 8 * q + cc, v);
+        for (int k = 0; k < OPS; ++k)
+            st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)(GR * k + g) * stride) + t * TV + CW * q + cc, v);
     };
-    // the column of this lane from the three words lanes cc, 8 + cc, 16 + cc polled
-    auto gather = [&](uint64_t wd) {
-        const uint64_t a[3] = {shfl64(wd, cc), shfl64(wd, 8 + cc), shfl64(wd, 16 + cc)};
+    auto poll = [&](const uint64_t* slot, uint64_t (&wd)[NWR]) {
+#pragma unroll
+        for (int r = 0; r < NWR; ++r)
+            wd[r] = wvalid(r) ? __hip_atomic_load(slot + woff(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+    };
+    auto fresh = [&](const uint64_t (&wd)[NWR]) {
+        bool f = true;
+#pragma unroll
+        for (int r = 0; r < NWR; ++r) f = f && (!wvalid(r) || (uint32_t)(wd[r] >> 48) == e8);
+        return f;
+    };
+    // the column of this lane from its three words: word k sits in round (k CW) / 64, lane (k CW) % 64 + cc
+    auto gather = [&](const uint64_t (&wd)[NWR]) {
+        const uint64_t a[3] = {shfl64(wd[0], cc), shfl64(wd[CW / 64], (CW % 64) + cc),
+                               shfl64(wd[(2 * CW) / 64], ((2 * CW) % 64) + cc)};
         return h_unpack(a);
     };
     int jo = next(0, true), jx = next(0, false), ko = 0;
@@ -906,27 +945,20 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
         const uint64_t to = ht.tile_a(jo < mine ? jo : 0), tx = ht.tile_a(jx < mine ? jx : 0);
         const uint64_t li = to - (uint64_t)me * tiles_per_owner;
         const bool own_lds = ko < kWsRing;
-        // one round: every word both cursors need, in flight at once (lanes 0-23, one word each)
-        uint64_t wr[kLLMaxGpus] = {}, wb = 0;
-        if (g < 3) {
-            if (jo < mine) {
+        // one round: every word both cursors need, in flight at once
+        uint64_t wr[kLLMaxGpus][NWR] = {}, wb[NWR] = {};
+        if (jo < mine) {
 #pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W && (src != me || !own_lds))
-                        wr[src] = __hip_atomic_load(my_ll + (li * W + src) * kHSlot + woff, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-            if (jx < mine)
-                wb = __hip_atomic_load(my_ll + box_words + tx * kHSlot + woff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W && (src != me || !own_lds)) poll(my_ll + (li * W + src) * kHSlot, wr[src]);
         }
+        if (jx < mine) poll(my_ll + box_words + tx * kHSlot, wb);
         bool moved = false;
         if (jo < mine) {
             bool f = !own_lds || __hip_atomic_load(&prod[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > (uint32_t)ko;
-            if (g < 3) {
 #pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W && (src != me || !own_lds)) f = f && (uint32_t)(wr[src] >> 48) == e8;
-            }
+            for (int src = 0; src < kLLMaxGpus; ++src)
+                if (src < W && (src != me || !own_lds)) f = f && fresh(wr[src]);
             if (__all(f)) {
                 asm volatile("" ::: "memory");   // the slot read stays behind the count read
                 uint4 y[kLLMaxGpus];
@@ -937,13 +969,16 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
                     else y[src] = gather(wr[src]);
                 }
                 const uint4 val = owner_sum(y, W, me);
-                if (g < 3) {
 #pragma unroll
-                    for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                        if (dst < W && dst != me)
-                            __hip_atomic_store(lp.ll[dst] + box_words + to * kHSlot + woff, h_pack(val, wk, e8),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                }
+                for (int dst = 0; dst < kLLMaxGpus; ++dst)
+                    if (dst < W && dst != me) {
+                        uint64_t* const box = lp.ll[dst] + box_words + to * kHSlot;
+#pragma unroll
+                        for (int r = 0; r < NWR; ++r)
+                            if (wvalid(r))
+                                __hip_atomic_store(box + woff(r), h_pack(val, wkey(r), e8), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
                 rows_out(to, val);
                 ++ko;
                 jo = next(jo + 1, true);
@@ -951,8 +986,7 @@ __global__ __launch_bounds__(512, 4) void k_hier_ws(uint16_t* __restrict__ ranks
             }
         }
         if (jx < mine) {
-            const bool f = g >= 3 || (uint32_t)(wb >> 48) == e8;
-            if (__all(f)) {
+            if (__all(fresh(wb))) {
                 rows_out(tx, gather(wb));
                 jx = next(jx + 1, false);
                 moved = true;
@@ -1633,8 +1667,12 @@ int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
     // 2 per CU (8 waves each): the whole grid resident (max_grid < 512 when processes share the GPU)
     const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    hipLaunchKernelGGL(tune(Tune::hier_ws_ahead) == 2 ? k_hier_ws<2> : k_hier_ws<1>, dim3(grid), dim3(512), 0,
-                       (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
+    const bool a2 = tune(Tune::hier_ws_ahead) == 2;
+    const int cw = tune(Tune::hier_ws_cols) >= 32 ? 32 : tune(Tune::hier_ws_cols) >= 16 ? 16 : 8;
+    decltype(&k_hier_ws<1, 8>) kern = cw == 32 ? (a2 ? k_hier_ws<2, 32> : k_hier_ws<1, 32>)
+                                      : cw == 16 ? (a2 ? k_hier_ws<2, 16> : k_hier_ws<1, 16>)
+                                                 : (a2 ? k_hier_ws<2, 8> : k_hier_ws<1, 8>);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(128 * (32 / cw)), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
                        ntiles, ntiles / nranks, box_words, epoch, status);
     return peer_last_error();
 }

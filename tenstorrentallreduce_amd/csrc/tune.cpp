@@ -49,6 +49,7 @@ const Key kKeys[] = {
     {"hier_x_latepoll", 1, 0, 1},     // k_hier_x / k_hier_x2 (LL, lag 1): 1 the earlier bucket's results polled after tile 0's tree
     {"peer_fence", 0, 0, 1},          // peer kernels: 1 system-scope release / acquire fences around every cross-GPU hand-off
     {"hier_ws_ahead", 1, 1, 2},       // k_hier_ws: the reducing waves' loads 1 | 2 tiles ahead
+    {"hier_ws_cols", 16, 8, 32},      // k_hier_ws: 16-byte columns per reducing wave, 8 (quarters) | 16 (halves) | 32 (whole tiles)
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

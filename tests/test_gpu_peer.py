@@ -149,7 +149,9 @@ def worker(rank, world, port, q, devs=None, tunes=None):
                                                      # partials past its 16 LDS slots go through the own inbox
                                                      ("hier_ws", 0, 2, 0), ("hier_ws_capped", 0, 2, 2),
                                                      ("hier_launches_then_ws", 0, 0, 0), ("hier_ws_again", 0, 2, 0),
-                                                     ("hier_ws_ring", 0, 2, 1, 20),
+                                                     ("hier_ws_ring", 0, 2, 1, 20), ("hier_ws_c8", 0, 2, 0),
+                                                     ("hier_ws_c8_ring", 0, 2, 1, 20), ("hier_ws_c32", 0, 2, 0),
+                                                     ("hier_ws_c32_ring", 0, 2, 1, 20),
                                                      ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
                                                      ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
@@ -182,7 +184,8 @@ def worker(rank, world, port, q, devs=None, tunes=None):
                         peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
                                                  torch.cuda.current_stream())
                 else:
-                    peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+                    with t.tuned(hier_ws_cols=8 if "_c8" in mode else 32 if "_c32" in mode else 16):
+                        peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
                 with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
@@ -382,17 +385,20 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
-        for ll, limit in ((1, 0), (0, 1 << 40), (2, 0), (0, 0), (1, 0), (2, 0), (0, 1 << 40), (1, 0), (2, 0)):
+        # (hier_ll, oneshot limit, k_hier_ws columns per reducing wave)
+        for ll, limit, cols in ((1, 0, 8), (0, 1 << 40, 8), (2, 0, 8), (2, 0, 16), (2, 0, 32), (0, 0, 8), (1, 0, 8),
+                                (2, 0, 16), (2, 0, 32), (0, 1 << 40, 8), (1, 0, 8), (2, 0, 8)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
             torch.cuda.synchronize()
-            for b in bufs:   # back to back: both LL parities / epochs
-                peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
+            with t.tuned(hier_ws_cols=cols):
+                for b in bufs:   # back to back: both LL parities / epochs
+                    peer.allreduce(b.data_ptr(), n, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
             torch.cuda.synchronize()
             for rep, (b, (_, want)) in enumerate(zip(bufs, cases)):
                 bad = int((b.cpu().numpy().view(np.uint16) != want[None, :]).sum())
-                assert bad == 0, (ll, limit, rep, bad)
+                assert bad == 0, (ll, limit, cols, rep, bad)
         assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.set_hier_ll(0)

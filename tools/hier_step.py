@@ -28,7 +28,10 @@ peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
 arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ll": (0, 1), "hier_ws": (0, 2),
-        "hier_ws_a2": (0, 2)}   # hier_ws_a2: tune hier_ws_ahead=2
+        "hier_ws_a2": (0, 2), "hier_ws_c8": (0, 2), "hier_ws_c8_a2": (0, 2),
+        "hier_ws_c32": (0, 2), "hier_ws_c32_a2": (0, 2)}
+# hier_ws_a2: tune hier_ws_ahead=2; _c8 / _c32: hier_ws_cols=8 / 32 (quarter / whole tiles per reducing wave;
+# default 16: halves)
 # pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _ch: the
 # chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned sums before the
 # last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last tile's row
@@ -81,6 +84,7 @@ for _ in range(rounds):
         peer.set_oneshot_max(limit)
         peer.set_hier_ll(ll)
         t.tune("hier_ws_ahead", 2 if name.endswith("_a2") else 1)
+        t.tune("hier_ws_cols", 8 if "_c8" in name else 32 if "_c32" in name else 16)
         for i in range(20):
             peer.allreduce(sets[i % NS].data_ptr(), n, s, P, 8, t.SWING, ws.data_ptr())
         torch.cuda.synchronize()
