@@ -974,7 +974,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #               mem_2D exchange over the peer windows (k_peer_oneshot)
     #   peer_hier_ws  ONE kernel: tree -> mem_2D across GPUs -> broadcast, every cross-GPU
     #                 hand-off an LL push; reducing and writing waves in every workgroup
-    #                 (k_hier_ws: 15.0 us at W = 1 against k_hier_ll's 16.2, which is not a candidate)
+    #                 (k_hier_ws: 14.6 us at W = 1 against k_hier_ll's 16.2, which is not a candidate)
     #   peer_hier_xr  the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
     #                 reads bucket i+1 while it writes bucket i; the last flush is timed), R(cur)
     #                 ahead of bucket i-1's last row stores (hier_x_rearly)

@@ -589,7 +589,7 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
 /* 0 = off (tree, the mem_2D exchange, broadcast as launches), 1 = k_hier_ll
  * (all tiles read, owned tiles summed, all tiles written: three phases),
  * 2 = k_hier_ws (round 5: the same hand-offs with reducing and writing waves
- * in every workgroup, so each CU reads and writes at once: 15.0 vs 16.2 us at
+ * in every workgroup, so each CU reads and writes at once: 14.6 vs 16.2 us at
  * W = 1); other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
  * profiles/README.md — the per-tile flag form k_hier_oneshot, 19.9 us at
  * W = 1, and the pipelined LL form k_hier_pipe, 17.8 us, in round 5; the
