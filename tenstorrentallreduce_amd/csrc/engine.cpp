@@ -956,7 +956,8 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     // (tree_order[0]), so a column chunk of every rank is an allreduce of its own —
     // H2D(c + 1) | pass(c) | D2H(c - 1) on three streams, each copy a 2D DMA straight into /
     // out of the skewed device layout (no staging pass); same bits as the whole-bucket pass.
-    // ALLRED_E2E_CHUNKS=c equal chunks, default 8 (1 = one copy each way around one pass).
+    // ALLRED_E2E_CHUNKS=c equal chunks (1 = one copy each way around one pass); unset: 8, where the
+    // box's strided copies keep the rate of plain ones (probed below), else 1.
     // Each 2D copy costs ~10 us over its bytes (measured: 8 chunks 1.09 ms, 16 1.19, 32 1.5,
     // a 1-2-4-9-9-4-2-1 32nds ramp 1.18; profiles/r05_e2e_probe.json)
     std::vector<size_t> csz;
@@ -967,7 +968,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         if (n % k == 0 && (n / k) % col_unit == 0) csz.assign(k, n / k);
     }
     const int chunks = (int)csz.size();
-    const bool chunked = !zero_copy && chunks > 1 && variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED &&
+    bool chunked = !zero_copy && chunks > 1 && variant == ALLRED_BO && a->exec == ALLRED_EXEC_FUSED &&
                          !profile_log;
     std::vector<std::pair<size_t, allred_plan*>> cplans;   // one plan per distinct chunk size
     auto chunk_plan = [&](size_t len) -> allred_plan* {
@@ -976,6 +977,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         return nullptr;
     };
     hipStream_t sh = nullptr, sd = nullptr;
+    hipEvent_t p[4] = {};   // the 2D / 1D copy-rate probe
     std::vector<hipEvent_t> cev;   // per chunk: H2D done, pass start, pass done
     if (a->seed < 0) {
         allred_constant_bf16_vector(bytes, 1.0f, src0.data());
@@ -1020,6 +1022,28 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     if (a->run_kernel)
         for (auto& cp : cplans) ST(allred_plan_execute(cp.second, d_scratch, stride, d_ws, s));
     HIPCK(hipStreamSynchronize(s));
+    if (chunked && !std::getenv("ALLRED_E2E_CHUNKS")) {
+        // (untimed) the chunks pay only where a strided (2D) copy keeps the rate of a plain one: on
+        // some boxes a 2D device-to-host copy into the rank-major host buckets runs at ~23 GB/s
+        // against ~52 for a 1D copy (8 chunks 2.1-2.2 ms there, one copy each way 1.55;
+        // profiles/r05_e2e_probe.json) — then the buckets go as one copy each way.  Each copy
+        // twice, the second timed (a first copy pays one-time costs)
+        float t2d = 0, t1d = 0;
+        for (auto& e : p) HIPCK(hipEventCreate(&e));
+        const size_t cb = csz[0] * 2 * (size_t)N;
+        HIPCK(hipMemcpy2DAsync(h_out, n * 2, d_scratch, stride * 2, csz[0] * 2, (size_t)N, hipMemcpyDeviceToHost, sd));
+        HIPCK(hipEventRecord(p[0], sd));
+        HIPCK(hipMemcpy2DAsync(h_out, n * 2, d_scratch, stride * 2, csz[0] * 2, (size_t)N, hipMemcpyDeviceToHost, sd));
+        HIPCK(hipEventRecord(p[1], sd));
+        HIPCK(hipMemcpyAsync(h_out, d_stage, cb, hipMemcpyDeviceToHost, sd));
+        HIPCK(hipEventRecord(p[2], sd));
+        HIPCK(hipMemcpyAsync(h_out, d_stage, cb, hipMemcpyDeviceToHost, sd));
+        HIPCK(hipEventRecord(p[3], sd));
+        HIPCK(hipStreamSynchronize(sd));
+        HIPCK(hipEventElapsedTime(&t2d, p[0], p[1]));
+        HIPCK(hipEventElapsedTime(&t1d, p[2], p[3]));
+        if (t2d > 1.5f * t1d) chunked = false;
+    }
     if (chunked) {
         // timed: chunk c's H2D on sh, its pass on s behind it, its D2H on sd behind the
         // pass; the two PCIe directions and the passes overlap across chunks
@@ -1116,6 +1140,8 @@ done:
     if (sh) (void)hipStreamSynchronize(sh);
     if (sd) (void)hipStreamSynchronize(sd);
     for (hipEvent_t e : cev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : p)
         if (e) (void)hipEventDestroy(e);
     if (sh) (void)hipStreamDestroy(sh);
     if (sd) (void)hipStreamDestroy(sd);
