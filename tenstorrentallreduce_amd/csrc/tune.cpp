@@ -66,6 +66,7 @@ int find(const char* key) {
 bool set(int i, int64_t v) {
     if (v < kKeys[i].lo || v > kKeys[i].hi) return false;
     if (i == (int)Tune::steps_groups && (v == 1 || v == 2)) return false;   // 0 auto, 3, 4, 5 only
+    if (i == (int)Tune::hier_ws_cols && v != 8 && v != 16 && v != 32) return false;   // quarters, halves, whole tiles
     g_val[i].store(v, std::memory_order_relaxed);
     return true;
 }

@@ -142,6 +142,16 @@ def test_tune_entry_point():
         assert t.tune("peer_fence") == 1
     with pytest.raises(t.AllredError):
         t.tune("peer_fence", 2)
+    # k_hier_ws: half tiles per reducing wave by default (8 / 16 / 32 columns only), loads one
+    # tile ahead (1 / 2)
+    assert (t.tune("hier_ws_cols"), t.tune("hier_ws_ahead")) == (16, 1)
+    for v in (8, 32):
+        with t.tuned(hier_ws_cols=v):
+            assert t.tune("hier_ws_cols") == v
+    for key, bad in (("hier_ws_cols", 12), ("hier_ws_cols", 64), ("hier_ws_ahead", 0), ("hier_ws_ahead", 3)):
+        with pytest.raises(t.AllredError):
+            t.tune(key, bad)
+    assert t.tune("hier_ws_cols") == 16
 
 
 def test_mem_program_stats_one_rank_has_no_launch():
