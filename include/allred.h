@@ -588,9 +588,11 @@ int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
  * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
 /* 0 = off (tree, the mem_2D exchange, broadcast as launches), 1 = k_hier_ll
  * (all tiles read, owned tiles summed, all tiles written: three phases),
- * 2 = k_hier_ws (round 5: the same hand-offs with reducing and writing waves
- * in every workgroup, so each CU reads and writes at once: 14.6 vs 16.2 us at
- * W = 1); other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
+ * 2 = k_hier_ws (round 5, the default: the same hand-offs with reducing and
+ * writing waves in every workgroup, so each CU reads and writes at once: 14.6
+ * vs 16.2 us at W = 1; buckets the one-launch forms cannot take — not a
+ * multiple of 256 x nranks elements, nranks > 8, larger than the hand-off
+ * area — run the launch form); other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
  * profiles/README.md — the per-tile flag form k_hier_oneshot, 19.9 us at
  * W = 1, and the pipelined LL form k_hier_pipe, 17.8 us, in round 5; the
  * specialised-wave form of round 1, 27-38 us.) */

@@ -476,8 +476,8 @@ class Peer:
     def set_hier_ll(self, mode) -> None:
         """64 local ranks: the hierarchical step with LL push hand-offs — 1 (or
         True) k_hier_ll (read / sum / write phases in one launch), 2 k_hier_ws
-        (one launch, reducing and writing waves in every workgroup), 0 (or
-        False) the launch form.  Same result bits every way."""
+        (one launch, reducing and writing waves in every workgroup; the
+        default), 0 (or False) the launch form.  Same result bits every way."""
         check(lib.allred_peer_set_hier_ll(self._h, int(mode)), "peer_set_hier_ll")
 
     def set_lo_ll_max(self, nbytes: int) -> None:

@@ -69,7 +69,7 @@ struct allred_peer {
     // range oldest (every call rewrites tiles [0, its tiles)); hier_area_prepare reads it
     std::vector<std::pair<uint64_t, uint32_t>> hl_stairs[2];
     uint64_t hl_clears = 0;         // barrier-protected clears of a parity's area so far
-    int hier_ll = 0;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs), 2 k_hier_ws
+    int hier_ll = 2;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs), 2 k_hier_ws
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll

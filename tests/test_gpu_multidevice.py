@@ -257,7 +257,8 @@ def test_rccl_pipelined_across_gpus(world):
 def test_peer_mem_and_hier_forms_across_gpus(world, tunes):
     """tests/test_gpu_peer.py's worker with one process per device: mem_2D
     (launches, k_peer_oneshot, k_peer_mem_ll), the hierarchical forms (k_hier_ll,
-    the launch form, k_hier_x / k_hier_x2 in every placement, capped grids)."""
+    k_hier_ws over quarter / half / whole tiles, the launch form, k_hier_x /
+    k_hier_x2 in every placement, capped grids)."""
     tgp.run_world(tgp.worker, world, 300, devs=devices(world), tunes=tunes)
 
 
