@@ -269,6 +269,44 @@ def bench_single(args) -> dict:
     torch.cuda.synchronize()
     hot_ms = e0.elapsed_time(e1) / args.steps
 
+    alg_bytes_hier = 2 * RANKS * ELEMS * 2
+    # the N > 1 path's per-GPU step on this GPU alone (a one-rank peer set, W = 1): the
+    # hierarchical step in one launch (k_hier_ws, the library default) and two buckets deep
+    # (k_hier_x2: K buckets in K + 1 launches), same buckets, eager; no cross-GPU bytes at W = 1
+    hier = {}
+    try:
+        peer = t.Peer(1, 0, 0, 2 * ELEMS)
+        peer.connect([peer.handle()])
+        ws_h = torch.empty(ELEMS, dtype=torch.int16, device=dev)
+        # 8 rotating buckets of 64 contiguous rank rows (the peer calls' layout; 336 MB > the Infinity Cache)
+        hsets = [torch.randint(0x3F80, 0x42C8, (RANKS, ELEMS), dtype=torch.int16, device=dev) for _ in range(8)]
+        try:
+            def one(i):
+                peer.allreduce(hsets[i % 8].data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_h.data_ptr())
+
+            def deep(k):
+                for i in range(k):
+                    peer.allreduce_pipelined2(hsets[i % 8].data_ptr(), ELEMS, stream)
+                peer.allreduce_pipelined2(None, ELEMS, stream)
+
+            for name, run_k in (("k_hier_ws", lambda k: [one(i) for i in range(k)]), ("k_hier_x2", deep)):
+                with torch.cuda.stream(stream):
+                    run_k(5)
+                torch.cuda.synchronize()
+                e0.record(stream)
+                with torch.cuda.stream(stream):
+                    run_k(args.steps)
+                e1.record(stream)
+                torch.cuda.synchronize()
+                us = e0.elapsed_time(e1) * 1e3 / args.steps
+                hier[name] = {"us_per_step": round(us, 3), "hbm_frac": round(alg_bytes_hier / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)}
+            hier["peer_status"] = peer.status()
+        finally:
+            peer.close()
+            del hsets
+    except Exception as e:  # reported, never silently dropped
+        hier["error"] = repr(e)
+
     # host-staged end to end (buckets start and end in pinned host memory), the
     # reference program surface: H2D of all 64 buckets + allreduce + D2H, one DMA
     # each way ("dma"), or the fused kernel reading / writing the pinned host
@@ -372,6 +410,8 @@ def bench_single(args) -> dict:
         "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
                               "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
+        "hierarchical_step_w1": dict(hier, note="the N > 1 transports' per-GPU kernel on this GPU alone (one-rank peer "
+                                     "set): tree of the 64 ranks, mem_2D hand-off, broadcast; eager launches"),
         "host_staged": e2e,
         "config1": config1,
         "tilesum": tsum,
