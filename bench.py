@@ -1015,9 +1015,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #   peer_hier_ws  ONE kernel: tree -> mem_2D across GPUs -> broadcast, every cross-GPU
     #                 hand-off an LL push; reducing and writing waves in every workgroup
     #                 (k_hier_ws: 14.6 us at W = 1 against k_hier_ll's 16.2, which is not a candidate)
-    #   peer_hier_xr  the same hand-offs, consecutive buckets pipelined (k_hier_x: one launch
-    #                 reads bucket i+1 while it writes bucket i; the last flush is timed), R(cur)
-    #                 ahead of bucket i-1's last row stores (hier_x_rearly)
+    #   (peer_hier_x / peer_hier_xr: the same hand-offs one bucket deep, k_hier_x — runnable
+    #                 here, not candidates since round 5: 15.2-15.3 us at W = 1, behind k_hier_x2
+    #                 (15.1, which also hides more of the xGMI trip) and k_hier_ws (14.5))
     #   peer_hier_x2t2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
     #                 owned tiles before its last row stores, writes bucket i-2; every poll waits
     #                 for the previous launch)
@@ -1251,7 +1251,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         # forms must equal bit for bit on random data
         check("peer_launches", 9090)
         comparator["peer_launches"] = verify.pop("peer_launches")
-        relaxed = ("peer_swing", "peer_mem_x", "peer_hier_ws", "peer_hier_xr", *X2_KINDS)
+        relaxed = ("peer_swing", "peer_mem_x", "peer_hier_ws", *X2_KINDS)
         passed = []
         for i, kind in enumerate(relaxed):
             if check(kind, 9100 + 10 * i):
