@@ -90,7 +90,6 @@ def main():
     out = [q.get(timeout=300) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    res = dict(out)
     r0 = [r for r in out if r[0] == 0][0][1]
     print(json.dumps({"world": world, "steps": steps, "us_per_step_max_over_ranks": r0,
                       "median": {k: statistics.median(v) for k, v in r0.items()},
