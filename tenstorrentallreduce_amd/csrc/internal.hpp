@@ -42,7 +42,7 @@ enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
     lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
     rccl_fault, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll, peer_fence,
-    hier_ws_ahead, hier_ws_cols, hier_ws_backoff, count
+    hier_ws_ahead, hier_ws_cols, count
 };
 int64_t tune(Tune key);
 

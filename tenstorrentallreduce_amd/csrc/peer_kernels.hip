@@ -814,7 +814,7 @@ constexpr int kWsRing = 16;
 template <int AHEAD, int CW>
 __global__ __launch_bounds__(128 * (32 / CW), (CW == 8 ? 4 : CW == 16 ? 2 : 1)) void k_hier_ws(
     uint16_t* __restrict__ ranks, uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
-    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words, uint32_t epoch, uint32_t* status, int backoff) {
+    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words, uint32_t epoch, uint32_t* status) {
     constexpr int TV = 32, NQ = TV / CW, GR = 64 / CW, LPL = CW, OPS = CW;
     constexpr int NWR = (3 * CW + 63) / 64;   // word rounds: a tile's 3 CW hand-off words of this wave's columns
     static_assert(CW == 8 || CW == 16 || CW == 32, "a quarter, a half or the whole tile per reducing wave");
@@ -941,7 +941,6 @@ __global__ __launch_bounds__(128 * (32 / CW), (CW == 8 ? 4 : CW == 16 ? 2 : 1)) 
     };
     int jo = next(0, true), jx = next(0, false), ko = 0;
     uint64_t spin = 0, t0 = 0;
-    int idle = 0;   // rounds in a row with nothing arrived (backoff > 0: longer sleeps between uncached polls)
     while (jo < mine || jx < mine) {
         const uint64_t to = ht.tile_a(jo < mine ? jo : 0), tx = ht.tile_a(jx < mine ? jx : 0);
         const uint64_t li = to - (uint64_t)me * tiles_per_owner;
@@ -993,18 +992,9 @@ __global__ __launch_bounds__(128 * (32 / CW), (CW == 8 ? 4 : CW == 16 ? 2 : 1)) 
                 moved = true;
             }
         }
-        if (moved) {
-            idle = 0;
-        } else {
+        if (!moved) {
             if (peer_give_up(spin++, t0, status)) break;
-            // a round that polled only the LDS count sleeps briefly; one that polled global words
-            // (other GPUs' partials or results) backs off, so waiting waves do not stream uncached
-            // polls through HBM beside the reducing waves' tile loads
-            const bool global = jx < mine || (jo < mine && (W > 1 || ko >= kWsRing));
-            if (!backoff || !global || idle < 2) __builtin_amdgcn_s_sleep(1);
-            else if (idle < 6) __builtin_amdgcn_s_sleep(8);
-            else __builtin_amdgcn_s_sleep(32);
-            ++idle;
+            __builtin_amdgcn_s_sleep(1);
         }
     }
 }
@@ -1683,7 +1673,7 @@ int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
                                       : cw == 16 ? (a2 ? k_hier_ws<2, 16> : k_hier_ws<1, 16>)
                                                  : (a2 ? k_hier_ws<2, 8> : k_hier_ws<1, 8>);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(128 * (32 / cw)), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
-                       ntiles, ntiles / nranks, box_words, epoch, status, (int)tune(Tune::hier_ws_backoff));
+                       ntiles, ntiles / nranks, box_words, epoch, status);
     return peer_last_error();
 }
 

@@ -50,7 +50,6 @@ const Key kKeys[] = {
     {"peer_fence", 0, 0, 1},          // peer kernels: 1 system-scope release / acquire fences around every cross-GPU hand-off
     {"hier_ws_ahead", 1, 1, 2},       // k_hier_ws: the reducing waves' loads 1 | 2 tiles ahead
     {"hier_ws_cols", 16, 8, 32},      // k_hier_ws: 16-byte columns per reducing wave, 8 (quarters) | 16 (halves) | 32 (whole tiles)
-    {"hier_ws_backoff", 0, 0, 1},     // k_hier_ws: 1 idle writing waves poll other GPUs' words at a falling rate
 };
 constexpr int kCount = (int)(sizeof(kKeys) / sizeof(kKeys[0]));
 static_assert(kCount == (int)Tune::count, "kKeys and enum Tune disagree");

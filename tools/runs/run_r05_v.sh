@@ -6,5 +6,5 @@ out=gpurun_out/r05v
 mkdir -p $out
 for w in 2 4 8; do
   timeout -k 10 300 python tools/hier_share_probe.py $w 40 3 > $out/share_$w.json 2> $out/share_$w.err || exit 1
-  python3 -c "import json; d=json.load(open('$out/share_$w.json')); print($w, d['median'], d['peer_status'])"
+  python3 -c "import json; d=json.loads(open('$out/share_$w.json').read().strip().splitlines()[-1]); print($w, d['median'], d['peer_status'])"
 done
