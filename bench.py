@@ -26,14 +26,18 @@ Rank 0 prints ONE JSON line.  See DESIGN.md §Measurement for every field.
 """
 from __future__ import annotations
 
-import argparse
-import json
-import os
-import statistics
-import subprocess
-import sys
-import threading
 import time
+
+_T0 = time.perf_counter()   # the N > 1 budget counts from here (imports included: the driver's clock does)
+
+import argparse  # noqa: E402
+import contextlib  # noqa: E402
+import json
+import os  # noqa: E402
+import statistics  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+import threading  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -240,6 +244,7 @@ def bench_single(args) -> dict:
     rep_ms = [ev[r].elapsed_time(ev[r + 1]) for r in range(reps)]
     ms_per_step = statistics.median(rep_ms) / args.steps
     e0, e1 = ev[0], ev[1]
+    fused_launch = t.last_launch()   # the bench kernel's grid and residency (launched in the warmup)
 
     bytes_all = RANKS * ELEMS * 2
     steps_ms = hot_ms = float("nan")
@@ -248,17 +253,11 @@ def bench_single(args) -> dict:
         steps_plan.close()
         return {"ms_per_step": ms_per_step, "value": bytes_all / (ms_per_step * 1e-3) / 1e9}
 
-    # schedule form (k_steps_reg: every RS / AG step of every rank in ONE persistent launch), same buckets, eager
-    with torch.cuda.stream(stream):
-        for i in range(3):
-            step(i, steps_plan)
-    torch.cuda.synchronize()
-    e0.record(stream)
-    for i in range(args.steps):
-        step(i, steps_plan)
-    e1.record(stream)
-    torch.cuda.synchronize()
-    steps_ms = e0.elapsed_time(e1) / args.steps
+    # schedule form (k_steps_reg: every RS / AG step of every rank in ONE persistent launch), same
+    # buckets, timed like the headline's eager path: behind a spin kernel, R repetitions, median
+    sched = timed_eager(stream, lambda: [step(i, steps_plan) for i in range(args.steps)], args.steps, reps)
+    sched["launch"] = t.last_launch()
+    steps_ms = sched["us_per_step"] * 1e-3
 
     # cache-resident (one bucket set, 40 MiB stays in the Infinity Cache)
     with torch.cuda.stream(stream):
@@ -290,16 +289,19 @@ def bench_single(args) -> dict:
                 peer.allreduce_pipelined2(None, ELEMS, stream)
 
             for name, run_k in (("k_hier_ws", lambda k: [one(i) for i in range(k)]), ("k_hier_x2", deep)):
-                with torch.cuda.stream(stream):
-                    run_k(5)
+                with torch.cuda.stream(stream):   # warm: the headline's kernels ran last; >= 50 steps of this one
+                    run_k(max(50, args.steps))
                 torch.cuda.synchronize()
-                e0.record(stream)
+                # timed like the headline's eager path (behind a spin kernel that outlasts the host's
+                # submission, R repetitions of K steps, the median; the pipelined form's finishing
+                # launch inside every repetition); the grid the launcher chose and its residency beside it
                 with torch.cuda.stream(stream):
-                    run_k(args.steps)
-                e1.record(stream)
+                    r = timed_eager(stream, lambda: run_k(args.steps), args.steps, reps)
+                    run_k(1)   # one more call: its launch is the one reported (a k_hier_x2 start, not a flush)
+                r["launch"] = t.last_launch()
                 torch.cuda.synchronize()
-                us = e0.elapsed_time(e1) * 1e3 / args.steps
-                hier[name] = {"us_per_step": round(us, 3), "hbm_frac": round(alg_bytes_hier / (us * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)}
+                r["hbm_frac"] = round(alg_bytes_hier / (r["us_per_step"] * 1e-6) / 1e9 / HBM_PEAK_GBPS, 4)
+                hier[name] = r
             hier["peer_status"] = peer.status()
         finally:
             peer.close()
@@ -406,12 +408,13 @@ def bench_single(args) -> dict:
                    "exec": "fused", "launches_per_step": plan.launches, "hip_graph": graph is not None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": pmc_traffic(FUSED_KERNEL),
-                     "kernel": FUSED_KERNEL, "algorithmic_bytes_per_launch": alg_bytes},
+                     "kernel": FUSED_KERNEL, "algorithmic_bytes_per_launch": alg_bytes, "launch": fused_launch},
         "schedule_faithful": {"launches_per_step": steps_plan.launches, "ms_per_step": round(steps_ms, 6),
-                              "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3)},
+                              "value": round(bytes_all / (steps_ms * 1e-3) / 1e9, 3), **sched},
         "cache_resident": {"ms_per_step": round(hot_ms, 6), "value": round(bytes_all / (hot_ms * 1e-3) / 1e9, 3)},
         "hierarchical_step_w1": dict(hier, note="the N > 1 transports' per-GPU kernel on this GPU alone (one-rank peer "
-                                     "set): tree of the 64 ranks, mem_2D hand-off, broadcast; eager launches"),
+                                     "set): tree of the 64 ranks, mem_2D hand-off, broadcast; eager launches behind a "
+                                     "spin kernel, median of R repetitions of K steps"),
         "host_staged": e2e,
         "config1": config1,
         "tilesum": tsum,
@@ -446,6 +449,55 @@ def timed_max(fn, reps, stream, after=None) -> float:
     return m.item()
 
 
+_SPIN_RATE = []
+
+
+def spin_cycles_per_us(stream) -> float:
+    """torch.cuda._sleep's cycles per microsecond on this GPU (measured once)"""
+    if not _SPIN_RATE:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(stream):
+            torch.cuda._sleep(10000)
+            e0.record(stream)
+            torch.cuda._sleep(4000000)
+            e1.record(stream)
+        torch.cuda.synchronize()
+        _SPIN_RATE.append(4000000 / max(1e-3, e0.elapsed_time(e1) * 1e3))
+    return _SPIN_RATE[0]
+
+
+def timed_eager(stream, run_rep, steps: int, reps: int) -> dict:
+    """A secondary kernel timed like the headline's eager path: R repetitions of
+    run_rep() (K steps, eager launches on `stream`) behind ONE spin kernel sized
+    from a measured host submission rate so that it outlasts the host's queueing
+    of every repetition, a HIP event between consecutive repetitions;
+    us_per_step = the median repetition / K, with every repetition and the
+    spread.  spin_covered_submission false = the host was still queueing when
+    the GPU reached the timed region (then the numbers include host gaps)."""
+    torch.cuda.synchronize()
+    h0 = time.perf_counter()
+    with torch.cuda.stream(stream):
+        run_rep()   # untimed: the host's cost of queueing one repetition
+    host_s = time.perf_counter() - h0
+    torch.cuda.synchronize()
+    spin_us = 3.0 * host_s * 1e6 * reps + 500.0
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(int(spin_us * spin_cycles_per_us(stream)))
+        ev[0].record(stream)
+        h0 = time.perf_counter()
+        for r in range(reps):
+            run_rep()
+            ev[r + 1].record(stream)
+        submit_s = time.perf_counter() - h0
+    torch.cuda.synchronize()
+    per = [ev[r].elapsed_time(ev[r + 1]) * 1e3 / steps for r in range(reps)]
+    return {"us_per_step": round(statistics.median(per), 3), "us_per_step_reps": [round(x, 3) for x in per],
+            "spread_us": round(max(per) - min(per), 3), "repetitions": reps, "steps_per_repetition": steps,
+            "host_submit_us_per_step": round(submit_s * 1e6 / (steps * reps), 3),
+            "spin_us": round(spin_us, 1), "spin_covered_submission": submit_s * 1e6 < spin_us}
+
+
 def prewarm(step, ms: float, batch: int = 50) -> float:
     """Untimed: run the workload for >= ms of wall time before the W warmup steps.
     A cold MI355X needs a few ms of sustained load to reach its steady clocks
@@ -460,6 +512,49 @@ def prewarm(step, ms: float, batch: int = 50) -> float:
             i += 1
         torch.cuda.synchronize()
     return time.perf_counter() - t0
+
+
+class Budget:
+    """The N > 1 run's wall clock (--deadline, default 420 s: well under the
+    driver's 600 s lease; counted from the start of bench.py, imports included).
+    Records seconds per phase (xgmi.phase_s) and decides, agreed over ranks,
+    when the remaining extras are skipped: a phase starts only while the budget
+    left covers max(60 s, 2 x the longest phase so far).  The verified headline
+    is measured first and is never skipped."""
+
+    def __init__(self, deadline_s: float, t0: float):
+        self.deadline, self.t0 = deadline_s, t0
+        self.phase_s, self.skipped = {}, []
+        self.longest = 0.0
+
+    def elapsed(self) -> float:
+        return time.perf_counter() - self.t0
+
+    def left(self) -> float:
+        return self.deadline - self.elapsed()
+
+    @contextlib.contextmanager
+    def phase(self, name: str):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            d = time.perf_counter() - t0
+            self.phase_s[name] = round(self.phase_s.get(name, 0.0) + d, 3)
+            self.longest = max(self.longest, d)
+
+    def allows(self, name: str, agree: bool = True) -> bool:
+        ok = self.left() > max(60.0, 2.0 * self.longest)
+        if agree:   # every rank runs the same collectives: the most pressed rank decides
+            ok = agreed(ok)
+        if not ok:
+            self.skipped.append(name)
+        return ok
+
+    def report(self) -> dict:
+        return {"deadline_s": self.deadline, "wall_s": round(self.elapsed(), 3), "phase_s": dict(self.phase_s),
+                "skipped_for_deadline": list(self.skipped),
+                "rule": "a phase starts only while the budget left covers max(60 s, 2 x the longest phase so far)"}
 
 
 def note(rank, msg):
@@ -700,7 +795,7 @@ def link_probe(rank, world, dev) -> dict:
             "spec_GBps_per_direction": XGMI_LINK_DIR_GBPS, "pairs": "2i<->2i+1, both directions at once"}
 
 
-def xgmi_arms(comm, peer, world, rank, dev, stream, side, total, crossed=True) -> dict:
+def xgmi_arms(comm, peer, world, rank, dev, stream, side, total, crossed=True, budget=None) -> dict:
     """Flat / hierarchical inter-GPU allreduces (BASELINE configs 3-5 regimes),
     each through RCCL (allred_dist_allreduce) and through the peer windows
     (allred_peer_dist_allreduce: same program, same bits, one kernel), each
@@ -720,12 +815,15 @@ def xgmi_arms(comm, peer, world, rank, dev, stream, side, total, crossed=True) -
     arms += [(f"mem_{kb}kB", t.SWING, t.MEM, kb << 10, 100, 1, 1) for kb in (2, 32)]
     arms += [("mem_640kB", t.SWING, t.MEM, ELEMS * 2, 100, 1, 1), ("mem_256MiB", t.SWING, t.MEM, 256 << 20, 5, 1, 1)]
     for arm in arms:
+        if budget is not None and not budget.allows("arm:" + arm[0]):   # agreed over ranks
+            continue
         # every arm runs the same calls with the same arguments on every rank, so an
         # error (an RCCL / HIP status turned exception) is raised on every rank alike:
         # record it, agree, and go on with the next arm instead of losing the line
         err = None
         try:
-            xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, *arm, crossed=crossed)
+            with (budget.phase("arm:" + arm[0]) if budget is not None else contextlib.nullcontext()):
+                xgmi_arm(out, comm, peer, world, rank, dev, stream, side, total, *arm, crossed=crossed)
         except Exception as e:  # reported, never silently dropped
             err = repr(e)
         if not agreed(err is None):
@@ -920,6 +1018,9 @@ def cli_config3(world: int, share: bool = False) -> dict:
 
 
 def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
+    budget = Budget(args.deadline, _T0)
+    setup = budget.phase("setup")
+    setup.__enter__()
     # --share-gpu (rehearsal only): every rank on cuda:0 and no RCCL (it refuses two
     # ranks on one device), so the whole N>1 path except RCCL runs on a 1-GPU box
     dev_index = 0 if args.share_gpu else local_rank
@@ -953,6 +1054,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     ws2 = torch.empty(2 * t.dist_workspace_bytes(desc), dtype=torch.uint8, device=dev)   # rccl_x: two parities
     vbuf = torch.empty((RANKS, ELEMS), dtype=torch.int16, device=dev)   # verification bucket
     t_start = time.perf_counter()
+    setup.__exit__(None, None, None)
 
     def timed_steps(step_fn, after=None, reps=None):
         """R repetitions of the K steps behind a spin kernel, an event between
@@ -1014,10 +1116,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #               mem_2D exchange over the peer windows (k_peer_oneshot)
     #   peer_hier_ws  ONE kernel: tree -> mem_2D across GPUs -> broadcast, every cross-GPU
     #                 hand-off an LL push; reducing and writing waves in every workgroup
-    #                 (k_hier_ws: 14.6 us at W = 1 against k_hier_ll's 16.2, which is not a candidate)
-    #   (peer_hier_x / peer_hier_xr: the same hand-offs one bucket deep, k_hier_x — runnable
-    #                 here, not candidates since round 5: 15.2-15.3 us at W = 1, behind k_hier_x2
-    #                 (15.1, which also hides more of the xGMI trip) and k_hier_ws (14.5))
+    #                 (k_hier_ws: 14.5-14.7 us at W = 1)
     #   peer_hier_x2t2  two buckets deep (k_hier_x2: launch i reads bucket i, sums bucket i-1's
     #                 owned tiles before its last row stores, writes bucket i-2; every poll waits
     #                 for the previous launch)
@@ -1025,10 +1124,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     #                 system-scope release fence before every flag store, an acquire fence after
     #                 every flag wait (same bits; the form that stays correct on a node that breaks
     #                 the ordering argument of DESIGN.md §5).  The LL forms have no separate flag
-    # (retired in round 5, every measurement slower — profiles/README.md: the per-tile flag
-    # form k_hier_oneshot, the pipelined LL form k_hier_pipe, the flag hand-off forms of
-    # k_hier_ll / _x / _x2, k_hier_x with R(cur) after the last row stores, and k_hier_x2's
-    # owned sums at the launch start / end)
+    # (retired, every measurement slower — profiles/README.md: in round 5 the per-tile flag
+    # form k_hier_oneshot, the pipelined LL form k_hier_pipe, the flag hand-off forms; in
+    # round 6 k_hier_ll (16.2 us at W = 1), the one-deep pipeline k_hier_x (15.1-15.3) and
+    # k_hier_x2's other placements)
     # Every transport runs only once verified on THIS machine (verify_transport: the
     # exact sum of per-row 0/1 inputs and the reference's closed form, both computed
     # without any transport); the one-kernel peer forms must also equal the launch
@@ -1036,34 +1135,17 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     # RCCL program's.  Then each verified one is timed and the fastest is the headline.
     peer_box = [None]
     mode = [None]   # the peer form currently set (set only on change: the timed loop is one C call a step)
-    pend = [None]   # peer_hier_x: the bucket the last call started (finished by the next call or flush())
-    pend_kind = [None]   # its transport (peer_hier_x / peer_hier_xr)
-    rearly = [None]
     pend2 = [False]   # peer_hier_x2t2: the kind whose buckets are started and not finished (flush())
     pend3 = [False]   # rccl_x: a bucket is started and not finished (flush())
     pend4 = [None, 0]   # peer_mem_x: the started bucket and the partial slot it used (flush())
     mem_parts = [torch.empty(ELEMS, dtype=torch.int16, device=dev) for _ in range(2)]
-    tail = [None]
     fence = [None]
     ws_mem = torch.empty(ELEMS, dtype=torch.int16, device=dev)
-
-    def x2_tail(v):   # the host-side switch between the k_hier_x2 owned-sum placements, read at launch
-        if tail[0] != v:
-            t.tune("hier_x2_tail", int(v))
-            tail[0] = v
 
     def set_fence(v):   # tune peer_fence, read at every peer launch
         if fence[0] != v:
             t.tune("peer_fence", v)
             fence[0] = v
-
-    def set_rearly(v):   # k_hier_x: R(cur) ahead of the previous bucket's last row stores (read at launch)
-        if rearly[0] != v:
-            t.tune("hier_x_rearly", v)
-            rearly[0] = v
-
-    def x2_kind(kind):   # owned-sum placement of a k_hier_x2 transport
-        x2_tail(2)
 
     def flush():
         peer = peer_box[0]
@@ -1073,12 +1155,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         if pend4[0] is not None:
             t.broadcast(pend4[0], ELEMS, ELEMS, RANKS, mem_parts[pend4[1]].data_ptr(), stream)
             pend4[0] = None
-        if pend[0] is not None:
-            set_rearly(int(pend_kind[0] == "peer_hier_xr"))
-            peer.allreduce_pipelined(None, pend[0], ELEMS, stream)
-            pend[0] = None
         if pend2[0]:
-            x2_kind(pend2[0])
             peer.allreduce_pipelined2(None, ELEMS, stream)
             pend2[0] = False
 
@@ -1091,13 +1168,13 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             set_fence(int(base != kind))
             kind = base
         if kind == "rccl_x":   # buckets pipelined: this call writes the previous one's rows
-            if pend[0] is not None or pend2[0] or pend4[0] is not None:
+            if pend2[0] or pend4[0] is not None:
                 flush()
             t.dist_allreduce_pipelined(comm, desc, b.data_ptr(), ws2.data_ptr(), stream)
             pend3[0] = True
             return
         if kind == "peer_mem_x":   # buckets pipelined: this call writes the previous one's rows
-            if pend[0] is not None or pend2[0] or pend3[0]:
+            if pend2[0] or pend3[0]:
                 flush()
             if mode[0] != kind:
                 peer.set_oneshot_max(4 << 20)
@@ -1113,17 +1190,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
             peer.allreduce(out.data_ptr(), ELEMS, stream)   # the partial: mem_2D across the GPUs
             pend4[0], pend4[1] = b.data_ptr(), slot
             return
-        if kind in ("peer_hier_x", "peer_hier_xr"):   # buckets pipelined: this call finishes the previous one
-            if pend2[0] or pend3[0] or pend4[0] is not None or (pend[0] is not None and pend_kind[0] != kind):
-                flush()
-            set_rearly(int(kind == "peer_hier_xr"))
-            peer.allreduce_pipelined(b.data_ptr(), pend[0], ELEMS, stream)
-            pend[0], pend_kind[0] = b.data_ptr(), kind
-            return
         if kind in X2_KINDS:   # two deep: this call writes the bucket started two calls ago
-            if pend[0] is not None or pend3[0] or pend4[0] is not None or (pend2[0] and pend2[0] != kind):
+            if pend3[0] or pend4[0] is not None or (pend2[0] and pend2[0] != kind):
                 flush()
-            x2_kind(kind)
             peer.allreduce_pipelined2(b.data_ptr(), ELEMS, stream)
             pend2[0] = kind
             return
@@ -1135,7 +1204,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         else:
             if mode[0] != kind:
                 peer.set_oneshot_max(0 if kind == "peer_launches" else (4 << 20))
-                peer.set_hier_ll(2 if kind == "peer_hier_ws" else 0)
+                peer.set_hier_ll(1 if kind == "peer_hier_ws" else 0)
                 mode[0] = kind
             peer.allreduce(b.data_ptr(), ELEMS, stream, RANKS, SIDE, t.SWING, ws_mem.data_ptr())
 
@@ -1143,6 +1212,10 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     comparator = {}   # peer_launches: verified like a candidate, the bit-identity reference of the one-kernel forms
 
     def check(kind, seed):
+        with budget.phase("verify:" + kind):
+            return check_(kind, seed)
+
+    def check_(kind, seed):
         note(rank, f"verify: {kind}")
         peer = peer_box[0]
 
@@ -1190,17 +1263,21 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         fb_local = local_phases_ms()
         FALLBACK_DONE.set()
 
+        # the peer phase may take --peer-timeout s, and never past the deadline (less the extras' margin)
+        peer_limit = max(30.0, min(args.peer_timeout, budget.left() - 90.0))
+
         def peer_give_up():
             if rank == 0:
                 emit(multi_line(args, world, "rccl", fb_ms, fb_local, time.perf_counter() - t_start,
                                 {"headline_transport": "rccl", "transport_verified": dict(verify), "peer_error":
-                                 f"peer setup / verification / timing did not finish within {args.peer_timeout:g} s"}))
+                                 f"peer setup / verification / timing did not finish within {peer_limit:g} s",
+                                 "budget": budget.report()}))
             os._exit(0)
 
         # every rank's timer started after the same barrier: all leave together; a rank
         # whose own timer was cancelled first and then loses rank 0 exits cleanly too
         # (FALLBACK_DONE, main())
-        peer_guard = threading.Timer(args.peer_timeout, peer_give_up)
+        peer_guard = threading.Timer(peer_limit, peer_give_up)
         peer_guard.daemon = True
         peer_guard.start()
     note(rank, f"world {world}, device {dev_index}: opening peer windows")
@@ -1226,23 +1303,27 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
 
     def quick_time(kinds):
         for kind in kinds:
-            note(rank, f"quick timing: {kind}")
-            it = iter(range(1 << 30))
-            quick[kind] = round(statistics.median(
-                timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
-                for _ in range(3)), 4)
-            if peer is not None and kind.startswith("peer"):
-                # a peer wait that gave up means wrong bytes: the candidate is out (every rank agrees),
-                # and the sticky status bit is cleared so the next candidates wait normally again
-                torch.cuda.synchronize()
-                st0 = torch.tensor([peer.status() & t.PEER_TIMEOUT], dtype=torch.int64)
-                dist.all_reduce(st0, op=dist.ReduceOp.MAX)
-                if st0.item():
-                    drop(kind, "quick_timing_timeout: a peer wait gave up during its timing")
-                    quick.pop(kind, None)
-                    verify.setdefault(kind, {}).update(verified=False, quick_timing_timeout=True)
-                    peer.clear_status()
-                    dist.barrier()
+            with budget.phase("quick:" + kind):
+                quick_time1(kind)
+
+    def quick_time1(kind):
+        note(rank, f"quick timing: {kind}")
+        it = iter(range(1 << 30))
+        quick[kind] = round(statistics.median(
+            timed_max(lambda: run(kind, bufs[next(it) % len(bufs)]), qk, stream, after=flush)
+            for _ in range(3)), 4)
+        if peer is not None and kind.startswith("peer"):
+            # a peer wait that gave up means wrong bytes: the candidate is out (every rank agrees),
+            # and the sticky status bit is cleared so the next candidates wait normally again
+            torch.cuda.synchronize()
+            st0 = torch.tensor([peer.status() & t.PEER_TIMEOUT], dtype=torch.int64)
+            dist.all_reduce(st0, op=dist.ReduceOp.MAX)
+            if st0.item():
+                drop(kind, "quick_timing_timeout: a peer wait gave up during its timing")
+                quick.pop(kind, None)
+                verify.setdefault(kind, {}).update(verified=False, quick_timing_timeout=True)
+                peer.clear_status()
+                dist.barrier()
 
     quick_time(list(candidates))
     if peer is not None:
@@ -1279,6 +1360,8 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         run(transport, bufs[i % len(bufs)])
 
     note(rank, f"timed: {transport}")
+    headline_phase = budget.phase("headline")
+    headline_phase.__enter__()
     # untimed prewarm (steady clocks): the SAME number of steps on every rank — the
     # ranks' calls must pair up (RCCL collectives, peer epochs) — derived from the
     # max-over-ranks quick timing, identical everywhere
@@ -1289,7 +1372,7 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         step(i)
     flush()
     t0 = time.perf_counter()
-    # rccl_x / peer_hier_x / _x2: the finishing launch is part of each repetition's K steps
+    # rccl_x / peer_mem_x / peer_hier_x2t2: the finishing launch is part of each repetition's K steps
     ms_per_step, rep_ms = timed_steps(step, after=flush)
     wall = time.perf_counter() - t0
     peer_timeout = False
@@ -1311,9 +1394,11 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         peer.set_hier_ll(0)
         set_fence(0)
         mode[0] = None
+    headline_phase.__exit__(None, None, None)
     fused_local = transport in ("rccl_x", "peer_mem_x")
-    local_ms = local_phases_ms(fused=fused_local)
-    local_split_ms = local_phases_ms() if fused_local else local_ms
+    with budget.phase("local_phases"):
+        local_ms = local_phases_ms(fused=fused_local)
+        local_split_ms = local_phases_ms() if fused_local else local_ms
     if peer_guard is not None:   # the headline is measured: the extras have their own watchdog
         peer_guard.cancel()
     HEADLINE_DONE.set()
@@ -1344,18 +1429,22 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                     ex = {k: v for k, v in list(extras.items())}
                 except Exception:  # extras being written concurrently: headline only
                     ex = {}
-                ex["extras_error"] = f"extras did not finish within {args.extras_timeout:g} s"
+                ex["extras_error"] = f"extras did not finish within {extras_limit:g} s"
+                ex["budget"] = budget.report()
                 emit(line(ex))
             os._exit(0)
 
-        guard = threading.Timer(args.extras_timeout + (0 if rank == 0 else 10), give_up)
+        # the extras end by the deadline whatever happens (rank 0 prints the line with what it has)
+        extras_limit = max(10.0, min(args.extras_timeout, budget.left() - 15.0))
+        guard = threading.Timer(extras_limit + (0 if rank == 0 else 10), give_up)
         guard.daemon = True
         guard.start()
         extras.update(xgmi_arms(comm, peer if verify.get("peer_swing", {}).get("verified") else None, world, rank,
-                                dev, stream, side, total, crossed=not args.share_gpu))
-        if world > 1 and comm is not None:
+                                dev, stream, side, total, crossed=not args.share_gpu, budget=budget))
+        if world > 1 and comm is not None and budget.allows("link_probe"):
             try:
-                extras["link_probe"] = link_probe(rank, world, dev)
+                with budget.phase("link_probe"):
+                    extras["link_probe"] = link_probe(rank, world, dev)
                 mb = extras["link_probe"]["GBps_per_direction"]
                 for v in extras.values():  # the fraction again against the MEASURED link rate
                     if isinstance(v, dict) and "busbw_GBps" in v:
@@ -1376,20 +1465,24 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     torch.cuda.synchronize()
     # rank 0 alone (the others wait at the barrier): the reference's program surface
     # across this node's GPUs (config 3), then the CPU baseline of configs 3-5
-    if rank == 0 and args.extras:
+    # (rank 0 alone: the others wait at the barrier, so no agreement is needed)
+    if rank == 0 and args.extras and budget.allows("cli_config3", agree=False):
         try:
-            extras["cli_config3"] = cli_config3(world, share=args.share_gpu)
+            with budget.phase("cli_config3"):
+                extras["cli_config3"] = cli_config3(world, share=args.share_gpu)
         except Exception as e:  # reported, never silently dropped
             extras["cli_config3"] = {"error": repr(e), "verified": False}
     cpu = None
-    if rank == 0 and args.cpu:
+    if rank == 0 and args.cpu and budget.allows("cpu_baseline", agree=False):
         try:
-            cpu = cpu_baseline_multi()
+            with budget.phase("cpu_baseline"):
+                cpu = cpu_baseline_multi()
         except Exception as e:  # reported, never silently dropped
             cpu = {"value": None, "error": repr(e)}
     dist.barrier()
     if rank != 0:
         return None
+    extras["budget"] = budget.report()
     out = line(extras)
     if cpu is not None:
         out["cpu_baseline"] = cpu
@@ -1404,8 +1497,7 @@ HEADLINE_DONE = threading.Event()
 FALLBACK_DONE = threading.Event()
 
 # the one-launch kernel of each one-kernel transport (its HBM bytes over the step time)
-ONE_LAUNCH = {"peer_hier_ws": "k_hier_ws", "peer_hier_x": "k_hier_x", "peer_hier_xr": "k_hier_x<re,late>",
-              "peer_hier_x2t2": "k_hier_x2<tail2,late>"}
+ONE_LAUNCH = {"peer_hier_ws": "k_hier_ws", "peer_hier_x2t2": "k_hier_x2"}
 # the k_hier_x2 transports (owned sums before a launch's last row stores)
 X2_KINDS = ("peer_hier_x2t2",)
 # the transports whose cross-GPU hand-offs are data + a separate flag (k_peer_sched, k_peer_oneshot):
@@ -1442,15 +1534,10 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
                      "2D Swing BO over RCCL/xGMI",
            "peer_launches": "on-GPU tree reduce, mem_2D across GPUs over peer-mapped windows (launches), broadcast",
            "peer_swing": "on-GPU tree reduce, 2D Swing BO over peer-mapped xGMI windows (one kernel), broadcast",
-           "peer_hier_x": "ONE kernel per bucket, consecutive buckets pipelined (K buckets in K + 1 launches, all "
-                          "inside the timed region): on-GPU tree reduce of bucket i+1 while bucket i's rows are written, "
-                          "mem_2D one-shot across GPUs with LL pushes into peer-mapped xGMI windows",
            "peer_hier_x2t2": "ONE kernel per bucket, two buckets deep (K buckets in K + 1 launches, all inside the "
                              "timed region): launch i reads bucket i, writes bucket i-2's rows and, before its last "
                              "row stores, sums bucket i-1's owned tiles; mem_2D one-shot across GPUs with LL pushes "
                              "into peer-mapped xGMI windows",
-           "peer_hier_xr": "ONE kernel per bucket, consecutive buckets pipelined (as peer_hier_x) with the owned "
-                           "sums ahead of the previous bucket's last row stores, LL pushes into peer-mapped xGMI windows",
            "peer_hier_ws": "ONE kernel: on-GPU tree reduce, mem_2D one-shot across GPUs with LL pushes "
                            "(data+epoch words) into peer-mapped xGMI windows, broadcast; every workgroup's reducing "
                            "waves stream tiles in while its writing waves write finished tiles' rows"}[base]
@@ -1504,6 +1591,9 @@ def main():
                     help="N > 1: seconds the peer-window phase may take before the RCCL-measured line is printed")
     ap.add_argument("--extras-timeout", type=float, default=240.0,
                     help="N > 1: seconds the extras may take before the headline line is printed without them")
+    ap.add_argument("--deadline", type=float, default=420.0,
+                    help="N > 1: seconds from the start of bench.py by which the line is printed; the extras "
+                         "after the verified headline are skipped as the deadline nears (xgmi.budget)")
     ap.add_argument("--main-only", action="store_true", help="timed workload only (for rocprofv3 runs)")
     ap.add_argument("--tilesum-only", type=int, nargs="*", default=None, metavar="MIB",
                     help="only the tile-sum part of the N = 1 line, at these sizes in MiB (default 256 1024; "

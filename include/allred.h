@@ -22,11 +22,13 @@
 extern "C" {
 #endif
 
-/* ABI 6 (round 5): allred_peer_set_hier_ll takes 0 / 1 / 2 (k_hier_pipe retired, k_hier_ws new), the tune
- * keys lose hier_handoff and gain peer_fence, allred_peer_clear_status refuses while a
- * pipelined sequence is pending, and the hierarchical forms' hand-off area moved (its own
- * words: 6 data bytes + a 16-bit epoch) — peers of different ABIs must not connect. */
-#define ALLRED_ABI_VERSION 6
+/* ABI 7 (round 6): the one-deep peer pipeline (allred_peer_allreduce_pipelined, k_hier_x) and
+ * k_hier_ll are retired, allred_peer_set_hier_ll takes 0 (launch form) / 1 (k_hier_ws, the
+ * default), the tune keys hier_x2_tail / hier_x_lag / hier_x_chunked / hier_x_rearly /
+ * hier_x_latepoll are gone (k_hier_x2 runs its measured product form only), and
+ * allred_last_launch is new.  ABI 6 (round 5): the hierarchical forms' hand-off area holds
+ * 6 data bytes + a 16-bit epoch per word — peers of different ABIs must not connect. */
+#define ALLRED_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------- */
 #define ALLRED_OK 0
@@ -244,9 +246,6 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   fused_chunk_tiles 1280: the persistent fused 64-rank passes run a bucket of T 256-element
  *                     tiles as max(1, round(T / 1280)) launches over consecutive tile ranges
  *                     (0 = one launch); allred_plan_launches counts them
- *   hier_x2_tail      2: k_hier_x2 (allred_peer_allreduce_pipelined2) sums the owned tiles of the
- *                     middle bucket before the launch's last row stores; 1: at the end of each
- *                     launch; 0: at its start
  *   lo_tree_min_tiles 64: a 64-rank rank-uniform LO plan (every RecDub schedule) takes the BO tree
  *                     pass from this many 256-element tiles per rank, the register butterfly below
  *   tree_bcast_lag    1: k_tree_bcast_x (allred_dist_allreduce_pipelined) stores the previous
@@ -256,20 +255,11 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *   steps_groups      0: workgroups per CU of the schedule form k_steps_reg — 0 auto (BO 3; LO 4,
  *                     or 3 where 4 would leave every wave exactly one strip), 3, 4 or 5 (1 and 2:
  *                     ALLRED_ERR_ARG)
- *   hier_x_lag        1: k_hier_x / k_hier_x2 store a tile's rows of the bucket being written one
- *                     iteration after the tree of the matching tile of the bucket being read; 0: in
- *                     the same iteration
- *   hier_x_chunked    0: k_hier_x / k_hier_x2 stage results in chunks of 8 tiles only when a workgroup
- *                     has more than 8 tiles; 1: always (A/B timing of the chunk bookkeeping)
  *   steps_tab         1: k_steps_reg (BO) stages only the programs of its own units' blocks (when fewer
  *                     than P); 0: every block's program (P x 256 bytes) per workgroup (round 3)
  *   steps_early       1: k_steps_reg issues the first strip's loads before it stages its programs when
  *                     its grid is full (units >= workgroups), else after; 2: always before; 0: always
  *                     after (round 3)
- *   hier_x_rearly     0: k_hier_x sums its owned tiles after the previous bucket's last row stores;
- *                     1: ahead of them (LL hand-offs, hier_x_lag 1)
- *   hier_x_latepoll   1: k_hier_x / k_hier_x2 poll the results of the bucket they write after tile 0's
- *                     tree (LL hand-offs, hier_x_lag 1; a flush launch polls at its start); 0: at the start
  *   peer_fence        0; 1: the flag protocols of the peer windows (k_peer_oneshot, k_peer_sched,
  *                     k_peer_sched_push) put a system-scope release fence before every flag store
  *                     and an acquire fence after every flag wait.  Same bits; the default relies on
@@ -277,6 +267,11 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  *                     before the workgroup barrier that precedes a flag).  The LL kernels have no
  *                     separate flag (each word carries its epoch) and take no fence.  Every rank
  *                     must use the same setting
+ *   hier_ws_ahead     1: k_hier_ws's reducing waves load one tile ahead; 2: two (measured slower,
+ *                     +0.3-0.5 us at W = 1)
+ *   hier_ws_cols      16: 16-byte columns of a tile per k_hier_ws reducing wave — 8 (quarters: 8
+ *                     waves per workgroup), 16 (halves: 4 waves) or 32 (whole tiles: 2 waves); other
+ *                     values ALLRED_ERR_ARG
  *   multi_fault       0; fault injection (tests only): 1..32: GPU value - 1 of allred_run_multi fails its
  *                     timed allreduce while its peers are in theirs (every thread must return);
  *                     33..64: GPU value - 33 fails its warm-up (every thread skips the timed region)
@@ -289,6 +284,27 @@ int allred_plan_rank_zones(const allred_plan* plan, const uint64_t* host_stamps,
  * allred_BO_2D.cpp:203-211). */
 int allred_tune_set(const char* key, int64_t value);
 int allred_tune_get(const char* key, int64_t* value);
+
+/* The last kernel launch of the calling thread among the ones the bench
+ * reports (the fused BO pass k_tree_lds_lag, the schedule form k_steps_reg,
+ * the hierarchical one-launch steps k_hier_ws / k_hier_x2): the kernel, the
+ * grid its launcher chose, and — queried at this call — its static LDS,
+ * VGPRs, resident workgroups per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor)
+ * and the device's CU count.  ALLRED_ERR_ARG when this thread launched none of
+ * them.  No reference counterpart (the reference fixes its core grid,
+ * allred_BO_2D.cpp:26). */
+typedef struct {
+    char kernel[64];
+    uint32_t grid;
+    uint32_t block;
+    uint32_t lds_bytes;
+    int32_t regs;
+    int32_t resident_per_cu;
+    int32_t cus;
+    int32_t device;
+    int32_t reserved;
+} allred_launch_info;
+int allred_last_launch(allred_launch_info* out);
 
 /* ======================================================================
  * Reference program surface: AllredConfig (allred_helper.hpp:47-97) +
@@ -545,22 +561,8 @@ int allred_peer_connect_all(int nranks, allred_peer* const* peers);
 int allred_peer_allreduce(allred_peer* peer, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream);
 /* The hierarchical step of allred_peer_allreduce (64 local ranks per GPU, the
- * same result bits) PIPELINED across consecutive buckets: one launch
- * (k_hier_x) finishes `prev` — the bucket the previous call started — and
- * starts `cur`, streaming cur's rank rows in while prev's rank rows go out
- * (a bucket's own rows can only be written after every GPU has reduced it).
- * A sequence of K buckets is K + 1 calls: (b0, NULL), (b1, b0), ...,
- * (NULL, b_{K-1}); on return (stream order) prev holds its allreduced rows.
- * While a bucket is pending, the other peer allreduce calls return
- * ALLRED_ERR_ARG; so does a prev that is not the pending bucket.
- * ALLRED_ERR_UNSUPPORTED: local_ranks != 64, more than 8 GPUs, flags not
- * uncached, or a bucket beyond the LL boxes (elems > min(max_elems, 4 Mi)).
- * Any grid cap (allred_peer_set_max_groups) works: a workgroup runs any number
- * of tiles, its results staged in LDS 8 tiles at a time.
- * No reference counterpart (the reference runs one vector per program). */
-int allred_peer_allreduce_pipelined(allred_peer* peer, uint16_t* cur, uint16_t* prev, uint64_t elems,
-                                    int local_ranks, int local_side, int local_algo, void* stream);
-/* The same step TWO buckets deep (k_hier_x2): the call with cur starts it
+ * same result bits) PIPELINED across consecutive buckets, two deep
+ * (k_hier_x2): the call with cur starts it
  * (tree, partials pushed to the owners), sums the owned tiles of the bucket
  * the previous call started and writes the rank rows of the bucket started
  * two calls earlier; cur == NULL (flush) finishes every pending bucket in one
@@ -568,9 +570,15 @@ int allred_peer_allreduce_pipelined(allred_peer* peer, uint16_t* cur, uint16_t* 
  * rows are final, in stream order, after the call that started the bucket
  * two calls later (or the flush); keep it alive until then.  Every poll of a
  * launch waits for pushes of the previous launch on the other GPUs, so a GPU
- * up to one launch late stalls nobody.  Same bits, arguments and limits as
- * allred_peer_allreduce_pipelined; the two sequences do not mix.
- * No reference counterpart. */
+ * up to one launch late stalls nobody.  While buckets are pending, the other
+ * peer allreduce calls return ALLRED_ERR_ARG; so does another bucket size
+ * mid-sequence or a flush with nothing pending.  ALLRED_ERR_UNSUPPORTED:
+ * local_ranks != 64, more than 8 GPUs, flags not uncached, or a bucket beyond
+ * the hand-off area (elems > min(max_elems, 4 Mi)).  Any grid cap
+ * (allred_peer_set_max_groups) works: a workgroup runs any number of tiles, its
+ * results staged in LDS 8 tiles at a time.  (The one-deep form of rounds 3-5,
+ * k_hier_x, is retired: 15.1-15.3 us at W = 1 against this form's 15.0.)
+ * No reference counterpart (the reference runs one vector per program). */
 int allred_peer_allreduce_pipelined2(allred_peer* peer, uint16_t* cur, uint64_t elems, int local_ranks,
                                      int local_side, int local_algo, void* stream);
 /* Buckets of at most `bytes` (default 4 MiB) run as one kernel (per-workgroup
@@ -578,24 +586,22 @@ int allred_peer_allreduce_pipelined2(allred_peer* peer, uint16_t* cur, uint64_t 
  * barrier / all-gather launches.  Same result bits either way.  Every rank
  * must use the same setting. */
 int allred_peer_set_oneshot_max(allred_peer* peer, uint64_t bytes);
-/* enable = 1: with local_ranks == 64 and nranks <= 8, allred_peer_allreduce
- * runs the hierarchical step as one kernel with LL hand-offs (each cross-GPU
- * transfer a push of self-validating 8-byte data+epoch words into the
- * consumer's own memory; no flags, no remote reads) for buckets of up to
- * min(max_elems, 4 Mi) elements.  Same result bits as the default form
- * (allred_mem_2D semantics over the per-GPU trees).  Every rank must use the
- * same setting.  Replaces nothing in the reference (its mem_2D phases sync
- * through semaphores, allred_mem_2D/kernels/dataflow_kernel.cpp:201-230). */
-/* 0 = off (tree, the mem_2D exchange, broadcast as launches), 1 = k_hier_ll
- * (all tiles read, owned tiles summed, all tiles written: three phases),
- * 2 = k_hier_ws (round 5, the default: the same hand-offs with reducing and
- * writing waves in every workgroup, so each CU reads and writes at once: 14.6
- * vs 16.2 us at W = 1; buckets the one-launch forms cannot take — not a
- * multiple of 256 x nranks elements, nranks > 8, larger than the hand-off
- * area — run the launch form); other values ALLRED_ERR_ARG.  (Retired forms and their numbers:
- * profiles/README.md — the per-tile flag form k_hier_oneshot, 19.9 us at
- * W = 1, and the pipelined LL form k_hier_pipe, 17.8 us, in round 5; the
- * specialised-wave form of round 1, 27-38 us.) */
+/* enable = 1 (the default): with local_ranks == 64 and nranks <= 8,
+ * allred_peer_allreduce runs the hierarchical step as ONE kernel, k_hier_ws,
+ * with LL hand-offs (each cross-GPU transfer a push of self-validating 8-byte
+ * data+epoch words into the consumer's own memory; no flags, no remote reads)
+ * and reducing and writing waves in every workgroup, so each CU reads and
+ * writes at once, for buckets of up to min(max_elems, 4 Mi) elements that are
+ * a multiple of 256 x nranks (others run the launch form).  0 = the launch
+ * form (tree, the mem_2D exchange, broadcast as launches).  Same result bits
+ * either way (allred_mem_2D semantics over the per-GPU trees); other values
+ * ALLRED_ERR_ARG.  Every rank must use the same setting.  Replaces nothing in
+ * the reference (its mem_2D phases sync through semaphores,
+ * allred_mem_2D/kernels/dataflow_kernel.cpp:201-230).  (Retired forms and
+ * their numbers at W = 1, profiles/README.md: k_hier_ll — the three phases in
+ * sequence, 16.2 us vs k_hier_ws's 14.5-14.6 — in round 6; the per-tile flag
+ * form, 19.9 us, and the pipelined LL form, 17.8 us, in round 5; the
+ * specialised-wave form of round 1, 27-38 us.)  ABI 7: 2 is no longer a value. */
 int allred_peer_set_hier_ll(allred_peer* peer, int enable);
 /* Caps the grid of the hierarchical one-kernel forms, k_peer_mem_ll and the
  * scheduled form (allred_peer_dist_allreduce) at `groups` workgroups (0 =
@@ -646,8 +652,8 @@ int allred_peer_check(allred_peer* peer, void* stream);
  * wait of this peer gives up at once) through the null stream, and nothing else.  Call
  * with no kernel of this peer in flight (after allred_peer_check).  The call counter
  * keeps advancing, so the next call's LL words and flags carry epochs no timed-out call
- * wrote.  Returns ALLRED_ERR_ARG while a pipelined sequence (allred_peer_hier_x /
- * allred_peer_hier_x2) is pending: finish it first.  ABI 5. */
+ * wrote.  Returns ALLRED_ERR_ARG while a pipelined sequence (allred_peer_allreduce_pipelined2)
+ * is pending: finish it first.  ABI 5. */
 int allred_peer_clear_status(allred_peer* peer);
 int allred_peer_destroy(allred_peer* peer);
 

@@ -28,7 +28,8 @@ __all__ = [
     "get_swing_block_comm_indexes", "get_recdub_block_comm_indexes", "normalize_tiles",
     "random_bf16_vector", "constant_bf16_vector", "validate_result_vector", "Plan", "preferred_rank_stride", "bf16_add",
     "bf16_add_masked", "tree_reduce", "broadcast", "parse_args", "run", "run_cli", "Comm", "dist_desc", "dist_allreduce",
-    "dist_allreduce_host", "dist_allreduce_pipelined", "tree_broadcast_pipelined", "dist_workspace_bytes", "dist_program_stats", "Peer", "tune", "tuned", "ACC_FP32",
+    "dist_allreduce_host", "dist_allreduce_pipelined", "tree_broadcast_pipelined", "dist_workspace_bytes", "dist_program_stats", "Peer", "tune", "tuned", "last_launch",
+    "ACC_FP32",
     "ACC_BF16", "multi_plan", "run_multi", "TRANSPORT_RCCL", "TRANSPORT_PEER", "TRANSPORT_HOST", "MULTI_FLAT",
     "MULTI_HIER", "MULTI_LOCAL",
 ]
@@ -59,6 +60,17 @@ class tuned:
     def __exit__(self, *exc):
         for k, v in self.old.items():
             tune(k, v)
+
+
+def last_launch() -> dict:
+    """allred_last_launch: the kernel this thread's last reported launch ran, the
+    grid its launcher chose, its static LDS / VGPRs, the workgroups per CU that can
+    be resident and the device's CU count."""
+    li = _lib.LaunchInfo()
+    check(lib.allred_last_launch(C.byref(li)), "last_launch")
+    return {"kernel": li.kernel.decode(), "grid": li.grid, "block": li.block, "lds_bytes": li.lds_bytes,
+            "vgprs": li.regs, "resident_per_cu": li.resident_per_cu, "cus": li.cus,
+            "grid_resident": li.grid <= li.resident_per_cu * li.cus}
 
 
 # ---------------------------------------------------------------- schedule
@@ -440,20 +452,12 @@ class Peer:
         if check_status:
             self.check(stream)
 
-    def allreduce_pipelined(self, cur_ptr: int | None, prev_ptr: int | None, elems: int, stream=None,
-                            local_ranks: int = 64, local_side: int = 8, local_algo: int = SWING) -> None:
-        """The hierarchical step pipelined across consecutive buckets (k_hier_x):
-        finishes prev (the bucket the previous call started) and starts cur.
-        K buckets = K + 1 calls: (b0, None), (b1, b0), ..., (None, b_{K-1})."""
-        check(lib.allred_peer_allreduce_pipelined(self._h, cur_ptr or None, prev_ptr or None, elems, local_ranks,
-                                                  local_side, local_algo, _stream_ptr(stream)), "peer_allreduce_pipelined")
-
     def allreduce_pipelined2(self, cur_ptr: int | None, elems: int, stream=None, local_ranks: int = 64,
                              local_side: int = 8, local_algo: int = SWING) -> None:
-        """The same step two buckets deep (k_hier_x2): starts cur, sums the owned
-        tiles of the previous call's bucket, writes the rows of the bucket started
-        two calls earlier; cur None finishes everything pending.  K buckets = K + 1
-        calls: b0, b1, ..., b_{K-1}, None."""
+        """The hierarchical step pipelined two buckets deep (k_hier_x2): starts cur,
+        sums the owned tiles of the previous call's bucket, writes the rows of the
+        bucket started two calls earlier; cur None finishes everything pending.
+        K buckets = K + 1 calls: b0, b1, ..., b_{K-1}, None."""
         check(lib.allred_peer_allreduce_pipelined2(self._h, cur_ptr or None, elems, local_ranks, local_side,
                                                    local_algo, _stream_ptr(stream)), "peer_allreduce_pipelined2")
 
@@ -474,10 +478,9 @@ class Peer:
         check(lib.allred_peer_set_oneshot_max(self._h, nbytes), "peer_set_oneshot_max")
 
     def set_hier_ll(self, mode) -> None:
-        """64 local ranks: the hierarchical step with LL push hand-offs — 1 (or
-        True) k_hier_ll (read / sum / write phases in one launch), 2 k_hier_ws
-        (one launch, reducing and writing waves in every workgroup; the
-        default), 0 (or False) the launch form.  Same result bits every way."""
+        """64 local ranks: 1 (or True, the default) the hierarchical step as one
+        launch with LL push hand-offs, reducing and writing waves in every
+        workgroup (k_hier_ws); 0 (or False) the launch form.  Same result bits."""
         check(lib.allred_peer_set_hier_ll(self._h, int(mode)), "peer_set_hier_ll")
 
     def set_lo_ll_max(self, nbytes: int) -> None:

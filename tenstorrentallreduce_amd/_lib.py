@@ -38,7 +38,7 @@ BO, LO, MEM = 0, 1, 2
 STEPS_REG = 0x100   # allred_steps_program: | ALLRED_BO -> the register-staged form's program
 EXEC_STEPS, EXEC_FUSED = 0, 1
 ACC_FP32, ACC_BF16 = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_NODES, MAX_STEPS = 64, 6
 UNIQUE_ID_BYTES = 128
 MULTI_FLAT, MULTI_HIER, MULTI_LOCAL = 0, 1, 2          # allred_multi_plan.mode
@@ -112,6 +112,12 @@ class MultiOpts(C.Structure):
                 ("reserved", C.c_int32)]
 
 
+class LaunchInfo(C.Structure):
+    _fields_ = [("kernel", C.c_char * 64), ("grid", C.c_uint32), ("block", C.c_uint32), ("lds_bytes", C.c_uint32),
+                ("regs", C.c_int32), ("resident_per_cu", C.c_int32), ("cus", C.c_int32), ("device", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
 class Seg(C.Structure):
     _fields_ = [("ptr", C.c_void_p), ("bytes", C.c_uint64)]
 
@@ -158,6 +164,7 @@ SIGNATURES = [
     ("allred_plan_rank_zones", C.c_int, [_P, _P, _P, _P]),
     ("allred_tune_set", C.c_int, [C.c_char_p, C.c_int64]),
     ("allred_tune_get", C.c_int, [C.c_char_p, C.POINTER(C.c_int64)]),
+    ("allred_last_launch", C.c_int, [C.POINTER(LaunchInfo)]),
     ("allred_args_parse", C.c_int, [C.c_int, C.POINTER(C.c_char_p), C.c_int, C.POINTER(Args)]),
     ("allred_run", C.c_int, [C.POINTER(Args), C.c_int, C.POINTER(Report)]),
     ("allred_comm_get_unique_id", C.c_int, [_P]),
@@ -182,7 +189,6 @@ SIGNATURES = [
     ("allred_peer_connect", C.c_int, [_P, _P]),
     ("allred_peer_connect_all", C.c_int, [C.c_int, C.POINTER(_P)]),
     ("allred_peer_allreduce", C.c_int, [_P, _u16p, C.c_uint64, C.c_int, C.c_int, C.c_int, _P, _P]),
-    ("allred_peer_allreduce_pipelined", C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_peer_allreduce_pipelined2", C.c_int, [_P, _P, C.c_uint64, C.c_int, C.c_int, C.c_int, _P]),
     ("allred_peer_set_oneshot_max", C.c_int, [_P, C.c_uint64]),
     ("allred_peer_set_hier_ll", C.c_int, [_P, C.c_int]),

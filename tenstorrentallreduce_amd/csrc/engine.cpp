@@ -957,7 +957,7 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
     // H2D(c + 1) | pass(c) | D2H(c - 1) on three streams, each copy a 2D DMA straight into /
     // out of the skewed device layout (no staging pass); same bits as the whole-bucket pass.
     // ALLRED_E2E_CHUNKS=c equal chunks (1 = one copy each way around one pass); unset: 8, where the
-    // box's strided copies keep the rate of plain ones (probed below), else 1.
+    // box's strided copies keep the rate of plain ones (probed below: ALLRED_E2E_STRIDED_RATIO), else 1.
     // Each 2D copy costs ~10 us over its bytes (measured: 8 chunks 1.09 ms, 16 1.19, 32 1.5,
     // a 1-2-4-9-9-4-2-1 32nds ramp 1.18; profiles/r05_e2e_probe.json)
     std::vector<size_t> csz;
@@ -1042,7 +1042,12 @@ int allred_run(const allred_args* a, int verbose, allred_report* rep) {
         HIPCK(hipStreamSynchronize(sd));
         HIPCK(hipEventElapsedTime(&t2d, p[0], p[1]));
         HIPCK(hipEventElapsedTime(&t1d, p[2], p[3]));
-        if (t2d > 1.5f * t1d) chunked = false;
+        // keep the chunks while the strided copy takes at most `ratio` x the plain one's time
+        // (ALLRED_E2E_STRIDED_RATIO, default 1.5; 0 forces the one-copy form, a huge ratio the
+        // chunks: tests/test_gpu_cli.py drives both outcomes of this decision)
+        const char* rs = std::getenv("ALLRED_E2E_STRIDED_RATIO");
+        const float ratio = rs ? std::strtof(rs, nullptr) : 1.5f;
+        if (t2d > ratio * t1d) chunked = false;
     }
     if (chunked) {
         // timed: chunk c's H2D on sh, its pass on s behind it, its D2H on sd behind the
@@ -1163,3 +1168,49 @@ done:
 }
 
 }  // extern "C"
+
+namespace tsa {
+namespace {
+struct LaunchNote {
+    const void* func = nullptr;
+    const char* name = "";
+    unsigned grid = 0, block = 0;
+    int device = -1;
+};
+thread_local LaunchNote g_last_launch;
+}  // namespace
+
+void note_launch(const void* func, const char* name, unsigned grid, unsigned block) {
+    LaunchNote& l = g_last_launch;
+    l.func = func;
+    l.name = name;
+    l.grid = grid;
+    l.block = block;
+    (void)hipGetDevice(&l.device);
+}
+}  // namespace tsa
+
+extern "C" int allred_last_launch(allred_launch_info* out) {
+    if (!out) return ALLRED_ERR_ARG;
+    std::memset(out, 0, sizeof(*out));
+    const tsa::LaunchNote& l = tsa::g_last_launch;
+    if (!l.func) return ALLRED_ERR_ARG;   // no recorded launch on this thread
+    std::snprintf(out->kernel, sizeof(out->kernel), "%s", l.name);
+    out->grid = l.grid;
+    out->block = l.block;
+    out->device = l.device;
+    // the attributes below are queried now, not at launch (the launch path stays cheap)
+    DeviceGuard guard(l.device);
+    if (!guard.ok) return ALLRED_ERR_HIP;
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, l.func) != hipSuccess) return ALLRED_ERR_HIP;
+    out->lds_bytes = (uint32_t)fa.sharedSizeBytes;
+    out->regs = fa.numRegs;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, l.func, (int)l.block, 0) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, l.device) != hipSuccess)
+        return ALLRED_ERR_HIP;
+    out->resident_per_cu = per_cu;
+    out->cus = cus;
+    return ALLRED_OK;
+}

@@ -40,11 +40,15 @@ int build_schedule(int algo, int side, int total, allred_schedule* out, std::str
 // Kernel-form switches between bit-identical forms; defaults = the product forms.
 enum class Tune {
     fused_form, lo_tree, lo_dag, lo_dag_place, lo_dag_min_tiles, mem_reduce_lds, steps_form, pipe_grid, lo_dag_reg,
-    lo_dag_reg_min_tiles, check, fused_chunk_tiles, hier_x2_tail, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, hier_x_lag, steps_groups,
-    rccl_fault, multi_fault, hier_x_chunked, steps_tab, steps_early, hier_x_rearly, hier_x_latepoll, peer_fence,
-    hier_ws_ahead, hier_ws_cols, count
+    lo_dag_reg_min_tiles, check, fused_chunk_tiles, lo_tree_min_tiles, tree_bcast_lag, tree_bcast_bal, steps_groups,
+    rccl_fault, multi_fault, steps_tab, steps_early, peer_fence, hier_ws_ahead, hier_ws_cols, count
 };
 int64_t tune(Tune key);
+
+// ---------------- the last kernel launch of this thread (allred_last_launch, engine.cpp) ----------------
+// The launchers of the kernels bench.py reports (the fused pass, the schedule form, the
+// hierarchical one-launch steps) record the kernel and the grid they chose.
+void note_launch(const void* func, const char* name, unsigned grid, unsigned block);
 
 // ---------------- device launchers (kernels.hip) ----------------
 // All take hipStream_t as void* and return ALLRED_OK / ALLRED_ERR_*.
@@ -157,21 +161,12 @@ int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint3
 // the hierarchical forms' hand-off words: a tile's 512 bytes as 3 x 32 8-byte words (6 data
 // bytes + a 16-bit epoch each), kHSlot words per tile slot (peer_kernels.hip h_pack)
 constexpr int kHSlot = 96;
-// hierarchical one-kernel form (64 local ranks): tree -> mem_2D across GPUs -> broadcast with LL
-// (push) hand-offs: ll[q] = GPU q's LL area for this parity, [inbox box_words words][result box
-// box_words words]; nranks <= 8; epoch grows by 1 per call
-int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   void* stream);
+// hierarchical one-kernel form (64 local ranks, k_hier_ws): tree -> mem_2D across GPUs -> broadcast
+// with LL (push) hand-offs: ll[q] = GPU q's LL area for this parity, [inbox box_words words][result
+// box box_words words]; nranks <= 8; epoch grows by 1 per call
 int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream);
-// the hierarchical step across consecutive buckets (k_hier_x): finishes `prev` (may be null)
-// and starts `cur` (may be null) in one launch; llc / llp: every GPU's LL area of cur's /
-// prev's parity; ALLRED_ERR_UNSUPPORTED beyond kHierXMaxTiles tiles per workgroup
-int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
-                  uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                  uint32_t* status, unsigned max_grid, void* stream);
 // the same step two buckets deep (k_hier_x2): starts `cur`, sums the owned tiles of the bucket
 // the previous launch started (llm non-null: its parity's LL areas), writes `old` (started two
 // launches ago; llo: its parity); the flush launch (cur null) also writes that middle bucket

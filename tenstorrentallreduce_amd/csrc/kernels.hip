@@ -1490,8 +1490,12 @@ bool launch_steps_reg(bool bo, int per_cu, uint16_t* ranks, uint64_t stride, int
     const int64_t early = tune(Tune::steps_early);
     const bool early_on = early == 2 || (early == 1 && units >= 256 * (uint64_t)per_cu);
     const int flags = (tune(Tune::steps_tab) ? 1 : 0) | (early_on ? 2 : 0);
-#define TSA_SR(PP, BOV, MW) hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, \
-                                               pairs, bv, slices, units, stamps, flags)
+#define TSA_SR(PP, BOV, MW) do { \
+        hipLaunchKernelGGL((k_steps_reg<PP, BOV, MW>), grid, dim3(256), 0, st, ranks, stride, tab, pairs, bv, slices, \
+                           units, stamps, flags); \
+        note_launch(reinterpret_cast<const void*>(&k_steps_reg<PP, BOV, MW>), "k_steps_reg<" #PP ", " #BOV ", " #MW ">", \
+                    grid.x, 256); \
+    } while (0)
 #define TSA_SRB(PP, BOV) do { if (per_cu >= 5) TSA_SR(PP, BOV, 5); else if (per_cu == 4) TSA_SR(PP, BOV, 4); \
                               else TSA_SR(PP, BOV, 3); } while (0)
 #define TSA_SRP(PP) do { if (bo) TSA_SRB(PP, true); else TSA_SRB(PP, false); } while (0)
@@ -1595,8 +1599,10 @@ int launch_tree_fused(uint16_t* ranks, uint64_t stride, size_t n, int total, con
     // per workgroup)
     if (whole_tiles && !host_memory && total == 64 && form == 0 && tiles >= 1024) {
         for_each_chunk(tiles, [&](uint64_t a, uint64_t b) {
-            hipLaunchKernelGGL((k_tree_lds_lag<64>), dim3(persistent_grid(b - a, 512)), dim3(kBlock), 0, st, ranks,
-                               stride, order, bv, a, b - a);
+            const unsigned grid = persistent_grid(b - a, 512);
+            hipLaunchKernelGGL((k_tree_lds_lag<64>), dim3(grid), dim3(kBlock), 0, st, ranks, stride, order, bv, a,
+                               b - a);
+            note_launch(reinterpret_cast<const void*>(&k_tree_lds_lag<64>), "k_tree_lds_lag<64>", grid, kBlock);
         });
         return last_error();
     }

@@ -16,8 +16,8 @@
 // same three phases as ONE kernel (k_peer_oneshot): workgroup g syncs only
 // with workgroup g of the peers, through per-workgroup flag slots.  With 64
 // local ranks per GPU the local tree and the broadcast join one kernel with LL
-// push hand-offs (k_hier_ll, k_hier_x, k_hier_x2; the LL boxes live in the
-// flag allocation behind the flags).
+// push hand-offs (k_hier_ws, or k_hier_x2 two buckets deep; their hand-off area
+// lives in the flag allocation behind the flags).
 // Windows are double-buffered by call parity: call k+2 can only overwrite a
 // window after every peer passed call k+1's first barrier, i.e. finished
 // reading call k's windows.
@@ -60,7 +60,7 @@ struct allred_peer {
     size_t ll_off = 0;
     uint64_t ll_box_words = 0;
     uint64_t* peer_ll[ALLRED_MAX_NODES] = {};
-    // the hierarchical forms' hand-off area (7 + 1 byte words, peer_kernels.hip h_word), behind
+    // the hierarchical forms' hand-off area (6 + 2-byte words, peer_kernels.hip h_pack), behind
     // the LL boxes: 2 parities x [inbox: tiles x kHSlot words][result box: same]
     size_t hl_off = 0;
     uint64_t hl_box_words = 0;
@@ -69,15 +69,10 @@ struct allred_peer {
     // range oldest (every call rewrites tiles [0, its tiles)); hier_area_prepare reads it
     std::vector<std::pair<uint64_t, uint32_t>> hl_stairs[2];
     uint64_t hl_clears = 0;         // barrier-protected clears of a parity's area so far
-    int hier_ll = 2;                // 0 off (launch form), 1 k_hier_ll (the step in one launch, LL push hand-offs), 2 k_hier_ws
+    int hier_ll = 1;                // 0 off (launch form), 1 k_hier_ws (the step in one launch, LL push hand-offs)
     uint32_t max_groups = 0;        // grid cap of the hierarchical one-kernel forms (0 = one grid per GPU)
     uint64_t lo_ll_max = 256u << 10;  // one-channel LO buckets up to this many bytes use k_peer_lo_ll
     uint64_t mem_ll_max = 256u << 10;  // mem_2D buckets up to this many bytes use k_peer_mem_ll
-    // allred_peer_allreduce_pipelined: a bucket started (its partials pushed) and not yet finished
-    bool pipe_pending = false;
-    uint32_t pipe_k = 0;            // that bucket's call number (epoch pipe_k + 1, LL parity pipe_k & 1)
-    uint16_t* pipe_buf = nullptr;   // that bucket, and its size: the next call must finish exactly it
-    uint64_t pipe_elems = 0;
     // allred_peer_allreduce_pipelined2: up to two started, unfinished buckets, older
     // first; with two, the older one's owned tiles are summed already
     int x2_n = 0;
@@ -272,17 +267,26 @@ void hier_area_note(allred_peer* p, uint64_t tiles, uint32_t k) {
     st.emplace_back(tiles, k);
 }
 
+// The call whose words are the oldest ones in slots [0, tiles) of a parity's area: the
+// newest call covering the highest written slot of the range, min(tiles, front's range) - 1
+// (the stairs' front covers the most slots; beyond them nothing was written since the last
+// clear).  A bucket larger than every entry therefore checks the front — the oldest call
+// still in the area — not nothing.  None: the area holds no word (nothing to clear).
+bool hier_area_oldest(const std::vector<std::pair<uint64_t, uint32_t>>& st, uint64_t tiles, uint32_t* call) {
+    if (st.empty() || tiles == 0) return false;
+    const uint64_t reach = tiles < st.front().first ? tiles : st.front().first;
+    for (auto it = st.rbegin(); it != st.rend(); ++it)
+        if (it->first >= reach) {
+            *call = it->second;
+            return true;
+        }
+    return false;   // unreachable: the front covers `reach`
+}
+
 int hier_area_prepare(allred_peer* p, uint64_t tiles, uint32_t k, void* stream) {
     auto& st = p->hl_stairs[k & 1u];
-    uint32_t newest = 0;
-    bool covered = false;
-    for (auto it = st.rbegin(); it != st.rend(); ++it)
-        if (it->first >= tiles) {
-            newest = it->second;
-            covered = true;
-            break;
-        }
-    if (covered && k - newest >= kHierWrapCalls) {
+    uint32_t oldest = 0;
+    if (hier_area_oldest(st, tiles, &oldest) && k - oldest >= kHierWrapCalls) {
         const uint32_t e = 2u * p->calls + 1u;   // barrier epochs: monotonic with every other barrier user
         int rc = launch_peer_barrier(p->peer_flags, p->nranks, p->rank, e, p->status, stream);
         if (rc != ALLRED_OK) return rc;
@@ -300,49 +304,9 @@ int hier_area_prepare(allred_peer* p, uint64_t tiles, uint32_t k, void* stream) 
 
 }  // namespace
 
-int allred_peer_allreduce_pipelined(allred_peer* p, uint16_t* cur, uint16_t* prev, uint64_t elems, int local_ranks,
-                                    int local_side, int local_algo, void* stream) {
-    if (!p || !p->connected || (!cur && !prev) || p->x2_n) return ALLRED_ERR_ARG;
-    const size_t n = (size_t)elems;
-    if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
-    if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * kHSlot > p->hl_box_words)
-        return ALLRED_ERR_UNSUPPORTED;
-    // prev must be the bucket the previous call started (same pointer, same size: the
-    // launch finishes prev with this call's tile count and owner split); a started
-    // bucket must be finished next
-    if (prev ? (!p->pipe_pending || p->pipe_k + 1u != p->calls || prev != p->pipe_buf || n != p->pipe_elems)
-             : p->pipe_pending)
-        return ALLRED_ERR_ARG;
-    const uint8_t* order = nullptr;
-    int st = local_tree_order(local_algo, local_side, local_ranks, &order);
-    if (st != ALLRED_OK) return st;
-    const uint32_t kc = p->calls, kp = p->pipe_k;
-    uint64_t* llc[ALLRED_MAX_NODES];
-    uint64_t* llp[ALLRED_MAX_NODES];
-    hier_areas(p, kc, llc);
-    hier_areas(p, kp, llp);
-    // cur's parity holds nothing pending (prev, if any, is on the other one)
-    if (cur && (st = hier_area_prepare(p, n / 256, kc, stream)) != ALLRED_OK) return st;
-    st = launch_hier_x(cur, prev, n, order, cur ? llc : nullptr, prev ? llp : nullptr, p->nranks, p->rank, n,
-                       p->hl_box_words, kc + 1u, kp + 1u, p->status, p->max_groups, stream);
-    if (st != ALLRED_OK) return st;
-    if (cur) {
-        p->pipe_k = kc;
-        p->pipe_pending = true;
-        p->pipe_buf = cur;
-        p->pipe_elems = n;
-        ++p->calls;
-    } else {
-        p->pipe_pending = false;
-        p->pipe_buf = nullptr;
-    }
-    p->last_all_peer = true;
-    return ALLRED_OK;
-}
-
 int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t elems, int local_ranks, int local_side,
                                      int local_algo, void* stream) {
-    if (!p || !p->connected || p->pipe_pending) return ALLRED_ERR_ARG;
+    if (!p || !p->connected) return ALLRED_ERR_ARG;
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (256 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     if (local_ranks != 64 || p->nranks > 8 || !p->flags_uncached || (n / 256) * kHSlot > p->hl_box_words)
@@ -393,23 +357,22 @@ int allred_peer_allreduce_pipelined2(allred_peer* p, uint16_t* cur, uint64_t ele
 int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int local_ranks, int local_side,
                           int local_algo, void* workspace, void* stream) {
     if (!p || !buf || !p->connected) return ALLRED_ERR_ARG;
-    if (p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;   // finish the pipelined sequence first
+    if (p->x2_n) return ALLRED_ERR_ARG;   // finish the pipelined sequence first
     const size_t n = (size_t)elems;
     if (n == 0 || n > p->max_elems || n % (8 * (size_t)p->nranks)) return ALLRED_ERR_ARG;
     uint16_t* bucket = buf;
     int st = ALLRED_OK;
     if (p->hier_ll && local_ranks == 64 && p->nranks <= 8 && p->flags_uncached && n % (256 * (size_t)p->nranks) == 0 &&
         (n / 256) * kHSlot <= p->hl_box_words) {
-        // the hierarchical step in one launch with LL (push) hand-offs (k_hier_ll): same bits
+        // the hierarchical step in one launch with LL (push) hand-offs (k_hier_ws): same bits
         const uint8_t* order = nullptr;
         st = local_tree_order(local_algo, local_side, local_ranks, &order);
         if (st != ALLRED_OK) return st;
         uint64_t* ll[ALLRED_MAX_NODES];
         hier_areas(p, p->calls, ll);
         if ((st = hier_area_prepare(p, n / 256, p->calls, stream)) != ALLRED_OK) return st;
-        st = (p->hier_ll == 2 ? launch_hier_ws : launch_hier_ll)(buf, n, order, ll, p->nranks, p->rank, n,
-                                                                 p->hl_box_words, p->calls + 1u, p->status,
-                                                                 p->max_groups, stream);
+        st = launch_hier_ws(buf, n, order, ll, p->nranks, p->rank, n, p->hl_box_words, p->calls + 1u, p->status,
+                            p->max_groups, stream);
         if (st != ALLRED_OK) return st;
         ++p->calls;
         p->last_all_peer = true;
@@ -452,7 +415,7 @@ int allred_peer_allreduce(allred_peer* p, uint16_t* buf, uint64_t elems, int loc
 int allred_peer_dist_allreduce(allred_peer* p, const allred_dist_desc* d, uint16_t* buf, void* workspace,
                                void* stream) {
     if (!p || !d || !buf || !p->connected) return ALLRED_ERR_ARG;
-    if (d->total_nodes != p->nranks || p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;
+    if (d->total_nodes != p->nranks || p->x2_n) return ALLRED_ERR_ARG;
     const size_t n = (size_t)d->elems;
     if (d->variant == ALLRED_MEM) {
         // the peer mem_2D kernels sum in fp32 with one rounding; the reference's bf16
@@ -515,7 +478,7 @@ int allred_peer_set_oneshot_max(allred_peer* p, uint64_t bytes) {
 
 int allred_peer_set_hier_ll(allred_peer* p, int enable) {
     if (!p) return ALLRED_ERR_ARG;
-    if (enable < 0 || enable > 2) return ALLRED_ERR_ARG;
+    if (enable < 0 || enable > 1) return ALLRED_ERR_ARG;
     p->hier_ll = enable;
     return ALLRED_OK;
 }
@@ -554,7 +517,7 @@ int allred_peer_status(allred_peer* p, uint32_t* out) {
 
 int allred_peer_clear_status(allred_peer* p) {
     if (!p) return ALLRED_ERR_ARG;
-    if (p->pipe_pending || p->x2_n) return ALLRED_ERR_ARG;   // a pipelined sequence is open: flush it first
+    if (p->x2_n) return ALLRED_ERR_ARG;   // a pipelined sequence is open: flush it first
     DeviceGuard guard(p->device);
     // the null stream only (no device-wide sync: other groups of this process may be mid-exchange)
     if (hipMemsetAsync(p->status, 0, 4, nullptr) != hipSuccess || hipStreamSynchronize(nullptr) != hipSuccess)

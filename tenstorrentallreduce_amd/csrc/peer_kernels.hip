@@ -447,29 +447,32 @@ __global__ __launch_bounds__(kBlock) void k_peer_sched_push(PeerPtrs pp, PeerSta
     }
 }
 
-// ---- hierarchical one-kernel form: 64 local ranks per GPU, LL (push) hand-offs
+// ---- hierarchical one-kernel forms: 64 local ranks per GPU, LL (push) hand-offs
 // The whole hierarchical step (local tree of the 64 virtual ranks -> mem_2D
 // across the W GPUs -> broadcast back to the 64 ranks) as ONE persistent
-// launch; the same bits as tree_reduce + the mem_2D exchange + broadcast
-// (fp32 owner first then ascending, one rounding).  Tile = 256 elements (512 B
-// per rank row); owner(t) = t / (tiles / W), the block ownership of
-// allred_mem_2D.  Every cross-GPU transfer is a PUSH of self-validating 8-byte
-// words (4 bytes of data + the call's epoch, RCCL's "LL" idea): the producer's
-// relaxed system-scope stores go straight into the consumer's uncached LL
-// area and the consumer polls its OWN memory until every word carries the
-// epoch.  No flag follows the data and no remote load is ever waited for, so
-// each hand-off costs one one-way xGMI trip.  (A per-tile flag form — publish,
-// then remote loads — ran 19.9 us at W = 1 and a pipelined LL form 17.8 us;
-// both were removed in round 5, profiles/README.md.)
-//   A (all my tiles, double-buffered LDS): tile t's partial -> owner o's inbox
-//     slot [t - o*tpo][me] (1 KiB of LL words per tile).
-//   R (my tiles that I own): poll the W slots, fp32 sum owner first then
+// launch (k_hier_ws), or pipelined two buckets deep (k_hier_x2); the same bits
+// as tree_reduce + the mem_2D exchange + broadcast (fp32 owner first then
+// ascending, one rounding).  Tile = 256 elements (512 B per rank row);
+// owner(t) = t / (tiles / W), the block ownership of allred_mem_2D.  Every
+// cross-GPU transfer is a PUSH of self-validating 8-byte words (data + the
+// call's epoch, RCCL's "LL" idea): the producer's relaxed system-scope stores
+// go straight into the consumer's uncached LL area and the consumer polls its
+// OWN memory until every word carries the epoch.  No flag follows the data and
+// no remote load is ever waited for, so each hand-off costs one one-way xGMI
+// trip.  Three roles per tile:
+//   A (every tile of the GPU): the local tree -> partial -> owner o's inbox
+//     slot [t - o*tpo][me].
+//   R (the tiles this GPU owns): poll the W slots, fp32 sum owner first then
 //     ascending, one rounding -> every GPU's result box [t].
-//   B (all my tiles): poll my result box [t], store to the 64 rank rows.
+//   B (every tile): poll the own result box [t], store to the 64 rank rows.
 // A never waits, R waits only for A, B only for R; the grid is resident (2
 // workgroups per CU), so every wait is reached and satisfied.  Epochs grow by
 // one per call and the LL areas alternate by call parity, so a word of an
-// earlier call never carries the awaited epoch.
+// earlier call never carries the awaited epoch.  (Retired forms and their
+// numbers, profiles/README.md: a per-tile flag form, 19.9 us at W = 1, and a
+// pipelined LL form, 17.8 us, in round 5; in round 6 k_hier_ll — A, R, B as
+// three phases of every workgroup, 16.2 us — and the one-deep pipeline k_hier_x,
+// 15.1-15.3 us, both behind k_hier_ws and k_hier_x2 in every measurement.)
 constexpr int kLLMaxGpus = 8;
 struct LLPtrs {
     uint64_t* ll[kLLMaxGpus];   // GPU q's LL area, this parity: [inbox: tiles x 128 words][result box: same]
@@ -625,149 +628,6 @@ struct HierTiles {
     __device__ int owner_of(uint64_t t) const { return (int)(t / tpo); }
 };
 
-// A of the one-launch forms for one reducing workgroup: its tiles' 64 rank rows
-// by LDS-DMA (double-buffered), the local tree out of LDS, each partial pushed
-// to its owner's inbox slot [t - o*tpo][me] as the 6 + 2-byte words (waves 0-2
-// one word of every column each, wave 3 none).  Never waits for a peer.
-__device__ __forceinline__ void hier_reduce(const HierTiles& ht, const uint16_t* __restrict__ ranks, uint64_t stride,
-                                            const uint8_t* __restrict__ order, const LLPtrs& lp, int W, int me,
-                                            uint32_t e8, uint4 (&buf)[2][64 * 32], uint4 (&part)[4 * 32],
-                                            uint8_t (&ord_lds)[ALLRED_MAX_NODES]) {
-    constexpr int P = 64, TV = 32, RPW = 16, LPL = 8, OPS = 8;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    uint32_t ob = 0;
-    if (w == 0) ob = order_byte_load(order, lane);
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
-    auto issue = [&](uint64_t t, int b) {
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) {
-            const int r = RPW * w + 2 * k + h;
-            const uint4* src = reinterpret_cast<const uint4*>(ranks + (uint64_t)r * stride) + t * TV + c;
-            lds_dma16(src, wbase + (uint32_t)(b * P * TV * 16 + 2 * k * TV * 16));
-        }
-    };
-    const int mine = ht.mine;
-    if (mine > 0) issue(ht.tile_a(0), 0);
-    if (w == 0) {   // the order byte (tile 0's loads may stay in flight); read after the loop's barrier
-        if (mine > 0) wait_vm<OPS>(); else wait_vm<0>();
-        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
-        ord_lds[lane] = (uint8_t)ob;
-    }
-    for (int j = 0; j < mine; ++j) {
-        // in flight after tile j's loads: this wave's LL store of tile j-1
-        if (j > 0 && w < 3) wait_vm<1>(); else wait_vm<0>();
-        lds_barrier();
-        if (j + 1 < mine) issue(ht.tile_a(j + 1), (j + 1) & 1);
-        const uint4* tile = buf[j & 1];
-        const uint64_t t = ht.tile_a(j);
-        const uint8_t* ord = ord_lds + RPW * w + LPL * h;
-        uint4 x[LPL];
-#pragma unroll
-        for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
-#pragma unroll
-        for (int s2 = 1; s2 < LPL; s2 *= 2)
-#pragma unroll
-            for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
-        const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
-        if (h == 0) part[w * TV + c] = pw;
-        lds_barrier();
-        // the partial -> its owner's inbox: wave w < 3 writing word w of every column (one store
-        // instruction; wave 3 none)
-        if (h == 0) {
-            const int o = ht.owner_of(t);
-            const uint4 res = add8(add8(part[0 * TV + c], part[1 * TV + c]), add8(part[2 * TV + c], part[3 * TV + c]));
-            const uint64_t slot = (t - (uint64_t)o * ht.tpo) * W + me;
-            if (w < 3)
-                __hip_atomic_store(lp.ll[o] + slot * kHSlot + 32 * w + c, h_pack(res, w, e8), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_hier_ll(uint16_t* __restrict__ ranks, uint64_t stride,
-                                                    const uint8_t* __restrict__ order, LLPtrs lp, int W, int me,
-                                                    uint64_t ntiles, uint64_t tiles_per_owner, uint64_t box_words,
-                                                    uint32_t epoch, uint32_t* status) {
-    constexpr int TV = 32, RPW = 16, OPS = 8;
-    const uint32_t e8 = h_epoch(epoch);
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][64 * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[4 * TV];
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane & 31, h = lane >> 5;
-    const HierTiles ht(blockIdx.x, gridDim.x, ntiles, tiles_per_owner, me);
-    const int mine = ht.mine;
-    auto tile_of = [&](int k) { return ht.tile_of(k); };
-    auto owner_of = [&](uint64_t t) { return ht.owner_of(t); };
-    uint64_t* const my_ll = lp.ll[me];
-    // ---- A: local trees, partials pushed to their owners
-    hier_reduce(ht, ranks, stride, order, lp, W, me, e8, buf, part, ord_lds);
-    __syncthreads();   // every wave is past A: buf may be reused below
-    uint4* xs = buf[0];   // [8][32] results of a batch
-    // ---- R + B, 8 tiles at a time; lane (jr, c) serves tile jr of the batch, column c.
-    // R: for a tile I own, the W partials of its column are polled from my inbox
-    // (all in flight at once), summed and pushed to every OTHER GPU's box; the
-    // result stays in the lane.  B: the owned tiles' 64 rank rows are written while
-    // every other tile's result is polled from my box, then those tiles' rows.  One poll round trip per
-    // batch for the owned tiles and one for the others; at W = 1 every tile is
-    // owned and B polls nothing.  B(batch k) waits only for R(batch k) of the
-    // owners (the same workgroup index there), which waits only for A.
-    constexpr int BB = 8;
-    for (int j0 = 0; j0 < mine; j0 += BB) {
-        const int nb = mine - j0 < BB ? mine - j0 : BB;
-        const int b = threadIdx.x >> 5;
-        const uint64_t t = tile_of(j0 + b);
-        const bool own = b < nb && owner_of(t) == me;
-        uint4 val = make_uint4(0, 0, 0, 0);
-        if (own) {
-            const uint64_t li = t - (uint64_t)me * tiles_per_owner;
-            uint64_t wr[kLLMaxGpus][3];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) h_load(my_ll + (li * W + src) * kHSlot, c, wr[src]);
-            uint4 y[kLLMaxGpus];
-#pragma unroll
-            for (int src = 0; src < kLLMaxGpus; ++src)
-                if (src < W) y[src] = h_take(wr[src], my_ll + (li * W + src) * kHSlot, c, e8, status);
-            val = owner_sum(y, W, me);
-#pragma unroll
-            for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                if (dst < W && dst != me) h_put(lp.ll[dst] + box_words + t * kHSlot, c, val, e8);
-        }
-        // every owned-tile push of this wave is issued before any of its result polls:
-        // a wave holds owned and other tiles, and a poll spinning ahead of the wave's
-        // own pushes could wait (circularly) for a GPU whose wave waits for those pushes
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        // the other GPUs' results: polls issued now, taken after the owned tiles' rows
-        // have gone out (their xGMI round trip overlaps those stores)
-        uint64_t wb[3];
-        if (!own && b < nb) h_load(my_ll + box_words + t * kHSlot, c, wb);
-        if (own) xs[b * 32 + c] = val;
-        __syncthreads();
-        auto store_batch = [&](bool owned) {   // the rows of the batch's owned / other tiles
-#pragma unroll
-            for (int bb = 0; bb < BB; ++bb) {
-                if (bb >= nb) break;
-                if ((owner_of(tile_of(j0 + bb)) == me) != owned) continue;
-                const uint4 rv = xs[bb * 32 + c];
-                const uint64_t v0 = tile_of(j0 + bb) * TV;
-#pragma unroll
-                for (int k = 0; k < OPS; ++k) {
-                    const int r = RPW * w + 2 * k + h;
-                    st_nt(reinterpret_cast<uint4*>(ranks + (uint64_t)r * stride) + v0 + c, rv);
-                }
-            }
-        };
-        store_batch(true);
-        if (!own && b < nb) xs[b * 32 + c] = h_take(wb, my_ll + box_words + t * kHSlot, c, e8, status);
-        __syncthreads();
-        store_batch(false);
-        __syncthreads();   // xs is reused by the next batch
-    }
-}
-
 __device__ __forceinline__ uint4 shfl4(uint4 v, int src) {
     return make_uint4((uint32_t)__shfl((int)v.x, src), (uint32_t)__shfl((int)v.y, src), (uint32_t)__shfl((int)v.z, src),
                       (uint32_t)__shfl((int)v.w, src));
@@ -776,18 +636,18 @@ __device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
     return (uint64_t)(uint32_t)__shfl((int)(uint32_t)v, src) | ((uint64_t)(uint32_t)__shfl((int)(v >> 32), src) << 32);
 }
 
-// k_hier_ws: the step of k_hier_ll (same hand-offs across GPUs, same bits) with
-// its two HBM phases on different waves of one workgroup, so every CU reads and
-// writes at once.  k_hier_ll's workgroups read all their tiles, then write
-// them: the chip reads, then writes (16.2 us at W = 1 against 14.2 for the
-// fused one-GPU pass, which interleaves a tile's stores with later tiles'
-// loads).  A workgroup has 2 * NQ waves and no barrier after its start; the
+// k_hier_ws: the hierarchical step in one launch with its two HBM phases on
+// different waves of one workgroup, so every CU reads and writes at once (a
+// workgroup that reads all its tiles, then writes them — round 4's k_hier_ll —
+// makes the chip read, then write: 16.2 us at W = 1 against 14.2 for the fused
+// one-GPU pass, which interleaves a tile's stores with later tiles' loads).
+// A workgroup has 2 * NQ waves and no barrier after its start; the
 // tile's 32 columns (16 bytes each) split into NQ = 32 / CW groups of CW:
 //   wave q < NQ (A) reduces columns CW q .. CW q + CW - 1 of the workgroup's
 //     tiles on its own: LDS-DMA of those columns of the 64 rank rows into its
 //     own two buffers (one tile ahead), CW leaves per lane (lane = leaf group g
 //     x column c) and the tree's last levels across lanes (xor CW .. 32 — the
-//     tree and operand order of k_hier_ll, whose lanes hold 8 leaves each).  A
+//     tree and operand order of k_hier_x2 and tree_reduce, 8 leaves a lane).  A
 //     partial another GPU owns is pushed to its inbox (the 6 + 2-byte words,
 //     one per lane); an owned one goes to an LDS slot for wave q + NQ (the
 //     first kWsRing owned tiles; later ones through the own inbox), so at W = 1
@@ -888,7 +748,7 @@ __global__ __launch_bounds__(128 * (32 / CW), (CW == 8 ? 4 : CW == 16 ? 2 : 1)) 
                 for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
 #pragma unroll
             for (int m = CW; m < 64; m *= 2) x[0] = add8(x[0], shfl_xor4(x[0], m));
-            const uint4 pr = CW == 32 ? x[0] : shfl4(x[0], cc);   // leaf group 0's sum: k_hier_ll's operand order
+            const uint4 pr = CW == 32 ? x[0] : shfl4(x[0], cc);   // leaf group 0's sum: k_hier_x2's operand order
             const uint64_t t = ht.tile_a(j);
             const int o = ht.owner_of(t);
             if (o == me && ko < kWsRing) {
@@ -992,201 +852,13 @@ __global__ __launch_bounds__(128 * (32 / CW), (CW == 8 ? 4 : CW == 16 ? 2 : 1)) 
                 moved = true;
             }
         }
-        if (!moved) {
+        if (moved) {
+            spin = 0;   // progress: the next wait gets a bound of its own (t0 re-armed), like h_get's
+        } else {
             if (peer_give_up(spin++, t0, status)) break;
             __builtin_amdgcn_s_sleep(1);
         }
     }
-}
-
-// ---- hierarchical step across consecutive buckets ----------------------------
-// k_hier_x: one launch finishes bucket `prev` and starts bucket `cur` (same
-// hand-offs and bits as k_hier_ll; the caller pipelines a sequence of buckets:
-// (cur 0, -), (cur 1, prev 0), ..., (-, prev K-1)).  Within one bucket the
-// read phase (tree -> partial) must finish on every GPU before its write phase
-// (result -> 64 rank rows) can start, so k_hier_ll reads only, then writes only
-// (17.6 us at W = 1 vs 14.1 for the fused one-GPU pass).  Across buckets there
-// is no such dependency: this launch streams cur's tiles in (LDS-DMA, two
-// tiles ahead, tree, partial pushed to the tile's owner) while writing prev's
-// tiles out, interleaved op by op as in k_tree_lds_lag.  Order in a launch:
-//   L(cur 0), L(cur 1) issued (HBM busy from the start), then prev's results
-//            of this workgroup's tiles polled into LDS (the owners pushed them
-//            at the end of the previous launch)
-//   loop j:  A(cur j) [tree, partial -> owner] | S(prev j) stores interleaved
-//            with L(cur j+2)
-//   R(cur)   the tiles of cur this GPU owns: the W partials (pushed during
-//            this launch's loops) polled, summed (fp32, owner first, one
-//            rounding), the result pushed to every GPU's box
-// Any number of tiles per workgroup: prev's results are staged in LDS chunks of
-// kHierXChunk tiles (lanes (j, c) of the whole workgroup serve tile j of a
-// chunk), two chunks resident — chunk k + 1 is polled when the row stores of
-// chunk k begin, into the slot chunk k - 1 left — and R(cur) runs chunk by
-// chunk.  Every poll waits for work that waits on nothing of the poller (the
-// results: the owners' previous launches; R(cur): every GPU's loop of this
-// launch, which polls only results of the previous launch), and the grid is
-// resident, so every wait is satisfied.
-constexpr int kHierXChunk = 8;
-
-// LAG (tune hier_x_lag): prev's / old's tile rows stored in the iteration of cur's tile j - LAG
-// (LAG 1: every workgroup's first loads go out ahead of any row store, the k_tree_bcast_x<1> order).
-// CH: the chunked form (a workgroup with more than kHierXChunk tiles); !CH holds one chunk's
-// results and none of the chunk bookkeeping (the launcher picks it when every workgroup has
-// at most kHierXChunk tiles: the staging costs ~0.3 us a launch at W = 1, profiles/r04_hier_x_chunk_ab.txt)
-// RE (LL form, LAG 1), bit 0 (tune hier_x_rearly): R(cur) ahead of prev's last tile's row stores, so
-// its polls and result pushes overlap those stores instead of queueing behind them; bit 1 (tune
-// hier_x_latepoll): prev's results polled after tile 0's tree (they are first read by iteration 1's
-// stores) instead of at the start, where the polls' wait also waited for tile 1's loads
-template <int LAG, bool CH, int RE>
-__global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, uint16_t* __restrict__ prev,
-                                                   uint64_t stride, const uint8_t* __restrict__ order, LLPtrs lc,
-                                                   LLPtrs lpv, int W, int me, uint64_t ntiles, uint64_t tiles_per_owner,
-                                                   uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                                                   uint32_t* status) {
-    const uint32_t e8c = h_epoch(ecur), e8p = h_epoch(eprev);
-    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
-    __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
-    __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
-    __shared__ __attribute__((aligned(16))) uint4 res[CH ? 2 : 1][kHierXChunk][TV];   // two chunks of prev's results
-    __shared__ __attribute__((aligned(16))) uint8_t ord_lds[ALLRED_MAX_NODES];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c = lane % TV, q = lane / TV;
-    const uint32_t wbase = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)&buf[0][0] + (uint32_t)(RPW * w * TV * 16));
-    const uint64_t row_off = (uint64_t)(RPW * w + q) * stride;   // + RPI * k * stride for op k
-    const uint64_t G = gridDim.x;
-    const int mine = blockIdx.x < ntiles ? (int)((ntiles - 1 - blockIdx.x) / G + 1) : 0;
-    auto tile_of = [&](int j) { return blockIdx.x + (uint64_t)j * G; };
-    auto owner_of = [&](uint64_t t) { return (int)(t / tiles_per_owner); };
-    auto issue = [&](uint64_t t, int b) {
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + t * TV + c,
-                      wbase + (uint32_t)(b * P * TV * 16 + RPI * k * TV * 16));
-    };
-    uint32_t ob = 0;
-    if (w == 0) ob = order_byte_load(order, lane);
-    if (cur && mine > 0) issue(tile_of(0), 0);
-    if (cur && mine > 1) issue(tile_of(1), 1);
-    if (w == 0) {   // the order byte only (the tiles' loads stay in flight)
-        wait_any((cur && mine > 0 ? OPS : 0) + (cur && mine > 1 ? OPS : 0));
-        asm volatile("" : "+v"(ob));   // no use of ob may move above the wait
-        ord_lds[lane] = (uint8_t)ob;
-    }
-    // ---- prev's results of this workgroup's tiles -> LDS: lane (jr, c) (32 jr + c)
-    // serves tile jr of a chunk, column c.  The owners pushed them at the end of the
-    // previous launch; the loads queue behind L(0), L(1) (in-order vmcnt), which keep
-    // HBM busy.  Chunks 0 and 1 now, chunk k + 1 when chunk k's row stores begin.
-    const int jr = threadIdx.x / TV;
-    // tile j's results in LDS, column c
-    auto rslot = [&](int j) { return CH ? res[(j / kHierXChunk) & 1][j % kHierXChunk][c] : res[0][j][c]; };
-    auto poll_prev = [&](int ch) {
-        const int j = ch * kHierXChunk + jr;
-        if (j >= mine) return;
-        uint4& slot = res[CH ? ch & 1 : 0][jr][c];
-        const uint64_t* at = lpv.ll[me] + box_words + tile_of(j) * kHSlot;
-        uint64_t wd[3];
-        h_load(at, c, wd);
-        slot = h_take(wd, at, c, e8p, status);
-    };
-    // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
-    const bool lp = (RE & 2) && LAG == 1 && cur;
-    if (prev && !lp) {
-        poll_prev(0);
-        if (CH && mine > kHierXChunk) poll_prev(1);
-    }
-    lds_barrier();   // order bytes (and results) in LDS
-    for (int j = 0; j < mine; ++j) {
-        if (cur) {   // ---- A(cur j)
-            // after L(j): the last row store interleaved behind it (of prev's tile j-2-LAG), this
-            // wave's partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
-            wait_any((j >= 2 + LAG && prev ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && prev ? OPS : 0) +
-                     (j >= 1 && w < 3 ? 1 : 0));
-            lds_barrier();   // tile j is in LDS
-            const uint4* tile = buf[j & 1];
-            const uint8_t* ord = ord_lds + RPW * w + LPL * q;
-            uint4 x[LPL];
-#pragma unroll
-            for (int i = 0; i < LPL; ++i) x[i] = tile[(int)ord[i] * TV + c];
-#pragma unroll
-            for (int s2 = 1; s2 < LPL; s2 *= 2)
-#pragma unroll
-                for (int i = 0; i < LPL; i += 2 * s2) x[i] = add8(x[i], x[i + s2]);
-            const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
-            if (q == 0) part[j & 1][w * TV + c] = pw;
-            lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            // the partial -> its owner's inbox: wave w < 3 writing word w of every column (one
-            // store instruction; wave 3 none)
-            if (q == 0) {
-                const uint64_t t = tile_of(j);
-                const int o = owner_of(t);
-                const uint4* pt = part[j & 1];
-                const uint4 pr = add8(add8(pt[0 * TV + c], pt[1 * TV + c]), add8(pt[2 * TV + c], pt[3 * TV + c]));
-                const uint64_t slot = (t - (uint64_t)o * tiles_per_owner) * W + me;
-                if (w < 3)
-                    __hip_atomic_store(lc.ll[o] + slot * kHSlot + 32 * w + c, h_pack(pr, w, e8c), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-        }
-        if (lp && j == 0 && prev) {   // read first by iteration 1's stores, behind its A-phase barrier
-            poll_prev(0);
-            if (CH && mine > kHierXChunk) poll_prev(1);
-        }
-        // ---- cur's tile j+2 in, prev's tile j - LAG out, interleaved op by op
-        const int sj = j - LAG;   // the tile whose rows this iteration stores
-        if (CH && prev && sj >= kHierXChunk && sj % kHierXChunk == 0) {
-            // chunk sj / 8 begins: every wave is past the reads of chunk sj / 8 - 1 (A's
-            // barrier, or this one in a flush launch), whose slot takes chunk sj / 8 + 1
-            if (!cur) lds_barrier();
-            poll_prev(sj / kHierXChunk + 1);
-        }
-        const uint64_t tl = tile_of(j + 2), ts = tile_of(sj);
-        const uint32_t bl = wbase + (uint32_t)((j & 1) * P * TV * 16);
-        const bool st = prev && sj >= 0;
-        const uint4 rv = st ? rslot(sj) : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = 0; k < OPS; ++k) {
-            if (cur && j + 2 < mine)
-                lds_dma16(reinterpret_cast<const uint4*>(cur + row_off + (uint64_t)(RPI * k) * stride) + tl * TV + c,
-                          bl + (uint32_t)(RPI * k * TV * 16));
-            if (st) st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
-        }
-    }
-    // ---- R(cur): the tiles of cur this GPU owns, once every GPU has pushed its
-    // partial (during this launch's loop): W partials summed (fp32, owner first,
-    // one rounding), the result pushed to every GPU's box for the next launch.
-    auto r_cur = [&]() {
-        for (int j0 = 0; cur && j0 < mine && (CH || j0 == 0); j0 += kHierXChunk) {
-            if (j0 + jr >= mine) break;
-            const uint64_t t = tile_of(j0 + jr);
-            if (owner_of(t) == me) {
-                const uint64_t lr = t - (uint64_t)me * tiles_per_owner;
-                uint4 y[kLLMaxGpus];
-                uint64_t wr[kLLMaxGpus][3];
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) h_load(lc.ll[me] + (lr * W + src) * kHSlot, c, wr[src]);
-#pragma unroll
-                for (int src = 0; src < kLLMaxGpus; ++src)
-                    if (src < W) y[src] = h_take(wr[src], lc.ll[me] + (lr * W + src) * kHSlot, c, e8c, status);
-                const uint4 o = owner_sum(y, W, me);
-#pragma unroll
-                for (int dst = 0; dst < kLLMaxGpus; ++dst)
-                    if (dst < W) h_put(lc.ll[dst] + box_words + t * kHSlot, c, o, e8c);
-            }
-        }
-    };
-    if constexpr ((RE & 1) != 0) r_cur();
-    if (LAG && prev && mine > 0) {   // prev's last tile
-        // a flush launch has no other barrier behind its chunk's poll, nor a one-tile workgroup
-        // behind its late polls (iteration 0 is its only A phase)
-        if (!cur || (lp && mine == 1)) lds_barrier();
-        const uint4 rv = rslot(mine - 1);
-        const int sj = mine - 1;
-#pragma unroll
-        for (int k = 0; k < OPS; ++k)
-            st_nt(reinterpret_cast<uint4*>(prev + row_off + (uint64_t)(RPI * k) * stride) + tile_of(sj) * TV + c, rv);
-    }
-    if constexpr ((RE & 1) == 0) r_cur();
 }
 
 // ---- hierarchical step, two-deep bucket pipeline ----------------------------
@@ -1196,34 +868,41 @@ __global__ __launch_bounds__(kBlock) void k_hier_x(uint16_t* __restrict__ cur, u
 // bucket i-2 (old: its results were pushed during launch i-1).  Every poll of
 // launch i waits for pushes of launch i-1, never for one of its own launch, so
 // a GPU that starts its launch late (launch jitter, a slower peer) costs the
-// others nothing as long as it is less than a launch behind; k_hier_x (one
-// bucket deep) polls at the end of every launch for partials pushed during it.
-// Order in a launch:
-//   L(cur 0), L(cur 1) issued (HBM busy from the start); the polls of mid's
-//            owned partials and of old's results of this workgroup's tiles, all
-//            in flight together; mid's owned sums pushed to every GPU's box
-//   loop j:  A(cur j) [tree, partial -> owner] | S(old j) stores interleaved
-//            with L(cur j+2)
+// others nothing as long as it is less than a launch behind.  Within one
+// bucket the read phase (tree -> partial) must finish on every GPU before its
+// write phase (result -> 64 rank rows) can start; across buckets there is no
+// such dependency, so a launch streams cur's tiles in while old's tiles go out,
+// interleaved op by op as in k_tree_lds_lag.  Order in a launch:
+//   L(cur 0), L(cur 1) issued (HBM busy from the start)
+//   loop j:  A(cur j) [tree, partial -> owner] | S(old j - 1) stores
+//            interleaved with L(cur j+2); in A(cur 0), between tile 0's tree
+//            and its partial push, old's results of this workgroup's tiles
+//            polled into LDS (behind a workgroup barrier, see below); before
+//            the last iteration's row stores, mid's owned sums (polls of its W
+//            partials, sum, result pushed to every GPU's box), so their xGMI
+//            trips overlap those stores
 //   fin:     (the flush launch, cur null) mid's results — pushed by the owned
-//            sums at the start of every GPU's flush launch — polled, mid's rows
-//            written
-// (the order of the TAIL 0 form without late polls; TAIL 1 / 2 move the owned
-// sums to the launch end / ahead of its last row stores, and late polls
-// (TAIL & 4, the default with TAIL 2) move old's result polls into A(cur 0),
-// between tile 0's tree and its partial push, behind a workgroup barrier)
+//            sums of every GPU's flush launch — polled, mid's rows written
 // Hand-offs per tile are ordered by the workgroup that serves the tile on every
 // GPU (the same index): GPU g polls old = bucket i-2's result of tile t before
 // it pushes bucket i's partial of t, and the owner reads bucket i's partials of
 // t (launch i+1) before it pushes bucket i's result of t, so LL parity k & 1
 // (inbox and box) is reused only after its previous reader is done.
-// Any number of tiles per workgroup, in chunks of kHierXChunk as in k_hier_x:
-// mid's owned sums chunk by chunk, old's results two chunks resident (chunk k
-// + 1 polled when chunk k's row stores begin — before cur's partial of any of
-// its tiles is pushed, so the order above holds per tile).
-// Same bits as k_hier_ll / k_hier_x.
-// TAIL & 3: 0 mid's owned sums at the launch start, 1 at its end, 2 before its last row stores;
-// TAIL & 4 (LAG 1, tune hier_x_latepoll): old's results polled after tile 0's tree, not at the start
-template <int TAIL, int LAG, bool CH>
+// Any number of tiles per workgroup: with CH old's results are staged in LDS
+// chunks of kHierXChunk tiles (lanes (j, c) of the whole workgroup serve tile j
+// of a chunk), two chunks resident — chunk k + 1 is polled when the row stores
+// of chunk k begin, into the slot chunk k - 1 left, before cur's partial of any
+// of its tiles is pushed (the order above holds per tile) — and mid's owned
+// sums run chunk by chunk; the launcher picks CH above kHierXChunk tiles per
+// workgroup (a capped grid: processes sharing a GPU), since the bookkeeping
+// costs 0.15-0.3 us at one chunk (profiles/r04_hier_x_chunk_ab.txt).
+// Same bits as k_hier_ws and the launch form.  (Round-4/5 placements measured
+// and retired with their tune keys in round 6, profiles/README.md: the owned
+// sums at the start / the end of a launch, the result polls at the start, a
+// tile's row stores in its own iteration.)
+constexpr int kHierXChunk = 8;
+
+template <bool CH>
 __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, uint16_t* __restrict__ old,
                                                     uint16_t* __restrict__ fin, uint64_t stride,
                                                     const uint8_t* __restrict__ order, LLPtrs lc, LLPtrs lm, LLPtrs lo,
@@ -1231,12 +910,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                                     uint64_t box_words, uint32_t ecur, uint32_t emid, uint32_t eold,
                                                     int has_mid, uint32_t* status) {
     const uint32_t e8c = h_epoch(ecur), e8m = h_epoch(emid), e8o = h_epoch(eold);
-    // TAIL 2 (tune hier_x2_tail=2, LL hand-offs): the owned sums run before the last iteration's row
-    // stores, not after them
-    constexpr bool tl2 = (TAIL & 3) == 2;
-    // late polls: not in a flush launch (no A phase, so no barrier between the polls and the reads)
-    const bool lp = (TAIL & 4) && LAG == 1 && cur;
-    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS;
+    // late polls (old's results in A(cur 0)); a flush launch (no A phase) polls at its start
+    const bool lp = cur != nullptr;
+    constexpr int P = 64, NW = 4, TV = 32, RPI = 2, RPW = P / NW, OPS = RPW / RPI, LPL = OPS, LAG = 1;
     __shared__ __attribute__((aligned(16))) uint4 buf[2][P * TV];
     __shared__ __attribute__((aligned(16))) uint4 part[2][NW * TV];
     __shared__ __attribute__((aligned(16))) uint4 res[CH ? 2 : 1][kHierXChunk][TV];   // two chunks of results
@@ -1304,29 +980,17 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
         h_load(at, c, wd);
         slot = h_take(wd, at, c, e8o, status);
     };
-    {
-        uint64_t wo[3];
-        const bool early_old = old && !lp;   // lp: polled in A(cur 0), ahead of its partial push
-        if (early_old && act_in(0)) h_load(lo.ll[me] + box_words + tile_of(jr) * kHSlot, c, wo);
-        if ((TAIL & 3) == 0)
-            for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
-        if (early_old && act_in(0))
-            res[0][jr][c] = h_take(wo, lo.ll[me] + box_words + tile_of(jr) * kHSlot, c, e8o, status);
-        if (CH && early_old && nch > 1) poll_old(1);
+    if (old && !lp) {   // the flush launch: old's results at the start (no A phase to hide them behind)
+        poll_old(0);
+        if (CH && nch > 1) poll_old(1);
     }
-    // the owned-sum pushes of this wave, still in flight behind L(cur 0), L(cur 1)
-    // (the polls before them have returned, and with them both tiles' loads).  With
-    // several chunks an earlier chunk's pushes may be in flight too: counting none
-    // only waits longer (the loads of tile j are never waited for too little)
-    const int pushed = (TAIL & 3) == 0 && nch == 1 && __ballot(rmid_in(0)) != 0 ? 3 * W : 0;
-    lds_barrier();   // order bytes and old's results in LDS
+    lds_barrier();   // order bytes (and a flush launch's results) in LDS
     for (int j = 0; j < mine; ++j) {
         if (cur) {   // ---- A(cur j)
             // after L(j): the last row store interleaved behind it (old's tile j-2-LAG), this wave's
-            // partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG), this
-            // wave's owned-sum pushes (j < 2)
+            // partial word of tile j-1, L(j+1), the row stores of iteration j-1 (tile j-1-LAG)
             wait_any((j >= 2 + LAG && old ? 1 : 0) + (j + 1 < mine ? OPS : 0) + (j - 1 >= LAG && old ? OPS : 0) +
-                     (j >= 1 && w < 3 ? 1 : 0) + (j < 2 ? pushed : 0));
+                     (j >= 1 && w < 3 ? 1 : 0));
             lds_barrier();   // tile j is in LDS
             const uint4* tile = buf[j & 1];
             const uint8_t* ord = ord_lds + RPW * w + LPL * q;
@@ -1340,9 +1004,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             const uint4 pw = add8(x[0], shfl_xor4(x[0], 32));
             if (q == 0) part[j & 1][w * TV + c] = pw;
             lds_barrier();   // partials in; every wave has read tile j out of buf[j & 1]
-            // lp: old's results of chunks 0 (and 1), ahead of this launch's first partial push (the
+            // old's results of chunks 0 (and 1), ahead of this launch's first partial push (the
             // order above holds per tile); first read by iteration 1's stores, behind its A barrier
-            if (lp && j == 0 && old) {
+            if (j == 0 && old) {
                 poll_old(0);
                 if (CH && nch > 1) poll_old(1);
                 // every wave's polls have read their slots before ANY wave pushes a word of this
@@ -1351,7 +1015,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                 // exists (the owner read the slot's previous partial first).  vmcnt(0): relaxed
                 // atomics to different addresses are not ordered; the barrier: the other waves
                 // (only the lanes of a chunk's tiles poll).  Costs little the polls' own wait did
-                // not (they were issued behind L(1))
+                // not (they were issued behind L(1)); profiles/r04_hier_latepoll_ab.txt
                 wait_vm<0>();
                 lds_barrier();
             }
@@ -1368,9 +1032,9 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
                                        __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
-        // tl2: mid's owned sums ahead of the last iteration's row stores, so their polls and pushes
+        // mid's owned sums ahead of the last iteration's row stores, so their polls and pushes
         // overlap those stores instead of queueing behind every store of the launch
-        if (tl2 && j == mine - 1)
+        if (j == mine - 1)
             for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
         // ---- cur's tile j+2 in, old's tile j - LAG out, interleaved op by op
         const int sj = j - LAG;   // the tile whose rows this iteration stores
@@ -1393,14 +1057,12 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
             if (st) st_nt(reinterpret_cast<uint4*>(old + row_off + (uint64_t)(RPI * k) * stride) + ts * TV + c, rv);
         }
     }
-    if (LAG && old && mine > 0) {   // old's last tile
+    if (old && mine > 0) {   // old's last tile
         // a flush launch has no other barrier behind its chunk's poll, nor a one-tile workgroup
         // behind its late polls
-        if (!cur || (lp && mine == 1)) lds_barrier();
+        if (!cur || mine == 1) lds_barrier();
         store_rows(old, mine - 1);
     }
-    if ((TAIL & 3) != 0 && (!tl2 || mine == 0))   // TAIL: mid's partials arrived during the launch i-1
-        for (int ch = 0; ch < nch; ++ch) owned_sums(ch);
     if (fin) {   // ---- the flush launch: mid's results (every GPU summed its owned tiles above)
         for (int ch = 0; ch < nch; ++ch) {
             __syncthreads();   // every wave has read the slot's previous results
@@ -1638,23 +1300,6 @@ int launch_peer_lo_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket,
     return peer_last_error();
 }
 
-int launch_hier_ll(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
-                   size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
-                   void* stream) {
-    const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || !aligned16(ranks) ||
-        ntiles * kHSlot > box_words)
-        return ALLRED_ERR_ARG;
-    LLPtrs lp{};
-    for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
-    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
-    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    hipLaunchKernelGGL(k_hier_ll, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks,
-                       me, ntiles, ntiles / nranks, box_words, epoch, status);
-    return peer_last_error();
-}
-
 int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint64_t* const* ll, int nranks, int me,
                    size_t n, uint64_t box_words, uint32_t epoch, uint32_t* status, unsigned max_grid,
                    void* stream) {
@@ -1674,43 +1319,10 @@ int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
                                                  : (a2 ? k_hier_ws<2, 8> : k_hier_ws<1, 8>);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(128 * (32 / cw)), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
                        ntiles, ntiles / nranks, box_words, epoch, status);
-    return peer_last_error();
-}
-
-int launch_hier_x(uint16_t* cur, uint16_t* prev, uint64_t stride, const uint8_t* order, uint64_t* const* llc,
-                  uint64_t* const* llp, int nranks, int me, size_t n, uint64_t box_words, uint32_t ecur, uint32_t eprev,
-                  uint32_t* status, unsigned max_grid, void* stream) {
-    const uint64_t nv = n / 8, ntiles = nv / 32;
-    if (nranks < 1 || nranks > kLLMaxGpus || nv % 32 || ntiles % nranks || stride % 8 || ntiles * kHSlot > box_words ||
-        (!cur && !prev) || (cur && !aligned16(cur)) || (prev && !aligned16(prev)))
-        return ALLRED_ERR_ARG;
-    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
-    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
-    LLPtrs lc{}, lp{};
-    for (int q = 0; q < nranks; ++q) {
-        lc.ll[q] = llc ? llc[q] : nullptr;
-        lp.ll[q] = llp ? llp[q] : nullptr;
-    }
-    const bool lag = tune(Tune::hier_x_lag) != 0;
-    const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    const int re = lag ? (tune(Tune::hier_x_rearly) ? 1 : 0) | (tune(Tune::hier_x_latepoll) ? 2 : 0) : 0;
-    decltype(&k_hier_x<0, false, 0>) kern;
-    switch ((lag ? 2 : 0) + (ch ? 1 : 0) + re * 4) {
-        case 15: kern = k_hier_x<1, true, 3>; break;
-        case 14: kern = k_hier_x<1, false, 3>; break;
-        case 11: kern = k_hier_x<1, true, 2>; break;
-        case 10: kern = k_hier_x<1, false, 2>; break;
-        case 7: kern = k_hier_x<1, true, 1>; break;
-        case 6: kern = k_hier_x<1, false, 1>; break;
-        case 3: kern = k_hier_x<1, true, 0>; break;
-        case 2: kern = k_hier_x<1, false, 0>; break;
-        case 1: kern = k_hier_x<0, true, 0>; break;
-        default: kern = k_hier_x<0, false, 0>; break;
-    }
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0,
-                       (hipStream_t)stream, cur, prev, stride, order, lc, lp, nranks, me, ntiles, ntiles / nranks,
-                       box_words, ecur, eprev, status);
+    static const char* const names[2][3] = {{"k_hier_ws<1, 8>", "k_hier_ws<1, 16>", "k_hier_ws<1, 32>"},
+                                            {"k_hier_ws<2, 8>", "k_hier_ws<2, 16>", "k_hier_ws<2, 32>"}};
+    note_launch(reinterpret_cast<const void*>(kern), names[a2 ? 1 : 0][cw == 8 ? 0 : cw == 16 ? 1 : 2], grid,
+                128 * (32 / cw));
     return peer_last_error();
 }
 
@@ -1732,36 +1344,12 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         lm.ll[q] = llm ? llm[q] : nullptr;
         lo.ll[q] = llo ? llo[q] : nullptr;
     }
-    // + 4: late result polls (lag 1)
-    const int tail = (int)tune(Tune::hier_x2_tail);
-    const int lag = tune(Tune::hier_x_lag) ? 1 : 0;
-    const int late = lag && tune(Tune::hier_x_latepoll) ? 4 : 0;
-    const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk || tune(Tune::hier_x_chunked) != 0;
-    decltype(&k_hier_x2<0, 0, false>) kern = nullptr;
-    // index: (tail + late) x 4 + lag x 2 + chunked
-    switch ((tail + late) * 4 + lag * 2 + (ch ? 1 : 0)) {
-        case 0: kern = k_hier_x2<0, 0, false>; break;
-        case 1: kern = k_hier_x2<0, 0, true>; break;
-        case 2: kern = k_hier_x2<0, 1, false>; break;
-        case 3: kern = k_hier_x2<0, 1, true>; break;
-        case 4: kern = k_hier_x2<1, 0, false>; break;
-        case 5: kern = k_hier_x2<1, 0, true>; break;
-        case 6: kern = k_hier_x2<1, 1, false>; break;
-        case 7: kern = k_hier_x2<1, 1, true>; break;
-        case 8: kern = k_hier_x2<2, 0, false>; break;
-        case 9: kern = k_hier_x2<2, 0, true>; break;
-        case 10: kern = k_hier_x2<2, 1, false>; break;
-        case 11: kern = k_hier_x2<2, 1, true>; break;
-        case 18: kern = k_hier_x2<4, 1, false>; break;
-        case 19: kern = k_hier_x2<4, 1, true>; break;
-        case 22: kern = k_hier_x2<5, 1, false>; break;
-        case 23: kern = k_hier_x2<5, 1, true>; break;
-        case 26: kern = k_hier_x2<6, 1, false>; break;
-        case 27: kern = k_hier_x2<6, 1, true>; break;
-        default: return ALLRED_ERR_ARG;
-    }
+    // the chunked form only where a workgroup has more than one chunk of tiles
+    const bool ch = (ntiles + grid - 1) / grid > (uint64_t)kHierXChunk;
+    decltype(&k_hier_x2<false>) kern = ch ? k_hier_x2<true> : k_hier_x2<false>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, cur, old, fin, stride, order, lc, lm, lo, nranks, me, ntiles, ntiles / nranks,
                        box_words, ecur, emid, eold, llm ? 1 : 0, status);
+    if (cur) note_launch(reinterpret_cast<const void*>(kern), ch ? "k_hier_x2<chunked>" : "k_hier_x2", grid, kBlock);
     return peer_last_error();
 }
 

@@ -34,19 +34,14 @@ const Key kKeys[] = {
     {"lo_dag_reg_min_tiles", 64, 1, 1ll << 40},   // 256-element tiles per rank (64: 32 kB)
     {"check", 0, 0, 1},               // N > 1 programs: verify against the partners', poison receive regions
     {"fused_chunk_tiles", 1280, 0, 1ll << 40},   // persistent fused passes: tiles per launch (0: one launch)
-    {"hier_x2_tail", 2, 0, 2},        // k_hier_x2: owned sums at the start | 1 the end of the launch | 2 before its last row stores
     {"lo_tree_min_tiles", 64, 0, 1ll << 40},   // 64-rank rank-uniform LO: tree pass from this many 256-element tiles
     {"tree_bcast_lag", 1, 0, 1},      // k_tree_bcast_x: the row stores one iteration behind the tree (0: same iteration)
     {"tree_bcast_bal", 0, 0, 1},      // k_tree_bcast_x: every wave stages / stores 8 result columns (0: wave 0 all)
-    {"hier_x_lag", 1, 0, 1},          // k_hier_x / k_hier_x2: a tile's row stores one iteration behind its tree (0: with it)
     {"steps_groups", 0, 0, 5},        // k_steps_reg: workgroups per CU, 0 auto (BO 3, LO 4 or 3) | 3 | 4 | 5
     {"rccl_fault", 0, 0, 7},          // fault injection (tests): 1 init, 2 group end, 4 stream drain never settle
     {"multi_fault", 0, 0, 64},        // fault injection (tests): 1..32 GPU value - 1 fails its timed allreduce, 33..64 its warm-up
-    {"hier_x_chunked", 0, 0, 1},      // k_hier_x / k_hier_x2: 1 the chunked form even at <= 8 tiles per workgroup (A/B)
     {"steps_tab", 1, 0, 1},           // k_steps_reg BO: 1 stages only its units' block programs (J < P), 0 every block's
     {"steps_early", 1, 0, 2},         // k_steps_reg: the first strip's loads before the program staging: 0 never | 1 auto (full grid) | 2 always
-    {"hier_x_rearly", 0, 0, 1},       // k_hier_x (LL, lag 1): 1 R(cur) ahead of the previous bucket's last row stores
-    {"hier_x_latepoll", 1, 0, 1},     // k_hier_x / k_hier_x2 (LL, lag 1): 1 the earlier bucket's results polled after tile 0's tree
     {"peer_fence", 0, 0, 1},          // peer kernels: 1 system-scope release / acquire fences around every cross-GPU hand-off
     {"hier_ws_ahead", 1, 1, 2},       // k_hier_ws: the reducing waves' loads 1 | 2 tiles ahead
     {"hier_ws_cols", 16, 8, 32},      // k_hier_ws: 16-byte columns per reducing wave, 8 (quarters) | 16 (halves) | 32 (whole tiles)

@@ -138,3 +138,98 @@ def argv_error0(argv, variant):
     a = list(argv)
     a[5] = "0"
     return a
+
+
+# ---------------------------------------------------------------- the RCCL multi-device cases
+# tests/test_gpu_multidevice.py runs these on real communicators (one thread per device); their
+# CPU twin, tests/test_multidevice_host.py, runs the SAME cases through the host twin of the RCCL
+# program (allred_dist_allreduce_host over gloo) against the SAME expectation code, so a red case
+# on the first multi-GPU box points at the product, not at the test (verdict r05 item 3).
+def rccl_cases(world, big=1 << 19):
+    """(variant, algo, local_ranks, channels, n): every case of tests/test_dist_host.py's gloo
+    matrix at n = 8 x total x 48, then flat BO / LO x RecDub / Swing at `big` elements per rank
+    with the auto channels (channels 0: every link from 1 MiB on)."""
+    import test_dist_host as tdh
+    side, total = tdh.GRIDS[world]
+    n = 8 * total * 16 * 3
+    out = [(v, a, loc, ch, n) for (v, a, loc, ch) in tdh.cases(world)]
+    for v in ("bo", "lo"):
+        for a in (t.RECDUB, t.SWING):
+            out.append((v, a, 1, 0, big))
+    return out
+
+
+def rccl_case_desc(world, variant, algo, local, chans, n):
+    import test_dist_host as tdh
+    side, total = tdh.GRIDS[world]
+    return t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
+                       local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
+
+
+def rccl_case_inputs(world, local, n, ci, rep):
+    """the per-rank inputs of case ci, repetition rep (identical on every rank: same seed)"""
+    import test_dist_host as tdh
+    return tdh.inputs(world, local, n, seed=5000 * world + 10 * ci + rep)
+
+
+def rccl_case_expected(world, variant, algo, local, chans, n, data):
+    """every rank's expected bucket (local rows concatenated) of a rccl_cases() case"""
+    import test_dist_host as tdh
+    desc = rccl_case_desc(world, variant, algo, local, chans, n)
+    C = chans if chans else channel_count(desc, n)
+    return [np.concatenate(x) for x in tdh.expected(variant, algo, world, local, data, C)]
+
+
+def rccl_mem_inputs(world, acc, n):
+    return [np.random.default_rng(77 * world + acc + g).integers(0x3F80, 0x42C8, n).astype(np.uint16)
+            for g in range(world)]
+
+
+def rccl_mem_expected(world, acc, data):
+    """mem_2D over RCCL (local_ranks 1): the oracle's allred_mem_2D restatement, fp32 or the
+    reference's bf16 accumulation"""
+    import test_dist_host as tdh
+    side, total = tdh.GRIDS[world]
+    want = [d.copy() for d in data]
+    oracle.allreduce("mem", t.SWING, side, want, total, acc == t.ACC_BF16)
+    return want
+
+
+def pipelined_inputs(world, n, local=64, K=3):
+    """data[k][g]: bucket k of GPU g, `local` rank rows of n elements"""
+    return [[np.random.default_rng(9000 + 97 * k + g).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+             for g in range(world)] for k in range(K)]
+
+
+def pipelined_expected(world, n, data_k, local=64):
+    """one bucket of the rccl_x transport (allred_dist_allreduce_pipelined with 64 local ranks):
+    every GPU's partial = the oracle's tree of its local rank 0 (8x8 Swing), the partials
+    allreduced by the 2D Swing BO over the GPU grid (link-spreading channels where the bucket
+    takes them), the result in all 64 rows -> expected partial of every GPU"""
+    import test_dist_host as tdh
+    side, total = tdh.GRIDS[world]
+    desc = t.dist_desc(t.SWING, t.BO, side, total, n, local_ranks=local, local_side=8, local_algo=t.SWING)
+    partials = []
+    for g in range(world):
+        loc = [x.copy() for x in data_k[g]]
+        oracle.allreduce("lo", t.SWING, 8, loc, local)   # tree of local rank 0
+        partials.append(loc[0])
+    channel_allreduce("bo", t.SWING, side, total, partials, channel_count(desc, n))
+    return partials
+
+
+def config4_ints(n, r, dev):
+    """BASELINE config 4's data for rank r: small integers 0..7 in bf16 (a per-element hash of
+    (e, r)), so every partial sum of up to 8 ranks is exact whatever the reduction order"""
+    import torch
+    e = torch.arange(n, dtype=torch.int64, device=dev)
+    return (((e * 2654435761 + r * 40503) >> 13) & 7).to(torch.bfloat16)
+
+
+def config4_exact(n, world, dev):
+    """the exact sum of the world's config4_ints, fp32"""
+    import torch
+    acc = torch.zeros(n, dtype=torch.float32, device=dev)
+    for r in range(world):
+        acc += config4_ints(n, r, dev).float()
+    return acc

@@ -47,7 +47,7 @@ def test_header_constants_match_python_bindings():
 
 
 def test_status_strings():
-    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 6
+    assert _lib.lib.allred_abi_version() == _lib.ABI_VERSION == 7
     for st in range(0, -8, -1):
         assert _lib.lib.allred_status_string(st)
 
@@ -128,11 +128,9 @@ def test_tune_entry_point():
             t.tune("steps_groups", v)
     assert t.tune("steps_groups") == 0
     # round-4 keys: defaults are the product forms / no fault injection
-    assert t.tune("hier_x_chunked") == 0
     assert (t.tune("rccl_fault"), t.tune("multi_fault")) == (0, 0)
-    for key, bad in (("hier_x2_tail", 3), ("rccl_fault", 8)):
-        with pytest.raises(t.AllredError):
-            t.tune(key, bad)
+    with pytest.raises(t.AllredError):
+        t.tune("rccl_fault", 8)
     # round 5: the flag hand-off forms are gone with their key (the trimmed table); peer_fence
     # (release / acquire fences around every cross-GPU hand-off) is off by default, 0 / 1 only
     with pytest.raises(t.AllredError):
@@ -291,3 +289,29 @@ def test_gpus_extension_parse_and_validation_without_gpu(monkeypatch):
         a = t.parse_args(argv, variant)
         r = _lib.Report()
         assert _lib.lib.allred_run(C.byref(a), 0, C.byref(r)) == want, argv
+
+
+# the whole tune table (tune.cpp kKeys, allred.h §Tuning): every key readable, the retired ones gone
+TUNE_KEYS = ("fused_form", "lo_tree", "lo_dag", "lo_dag_place", "lo_dag_min_tiles", "mem_reduce_lds", "steps_form",
+             "pipe_grid", "lo_dag_reg", "lo_dag_reg_min_tiles", "check", "fused_chunk_tiles", "lo_tree_min_tiles",
+             "tree_bcast_lag", "tree_bcast_bal", "steps_groups", "rccl_fault", "multi_fault", "steps_tab",
+             "steps_early", "peer_fence", "hier_ws_ahead", "hier_ws_cols")
+RETIRED_KEYS = ("hier_handoff", "hier_x2_tail", "hier_x_lag", "hier_x_chunked", "hier_x_rearly", "hier_x_latepoll")
+
+
+def test_tune_table_is_the_product_forms_only():
+    """ABI 7 (round 6): the keys that served only the retired hierarchical forms (k_hier_ll,
+    the one-deep pipeline k_hier_x, k_hier_x2's other placements) are gone; the table is at
+    most 24 keys, each with its documented default."""
+    assert len(TUNE_KEYS) <= 24
+    for key in TUNE_KEYS:
+        t.tune(key)   # readable (raises if unknown)
+    for key in RETIRED_KEYS:
+        with pytest.raises(t.AllredError):
+            t.tune(key)
+    hdr = open(os.path.join(ROOT, "include", "allred.h")).read()
+    tune_doc = hdr[hdr.index("Tuning: the one entry point"):hdr.index("int allred_tune_set")]
+    for key in TUNE_KEYS:
+        assert f" {key} " in tune_doc, f"{key} undocumented in allred.h"
+    for key in RETIRED_KEYS:
+        assert f" {key} " not in tune_doc, key

@@ -146,10 +146,10 @@ def test_dropped_candidates_are_listed_with_a_reason():
               "peer_hier_ws": {"verified": False, "exact_sum": True, "closed_form": True,
                                "matches_peer_launches": False},
               "peer_swing": {"verified": False, "exact_sum": False, "closed_form": True},
-              "peer_hier_x_fenced": {"verified": True, "exact_sum": True, "closed_form": True,
+              "peer_hier_ws_fenced": {"verified": True, "exact_sum": True, "closed_form": True,
                                      "matches_peer_launches": True}}
-    quick = {"rccl": 1.0, "peer_hier_x_fenced": 0.6}
-    assert bench.choose_transport(quick, verify) == "peer_hier_x_fenced"
+    quick = {"rccl": 1.0, "peer_hier_ws_fenced": 0.6}
+    assert bench.choose_transport(quick, verify) == "peer_hier_ws_fenced"
     got = {d["transport"]: d["reason"] for d in bench.dropped_candidates(verify)}
     assert set(got) == {"peer_hier_x", "peer_hier_ws", "peer_swing"}
     assert got["peer_hier_x"].startswith("quick_timing_timeout")

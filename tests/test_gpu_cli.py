@@ -110,6 +110,29 @@ def test_dma_end_to_end_chunked_is_exact(argv, chunks):
     assert rep["mismatches"] == 0 and rep["e2e_s"] > rep["device_s"] > 0
 
 
+@pytest.mark.parametrize("ratio,launches", [("0", 1), ("1e9", 8), ("default", None)])
+def test_dma_strided_copy_probe_both_outcomes(ratio, launches):
+    """The chunk-or-not decision of the DMA end-to-end form (engine.cpp): with no
+    ALLRED_E2E_CHUNKS, allred_run times one strided (2D) and one plain device-to-host
+    copy of a chunk in its untimed warm-up and keeps the 8 column chunks only where
+    the strided one takes at most ALLRED_E2E_STRIDED_RATIO (default 1.5) x the plain
+    one's time — some boxes move 2D copies at ~23 GB/s against ~52 for plain ones
+    (DESIGN.md §6).  Ratio 0 forces the one-copy outcome (one pass: 1 launch), a huge
+    ratio the chunked one (8 passes); the default takes whichever this box's probe
+    picks.  Every outcome: "All values match!" on every rank at ERROR 0 (RNE ctor).
+    The reference's own H2D / D2H around the run: allred_helper.cpp:287-288,
+    allred_helper.hpp:92."""
+    env = {} if ratio == "default" else {"ALLRED_E2E_STRIDED_RATIO": ratio}
+    out, rep = run("allred_BO_2D", ["1", "1", "8", "13", "5", "0", "0", "1"], ALLRED_EXEC="fused", ALLRED_E2E="dma",
+                   ALLRED_BF16_ROUND="rne", **env)
+    assert out.strip() == "All values match!", out
+    assert rep["mismatches"] == 0 and rep["e2e_s"] > rep["device_s"] > 0
+    if launches is not None:
+        assert rep["launches"] == launches, rep
+    else:
+        assert rep["launches"] in (1, 8), rep
+
+
 @pytest.mark.parametrize("exec_mode", ["steps", "fused"])
 def test_allredconfig_runprogram_cpp_program(exec_mode):
     """A reference-style C++ program against include/allred_helper.hpp alone

@@ -34,11 +34,11 @@ import threading
 import numpy as np
 import pytest
 
-import oracle
 import tenstorrentallreduce_amd as t
 import test_dist_host as tdh
 import test_gpu_peer as tgp
-from multi_cases import BIN, argv_error0, channel_allreduce, channel_count, expected, invocations
+import multi_cases as mc
+from multi_cases import BIN, argv_error0, expected, invocations
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -136,23 +136,14 @@ def _threads(world, fn):
     assert not errs, errs
 
 
-def _rccl_cases(world):
-    side, total = tdh.GRIDS[world]
-    n = 8 * total * 16 * 3
-    out = [(v, a, loc, ch, n) for (v, a, loc, ch) in tdh.cases(world)]
-    big = 1 << 19   # 1 MiB per rank: the link-spreading channels by default (channels = 0)
-    for v in ("bo", "lo"):
-        for a in (t.RECDUB, t.SWING):
-            out.append((v, a, 1, 0, big))
-    return out
-
-
 @pytest.mark.parametrize("world", WORLDS)
 def test_rccl_programs_across_gpus(world):
     """allred_dist_allreduce over real RCCL communicators (allred_comm_init_all,
     one thread per device): every case of tests/test_dist_host.py's gloo matrix,
     the auto channels on a 1 MiB bucket and mem_2D (fp32 and the reference's
-    bf16 accumulation), each twice back to back, bit-exact vs the oracle."""
+    bf16 accumulation), each twice back to back, bit-exact vs the oracle.  The
+    cases and the expected values are tests/multi_cases.py's, run on CPU through
+    the host twin of the same program by tests/test_multidevice_host.py."""
     devs = devices(world, peer=False)
     side, total = tdh.GRIDS[world]
     torch.cuda.set_device(0)
@@ -160,11 +151,9 @@ def test_rccl_programs_across_gpus(world):
     try:
         torch.cuda.synchronize(0)
         assert torch.cuda.current_device() == 0   # init_all leaves the caller's device alone (advisor r04)
-        for ci, (variant, algo, local, chans, n) in enumerate(_rccl_cases(world)):
-            desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, 1 if algo >= 2 else side, total, n,
-                               local_ranks=local, local_side=2, local_algo=t.SWING, channels=chans)
-            C = chans if chans else channel_count(desc, n)
-            runs = [tdh.inputs(world, local, n, seed=5000 * world + 10 * ci + rep) for rep in range(2)]
+        for ci, (variant, algo, local, chans, n) in enumerate(mc.rccl_cases(world)):
+            desc = mc.rccl_case_desc(world, variant, algo, local, chans, n)
+            runs = [mc.rccl_case_inputs(world, local, n, ci, rep) for rep in range(2)]
             got = [[None] * world for _ in runs]
 
             def step(g):
@@ -179,14 +168,13 @@ def test_rccl_programs_across_gpus(world):
 
             _threads(world, step)
             for k, data in enumerate(runs):
-                want = tdh.expected(variant, algo, world, local, data, C)
+                want = mc.rccl_case_expected(world, variant, algo, local, chans, n, data)
                 for g in range(world):
-                    assert np.array_equal(got[k][g], np.concatenate(want[g])), (variant, algo, local, chans, n, k, g)
+                    assert np.array_equal(got[k][g], want[g]), (variant, algo, local, chans, n, k, g)
         for acc in (t.ACC_FP32, t.ACC_BF16):
             n = 8 * total * 640
             desc = t.dist_desc(t.SWING, t.MEM, side, total, n, mem_accum=acc)
-            data = [np.random.default_rng(77 * world + acc + g).integers(0x3F80, 0x42C8, n).astype(np.uint16)
-                    for g in range(world)]
+            data = mc.rccl_mem_inputs(world, acc, n)
             got = [None] * world
 
             def mem(g):
@@ -198,8 +186,7 @@ def test_rccl_programs_across_gpus(world):
                 got[g] = b.cpu().numpy().view(np.uint16)
 
             _threads(world, mem)
-            want = [d.copy() for d in data]
-            oracle.allreduce("mem", t.SWING, side, want, total, acc == t.ACC_BF16)
+            want = mc.rccl_mem_expected(world, acc, data)
             for g in range(world):
                 assert np.array_equal(got[g], want[g]), ("mem", acc, g)
     finally:
@@ -218,9 +205,7 @@ def test_rccl_pipelined_across_gpus(world):
     side, total = tdh.GRIDS[world]
     n, local, K = 327680, 64, 3
     desc = t.dist_desc(t.SWING, t.BO, side, total, n, local_ranks=local, local_side=8, local_algo=t.SWING)
-    C = channel_count(desc, n)
-    data = [[np.random.default_rng(9000 + 97 * k + g).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
-             for g in range(world)] for k in range(K)]
+    data = mc.pipelined_inputs(world, n, local, K)
     comms = t.Comm.init_all(devs)
     got = [[None] * world for _ in range(K)]
     try:
@@ -240,12 +225,7 @@ def test_rccl_pipelined_across_gpus(world):
         for c in comms:
             c.close()
     for k in range(K):
-        partials = []
-        for g in range(world):
-            loc = [x.copy() for x in data[k][g]]
-            oracle.allreduce("lo", t.SWING, 8, loc, local)   # tree of local rank 0
-            partials.append(loc[0])
-        channel_allreduce("bo", t.SWING, side, total, partials, C)
+        partials = mc.pipelined_expected(world, n, data[k], local)
         for g in range(world):
             bad = int((got[k][g] != partials[g][None, :]).sum())
             assert bad == 0, (k, g, bad)
@@ -256,9 +236,8 @@ def test_rccl_pipelined_across_gpus(world):
 @pytest.mark.parametrize("world", WORLDS)
 def test_peer_mem_and_hier_forms_across_gpus(world, tunes):
     """tests/test_gpu_peer.py's worker with one process per device: mem_2D
-    (launches, k_peer_oneshot, k_peer_mem_ll), the hierarchical forms (k_hier_ll,
-    k_hier_ws over quarter / half / whole tiles, the launch form, k_hier_x /
-    k_hier_x2 in every placement, capped grids)."""
+    (launches, k_peer_oneshot, k_peer_mem_ll), the hierarchical forms (k_hier_ws
+    over quarter / half / whole tiles, the launch form, k_hier_x2, capped grids)."""
     tgp.run_world(tgp.worker, world, 300, devs=devices(world), tunes=tunes)
 
 
@@ -281,18 +260,8 @@ def test_peer_config3_config5_across_8_gpus(tunes):
 GIB_ELEMS = 1 << 29   # 1 GiB of bf16 per GPU
 
 
-def _ints(n, r, dev):
-    """Rank r's bucket: small integers 0..7 in bf16 (a per-element hash of (e, r)),
-    so every partial sum of up to 8 ranks is exact whatever the reduction order."""
-    e = torch.arange(n, dtype=torch.int64, device=dev)
-    return (((e * 2654435761 + r * 40503) >> 13) & 7).to(torch.bfloat16)
-
-
-def _exact(n, world, dev):
-    acc = torch.zeros(n, dtype=torch.float32, device=dev)
-    for r in range(world):
-        acc += _ints(n, r, dev).float()
-    return acc
+_ints = mc.config4_ints     # rank r's bucket: small integers 0..7 in bf16, exact sums in any order
+_exact = mc.config4_exact
 
 
 @pytest.mark.parametrize("world", WORLDS)

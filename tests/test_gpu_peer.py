@@ -136,35 +136,28 @@ def worker(rank, world, port, q, devs=None, tunes=None):
         got = buf.cpu().numpy().view(np.uint16)
         if not all(np.array_equal(got[i], partials[rank]) for i in range(local)):
             fails.append(("hier", 0, 1))
-        # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form
-        # with LL push hand-offs (k_hier_ll), the launch form (the mem_2D exchange as one kernel or as
-        # launches) and the bucket pipelines (k_hier_x, k_hier_x2), two or three calls back to back each
-        # (then LL once more after the launch form: its LL boxes must not accept the older calls' words)
+        # 64 local ranks (8x8 Swing tree per GPU): the one-kernel hierarchical form with LL push
+        # hand-offs (k_hier_ws), the launch form (the mem_2D exchange as one kernel or as launches)
+        # and the two-deep bucket pipeline (k_hier_x2), two or three calls back to back each (then
+        # k_hier_ws once more after the launch form: its boxes must not accept the older calls' words)
         local, m = 64, 256 * world * 3
         # in full and capped grids (a capped grid gives every workgroup many tiles)
-        for mi, (mode, limit, ll, cap, *more) in enumerate((("hier_oneshot_exchange", 1 << 40, 0, 0), ("hier_ll", 1 << 40, 1, 0),
-                                                     ("hier_launches", 0, 0, 0), ("hier_ll_again", 0, 1, 0),
-                                                     ("hier_ll_capped", 0, 1, 2), ("hier_oneshot_exchange_capped", 1 << 40, 0, 1),
+        for mi, (mode, limit, ll, cap, *more) in enumerate((("hier_oneshot_exchange", 1 << 40, 0, 0),
+                                                     ("hier_launches", 0, 0, 0), ("hier_oneshot_exchange_capped", 1 << 40, 0, 1),
                                                      # k_hier_ws; one workgroup with 20 tiles per owner: owned
                                                      # partials past its 16 LDS slots go through the own inbox
-                                                     ("hier_ws", 0, 2, 0), ("hier_ws_capped", 0, 2, 2),
-                                                     ("hier_launches_then_ws", 0, 0, 0), ("hier_ws_again", 0, 2, 0),
-                                                     ("hier_ws_ring", 0, 2, 1, 20), ("hier_ws_c8", 0, 2, 0),
-                                                     ("hier_ws_c8_ring", 0, 2, 1, 20), ("hier_ws_c32", 0, 2, 0),
-                                                     ("hier_ws_c32_ring", 0, 2, 1, 20),
-                                                     ("hier_x", 0, 0, 0), ("hier_x_capped", 0, 0, -1),
+                                                     ("hier_ws", 0, 1, 0), ("hier_ws_capped", 0, 1, 2),
+                                                     ("hier_launches_then_ws", 0, 0, 0), ("hier_ws_again", 0, 1, 0),
+                                                     ("hier_ws_ring", 0, 1, 1, 20), ("hier_ws_c8", 0, 1, 0),
+                                                     ("hier_ws_c8_ring", 0, 1, 1, 20), ("hier_ws_c32", 0, 1, 0),
+                                                     ("hier_ws_c32_ring", 0, 1, 1, 20),
                                                      ("hier_x2", 0, 0, 0), ("hier_x2_capped", 0, 0, -1),
-                                                     ("hier_x2_tail", 0, 0, 0), ("hier_x2_tail2", 0, 0, 0), ("hier_x_re", 0, 0, 0),
-                                                     ("hier_x_re_lp", 0, 0, 0), ("hier_x_re_lp_one_group", 0, 0, 1),
-                                                     ("hier_x_lp", 0, 0, 0), ("hier_x2_tail2_lp", 0, 0, 0),
-                                                     ("hier_x2_lp", 0, 0, 0), ("hier_x2_tail_lp", 0, 0, 0),
-                                                     ("hier_x2_tail_lp_one_group", 0, 0, 1),
                                                      # one workgroup: 3 * world tiles, results staged 8 at a time
                                                      # (two chunks resident, the third reusing the first's slot)
-                                                     ("hier_x_one_group", 0, 0, 1), ("hier_x2_one_group", 0, 0, 1),
-                                                     ("hier_x2_tail_one_group", 0, 0, 1))):
+                                                     ("hier_x2_one_group", 0, 0, 1),
+                                                     ("hier_ws_after_x2", 0, 1, 0))):
             m = 256 * world * (more[0] if more else 3)
-            if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x / k_hier_x2
+            if cap < 0:   # exactly 8 tiles per workgroup: one chunk of k_hier_x2
                 cap = (m // 256 + 7) // 8
             peer.set_oneshot_max(limit)
             peer.set_hier_ll(ll)
@@ -176,24 +169,13 @@ def worker(rank, world, port, q, devs=None, tunes=None):
                 buf = torch.from_numpy(data[rank].view(np.int16)).to(dev)
                 ws = torch.empty(m, dtype=torch.int16, device=dev)
                 if mode.startswith("hier_x2"):   # two deep: b0, b1, b2, then the flush below
-                    with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
-                                 hier_x_latepoll=int("_lp" in mode)):
-                        peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
-                elif mode.startswith("hier_x"):   # pipelined: (b0, -), (b1, b0), then (-, b1) below
-                    with t.tuned(hier_x_rearly=int("_re" in mode), hier_x_latepoll=int("_lp" in mode)):
-                        peer.allreduce_pipelined(buf.data_ptr(), runs[-1][1].data_ptr() if runs else None, m,
-                                                 torch.cuda.current_stream())
+                    peer.allreduce_pipelined2(buf.data_ptr(), m, torch.cuda.current_stream())
                 else:
                     with t.tuned(hier_ws_cols=8 if "_c8" in mode else 32 if "_c32" in mode else 16):
                         peer.allreduce(buf.data_ptr(), m, torch.cuda.current_stream(), local, 8, t.SWING, ws.data_ptr())
                 runs.append((data, buf, ws))
             if mode.startswith("hier_x2"):
-                with t.tuned(hier_x2_tail=2 if mode.startswith("hier_x2_tail2") else int(mode.startswith("hier_x2_tail")),
-                             hier_x_latepoll=int("_lp" in mode)):
-                    peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
-            elif mode.startswith("hier_x"):
-                with t.tuned(hier_x_rearly=int("_re" in mode), hier_x_latepoll=int("_lp" in mode)):
-                    peer.allreduce_pipelined(None, runs[-1][1].data_ptr(), m, torch.cuda.current_stream())
+                peer.allreduce_pipelined2(None, m, torch.cuda.current_stream())
             torch.cuda.synchronize()
             for rep, (data, buf, _) in enumerate(runs):
                 partials = []
@@ -363,8 +345,9 @@ def t_timeout_bit():
 
 @pytest.mark.parametrize("n,cap", [(327680, 0), (327680, 7), (256 * 5, 0), (256 * 40, 3)])
 def test_hier_forms_single_gpu_bit_exact(n, cap):
-    """One GPU (W = 1), 64 local ranks: the LL forms k_hier_ll / k_hier_ws and the launch
-    form (mem_2D exchange as one kernel or as launches) give the same
+    """One GPU (W = 1), 64 local ranks: the one-launch form k_hier_ws (quarter / half /
+    whole tiles per reducing wave) and the launch form (mem_2D exchange as one kernel or
+    as launches) give the same
     bits as the oracle (tree of local rank 0 of the 8x8 Swing grid, then the
     mem_2D owner-first fp32 sum — one rank: the partial itself), twice in a row
     (both LL parities).  Config-2 size full grid and with capped grids (many
@@ -386,8 +369,8 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
             cases.append((data, loc[0]))
         ws = torch.empty(n, dtype=torch.int16, device="cuda:0")
         # (hier_ll, oneshot limit, k_hier_ws columns per reducing wave)
-        for ll, limit, cols in ((1, 0, 8), (0, 1 << 40, 8), (2, 0, 8), (2, 0, 16), (2, 0, 32), (0, 0, 8), (1, 0, 8),
-                                (2, 0, 16), (2, 0, 32), (0, 1 << 40, 8), (1, 0, 8), (2, 0, 8)):
+        for ll, limit, cols in ((1, 0, 16), (0, 1 << 40, 8), (1, 0, 8), (1, 0, 16), (1, 0, 32), (0, 0, 8),
+                                (1, 0, 16), (1, 0, 32), (0, 1 << 40, 8), (1, 0, 8)):
             peer.set_hier_ll(ll)
             peer.set_oneshot_max(limit)
             bufs = [torch.from_numpy(d.view(np.int16)).to("cuda:0") for d, _ in cases]
@@ -405,70 +388,6 @@ def test_hier_forms_single_gpu_bit_exact(n, cap):
         peer.close()
 
 
-@pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 4), (256 * 5, 0, 3), (256 * 40, 5, 2), (327680, 160, 1),
-                                           (256 * 40, 1, 3), (327680, 64, 2)])
-def test_hier_pipelined_single_gpu_bit_exact(n, cap, buckets):
-    """One GPU (W = 1), 64 local ranks: a sequence of buckets through the
-    pipelined hierarchical step (k_hier_x: each launch finishes the previous
-    bucket while it reads the next), buckets + 1 calls, every bucket bit-exact
-    vs the oracle (tree of local rank 0, the mem_2D sum of one partial, rows
-    overwritten with it); full and capped grids (one workgroup with 40 tiles:
-    five chunks of staged results).
-    Protocol errors: a prev that is not the pending bucket, another peer call
-    while a bucket is pending, finishing with nothing pending."""
-    sys.path.insert(0, ROOT)
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import tenstorrentallreduce_amd as t
-    from tenstorrentallreduce_amd import _lib
-    import oracle
-    local = 64
-    peer = t.Peer(1, 0, 0, 2 * n)
-    peer.connect([peer.handle()])
-    try:
-        peer.set_max_groups(cap)
-        data, want = [], []
-        for b in range(buckets):
-            d = np.random.default_rng(1300 + b).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
-            loc = [x.copy() for x in d]
-            oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
-            data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
-            want.append(loc[0])
-        s = torch.cuda.current_stream()
-        for rep in range(14):   # row stores with the tree's tile / one behind; both LL
-            bufs = [x.clone() for x in data]   # parities; the chunked form forced (reps 8, 9); R early (10, 11);
-            prev = None                        # result polls at the start (12), R early + late polls (13)
-            with t.tuned(hier_x_lag=rep % 2 if rep < 10 else 1,
-                         hier_x_chunked=int(8 <= rep < 10), hier_x_rearly=int(rep in (10, 11, 13)),
-                         hier_x_latepoll=int(rep != 12)):
-                for b in bufs:
-                    peer.allreduce_pipelined(b.data_ptr(), prev, n, s)
-                    prev = b.data_ptr()
-                peer.allreduce_pipelined(None, prev, n, s)
-                torch.cuda.synchronize()
-            for i, (b, w) in enumerate(zip(bufs, want)):
-                bad = int((b.cpu().numpy().view(np.uint16) != w[None, :]).sum())
-                assert bad == 0, (i, bad)
-        assert peer.status() & t.PEER_TIMEOUT == 0
-        x = data[0].clone()
-        peer.allreduce_pipelined(x.data_ptr(), None, n, s)
-        with pytest.raises(_lib.AllredError):   # another call while a bucket is pending
-            peer.allreduce(x.data_ptr(), n, s, local, 8, t.SWING, x.data_ptr())
-        with pytest.raises(_lib.AllredError):   # a second start without finishing the first
-            peer.allreduce_pipelined(x.data_ptr(), None, n, s)
-        y = data[0].clone()
-        with pytest.raises(_lib.AllredError):   # prev is not the pending bucket
-            peer.allreduce_pipelined(None, y.data_ptr(), n, s)
-        if n % (2 * 256) == 0:
-            with pytest.raises(_lib.AllredError):   # the pending bucket with another size
-                peer.allreduce_pipelined(None, x.data_ptr(), n // 2, s)
-        peer.allreduce_pipelined(None, x.data_ptr(), n, s)
-        with pytest.raises(_lib.AllredError):   # nothing pending
-            peer.allreduce_pipelined(None, x.data_ptr(), n, s)
-        torch.cuda.synchronize()
-    finally:
-        peer.close()
-
-
 def test_peer_knob_argument_errors():
     """The peer knobs reject what they cannot honour (ALLRED_ERR_ARG), like the
     rest of the C-ABI; a one-rank peer set needs no second process."""
@@ -479,7 +398,7 @@ def test_peer_knob_argument_errors():
     peer.connect([peer.handle()])
     try:
         with pytest.raises(_lib.AllredError):
-            peer.set_hier_ll(3)            # 0 off, 1 k_hier_ll, 2 k_hier_ws
+            peer.set_hier_ll(2)            # 0 the launch form, 1 k_hier_ws (ABI 7: 2 retired with k_hier_ll)
         with pytest.raises(_lib.AllredError):
             peer.set_hier_ll(-1)
         peer.set_lo_ll_max(0)
@@ -582,17 +501,17 @@ def test_config3_config5_eight_processes(tunes):
 
 
 @pytest.mark.parametrize("n,cap,buckets", [(327680, 0, 5), (327680, 0, 1), (256 * 5, 0, 2), (256 * 40, 5, 3),
-                                           (327680, 160, 4), (256 * 40, 1, 3), (327680, 64, 3)])
+                                           (327680, 160, 4), (256 * 40, 1, 3), (327680, 64, 3), (256 * 16, 2, 3)])
 def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
     """One GPU (W = 1), 64 local ranks: a sequence of buckets through the
     two-deep pipelined hierarchical step (k_hier_x2: launch i starts bucket i,
     sums bucket i-1's owned tiles and writes bucket i-2), buckets + 1 calls
     (1 bucket: the flush sums and writes it; 2: the flush writes both), every
     bucket bit-exact vs the oracle; full and capped grids (one workgroup with
-    40 tiles: five chunks of staged results), the sequence repeated (both LL
-    parities reused).  Protocol errors:
-    another peer call or the one-deep pipeline while buckets are pending, a
-    different bucket size mid-sequence, a flush with nothing pending."""
+    40 tiles: five chunks of staged results; exactly one chunk per workgroup),
+    the sequence repeated (both LL parities reused).  Protocol errors: another
+    peer call while buckets are pending, a different bucket size mid-sequence, a
+    flush with nothing pending."""
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import tenstorrentallreduce_amd as t
@@ -611,16 +530,12 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
             data.append(torch.from_numpy(d.view(np.int16)).to("cuda:0"))
             want.append(loc[0])
         s = torch.cuda.current_stream()
-        for rep in range(16):   # owned sums at the start / the end of a launch / before its last stores (12-15);
-            # chunked form forced; results polled at the start (14, 15) or after tile 0
-            with t.tuned(hier_x2_tail=2 if rep >= 12 else (rep // 2) % 2, hier_x_lag=rep % 2,
-                         hier_x_chunked=int(8 <= rep < 12),
-                         hier_x_latepoll=int(rep < 14)):
-                bufs = [x.clone() for x in data]
-                for b in bufs:
-                    peer.allreduce_pipelined2(b.data_ptr(), n, s)
-                peer.allreduce_pipelined2(None, n, s)
-                torch.cuda.synchronize()
+        for rep in range(4):   # the sequence again and again: both parities, epochs advancing
+            bufs = [x.clone() for x in data]
+            for b in bufs:
+                peer.allreduce_pipelined2(b.data_ptr(), n, s)
+            peer.allreduce_pipelined2(None, n, s)
+            torch.cuda.synchronize()
             for i, (b, w) in enumerate(zip(bufs, want)):
                 bad = int((b.cpu().numpy().view(np.uint16) != w[None, :]).sum())
                 assert bad == 0, (rep, i, bad)
@@ -629,8 +544,6 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
         peer.allreduce_pipelined2(x.data_ptr(), n, s)
         with pytest.raises(_lib.AllredError):   # another call while a bucket is pending
             peer.allreduce(x.data_ptr(), n, s, local, 8, t.SWING, x.data_ptr())
-        with pytest.raises(_lib.AllredError):   # the one-deep pipeline does not mix in
-            peer.allreduce_pipelined(x.data_ptr(), None, n, s)
         if n % (2 * 256) == 0:
             with pytest.raises(_lib.AllredError):   # another bucket size mid-sequence
                 peer.allreduce_pipelined2(x.data_ptr(), n // 2, s)
@@ -653,15 +566,20 @@ def test_hier_pipelined2_single_gpu_bit_exact(n, cap, buckets):
         peer.close()
 
 
-def test_hier_handoff_epoch_wrap_is_cleared():
+@pytest.mark.parametrize("first_tiles", [64, 32])
+def test_hier_handoff_epoch_wrap_is_cleared(first_tiles):
     """The hierarchical forms' hand-off words carry a 16-bit epoch ((k + 1) %
     65535 + 1 for call k), so call k + 131070 (same parity) awaits the epoch
-    call k's words carry.  A large bucket at call 0, then 131069 small ones,
-    then the large bucket again at call 131070: the slots beyond the small
-    buckets' range still hold call 0's words with call 131070's epoch.  The host
-    sees it coming (hier_area_prepare) and clears the parity's area between two
-    barriers; the result must be call 131070's own data, bit-exact (W = 1,
-    k_hier_ll).  ~1 s of tiny launches."""
+    call k's words carry.  A bucket of `first_tiles` tiles at call 0, then
+    131069 two-tile ones, then a 64-tile bucket at call 131070: the slots beyond
+    the small buckets' range still hold call 0's words with call 131070's epoch
+    — also when the last bucket is LARGER than call 0's (32 -> 64 tiles: slots
+    32..63 were never written, slots 2..31 hold call 0's words; advisor r05).
+    The host sees it coming (hier_area_prepare) and clears the parity's area
+    between two barriers; the result must be call 131070's own data, bit-exact
+    (W = 1, k_hier_ws with ONE workgroup: every owned tile past its 16 LDS
+    slots crosses the own inbox, so a stale word would be read).  ~2 s of tiny
+    launches."""
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import tenstorrentallreduce_amd as t
@@ -671,6 +589,7 @@ def test_hier_handoff_epoch_wrap_is_cleared():
     peer.connect([peer.handle()])
     try:
         peer.set_hier_ll(1)
+        peer.set_max_groups(1)
         s = torch.cuda.current_stream()
         ws = torch.empty(large, dtype=torch.int16, device="cuda:0")
 
@@ -680,8 +599,10 @@ def test_hier_handoff_epoch_wrap_is_cleared():
             oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
             return torch.from_numpy(d.view(np.int16)).to("cuda:0"), loc[0]
 
-        first, _ = bucket(1, large)
-        peer.allreduce(first.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())    # call 0
+        first, want0 = bucket(1, 256 * first_tiles)
+        peer.allreduce(first.data_ptr(), 256 * first_tiles, s, local, 8, t.SWING, ws.data_ptr())    # call 0
+        torch.cuda.synchronize()
+        assert int((first.cpu().numpy().view(np.uint16) != want0[None, :]).sum()) == 0
         sm, _ = bucket(2, small)   # reduced in place over and over: only its launches matter
         for i in range(131069):                                                         # calls 1 .. 131069
             peer.allreduce(sm.data_ptr(), small, s, local, 8, t.SWING, ws.data_ptr())
@@ -697,4 +618,5 @@ def test_hier_handoff_epoch_wrap_is_cleared():
         assert peer.status() & t.PEER_TIMEOUT == 0
     finally:
         peer.set_hier_ll(0)
+        peer.set_max_groups(0)
         peer.close()

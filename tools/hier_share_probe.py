@@ -59,7 +59,7 @@ def worker(rank, world, port, steps, rounds, q):
         for name, knobs in ARMS.items():
             for key, v in knobs.items():
                 t.tune(key, v)
-            peer.set_hier_ll(2)
+            peer.set_hier_ll(1)
             run(name, 3)
             torch.cuda.synchronize()
             dist.barrier()

@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
 """Timing of the hierarchical step on ONE GPU (W = 1 peer set, 64 virtual ranks
-x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ll, k_hier_ws, k_hier_x
-and k_hier_x2 (buckets pipelined one / two deep, k_hier_x2 with its owned sums
-at the start, the end or before the last row stores of a launch: K buckets in
-K + 1 launches, the timed region includes the finishing launch) — the N > 1 bench's candidates with the cross-GPU
-hand-offs reduced to this GPU's own LL boxes.  Eager launches behind a spin
+x 640 kB): the launch form (tree + mem_2D + broadcast), k_hier_ws (and its A/B
+column splits / load depth) and k_hier_x2 (buckets pipelined two deep: K buckets
+in K + 1 launches, the timed region includes the finishing launch) — the N > 1
+bench's candidates with the cross-GPU hand-offs reduced to this GPU's own boxes.  Eager launches behind a spin
 kernel (peer calls advance host-side epochs, so no graph), 32 rotating sets,
 arms interleaved.   python tools/hier_step.py [steps] [rounds]   (HIER_CAP: grid cap)"""
 import json
@@ -27,55 +26,38 @@ peer = t.Peer(1, 0, 0, 2 * n)
 peer.connect([peer.handle()])
 peer.set_max_groups(int(os.environ.get("HIER_CAP", "0")))   # 0: the default grid (2 workgroups per CU)
 s = torch.cuda.Stream()
-arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ll": (0, 1), "hier_ws": (0, 2),
-        "hier_ws_a2": (0, 2), "hier_ws_c8": (0, 2), "hier_ws_c8_a2": (0, 2),
-        "hier_ws_c32": (0, 2), "hier_ws_c32_a2": (0, 2)}
+arms = {"launches": (0, 0), "oneshot_exchange": (1 << 40, 0), "hier_ws": (0, 1),
+        "hier_ws_a2": (0, 1), "hier_ws_c8": (0, 1), "hier_ws_c8_a2": (0, 1),
+        "hier_ws_c32": (0, 1), "hier_ws_c32_a2": (0, 1)}
 # hier_ws_a2: tune hier_ws_ahead=2; _c8 / _c32: hier_ws_cols=8 / 32 (quarter / whole tiles per reducing wave;
 # default 16: halves)
-# pipelined arms: hier_x* one bucket deep, hier_x2* two; _tail: owned sums at the launch end; _ch: the
-# chunked form at <= 8 tiles per workgroup (tune hier_x_chunked); hier_x2_tail2: the owned sums before the
-# last iteration's row stores (tune hier_x2_tail=2); hier_x_re: k_hier_x's R ahead of the last tile's row
-# stores (tune hier_x_rearly); _lp: late result polls (tune hier_x_latepoll)
-PIPE = ["hier_x_lp", "hier_x_re_lp", "hier_x2_tail2_lp"]
-if os.environ.get("HIER_ARMS"):   # a subset, comma separated (any of the names above, + _ch variants)
+# the pipelined arm: k_hier_x2, two buckets deep
+PIPE = ["hier_x2"]
+if os.environ.get("HIER_ARMS"):   # a subset, comma separated (any of the names above)
     sel = os.environ["HIER_ARMS"].split(",")
     arms = {k: v for k, v in arms.items() if k in sel}
-    PIPE = [k for k in sel if k.startswith("hier_x")]
+    PIPE = [k for k in sel if k.startswith("hier_x2")]
 res = {k: [] for k in list(arms) + PIPE}
 host = {k: [] for k in res}   # host submission time per call: must stay below the GPU time
 SPIN = int(os.environ.get("SPIN_CYCLES", "20000000"))   # the GPU busy until the host has queued every step
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
 
-def pipelined(k, deep):   # k buckets in k + 1 calls: k_hier_x (each call finishes the previous bucket) / k_hier_x2
-    prev = None
+def pipelined(k):   # k buckets in k + 1 calls (k_hier_x2)
     for i in range(k):
-        cur = sets[i % NS].data_ptr()
-        if deep:
-            peer.allreduce_pipelined2(cur, n, s)
-        else:
-            peer.allreduce_pipelined(cur, prev, n, s)
-        prev = cur
-    if deep:
-        peer.allreduce_pipelined2(None, n, s)
-    else:
-        peer.allreduce_pipelined(None, prev, n, s)
+        peer.allreduce_pipelined2(sets[i % NS].data_ptr(), n, s)
+    peer.allreduce_pipelined2(None, n, s)
 
 
 for _ in range(rounds):
     for name in PIPE:
-        deep = name.startswith("hier_x2")
-        t.tune("hier_x2_tail", 2 if name.startswith("hier_x2_tail2") else int(name.startswith("hier_x2_tail")))
-        t.tune("hier_x_chunked", int("_ch" in name))
-        t.tune("hier_x_rearly", int("_re" in name))
-        t.tune("hier_x_latepoll", int("_lp" in name))
-        pipelined(20, deep)
+        pipelined(20)
         torch.cuda.synchronize()
         with torch.cuda.stream(s):
             torch.cuda._sleep(SPIN)
         e0.record(s)
         h0 = time.perf_counter()
-        pipelined(steps, deep)
+        pipelined(steps)
         host[name].append(round((time.perf_counter() - h0) * 1e6 / steps, 2))
         e1.record(s)
         torch.cuda.synchronize()
