@@ -52,3 +52,8 @@ def test_bench_two_ranks_share_gpu():
     assert x["timing"]["repetitions"] >= 3   # median of >= 3 K-step repetitions
     assert d["ms_per_step"] == pytest.approx(sorted(x["timing"]["ms_per_step_per_repetition"])[
         len(x["timing"]["ms_per_step_per_repetition"]) // 2], rel=1e-3)
+    # the wall-clock budget (--deadline, default 420 s from the start of bench.py): every phase timed
+    b = x["budget"]
+    assert b["deadline_s"] == 420.0 and 0 < b["wall_s"] < b["deadline_s"]
+    assert {"setup", "headline", "local_phases"} <= set(b["phase_s"]) and b["skipped_for_deadline"] == []
+    assert any(k.startswith("verify:") for k in b["phase_s"]) and any(k.startswith("quick:") for k in b["phase_s"])
