@@ -6,6 +6,10 @@
 // the LL (data + epoch word) push forms for small buckets.
 // Every cross-GPU wait is bounded (device.hpp peer_give_up): a dead or slow
 // peer sets ALLRED_PEER_TIMEOUT in the status word instead of hanging.
+#include <map>
+#include <mutex>
+#include <utility>
+
 #include "device.hpp"
 
 namespace tsa {
@@ -1076,7 +1080,7 @@ __global__ __launch_bounds__(kBlock) void k_hier_x2(uint16_t* __restrict__ cur, 
 
 // ---------------------------------------------------------------------------
 // k_peer_mem_ll: allred_mem_2D across GPUs for small buckets with LL hand-offs
-// (the flat counterpart of k_hier_ll).  A: every vector is pushed as four
+// (the flat counterpart of the hierarchical forms).  A: every vector is pushed as four
 // data+epoch words to its block owner's inbox; R: the owner polls the W
 // copies of each of its vectors (all loads in flight at once), sums them in
 // fp32 owner first then ascending, one rounding (allred_mem_2D semantics, the
@@ -1181,6 +1185,29 @@ __global__ __launch_bounds__(kBlock) void k_peer_lo_ll(LLPtrs lp, PeerProg pr, i
 }
 
 int peer_last_error() { return hip_status((int)hipGetLastError()); }
+
+// Workgroups of `func` (block threads) resident on the current device at once: the grid cap of
+// the hierarchical forms, whose workgroups wait for each other across GPUs (every one must be
+// resident).  512 on a whole MI355X (2 per CU x 256 CUs: 73.7 KiB of LDS each); fewer on a
+// partitioned GPU, where a 512-workgroup grid would wait for workgroups that cannot start.
+// Cached per (device, kernel); 0 when the runtime cannot say (the caller keeps its cap).
+unsigned resident_limit(const void* func, int block) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, unsigned> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    const auto key = std::make_pair(dev, func);
+    const auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int cus = 0, per = 0;
+    unsigned lim = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, func, block, 0) == hipSuccess && cus > 0 && per > 0)
+        lim = (unsigned)cus * (unsigned)per;
+    cache.emplace(key, lim);
+    return lim;
+}
 
 }  // namespace
 
@@ -1309,14 +1336,17 @@ int launch_hier_ws(uint16_t* ranks, uint64_t stride, const uint8_t* order, uint6
         return ALLRED_ERR_ARG;
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
-    // 2 per CU (8 waves each): the whole grid resident (max_grid < 512 when processes share the GPU)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
-    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     const bool a2 = tune(Tune::hier_ws_ahead) == 2;
     const int cw = tune(Tune::hier_ws_cols) >= 32 ? 32 : tune(Tune::hier_ws_cols) >= 16 ? 16 : 8;
     decltype(&k_hier_ws<1, 8>) kern = cw == 32 ? (a2 ? k_hier_ws<2, 32> : k_hier_ws<1, 32>)
                                       : cw == 16 ? (a2 ? k_hier_ws<2, 16> : k_hier_ws<1, 16>)
                                                  : (a2 ? k_hier_ws<2, 8> : k_hier_ws<1, 8>);
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU; fewer
+    // where the device holds fewer at once)
+    unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned res = resident_limit(reinterpret_cast<const void*>(kern), 128 * (32 / cw));
+    if (res && cap > res) cap = res;
+    const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(128 * (32 / cw)), 0, (hipStream_t)stream, ranks, stride, order, lp, nranks, me,
                        ntiles, ntiles / nranks, box_words, epoch, status);
     static const char* const names[2][3] = {{"k_hier_ws<1, 8>", "k_hier_ws<1, 16>", "k_hier_ws<1, 32>"},
@@ -1335,8 +1365,11 @@ int launch_hier_x2(uint16_t* cur, uint16_t* old, uint16_t* fin, uint64_t stride,
         (!cur && !old && !fin) || (cur && !llc) || (old && !llo) || (fin && (cur || !llm)) ||
         (cur && !aligned16(cur)) || (old && !aligned16(old)) || (fin && !aligned16(fin)))
         return ALLRED_ERR_ARG;
-    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU)
-    const unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    // 2 per CU: the whole grid resident (max_grid < 512 when processes share the GPU; fewer
+    // where the device holds fewer at once — the chunked form's LDS, the larger, decides)
+    unsigned cap = max_grid && max_grid < 512 ? max_grid : 512;
+    const unsigned res = resident_limit(reinterpret_cast<const void*>(&k_hier_x2<true>), kBlock);
+    if (res && cap > res) cap = res;
     const unsigned grid = (unsigned)(ntiles < cap ? ntiles : cap);
     LLPtrs lc{}, lm{}, lo{};
     for (int q = 0; q < nranks; ++q) {
