@@ -1261,7 +1261,9 @@ int launch_peer_sched(uint16_t* const* wins, uint32_t* const* flags, int me, uin
     uint64_t gc = (per + kBlock - 1) / kBlock;
     // workgroup g waits for workgroup g of its partners: every GPU's grid must be resident
     // at once (max_groups < kPeerSchedMaxGroups when processes share one GPU)
-    const uint64_t cap = max_groups && max_groups < kPeerSchedMaxGroups ? max_groups : kPeerSchedMaxGroups;
+    uint64_t cap = max_groups && max_groups < kPeerSchedMaxGroups ? max_groups : kPeerSchedMaxGroups;
+    const uint64_t res = resident_limit(reinterpret_cast<const void*>(&k_peer_sched), kBlock);   // all resident
+    if (res && cap > res) cap = res;
     const uint64_t gmax = cap / prog.C > 0 ? cap / prog.C : 1;
     if (gc > gmax) gc = gmax;
     if (gc < 1) gc = 1;
@@ -1288,7 +1290,9 @@ int launch_peer_sched_push(uint16_t* const* wins, uint16_t* const* stages, uint3
     uint64_t per = 0;
     for (int c = 0; c < prog.C; ++c) per = prog.len[c] / prog.N > per ? prog.len[c] / prog.N : per;
     uint64_t gc = (per + kBlock - 1) / kBlock;
-    const uint64_t cap = max_groups && max_groups < kPeerSchedMaxGroups ? max_groups : kPeerSchedMaxGroups;
+    uint64_t cap = max_groups && max_groups < kPeerSchedMaxGroups ? max_groups : kPeerSchedMaxGroups;
+    const uint64_t res = resident_limit(reinterpret_cast<const void*>(&k_peer_sched_push), kBlock);   // all resident
+    if (res && cap > res) cap = res;
     const uint64_t gmax = cap / prog.C > 0 ? cap / prog.C : 1;
     if (gc > gmax) gc = gmax;
     if (gc < 1) gc = 1;
@@ -1307,7 +1311,9 @@ int launch_peer_mem_ll(uint64_t* const* ll, int nranks, int me, uint16_t* bucket
     LLPtrs lp{};
     for (int q = 0; q < nranks; ++q) lp.ll[q] = ll[q];
     uint64_t groups = (nv + kBlock - 1) / kBlock;
-    const uint64_t cap = max_groups && max_groups < kPeerFusedMaxGroups ? max_groups : kPeerFusedMaxGroups;
+    uint64_t cap = max_groups && max_groups < kPeerFusedMaxGroups ? max_groups : kPeerFusedMaxGroups;
+    const uint64_t res = resident_limit(reinterpret_cast<const void*>(&k_peer_mem_ll), kBlock);   // all resident
+    if (res && cap > res) cap = res;
     if (groups > cap) groups = cap;   // resident: every wait is reached
     hipLaunchKernelGGL(k_peer_mem_ll, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, lp, nranks, me,
                        bucket, nv, nv / nranks, epoch, status);
@@ -1397,6 +1403,8 @@ int launch_peer_oneshot(uint16_t* const* wins, uint32_t* const* flags, int nrank
     const uint64_t bv = n / 8 / nranks;
     uint64_t groups = (bv + 63) / 64;
     if (groups > kPeerFusedMaxGroups) groups = kPeerFusedMaxGroups;
+    const uint64_t res = resident_limit(reinterpret_cast<const void*>(&k_peer_oneshot), kBlock);   // all resident
+    if (res && groups > res) groups = res;
     if (groups < 1) groups = 1;
     const uint64_t chunk = (bv + groups - 1) / groups;
     hipLaunchKernelGGL(k_peer_oneshot, dim3((unsigned)groups), dim3(kBlock), 0, (hipStream_t)stream, pp, nranks, me,
