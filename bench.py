@@ -758,7 +758,10 @@ def roofline_xgmi(extras: dict, world: int, crossed: bool = True) -> dict | None
                            else "not measured (no RCCL link probe: --share-gpu); frac null",
             "frac_unbounded": round(frac, 4) if frac is not None and not sane else None,
             "peak_spec": peak_spec, "frac_spec": bounded_frac(bus / peak_spec, crossed),
-            "achieved_def": "busbw = 2(p-1)/p * bytes_per_gpu / t"}
+            "achieved_def": "busbw = 2(p-1)/p * bytes_per_gpu / t",
+            # RCCL's own allreduce of the same 1 GiB per GPU (a comparator, not the product path)
+            "rccl_allreduce_busbw": (extras.get("rccl_allreduce_comparator") or {}).get("config4_1GiB", {}).get(
+                "busbw_GBps")}
 
 
 def link_probe(rank, world, dev) -> dict:
@@ -793,6 +796,61 @@ def link_probe(rank, world, dev) -> dict:
     dist.destroy_process_group(pg)
     return {"bytes": nbytes, "reps": reps, "GBps_per_direction": round(gbps, 2),
             "spec_GBps_per_direction": XGMI_LINK_DIR_GBPS, "pairs": "2i<->2i+1, both directions at once"}
+
+
+def rccl_allreduce_comparator(rank, world, dev, backend="nccl", sizes=None) -> dict:
+    """RCCL's own ncclAllReduce (torch.distributed's nccl backend = RCCL), bf16 SUM, on config 3's
+    640 kB and config 4's 1 GiB per GPU: an external comparator only, never the product path
+    (SURVEY §8(e)).  Each size verified first (small integers 0..7 per element from a hash of
+    (element, rank), so the sum is exact in any order), then timed like the arms (median of the
+    reps' wall over ranks, MAX); busbw as nccl-tests.  (backend / sizes: the CPU test runs the
+    same function over gloo on small buckets.)"""
+    pg = dist.new_group(backend=backend)
+    out = {}
+    chunk = 1 << 26
+
+    def sync():
+        if torch.device(dev).type == "cuda":
+            torch.cuda.synchronize()
+
+    def ints_(x, r):   # x (bf16) <- the small integers of rank r
+        for s0 in range(0, x.numel(), chunk):
+            e = torch.arange(s0, min(x.numel(), s0 + chunk), dtype=torch.int64, device=dev)
+            x[s0:s0 + e.numel()] = (((e * 2654435761 + r * 40503) >> 13) & 7).to(torch.bfloat16)
+
+    try:
+        for name, nbytes, reps in sizes or (("config3_640kB", ELEMS * 2, 50), ("config4_1GiB", 1 << 30, 5)):
+            n = nbytes // 2
+            x = torch.empty(n, dtype=torch.bfloat16, device=dev)
+            want = torch.zeros(n, dtype=torch.bfloat16, device=dev)
+            tmp = torch.empty_like(x)
+            for r in range(world):
+                ints_(tmp, r)
+                want += tmp   # exact: every partial sum <= 56
+            del tmp
+            ints_(x, rank)
+            dist.all_reduce(x, group=pg)
+            sync()
+            ok = agreed(bool(torch.equal(x, want)))
+            del want
+            for _ in range(2):
+                dist.all_reduce(x, group=pg)
+            sync()
+            dist.barrier()
+            per = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                dist.all_reduce(x, group=pg)
+                sync()
+                per.append(time.perf_counter() - t0)
+            dt = torch.tensor([statistics.median(per)], dtype=torch.float64)
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+            out[name] = {**arm_stats(dt.item() * 1e3, nbytes, world), "verified_exact": ok, "reps": reps,
+                         "op": "torch.distributed.all_reduce (RCCL ncclAllReduce), bf16 SUM"}
+            del x
+    finally:
+        dist.destroy_process_group(pg)
+    return out
 
 
 def xgmi_arms(comm, peer, world, rank, dev, stream, side, total, crossed=True, budget=None) -> dict:
@@ -1452,6 +1510,16 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
                                                                     not args.share_gpu)
             except Exception as e:  # reported, never silently dropped
                 extras["link_probe"] = {"error": repr(e)}
+        if world > 1 and comm is not None and budget.allows("rccl_allreduce_comparator"):
+            try:
+                with budget.phase("rccl_allreduce_comparator"):
+                    extras["rccl_allreduce_comparator"] = rccl_allreduce_comparator(rank, world, dev)
+                mb = extras.get("link_probe", {}).get("GBps_per_direction")
+                if mb:
+                    for v in extras["rccl_allreduce_comparator"].values():
+                        v["xgmi_frac_measured_link"] = bounded_frac(v["busbw_GBps"] / ((world - 1) * mb), True)
+            except Exception as e:  # reported, never silently dropped
+                extras["rccl_allreduce_comparator"] = {"error": repr(e)}
         guard.cancel()
     if peer is not None:
         st = torch.tensor([peer.status()], dtype=torch.int64)

@@ -176,3 +176,38 @@ def test_unverified_never_headline_nor_roofline():
     assert r["frac"] is None and r["peak"] is None and r["frac_spec"] > 0
     extras[arm]["verified"] = False
     assert bench.roofline_xgmi(extras, 8)["achieved"] is None
+
+
+def comparator_worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        out = bench.rccl_allreduce_comparator(rank, world, "cpu", backend="gloo",
+                                             sizes=(("small", 8 * 1024 * 2, 3), ("odd", 3000 * 2, 2)))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, {"exception": repr(e), "tb": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rccl_allreduce_comparator_verifies_and_reports_busbw(world):
+    """The N > 1 line's RCCL ncclAllReduce comparator (an external comparator,
+    never the product path) run over gloo on CPU: each size is verified exact on small integers
+    before it is timed, and reports busbw like the arms."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=comparator_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = dict(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for rank, out in results.items():
+        assert "exception" not in out, out
+        for name in ("small", "odd"):
+            v = out[name]
+            assert v["verified_exact"] is True and v["ms"] > 0 and v["busbw_GBps"] > 0, v
