@@ -315,3 +315,31 @@ def test_tune_table_is_the_product_forms_only():
         assert f" {key} " in tune_doc, f"{key} undocumented in allred.h"
     for key in RETIRED_KEYS:
         assert f" {key} " not in tune_doc, key
+
+
+def test_ctypes_structures_match_the_header_layout(tmp_path):
+    """Every struct _lib.py mirrors has the header's size and field offsets (a C program
+    compiled against include/allred.h prints them): a binding that drops or reorders a
+    field — e.g. a PlanDesc without mem_accum — reads past the caller's struct."""
+    structs = {"allred_plan_desc": _lib.PlanDesc, "allred_args": _lib.Args, "allred_report": _lib.Report,
+               "allred_dist_desc": _lib.DistDesc, "allred_multi_plan": _lib.MultiPlan,
+               "allred_multi_opts": _lib.MultiOpts, "allred_launch_info": _lib.LaunchInfo,
+               "allred_seg": _lib.Seg, "allred_schedule": _lib.Schedule}
+    lines = []
+    for cname, py in structs.items():
+        lines.append(f'    std::printf("{cname} size %zu\\n", sizeof({cname}));')
+        for fname, _ in py._fields_:
+            lines.append(f'    std::printf("{cname} {fname} %zu\\n", offsetof({cname}, {fname}));')
+    prog = tmp_path / "layout.cpp"
+    prog.write_text('#include <cstddef>\n#include <cstdio>\n#include "allred.h"\nint main() {\n' + "\n".join(lines) +
+                    "\n    return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        cname, field, value = line.split()
+        got[(cname, field)] = int(value)
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == C.sizeof(py), cname
+        for fname, _ in py._fields_:
+            assert got[(cname, fname)] == getattr(py, fname).offset, (cname, fname)
