@@ -250,6 +250,13 @@ def test_peer_scheduled_programs_across_gpus(world, tunes):
     tgp.run_world(tgp.dist_worker, world, 300, devs=devices(world), tunes=tunes)
 
 
+@pytest.mark.parametrize("world", WORLDS)
+def test_peer_hier_handoffs_under_launch_skew_across_gpus(world):
+    """tests/test_gpu_peer.py's skew_worker with one process per device: k_hier_ws calls and a
+    k_hier_x2 sequence with random spins (0-300 us) ahead of every call, bit-exact."""
+    tgp.run_world(tgp.skew_worker, world, 300, devs=devices(world))
+
+
 @pytest.mark.parametrize("tunes", FENCES, ids=["relaxed", "fenced"])
 def test_peer_config3_config5_across_8_gpus(tunes):
     """BASELINE configs 3 and 5 over the peer windows with one process per device."""

@@ -280,6 +280,84 @@ def test_peer_scheduled_program_multi_process_one_gpu(world, tunes):
     run_world(dist_worker, world, 300, tunes=tunes)
 
 
+def skew_worker(rank, world, port, q, devs=None, tunes=None):
+    """The hierarchical hand-offs under launch skew: before each call every process queues a
+    spin of a random length (per rank and call, 0-300 us: up to twenty kernels' time) on its
+    stream, so the processes' launches run out of step — 12 back-to-back k_hier_ws calls, then
+    a k_hier_x2 sequence of 8 buckets with the same skew between its calls.  Every bucket must
+    equal the oracle's composition bit for bit: a launch may overwrite a parity's hand-off
+    slots only once every consumer of that parity's previous call is done, and
+    skew is what would break a protocol that leans on the processes running in step."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import tenstorrentallreduce_amd as t
+        import oracle
+        import bench
+        devs, dev, shared = placement(rank, world, devs, tunes)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        local, m = 64, 256 * world * 4
+        peer = t.Peer(world, rank, devs[rank], m)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        peer.set_max_groups(256 // world if shared else 0)
+        peer.set_hier_ll(1)
+        s = torch.cuda.current_stream()
+        cyc = bench.spin_cycles_per_us(s)
+        rng = np.random.default_rng(4242 + rank)
+
+        def data(c, r):
+            return np.random.default_rng(6000 + 100 * c + r).integers(0x3F80, 0x42C8, (local, m)).astype(np.uint16)
+
+        def expected(c):
+            partials = []
+            for r in range(world):
+                loc = [x.copy() for x in data(c, r)]
+                oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+                partials.append(loc[0])
+            oracle.allreduce("mem", 0, 1, partials, world)
+            return partials[rank]
+
+        def skew():
+            torch.cuda._sleep(int(rng.integers(0, 300) * cyc))
+
+        fails = []
+        ws = torch.empty(m, dtype=torch.int16, device=dev)
+        bufs = [torch.from_numpy(data(c, rank).view(np.int16)).to(dev) for c in range(20)]
+        torch.cuda.synchronize()
+        dist.barrier()
+        for c in range(12):   # k_hier_ws, one launch per bucket
+            skew()
+            peer.allreduce(bufs[c].data_ptr(), m, s, local, 8, t.SWING, ws.data_ptr())
+        for c in range(12, 20):   # k_hier_x2, two buckets deep
+            skew()
+            peer.allreduce_pipelined2(bufs[c].data_ptr(), m, s)
+        skew()
+        peer.allreduce_pipelined2(None, m, s)
+        torch.cuda.synchronize()
+        for c, b in enumerate(bufs):
+            bad = int((b.cpu().numpy().view(np.uint16) != expected(c)[None, :]).sum())
+            if bad:
+                fails.append(("skew", c, bad))
+        status = peer.status()
+        dist.barrier()
+        peer.set_hier_ll(0)
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_hier_handoffs_under_launch_skew_one_gpu(world):
+    run_world(skew_worker, world, 300)
+
+
 def big_window_worker(rank, world, port, q):
     """allred_peer_create / connect with the bench's windows (1 GiB buckets,
     2 parities): an IPC-exported allocation of ~2 GiB hung in the peer's
