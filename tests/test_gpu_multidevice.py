@@ -258,6 +258,15 @@ def test_peer_hier_handoffs_under_launch_skew_across_gpus(world):
 
 
 @pytest.mark.parametrize("tunes", FENCES, ids=["relaxed", "fenced"])
+@pytest.mark.parametrize("world", WORLDS)
+def test_peer_flat_programs_under_launch_skew_across_gpus(world, tunes):
+    """tests/test_gpu_peer.py's skew_flat_worker with one process per device: mem_2D (launches,
+    one-shot, LL) and the scheduled BO / LO programs (pull, push, LL) with random spins ahead of
+    every call, bit-exact."""
+    tgp.run_world(tgp.skew_flat_worker, world, 300, devs=devices(world), tunes=tunes)
+
+
+@pytest.mark.parametrize("tunes", FENCES, ids=["relaxed", "fenced"])
 def test_peer_config3_config5_across_8_gpus(tunes):
     """BASELINE configs 3 and 5 over the peer windows with one process per device."""
     tgp.run_world(tgp.config35_worker, 8, 300, devs=devices(8), tunes=tunes)

@@ -358,6 +358,86 @@ def test_hier_handoffs_under_launch_skew_one_gpu(world):
     run_world(skew_worker, world, 300)
 
 
+def skew_flat_worker(rank, world, port, q, devs=None, tunes=None):
+    """The flat peer programs under launch skew (a random 0-300 us spin ahead of every call, per
+    rank): mem_2D in its three forms (launches, k_peer_oneshot, k_peer_mem_ll) and the scheduled
+    BO / LO programs (k_peer_sched, its push form, k_peer_lo_ll), 6 calls of each back to back
+    with no host sync, every result bit-exact vs the oracle — window parities, epochs and flag
+    values must hold while the processes run out of step."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import tenstorrentallreduce_amd as t
+        import oracle
+        import bench
+        import test_dist_host as tdh
+        devs, dev, shared = placement(rank, world, devs, tunes)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        side, total = tdh.GRIDS[world]
+        n = 8 * total * 16 * 12
+        peer = t.Peer(world, rank, devs[rank], 4 * n)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        peer.set_max_groups(256 // world if shared else 0)
+        s = torch.cuda.current_stream()
+        cyc = bench.spin_cycles_per_us(s)
+        rng = np.random.default_rng(777 + rank)
+        fails = []
+        # (name, setup, call, expected) per form
+        forms = [("mem_launches", dict(oneshot=0, mem_ll=0), None), ("mem_oneshot", dict(oneshot=1 << 40, mem_ll=0), None),
+                 ("mem_ll", dict(oneshot=0, mem_ll=1 << 40), None),
+                 ("bo_sched", dict(lo_ll=0, push=0), ("bo", t.SWING)), ("bo_push", dict(lo_ll=0, push=1), ("bo", t.SWING)),
+                 ("lo_ll", dict(lo_ll=256 << 10, push=0), ("lo", t.RECDUB)), ("lo_sched", dict(lo_ll=0, push=0), ("lo", t.SWING))]
+        for fi, (name, knobs, prog) in enumerate(forms):
+            peer.set_oneshot_max(knobs.get("oneshot", 4 << 20))
+            peer.set_mem_ll_max(knobs.get("mem_ll", 256 << 10))
+            peer.set_lo_ll_max(knobs.get("lo_ll", 256 << 10))
+            peer.set_sched_push(knobs.get("push", 0))
+            calls = []
+            torch.cuda.synchronize()
+            dist.barrier()
+            for c in range(6):
+                data = tdh.inputs(world, 1, n, seed=90000 + 1000 * fi + 10 * c)
+                buf = torch.from_numpy(data[rank][0].view(np.int16)).to(dev)
+                torch.cuda._sleep(int(rng.integers(0, 300) * cyc))
+                if prog is None:
+                    peer.allreduce(buf.data_ptr(), n, s)
+                else:
+                    variant, algo = prog
+                    desc = t.dist_desc(algo, t.BO if variant == "bo" else t.LO, side, total, n)
+                    peer.dist_allreduce(desc, buf.data_ptr(), None, s)
+                calls.append((data, buf))
+            torch.cuda.synchronize()
+            for c, (data, buf) in enumerate(calls):
+                if prog is None:
+                    want = [d[0].copy() for d in data]
+                    oracle.allreduce("mem", 0, 1, want, world)
+                    want = want[rank]
+                else:
+                    want = tdh.expected(prog[0], prog[1], world, 1, data, 1)[rank][0]
+                bad = int((buf.cpu().numpy().view(np.uint16) != want).sum())
+                if bad:
+                    fails.append((name, c, bad))
+        status = peer.status()
+        dist.barrier()
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+@FENCES
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_peer_flat_programs_under_launch_skew_one_gpu(world, tunes):
+    run_world(skew_flat_worker, world, 300, tunes=tunes)
+
+
 def big_window_worker(rank, world, port, q):
     """allred_peer_create / connect with the bench's windows (1 GiB buckets,
     2 parities): an IPC-exported allocation of ~2 GiB hung in the peer's

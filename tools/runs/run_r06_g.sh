@@ -1,8 +1,8 @@
-# round-6: the hierarchical hand-offs under launch skew (random spins ahead of every call) with 2 / 4 / 8
-# processes sharing the GPU, and the same cases rehearsed through the multi-device test (every rank on device 0)
+# round-6: the peer hand-offs under launch skew (random spins ahead of every call) — the hierarchical forms and the
+# flat programs, 2 / 4 / 8 processes sharing the GPU, and the multi-device twins rehearsed on device 0
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/r06g
+out=gpurun_out/${R06G_OUT:-r06g}
 mkdir -p $out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_peer.py -k skew -v --timeout 300 --timeout-method thread \
     > $out/tests.log 2>&1 &&
