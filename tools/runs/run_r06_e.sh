@@ -2,7 +2,7 @@
 # its rocprofv3 kernel stats, and the 8-process N > 1 rehearsal under the budget
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/r06e
+out=gpurun_out/${R06E_OUT:-r06e}
 mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rs --maxfail=5 --timeout 400 --timeout-method thread \
     > $out/tests.log 2>&1
