@@ -387,7 +387,7 @@ def skew_flat_worker(rank, world, port, q, devs=None, tunes=None):
         cyc = bench.spin_cycles_per_us(s)
         rng = np.random.default_rng(777 + rank)
         fails = []
-        # (name, setup, call, expected) per form
+        # (name, knobs, program: None = mem_2D through allred_peer_allreduce, else (variant, algo))
         forms = [("mem_launches", dict(oneshot=0, mem_ll=0), None), ("mem_oneshot", dict(oneshot=1 << 40, mem_ll=0), None),
                  ("mem_ll", dict(oneshot=0, mem_ll=1 << 40), None),
                  ("bo_sched", dict(lo_ll=0, push=0), ("bo", t.SWING)), ("bo_push", dict(lo_ll=0, push=1), ("bo", t.SWING)),
