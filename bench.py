@@ -426,17 +426,34 @@ def bench_single(args) -> dict:
     return out
 
 
+def agreed_spin_cycles(stream, host_s: float) -> int:
+    """torch.cuda._sleep cycles that outlast the slowest rank's host queueing of a timed
+    region (host_s seconds on that rank): 3x the MAX over ranks + 200 us — the same spin on
+    every rank, so no rank's timed region starts waiting for another's longer spin"""
+    h = torch.tensor([host_s], dtype=torch.float64)
+    dist.all_reduce(h, op=dist.ReduceOp.MAX)
+    return int((3.0 * h.item() * 1e6 + 200.0) * spin_cycles_per_us(stream))
+
+
 def timed_max(fn, reps, stream, after=None) -> float:
     """ms per call on `stream`, max over ranks.  after(): completes the calls
-    (the pipelined transport's last bucket), inside the timed region."""
+    (the pipelined transport's last bucket), inside the timed region.  The calls
+    are queued behind a spin kernel sized from the warm calls' host time, so the
+    GPU does not wait for the host inside the timed region (round 6; round 5's
+    W = 1 k_hier_ws figure was such a wait)."""
+    h0 = time.perf_counter()
     for _ in range(2):
         fn()
     if after:
         after()
+    host_s = (time.perf_counter() - h0) / 2 * reps
     torch.cuda.synchronize()
+    cycles = agreed_spin_cycles(stream, host_s)
     dist.barrier()
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        torch.cuda._sleep(cycles)
     e0.record(stream)
     for _ in range(reps):
         fn()
@@ -1121,10 +1138,21 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         reps = reps or max(3, min(args.reps, 5))
         torch.cuda.synchronize()
         dist.barrier()
+        # one untimed repetition: the host's cost of queueing K steps sizes the spin kernel
+        # below (the same on every rank), so the GPU never waits for the host in the timed region
+        h0 = time.perf_counter()
+        for i in range(args.steps):
+            step_fn(i)
+        if after is not None:
+            after()
+        host_s = (time.perf_counter() - h0) * reps
+        torch.cuda.synchronize()
+        cycles = agreed_spin_cycles(stream, host_s)
+        dist.barrier()
         torch.cuda.synchronize()
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
         with torch.cuda.stream(stream):
-            torch.cuda._sleep(200000)
+            torch.cuda._sleep(cycles)
         ev[0].record(stream)
         for r in range(reps):
             for i in range(args.steps):

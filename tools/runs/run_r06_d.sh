@@ -3,7 +3,7 @@
 # recording xgmi.budget (phase seconds, total wall, skipped phases)
 set -o pipefail
 export TMPDIR=/tmp
-out=gpurun_out/r06d
+out=gpurun_out/${R06D_OUT:-r06d}
 mkdir -p $out
 timeout -k 10 500 python bench.py --force-dist --steps 20 --warmup 5 > $out/force_dist.json 2> $out/force_dist.err &&
 timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
