@@ -778,3 +778,81 @@ def test_hier_handoff_epoch_wrap_is_cleared(first_tiles):
         peer.set_hier_ll(0)
         peer.set_max_groups(0)
         peer.close()
+
+
+def wrap_worker(rank, world, port, q, devs=None, tunes=None):
+    """The epoch-wrap clear where a stale word would be READ: W processes, one bucket of
+    `first` tiles at call 0, 131069 two-tile calls, then a bucket of 64 tiles at call 131070
+    that rank W-1 joins ~3 ms late (a spin ahead of its launch).  The other ranks' writing
+    waves poll their inbox slots for rank W-1's partials at once; slots that still hold call
+    0's words carry call 131070's 16-bit epoch, so without the clear they are taken as this
+    call's partials (wrong sums); with it every word waits for rank W-1."""
+    try:
+        import torch.distributed as dist
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import tenstorrentallreduce_amd as t
+        import oracle
+        import bench
+        first = int(os.environ.get("WRAP_FIRST_TILES", "32"))
+        devs, dev, shared = placement(rank, world, devs, tunes)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        local, small, large = 64, 256 * world, 256 * 64
+        peer = t.Peer(world, rank, devs[rank], large)
+        handles = [None] * world
+        dist.all_gather_object(handles, peer.handle())
+        peer.connect(handles)
+        peer.set_max_groups(256 // world if shared else 0)
+        peer.set_hier_ll(1)
+        s = torch.cuda.current_stream()
+        ws = torch.empty(large, dtype=torch.int16, device=dev)
+
+        def data(c, r, n):
+            return np.random.default_rng(7000 + 100 * c + r).integers(0x3F80, 0x42C8, (local, n)).astype(np.uint16)
+
+        def expected(c, n):
+            partials = []
+            for r in range(world):
+                loc = [x.copy() for x in data(c, r, n)]
+                oracle.allreduce("lo", 1, 8, loc, local)   # tree of local rank 0
+                partials.append(loc[0])
+            oracle.allreduce("mem", 0, 1, partials, world)
+            return partials[rank]
+
+        fails = []
+        b0 = torch.from_numpy(data(0, rank, 256 * first).view(np.int16)).to(dev)
+        peer.allreduce(b0.data_ptr(), 256 * first, s, local, 8, t.SWING, ws.data_ptr())   # call 0
+        sm = torch.from_numpy(data(1, rank, small).view(np.int16)).to(dev)
+        for i in range(131069):                                                         # calls 1 .. 131069
+            peer.allreduce(sm.data_ptr(), small, s, local, 8, t.SWING, ws.data_ptr())
+            if i % 16384 == 16383:
+                torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        b2 = torch.from_numpy(data(2, rank, large).view(np.int16)).to(dev)
+        torch.cuda.synchronize()
+        dist.barrier()
+        if rank == world - 1:
+            torch.cuda._sleep(int(3000 * bench.spin_cycles_per_us(s)))
+        peer.allreduce(b2.data_ptr(), large, s, local, 8, t.SWING, ws.data_ptr())     # call 131070
+        torch.cuda.synchronize()
+        bad = int((b2.cpu().numpy().view(np.uint16) != expected(2, large)[None, :]).sum())
+        if bad:
+            fails.append(("call 131070", bad))
+        status = peer.status()
+        dist.barrier()
+        peer.set_hier_ll(0)
+        peer.close()
+        dist.destroy_process_group()
+        q.put((rank, fails, status))
+    except Exception as e:  # pragma: no cover
+        import traceback
+        q.put((rank, [("exception", repr(e), traceback.format_exc())], -1))
+
+
+@pytest.mark.parametrize("first_tiles", [64, 32])
+def test_hier_handoff_epoch_wrap_across_processes(first_tiles, monkeypatch):
+    """tests the clear where a late peer makes a stale word readable (2 processes, rank 1 late)."""
+    monkeypatch.setenv("WRAP_FIRST_TILES", str(first_tiles))
+    run_world(wrap_worker, 2, 300)
+
