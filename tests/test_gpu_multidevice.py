@@ -257,6 +257,14 @@ def test_peer_hier_handoffs_under_launch_skew_across_gpus(world):
     tgp.run_world(tgp.skew_worker, world, 300, devs=devices(world))
 
 
+@pytest.mark.parametrize("first_tiles", [64, 32])
+def test_peer_hier_epoch_wrap_across_gpus(first_tiles, monkeypatch):
+    """tests/test_gpu_peer.py's wrap_worker with one process per device: the hand-off area's
+    epoch-wrap clear where a late peer makes a stale word readable, bit-exact."""
+    monkeypatch.setenv("WRAP_FIRST_TILES", str(first_tiles))
+    tgp.run_world(tgp.wrap_worker, 2, 300, devs=devices(2))
+
+
 @pytest.mark.parametrize("tunes", FENCES, ids=["relaxed", "fenced"])
 @pytest.mark.parametrize("world", WORLDS)
 def test_peer_flat_programs_under_launch_skew_across_gpus(world, tunes):
