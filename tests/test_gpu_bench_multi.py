@@ -57,3 +57,35 @@ def test_bench_two_ranks_share_gpu():
     assert b["deadline_s"] == 420.0 and 0 < b["wall_s"] < b["deadline_s"]
     assert {"setup", "headline", "local_phases"} <= set(b["phase_s"]) and b["skipped_for_deadline"] == []
     assert any(k.startswith("verify:") for k in b["phase_s"]) and any(k.startswith("quick:") for k in b["phase_s"])
+
+
+ONE_RANK_RCCL = r"""
+import json, os, sys
+sys.path.insert(0, sys.argv[1])
+import torch, torch.distributed as dist
+import bench
+dist.init_process_group("gloo", rank=0, world_size=1)
+torch.cuda.set_device(0)
+probe = bench.link_probe(0, 1, "cuda:0")
+comp = bench.rccl_allreduce_comparator(0, 1, "cuda:0", sizes=(("small_64kB", 64 << 10, 5), ("config4_1GiB", 1 << 30, 2)))
+dist.destroy_process_group()
+print(json.dumps({"probe": probe, "comp": comp}))
+"""
+
+
+def test_rccl_side_extras_run_over_torch_nccl_with_one_rank():
+    """The two N > 1 extras that only run with an RCCL communicator and world > 1
+    (link_probe, rccl_allreduce_comparator) have no --share-gpu rehearsal: RCCL
+    refuses two ranks on one device.  Their code — torch's nccl group created from
+    the gloo default group, the batched sendrecv, the exact-integer fill and check
+    of a 1 GiB bf16 bucket on the device, the group's teardown — runs here on one
+    rank, so the first multi-GPU node meets code that already ran on this chip."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()))
+    p = subprocess.run([sys.executable, "-c", ONE_RANK_RCCL, ROOT], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["probe"]["bytes"] == 128 << 20 and d["probe"]["reps"] == 5
+    for name in ("small_64kB", "config4_1GiB"):
+        c = d["comp"][name]
+        assert c["verified_exact"] is True and c["ms"] > 0 and c["busbw_GBps"] == 0.0   # 2(p-1)/p = 0 at p = 1
