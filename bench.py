@@ -543,6 +543,7 @@ class Budget:
         self.deadline, self.t0 = deadline_s, t0
         self.phase_s, self.skipped = {}, []
         self.longest = 0.0
+        self.current = "start"   # the phase running now, or "after <phase>" (the watchdog's diagnosis)
 
     def elapsed(self) -> float:
         return time.perf_counter() - self.t0
@@ -553,12 +554,16 @@ class Budget:
     @contextlib.contextmanager
     def phase(self, name: str):
         t0 = time.perf_counter()
+        self.current = name
+        if os.environ.get("ALLRED_BENCH_TEST_HANG_IN") == name:   # tests only: a host-side hang in this phase
+            time.sleep(1e6)
         try:
             yield
         finally:
             d = time.perf_counter() - t0
             self.phase_s[name] = round(self.phase_s.get(name, 0.0) + d, 3)
             self.longest = max(self.longest, d)
+            self.current = "after " + name
 
     def allows(self, name: str, agree: bool = True) -> bool:
         ok = self.left() > max(60.0, 2.0 * self.longest)
@@ -570,7 +575,7 @@ class Budget:
 
     def report(self) -> dict:
         return {"deadline_s": self.deadline, "wall_s": round(self.elapsed(), 3), "phase_s": dict(self.phase_s),
-                "skipped_for_deadline": list(self.skipped),
+                "skipped_for_deadline": list(self.skipped), "phase_now": self.current,
                 "rule": "a phase starts only while the budget left covers max(60 s, 2 x the longest phase so far)"}
 
 
@@ -1094,6 +1099,7 @@ def cli_config3(world: int, share: bool = False) -> dict:
 
 def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     budget = Budget(args.deadline, _T0)
+    BUDGET[0] = budget
     setup = budget.phase("setup")
     setup.__enter__()
     # --share-gpu (rehearsal only): every rank on cuda:0 and no RCCL (it refuses two
@@ -1348,6 +1354,9 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
         fb_ms, _ = timed_steps(lambda i: run("rccl", bufs[i % len(bufs)]))
         fb_local = local_phases_ms()
         FALLBACK_DONE.set()
+        BEST_LINE[0] = lambda: multi_line(args, world, "rccl", fb_ms, fb_local, time.perf_counter() - t_start,
+                                          {"headline_transport": "rccl", "transport_verified": dict(verify),
+                                           "budget": budget.report()})
 
         # the peer phase may take --peer-timeout s, and never past the deadline (less the extras' margin)
         peer_limit = max(30.0, min(args.peer_timeout, budget.left() - 90.0))
@@ -1504,6 +1513,16 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     def line(ex):
         return multi_line(args, world, transport, ms_per_step, local_ms, wall, ex)
 
+    def best_line():   # the headline with the extras gathered so far (main()'s last-resort watchdog)
+        try:
+            ex = {k: v for k, v in list(extras.items())}
+        except Exception:  # extras being written concurrently: headline only
+            ex = {}
+        ex["budget"] = budget.report()
+        return line(ex)
+
+    BEST_LINE[0] = best_line
+
     if args.extras:
         # The headline is measured; the extras must not be able to lose it.  If
         # they have not finished after --extras-timeout s (a hung transport on an
@@ -1583,6 +1602,40 @@ def bench_multi(args, rank, world, local_rank, emit) -> dict | None:
     if cpu is not None:
         out["cpu_baseline"] = cpu
     return out
+
+
+# the N > 1 run's budget and the best line it could print so far (a callable: the RCCL fallback
+# once measured, then the headline with the extras gathered so far), for main()'s last-resort watchdog
+BUDGET = [None]
+BEST_LINE = [None]
+# rank 0's one JSON line goes out once, whichever of the normal path and the watchdogs gets there first
+EMITTED = threading.Event()
+_EMIT_LOCK = threading.Lock()
+
+
+def watchdog_line(args, world: int, limit_s: float) -> dict:
+    """What main()'s last-resort watchdog prints when the N > 1 run has not printed its line
+    limit_s seconds after bench.py started (a host-side hang no phase watchdog covers: RCCL
+    setup or verification before the fallback is measured, teardown): the best line measured
+    so far with xgmi.watchdog, else a line with value null and the phase it hung in."""
+    b = BUDGET[0]
+    where = b.current if b is not None else "before the N > 1 setup"
+    msg = f"the N > 1 run had not printed its line {limit_s:.0f} s after bench.py started (phase: {where})"
+    ln = None
+    if BEST_LINE[0] is not None:
+        try:
+            ln = BEST_LINE[0]()
+        except Exception as e:  # reported below, never silently dropped
+            msg += f"; the measured line could not be rebuilt: {e!r}"
+    if ln is not None:
+        ln.setdefault("xgmi", {})["watchdog"] = msg
+        return ln
+    return {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": None, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+            "config": {"workload": f"config 2 per GPU (64 virtual ranks x 655,360 B, 8x8 Swing) x {world} GPUs",
+                       "parallelism": f"dp{world}"},
+            "error": msg, "xgmi": {"budget": b.report() if b is not None else None}}
 
 
 # set once the N > 1 headline is measured: a rank that then loses its peers
@@ -1708,10 +1761,34 @@ def main():
             dist.init_process_group("gloo", rank=0, world_size=1)
         else:
             dist.init_process_group("gloo")
-        def emit(line):
-            sys.stdout.flush()
-            os.write(real_stdout, (json.dumps(line) + "\n").encode())
+        def emit(line):   # rank 0's one line, whoever gets there first
+            with _EMIT_LOCK:
+                if EMITTED.is_set():
+                    return
+                sys.stdout.flush()
+                os.write(real_stdout, (json.dumps(line) + "\n").encode())
+                EMITTED.set()
 
+        # last resort: the phase watchdogs (peer phase, extras) cover the hangs they can fall back
+        # from; anything else (RCCL setup / verification before the fallback, teardown) ends here,
+        # --deadline + 120 s after bench.py started (the driver's lease is 600 s), with a line
+        hard_s = float(os.environ.get("ALLRED_BENCH_HARD_S", args.deadline + 120.0))
+
+        def last_resort():
+            code = 0
+            if rank == 0 and not EMITTED.is_set():
+                ln = watchdog_line(args, world, hard_s)
+                note(rank, ln.get("error") or ln["xgmi"]["watchdog"])
+                emit(ln)
+                code = 0 if ln.get("value") is not None else 1
+            sys.stderr.flush()
+            os._exit(code)
+
+        # rank 0 first: the others leave 15 s later, so rank 0's line is not lost to their exit
+        hard = threading.Timer(max(1.0, hard_s - (time.perf_counter() - _T0)) + (0 if rank == 0 else 15),
+                               last_resort)
+        hard.daemon = True
+        hard.start()
         try:
             out = bench_multi(args, rank, world, local_rank, emit)
         except Exception as e:
@@ -1720,6 +1797,9 @@ def main():
             note(rank, f"ended by a peer's exit ({e!r}); rank 0 reports the line")
             sys.stderr.flush()
             os._exit(0)
+        if out is not None:
+            emit(out)
+            out = None
         dist.destroy_process_group()
     elif args.tilesum_only is not None:
         sizes = [m << 20 for m in (args.tilesum_only or [256, 1024])]

@@ -52,3 +52,37 @@ def test_n_gt_1_budget_skips_extras_before_the_deadline(monkeypatch):
     assert r["wall_s"] == 320.0 and r["deadline_s"] == 420.0
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert 'ap.add_argument("--deadline", type=float, default=420.0' in src   # < the driver's 600 s
+
+
+def test_last_resort_watchdog_line(monkeypatch):
+    """main()'s last-resort watchdog for the N > 1 run (a host-side hang no phase watchdog
+    covers): with nothing measured it prints a line with value null, the metric and the phase
+    it hung in; once a line was measured (the RCCL fallback, then the headline) it prints that
+    line with xgmi.watchdog."""
+    import argparse
+    args = argparse.Namespace(steps=20, warmup=5)
+    now = [0.0]
+    monkeypatch.setattr(bench.time, "perf_counter", lambda: now[0])
+    b = bench.Budget(420.0, t0=0.0)
+    monkeypatch.setattr(bench, "BUDGET", [b])
+    monkeypatch.setattr(bench, "BEST_LINE", [None])
+    with b.phase("setup"):
+        now[0] += 3.0
+    cm = b.phase("verify:rccl")
+    cm.__enter__()                                   # hangs in here
+    now[0] += 537.0
+    ln = bench.watchdog_line(args, 8, 540.0)
+    assert ln["metric"] == bench.METRIC and ln["value"] is None and ln["n_gpus"] == 8
+    assert "phase: verify:rccl" in ln["error"] and ln["xgmi"]["budget"]["phase_now"] == "verify:rccl"
+    assert ln["xgmi"]["budget"]["phase_s"] == {"setup": 3.0}
+    bench.BEST_LINE[0] = lambda: {"metric": bench.METRIC, "value": 123.0, "xgmi": {"headline_transport": "rccl"}}
+    ln = bench.watchdog_line(args, 8, 540.0)
+    assert ln["value"] == 123.0 and "phase: verify:rccl" in ln["xgmi"]["watchdog"]
+
+    def broken():
+        raise RuntimeError("boom")
+    bench.BEST_LINE[0] = broken                       # a line that cannot be rebuilt: still a line
+    ln = bench.watchdog_line(args, 8, 540.0)
+    assert ln["value"] is None and "boom" in ln["error"]
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert 'os.environ.get("ALLRED_BENCH_HARD_S", args.deadline + 120.0)' in src   # 540 s < the 600 s lease

@@ -89,3 +89,36 @@ def test_rccl_side_extras_run_over_torch_nccl_with_one_rank():
     for name in ("small_64kB", "config4_1GiB"):
         c = d["comp"][name]
         assert c["verified_exact"] is True and c["ms"] > 0 and c["busbw_GBps"] == 0.0   # 2(p-1)/p = 0 at p = 1
+
+
+def run_hung(phase: str, hard_s: int):
+    env = dict(os.environ, ALLRED_BENCH_TEST_HANG_IN=phase, ALLRED_BENCH_HARD_S=str(hard_s))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--share-gpu", "--steps", "10", "--warmup", "2", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=hard_s + 120)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, (p.stdout[-2000:], p.stderr[-3000:])
+    return p, json.loads(lines[0])
+
+
+def test_last_resort_watchdog_before_anything_is_measured():
+    """A host-side hang before any number exists (here: in the peer comparator's
+    verification; on a node, e.g. RCCL setup) ends at the last-resort watchdog with one
+    line: value null, the phase it hung in, and a failing exit status."""
+    p, d = run_hung("verify:peer_launches", 45)
+    assert p.returncode != 0
+    assert d["metric"] == bench.METRIC and d["value"] is None and d["n_gpus"] == 2
+    assert "phase: verify:peer_launches" in d["error"] and d["xgmi"]["budget"]["phase_now"] == "verify:peer_launches"
+
+
+def test_last_resort_watchdog_after_the_headline():
+    """A hang after the headline (here: rank 0 entering cli_config3 while the others wait at
+    the final barrier) still prints the measured line — the verified headline with the extras
+    gathered so far and xgmi.watchdog — and every rank exits 0."""
+    p, d = run_hung("cli_config3", 90)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert d["metric"] == bench.METRIC and d["value"] > 0 and d["config"]["verified"] is True
+    x = d["xgmi"]
+    assert "phase: cli_config3" in x["watchdog"] and x["budget"]["phase_now"] == "cli_config3"
+    assert "headline" in x["budget"]["phase_s"] and "cli_config3" not in x
