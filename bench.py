@@ -1713,6 +1713,8 @@ def multi_line(args, world, transport, ms_per_step, local_ms, wall, extras) -> d
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": roof["traffic"], "kernel": roof["kernel"],
                      "algorithmic_bytes_per_launch": roof["algorithmic_bytes_per_launch"],
+                     # the PMC pass runs on one GPU: at W > 1 the hand-off words add to it
+                     "traffic_source": "profiles/pmc_traffic.json, measured at W = 1",
                      "local_phases_ms": round(local_ms, 6)},
         "roofline_xgmi": roofline_xgmi(extras, world, crossed=not args.share_gpu),
         "xgmi": extras,
