@@ -38,6 +38,7 @@ import statistics  # noqa: E402
 import subprocess  # noqa: E402
 import sys  # noqa: E402
 import threading  # noqa: E402
+import traceback  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -557,6 +558,8 @@ class Budget:
         self.current = name
         if os.environ.get("ALLRED_BENCH_TEST_HANG_IN") == name:   # tests only: a host-side hang in this phase
             time.sleep(1e6)
+        if os.environ.get("ALLRED_BENCH_TEST_RAISE_IN") == name:   # tests only: an error in this phase
+            raise RuntimeError(f"test error in {name}")
         try:
             yield
         finally:
@@ -1613,14 +1616,14 @@ EMITTED = threading.Event()
 _EMIT_LOCK = threading.Lock()
 
 
-def watchdog_line(args, world: int, limit_s: float) -> dict:
-    """What main()'s last-resort watchdog prints when the N > 1 run has not printed its line
-    limit_s seconds after bench.py started (a host-side hang no phase watchdog covers: RCCL
-    setup or verification before the fallback is measured, teardown): the best line measured
-    so far with xgmi.watchdog, else a line with value null and the phase it hung in."""
+def watchdog_line(args, world: int, reason: str) -> dict:
+    """What rank 0 prints when the N > 1 run cannot finish its line (reason): main()'s
+    last-resort watchdog (a host-side hang no phase watchdog covers: RCCL setup or
+    verification before the fallback is measured, teardown) or an exception: the best line
+    measured so far with xgmi.watchdog, else a line with value null and the phase it was in."""
     b = BUDGET[0]
     where = b.current if b is not None else "before the N > 1 setup"
-    msg = f"the N > 1 run had not printed its line {limit_s:.0f} s after bench.py started (phase: {where})"
+    msg = f"{reason} (phase: {where})"
     ln = None
     if BEST_LINE[0] is not None:
         try:
@@ -1779,7 +1782,8 @@ def main():
         def last_resort():
             code = 0
             if rank == 0 and not EMITTED.is_set():
-                ln = watchdog_line(args, world, hard_s)
+                ln = watchdog_line(args, world, f"the N > 1 run had not printed its line {hard_s:.0f} s after "
+                                                "bench.py started")
                 note(rank, ln.get("error") or ln["xgmi"]["watchdog"])
                 emit(ln)
                 code = 0 if ln.get("value") is not None else 1
@@ -1794,7 +1798,13 @@ def main():
         try:
             out = bench_multi(args, rank, world, local_rank, emit)
         except Exception as e:
-            if rank == 0 or not (HEADLINE_DONE.is_set() or FALLBACK_DONE.is_set()):
+            if rank == 0:   # still one line: the best measured so far, else value null and the error
+                traceback.print_exc()
+                ln = watchdog_line(args, world, f"the N > 1 run raised {e!r}")
+                emit(ln)
+                sys.stderr.flush()
+                os._exit(0 if ln.get("value") is not None else 1)
+            if not (HEADLINE_DONE.is_set() or FALLBACK_DONE.is_set()):
                 raise
             note(rank, f"ended by a peer's exit ({e!r}); rank 0 reports the line")
             sys.stderr.flush()

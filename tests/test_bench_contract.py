@@ -71,18 +71,18 @@ def test_last_resort_watchdog_line(monkeypatch):
     cm = b.phase("verify:rccl")
     cm.__enter__()                                   # hangs in here
     now[0] += 537.0
-    ln = bench.watchdog_line(args, 8, 540.0)
+    ln = bench.watchdog_line(args, 8, "hung")
     assert ln["metric"] == bench.METRIC and ln["value"] is None and ln["n_gpus"] == 8
-    assert "phase: verify:rccl" in ln["error"] and ln["xgmi"]["budget"]["phase_now"] == "verify:rccl"
+    assert ln["error"] == "hung (phase: verify:rccl)" and ln["xgmi"]["budget"]["phase_now"] == "verify:rccl"
     assert ln["xgmi"]["budget"]["phase_s"] == {"setup": 3.0}
     bench.BEST_LINE[0] = lambda: {"metric": bench.METRIC, "value": 123.0, "xgmi": {"headline_transport": "rccl"}}
-    ln = bench.watchdog_line(args, 8, 540.0)
+    ln = bench.watchdog_line(args, 8, "hung")
     assert ln["value"] == 123.0 and "phase: verify:rccl" in ln["xgmi"]["watchdog"]
 
     def broken():
         raise RuntimeError("boom")
     bench.BEST_LINE[0] = broken                       # a line that cannot be rebuilt: still a line
-    ln = bench.watchdog_line(args, 8, 540.0)
+    ln = bench.watchdog_line(args, 8, "hung")
     assert ln["value"] is None and "boom" in ln["error"]
     src = open(os.path.join(ROOT, "bench.py")).read()
     assert 'os.environ.get("ALLRED_BENCH_HARD_S", args.deadline + 120.0)' in src   # 540 s < the 600 s lease

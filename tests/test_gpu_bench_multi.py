@@ -91,8 +91,9 @@ def test_rccl_side_extras_run_over_torch_nccl_with_one_rank():
         assert c["verified_exact"] is True and c["ms"] > 0 and c["busbw_GBps"] == 0.0   # 2(p-1)/p = 0 at p = 1
 
 
-def run_hung(phase: str, hard_s: int):
-    env = dict(os.environ, ALLRED_BENCH_TEST_HANG_IN=phase, ALLRED_BENCH_HARD_S=str(hard_s))
+def run_hung(phase: str, hard_s: int, how: str = "HANG"):
+    env = dict(os.environ, ALLRED_BENCH_HARD_S=str(hard_s))
+    env[f"ALLRED_BENCH_TEST_{how}_IN"] = phase
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--share-gpu", "--steps", "10", "--warmup", "2", "--no-cpu-baseline"]
@@ -122,3 +123,12 @@ def test_last_resort_watchdog_after_the_headline():
     x = d["xgmi"]
     assert "phase: cli_config3" in x["watchdog"] and x["budget"]["phase_now"] == "cli_config3"
     assert "headline" in x["budget"]["phase_s"] and "cli_config3" not in x
+
+
+def test_an_error_before_anything_is_measured_still_prints_one_line():
+    """An exception on rank 0 before any number exists (here: raised entering the headline
+    phase) prints one line — value null, the error and the phase — and fails the run."""
+    p, d = run_hung("headline", 120, how="RAISE")
+    assert p.returncode != 0
+    assert d["metric"] == bench.METRIC and d["value"] is None
+    assert "test error in headline" in d["error"] and "(phase: headline)" in d["error"]
